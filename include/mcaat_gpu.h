@@ -1,0 +1,150 @@
+/*
+ * mcaat_gpu.h — C ABI of the MI355X-native mcaat hot path
+ * (node_counter -> sdbg_build -> cycle_finder). Plain pointers and sizes only.
+ *
+ * The reference has no FFI for this path; its boundary is three C++ classes that
+ * share one Settings object. Each entry point below names the
+ * reference interface it replaces. The host-side C++ mirror (mcaat_amd/host/)
+ * keeps the reference class names (SDBGBuild, SDBG, CycleFinder) on top of this ABI.
+ *
+ * Conventions: every int-returning call returns 0 (MCAAT_OK) on success or a negative
+ * mcaat_status; mcaat_last_error() gives a thread-local message (the host mirror turns
+ * it into std::runtime_error, as cycle_finder.cpp:135 does). The library owns device
+ * buffers; the caller owns handles and frees them. Calls on one mcaat_ctx must come
+ * from one host thread (not reentrant per ctx); one ctx drives one GPU on one HIP stream.
+ * Every call is synchronous with respect to the host unless stated.
+ */
+#ifndef MCAAT_GPU_H
+#define MCAAT_GPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum mcaat_status {
+    MCAAT_OK = 0,
+    MCAAT_E_INVALID = -1,  /* bad argument */
+    MCAAT_E_HIP = -2,      /* HIP runtime error (no GPU, launch failure) */
+    MCAAT_E_NOMEM = -3,    /* device or host allocation failed */
+    MCAAT_E_IO = -4,       /* file open/parse failure */
+    MCAAT_E_CAPACITY = -5  /* a bounded structure overflowed and could not be regrown */
+};
+
+typedef struct mcaat_ctx mcaat_ctx;
+typedef struct mcaat_reads mcaat_reads;
+typedef struct mcaat_graph mcaat_graph;
+typedef struct mcaat_cycles mcaat_cycles;
+
+/* ---- context ------------------------------------------------------------- */
+/* Replaces: nothing in the reference (single process, OpenMP). Binds one GPU. */
+int mcaat_init(int device, mcaat_ctx **out);
+void mcaat_finalize(mcaat_ctx *ctx);
+const char *mcaat_last_error(void);
+int mcaat_device_count(int *n);
+
+/* ---- reads ----------------------------------------------------------------
+ * Replaces: SDBGBuild::BuildLib / SequenceLibCollection::Build (sdbg_build.cpp:82-115):
+ * FASTQ/FASTA(.gz) -> 2-bit packed read library, here resident in HBM.
+ * Packed stream: base j at word j>>5, bits 2*(j&31), A=0 C=1 G=2 T=3.
+ * offsets[n_reads+1] are base offsets of each read in the stream. */
+int mcaat_reads_from_host(mcaat_ctx *ctx, const uint64_t *packed, uint64_t n_words,
+                          const uint64_t *offsets, uint64_t n_reads, mcaat_reads **out);
+/* Non-ACGT symbols split a read (k-mers spanning them are dropped). gz via zlib. */
+int mcaat_reads_from_fastx(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_reads **out);
+int mcaat_reads_info(const mcaat_reads *r, uint64_t *n_reads, uint64_t *n_bases);
+int mcaat_reads_download(const mcaat_reads *r, uint64_t *packed, uint64_t *offsets);
+void mcaat_reads_free(mcaat_reads *r);
+
+/* Synthetic metagenome: iid genomes with CRISPR arrays inserted,
+ * reads with substitution errors, generated directly in HBM by a counter-based RNG. */
+typedef struct {
+    uint64_t seed;
+    uint32_t n_genomes;
+    uint64_t genome_len;
+    uint32_t arrays_per_genome;
+    uint32_t spacers_per_array;
+    uint32_t repeat_len_min, repeat_len_max;
+    uint32_t spacer_len_min, spacer_len_max;
+    uint32_t read_len;
+    uint64_t n_reads;
+    double error_rate;
+    int32_t paired; /* 1: pairs (fragment 300+-30, R2 = reverse complement of fragment end) */
+} mcaat_synth_spec;
+int mcaat_reads_synth(mcaat_ctx *ctx, const mcaat_synth_spec *spec, mcaat_reads **out);
+/* host-side generator of the same reads (for tests and FASTQ fixtures) */
+int mcaat_synth_host(const mcaat_synth_spec *spec, uint64_t *packed, uint64_t *offsets);
+/* the genome sequences (n_genomes*genome_len bases, packed) and array truth */
+int mcaat_synth_genome_host(const mcaat_synth_spec *spec, uint64_t *packed);
+
+/* ---- node_counter ----------------------------------------------------------
+ * Replaces: the multiplicity counting inside MEGAHIT Read2SdbgS2::Run
+ * (sdbg_build.cpp:171-187). Exact canonical (k+1)-mer counts; results copied to
+ * host buffers allocated with malloc (free with mcaat_free). Keys are LSB-first
+ * canonical (k+1)-mers, sorted ascending. */
+int mcaat_count_edges(mcaat_ctx *ctx, const mcaat_reads *r, int k, uint64_t *n_distinct,
+                      uint64_t **keys, uint32_t **counts);
+void mcaat_free(void *p);
+
+/* ---- sdbg_build --------------------------------------------------------------
+ * Replaces: SDBGBuild::SDBGBuild(Settings) + SDBG::LoadFromFile (sdbg_build.cpp:3-13,
+ * 196-232; main.cpp:517-530). k is hard-coded to 23 in the reference
+ * (sdbg_build.cpp:217); any 2 <= k <= 30 is accepted here. The graph stays in HBM. */
+int mcaat_build_graph(mcaat_ctx *ctx, const mcaat_reads *r, int k, mcaat_graph **out);
+int mcaat_graph_info(const mcaat_graph *g, int *k, uint64_t *n_edges);
+/* Host view for the SDBG mirror (MEGAHIT SDBG API subset):
+ * BOSS keys, multiplicities and one valid byte per edge (any pointer may be NULL). */
+int mcaat_graph_download(const mcaat_graph *g, uint64_t *keys, uint16_t *mult, uint8_t *valid);
+/* Keeps device valid bits coherent with host SetInvalidEdge/SetValidEdge
+ * (spacer_ordering.cpp:96-138 mutates them downstream). */
+int mcaat_graph_set_valid(mcaat_graph *g, const uint64_t *ids, size_t n, int valid);
+/* Batched device queries (OutgoingEdges/IncomingEdges, valid-only): out[4*i..] and
+ * counts[i] for each id; order DESCENDING for outgoing, ASCENDING for incoming. */
+int mcaat_graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, int incoming,
+                          uint64_t *out, int32_t *counts);
+void mcaat_graph_free(mcaat_graph *g);
+
+/* ---- cycle_finder ------------------------------------------------------------
+ * Replaces: CycleFinder::CycleFinder(Settings&) -> FindApproximateCRISPRArrays
+ * (cycle_finder.cpp:131-138, 433-492). Mutates the graph's valid bits exactly as the
+ * reference mutates the SDBG. Results follow the reference's threads=1 commit order
+ * (bucket by descending ceil(log2 mult), ascending edge id inside a bucket). */
+typedef struct {
+    uint64_t threshold_multiplicity; /* settings.h:34 (default 20) */
+    int32_t low_abundance;           /* settings.h:35 (default 1)  */
+    int32_t cycle_max_length;        /* settings.h:36 (default 77) */
+    int32_t cycle_min_length;        /* settings.h:37 (default 27) */
+    int32_t cluster_bound;           /* cycle_finder.cpp:132 (500) */
+    int64_t step_cap;                /* cycle_finder.cpp:149 (10000000) */
+} mcaat_cf_params;
+void mcaat_cf_default_params(mcaat_cf_params *p);
+int mcaat_cycle_finder(mcaat_graph *g, const mcaat_cf_params *p, mcaat_cycles **out);
+/* number of `results` entries (start nodes with an entry, possibly empty) */
+int mcaat_cycles_count(const mcaat_cycles *c, size_t *n_entries);
+/* entry i in commit order: start node, its cycles as one flat node array plus
+ * n_cycles+1 offsets into it; pointers stay valid until mcaat_cycles_free */
+int mcaat_cycles_get(const mcaat_cycles *c, size_t i, uint64_t *start, const uint64_t **flat,
+                     const uint64_t **offsets, size_t *n_cycles);
+/* stats: [0] tips before pruning, [1] invalidated mult<=1, [2] valid after pruning,
+ * [3] tips after pruning, [4] start candidates passing DLS, [5] total cycles,
+ * [6] FindCycle speculation rounds, [7] FindCycle re-runs after conflicts */
+int mcaat_cycles_stats(const mcaat_cycles *c, uint64_t *stats);
+/* start candidates in processing order and their ceil(log2 mult) bucket */
+int mcaat_cycles_candidates(const mcaat_cycles *c, size_t *n, const uint64_t **ids, const int32_t **buckets);
+void mcaat_cycles_free(mcaat_cycles *c);
+
+/* ---- measurement -------------------------------------------------------------
+ * Per-stage device time of the last build/cycle_finder call on this ctx, measured
+ * with HIP events on the library's stream. names[i] are static strings. */
+int mcaat_stage_times(const mcaat_ctx *ctx, int max, const char **names, double *ms, int *n);
+/* average duration (ms) and launch count of the dominant counting kernel since the
+ * last reset, measured with HIP events around each launch on the library's stream */
+int mcaat_kernel_timing(const mcaat_ctx *ctx, const char *kernel, double *avg_ms, uint64_t *launches,
+                        double *bytes_per_launch);
+void mcaat_reset_timing(mcaat_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

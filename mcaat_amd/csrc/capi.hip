@@ -1,0 +1,539 @@
+// capi.hip — extern "C" boundary of libmcaat_gpu.so (include/mcaat_gpu.h).
+// Every entry point converts internal exceptions into a negative status plus a
+// thread-local message (mcaat_last_error), the way the host mirror expects.
+#include <zlib.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+
+#include "internal.h"
+#include "synth.h"
+
+using namespace mcaat;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+template <class F>
+int guarded(F &&f) {
+    try {
+        f();
+        return MCAAT_OK;
+    } catch (const Error &e) {
+        g_last_error = e.what();
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        g_last_error = "host allocation failed";
+        return MCAAT_E_NOMEM;
+    } catch (const std::exception &e) {
+        g_last_error = e.what();
+        return MCAAT_E_INVALID;
+    }
+}
+
+void require(bool c, const char *msg) {
+    if (!c) throw Error(MCAAT_E_INVALID, msg);
+}
+
+constexpr int kBlock = 256;
+
+__global__ void k_synth(mcaat_synth_spec s, const uint64_t *genome, uint64_t *packed, uint64_t n_words) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < n_words; w += stride)
+        packed[w] = synth_word(s, genome, w);
+}
+
+__global__ void k_fixed_offsets(uint64_t *off, uint64_t n, uint64_t L) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += stride) off[i] = i * L;
+}
+
+void check_spec(const mcaat_synth_spec &s) {
+    require(s.n_genomes > 0 && s.genome_len > 0 && s.read_len > 0, "synth: empty genome or read length");
+    require(s.read_len <= s.genome_len, "synth: read longer than genome");
+    require(s.repeat_len_min <= s.repeat_len_max && s.spacer_len_min <= s.spacer_len_max, "synth: bad length range");
+    if (s.arrays_per_genome) {
+        const uint64_t worst = (uint64_t)(s.spacers_per_array + 1) * s.repeat_len_max +
+                               (uint64_t)s.spacers_per_array * s.spacer_len_max;
+        require(worst * s.arrays_per_genome <= s.genome_len, "synth: arrays do not fit the genome");
+    }
+}
+
+void upload_reads(mcaat_ctx *ctx, const uint64_t *packed, uint64_t n_words, const uint64_t *offsets,
+                  uint64_t n_reads, mcaat_reads *r) {
+    r->ctx = ctx;
+    r->n_reads = n_reads;
+    r->n_bases = offsets[n_reads];
+    r->n_words = n_words;
+    require((r->n_bases + 31) / 32 <= n_words, "reads: packed stream shorter than the offsets say");
+    r->fixed_len = 0;
+    if (n_reads > 0) {
+        const uint64_t L = offsets[1] - offsets[0];
+        bool fixed = offsets[0] == 0 && L > 0;
+        for (uint64_t i = 0; fixed && i <= n_reads; ++i) fixed = offsets[i] == i * L;
+        if (fixed) r->fixed_len = L;
+    }
+    r->packed.alloc(n_words + 1);
+    r->offsets.alloc(n_reads + 1);
+    HIP_OK(hipMemsetAsync(r->packed.p, 0, r->packed.bytes(), ctx->stream));
+    HIP_OK(hipMemcpyAsync(r->packed.p, packed, 8 * n_words, hipMemcpyHostToDevice, ctx->stream));
+    HIP_OK(hipMemcpyAsync(r->offsets.p, offsets, 8 * (n_reads + 1), hipMemcpyHostToDevice, ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+}
+
+// FASTQ/FASTA(.gz) -> packed reads. Records are split at non-ACGT symbols.
+struct Packer {
+    std::vector<uint64_t> words;
+    std::vector<uint64_t> offsets{0};
+    uint64_t n = 0;
+    void put(int b) {
+        if ((n >> 5) >= words.size()) words.push_back(0);
+        words[n >> 5] |= (uint64_t)b << (2 * (n & 31));
+        ++n;
+    }
+    void end_read() {
+        if (n != offsets.back()) offsets.push_back(n);
+    }
+    void add_sequence(const std::string &s) {
+        for (char ch : s) {
+            int b;
+            switch (ch) {
+                case 'A': case 'a': b = 0; break;
+                case 'C': case 'c': b = 1; break;
+                case 'G': case 'g': b = 2; break;
+                case 'T': case 't': b = 3; break;
+                default: b = -1;
+            }
+            if (b < 0) end_read();
+            else put(b);
+        }
+        end_read();
+    }
+};
+
+void read_fastx(const char *path, Packer &pk) {
+    gzFile f = gzopen(path, "rb");
+    if (!f) throw Error(MCAAT_E_IO, std::string("cannot open ") + path);
+    std::string line, seq;
+    char buf[1 << 16];
+    auto getline = [&](std::string &out) -> bool {
+        out.clear();
+        for (;;) {
+            if (!gzgets(f, buf, sizeof(buf))) return !out.empty();
+            out += buf;
+            if (!out.empty() && out.back() == '\n') {
+                out.pop_back();
+                if (!out.empty() && out.back() == '\r') out.pop_back();
+                return true;
+            }
+        }
+    };
+    bool fastq = false, first = true;
+    std::string pending_header;
+    while (true) {
+        if (!getline(line)) break;
+        if (line.empty()) continue;
+        if (first) {
+            first = false;
+            if (line[0] == '@') fastq = true;
+            else if (line[0] != '>') { gzclose(f); throw Error(MCAAT_E_IO, std::string("not FASTA/FASTQ: ") + path); }
+        }
+        if (fastq) {
+            if (line[0] != '@') { gzclose(f); throw Error(MCAAT_E_IO, std::string("malformed FASTQ: ") + path); }
+            std::string s, plus, q;
+            getline(s);
+            getline(plus);
+            getline(q);
+            pk.add_sequence(s);
+        } else {
+            if (line[0] == '>') {
+                if (!seq.empty()) pk.add_sequence(seq);
+                seq.clear();
+            } else {
+                seq += line;
+            }
+        }
+    }
+    if (!fastq && !seq.empty()) pk.add_sequence(seq);
+    gzclose(f);
+}
+
+}  // namespace
+
+namespace mcaat {
+
+// genome of the synthetic community: iid bases, arrays R S1 R S2 ... R Sn R written
+// into disjoint slots (one slot per array) of each genome
+void synth_genome_host(const mcaat_synth_spec &s, std::vector<uint64_t> &genome) {
+    check_spec(s);
+    const uint64_t total = (uint64_t)s.n_genomes * s.genome_len;
+    genome.assign((total + 31) / 32 + 1, 0);
+    auto setb = [&](uint64_t j, int b) {
+        uint64_t &w = genome[j >> 5];
+        const int sh = 2 * (int)(j & 31);
+        w = (w & ~(3ULL << sh)) | ((uint64_t)b << sh);
+    };
+    for (uint64_t g = 0; g < s.n_genomes; ++g)
+        for (uint64_t i = 0; i < s.genome_len; ++i) setb(g * s.genome_len + i, (int)(hash3(s.seed, g, i ^ 0xA11) & 3));
+    for (uint64_t g = 0; g < s.n_genomes; ++g) {
+        for (uint32_t a = 0; a < s.arrays_per_genome; ++a) {
+            const uint64_t h0 = hash3(s.seed ^ 0xC415, g, a);
+            const uint32_t lr = s.repeat_len_min + (uint32_t)(h0 % (s.repeat_len_max - s.repeat_len_min + 1));
+            const uint32_t ls_max = s.spacer_len_max;
+            const uint64_t slot = s.genome_len / s.arrays_per_genome;
+            uint64_t len = (uint64_t)(s.spacers_per_array + 1) * lr + (uint64_t)s.spacers_per_array * ls_max;
+            const uint64_t room = slot > len ? slot - len : 0;
+            uint64_t pos = g * s.genome_len + a * slot + (room ? hash3(s.seed ^ 0x9051, g, a) % room : 0);
+            std::vector<int> rep(lr);
+            for (uint32_t i = 0; i < lr; ++i) rep[i] = (int)(hash3(s.seed ^ 0x4e9, g * 1000003 + a, i) & 3);
+            for (uint32_t c = 0; c <= s.spacers_per_array; ++c) {
+                for (uint32_t i = 0; i < lr; ++i) setb(pos++, rep[i]);
+                if (c == s.spacers_per_array) break;
+                const uint64_t hs = hash3(s.seed ^ 0x5ACE, g * 1000003 + a, c);
+                const uint32_t ls = s.spacer_len_min + (uint32_t)(hs % (s.spacer_len_max - s.spacer_len_min + 1));
+                for (uint32_t i = 0; i < ls; ++i) setb(pos++, (int)(hash3(hs, c, i) & 3));
+            }
+        }
+    }
+}
+
+void synth_reads(mcaat_ctx *ctx, const mcaat_synth_spec &s, mcaat_reads *out) {
+    std::vector<uint64_t> genome;
+    synth_genome_host(s, genome);
+    hipStream_t st = ctx->stream;
+    DevBuf<uint64_t> dg(genome.size());
+    HIP_OK(hipMemcpyAsync(dg.p, genome.data(), 8 * genome.size(), hipMemcpyHostToDevice, st));
+    out->ctx = ctx;
+    out->n_reads = s.n_reads;
+    out->n_bases = s.n_reads * s.read_len;
+    out->n_words = (out->n_bases + 31) / 32;
+    out->fixed_len = s.read_len;
+    out->packed.alloc(out->n_words + 1);
+    out->offsets.alloc(s.n_reads + 1);
+    HIP_OK(hipMemsetAsync(out->packed.p, 0, out->packed.bytes(), st));
+    hipLaunchKernelGGL(k_synth, dim3(grid_for(out->n_words, kBlock)), dim3(kBlock), 0, st, s, dg.p, out->packed.p,
+                       out->n_words);
+    LAUNCH_OK();
+    hipLaunchKernelGGL(k_fixed_offsets, dim3(grid_for(s.n_reads + 1, kBlock)), dim3(kBlock), 0, st,
+                       out->offsets.p, s.n_reads, (uint64_t)s.read_len);
+    LAUNCH_OK();
+    HIP_OK(hipStreamSynchronize(st));
+}
+
+}  // namespace mcaat
+
+extern "C" {
+
+const char *mcaat_last_error(void) { return g_last_error.c_str(); }
+
+int mcaat_device_count(int *n) {
+    return guarded([&] {
+        require(n != nullptr, "null argument");
+        int c = 0;
+        hipError_t e = hipGetDeviceCount(&c);
+        if (e != hipSuccess) { (void)hipGetLastError(); c = 0; }
+        *n = c;
+    });
+}
+
+int mcaat_init(int device, mcaat_ctx **out) {
+    return guarded([&] {
+        require(out != nullptr, "null argument");
+        int c = 0;
+        hipError_t e = hipGetDeviceCount(&c);
+        if (e != hipSuccess || c == 0) {
+            (void)hipGetLastError();
+            throw Error(MCAAT_E_HIP, "no HIP device available");
+        }
+        require(device >= 0 && device < c, "device index out of range");
+        HIP_OK(hipSetDevice(device));
+        auto *ctx = new mcaat_ctx;
+        ctx->device = device;
+        hipError_t se = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+        if (se != hipSuccess) {
+            delete ctx;
+            throw Error(MCAAT_E_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(se));
+        }
+        *out = ctx;
+    });
+}
+
+void mcaat_finalize(mcaat_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int mcaat_reads_from_host(mcaat_ctx *ctx, const uint64_t *packed, uint64_t n_words, const uint64_t *offsets,
+                          uint64_t n_reads, mcaat_reads **out) {
+    return guarded([&] {
+        require(ctx && out && offsets && (packed || n_words == 0), "null argument");
+        HIP_OK(hipSetDevice(ctx->device));
+        auto *r = new mcaat_reads;
+        try {
+            upload_reads(ctx, packed, n_words, offsets, n_reads, r);
+        } catch (...) {
+            delete r;
+            throw;
+        }
+        *out = r;
+    });
+}
+
+int mcaat_reads_from_fastx(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_reads **out) {
+    return guarded([&] {
+        require(ctx && out && files && n_files > 0, "null argument");
+        HIP_OK(hipSetDevice(ctx->device));
+        Packer pk;
+        for (int i = 0; i < n_files; ++i) read_fastx(files[i], pk);
+        auto *r = new mcaat_reads;
+        try {
+            upload_reads(ctx, pk.words.data(), pk.words.size(), pk.offsets.data(), pk.offsets.size() - 1, r);
+        } catch (...) {
+            delete r;
+            throw;
+        }
+        *out = r;
+    });
+}
+
+int mcaat_reads_info(const mcaat_reads *r, uint64_t *n_reads, uint64_t *n_bases) {
+    return guarded([&] {
+        require(r != nullptr, "null argument");
+        if (n_reads) *n_reads = r->n_reads;
+        if (n_bases) *n_bases = r->n_bases;
+    });
+}
+
+int mcaat_reads_download(const mcaat_reads *r, uint64_t *packed, uint64_t *offsets) {
+    return guarded([&] {
+        require(r != nullptr, "null argument");
+        HIP_OK(hipSetDevice(r->ctx->device));
+        if (packed) HIP_OK(hipMemcpy(packed, r->packed.p, 8 * r->n_words, hipMemcpyDeviceToHost));
+        if (offsets) HIP_OK(hipMemcpy(offsets, r->offsets.p, 8 * (r->n_reads + 1), hipMemcpyDeviceToHost));
+    });
+}
+
+void mcaat_reads_free(mcaat_reads *r) { delete r; }
+
+int mcaat_reads_synth(mcaat_ctx *ctx, const mcaat_synth_spec *spec, mcaat_reads **out) {
+    return guarded([&] {
+        require(ctx && spec && out, "null argument");
+        check_spec(*spec);
+        HIP_OK(hipSetDevice(ctx->device));
+        auto *r = new mcaat_reads;
+        try {
+            synth_reads(ctx, *spec, r);
+        } catch (...) {
+            delete r;
+            throw;
+        }
+        *out = r;
+    });
+}
+
+int mcaat_synth_host(const mcaat_synth_spec *spec, uint64_t *packed, uint64_t *offsets) {
+    return guarded([&] {
+        require(spec && packed && offsets, "null argument");
+        std::vector<uint64_t> genome;
+        synth_genome_host(*spec, genome);
+        const uint64_t nb = spec->n_reads * spec->read_len, nw = (nb + 31) / 32;
+        for (uint64_t w = 0; w < nw; ++w) packed[w] = synth_word(*spec, genome.data(), w);
+        for (uint64_t i = 0; i <= spec->n_reads; ++i) offsets[i] = i * spec->read_len;
+    });
+}
+
+int mcaat_synth_genome_host(const mcaat_synth_spec *spec, uint64_t *packed) {
+    return guarded([&] {
+        require(spec && packed, "null argument");
+        std::vector<uint64_t> genome;
+        synth_genome_host(*spec, genome);
+        const uint64_t total = (uint64_t)spec->n_genomes * spec->genome_len;
+        memcpy(packed, genome.data(), 8 * ((total + 31) / 32));
+    });
+}
+
+int mcaat_count_edges(mcaat_ctx *ctx, const mcaat_reads *r, int k, uint64_t *n_distinct, uint64_t **keys,
+                      uint32_t **counts) {
+    return guarded([&] {
+        require(ctx && r && n_distinct && keys && counts, "null argument");
+        require(k >= 2 && k <= kMaxK, "k must be in [2, 30]");
+        HIP_OK(hipSetDevice(ctx->device));
+        CountResult c;
+        node_counter(ctx, r, k, c);
+        sort_counts(ctx, c, k);
+        *n_distinct = c.n;
+        *keys = (uint64_t *)malloc(8 * (c.n ? c.n : 1));
+        *counts = (uint32_t *)malloc(4 * (c.n ? c.n : 1));
+        if (!*keys || !*counts) throw std::bad_alloc();
+        if (c.n) {
+            HIP_OK(hipMemcpy(*keys, c.keys.p, 8 * c.n, hipMemcpyDeviceToHost));
+            HIP_OK(hipMemcpy(*counts, c.counts.p, 4 * c.n, hipMemcpyDeviceToHost));
+        }
+    });
+}
+
+void mcaat_free(void *p) { free(p); }
+
+int mcaat_build_graph(mcaat_ctx *ctx, const mcaat_reads *r, int k, mcaat_graph **out) {
+    return guarded([&] {
+        require(ctx && r && out, "null argument");
+        require(k >= 2 && k <= kMaxK, "k must be in [2, 30]");
+        HIP_OK(hipSetDevice(ctx->device));
+        auto *g = new mcaat_graph;
+        g->ctx = ctx;
+        try {
+            StageTimer timer(ctx);
+            CountResult c;
+            node_counter(ctx, r, k, c);
+            timer.mark("node_counter");
+            sdbg_build(ctx, c, k, g);
+            timer.mark("sdbg_build");
+            HIP_OK(hipStreamSynchronize(ctx->stream));
+            timer.finish();
+        } catch (...) {
+            delete g;
+            throw;
+        }
+        *out = g;
+    });
+}
+
+int mcaat_graph_info(const mcaat_graph *g, int *k, uint64_t *n_edges) {
+    return guarded([&] {
+        require(g != nullptr, "null argument");
+        if (k) *k = g->k;
+        if (n_edges) *n_edges = g->D;
+    });
+}
+
+int mcaat_graph_download(const mcaat_graph *g, uint64_t *keys, uint16_t *mult, uint8_t *valid) {
+    return guarded([&] {
+        require(g != nullptr, "null argument");
+        HIP_OK(hipSetDevice(g->ctx->device));
+        if (keys && g->D) HIP_OK(hipMemcpy(keys, g->key.p, 8 * g->D, hipMemcpyDeviceToHost));
+        if (mult && g->D) HIP_OK(hipMemcpy(mult, g->mult.p, 2 * g->D, hipMemcpyDeviceToHost));
+        if (valid) graph_download_valid(g, valid);
+    });
+}
+
+int mcaat_graph_set_valid(mcaat_graph *g, const uint64_t *ids, size_t n, int valid) {
+    return guarded([&] {
+        require(g && (ids || n == 0), "null argument");
+        HIP_OK(hipSetDevice(g->ctx->device));
+        graph_set_valid(g, ids, n, valid);
+    });
+}
+
+int mcaat_graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, int incoming, uint64_t *out,
+                          int32_t *counts) {
+    return guarded([&] {
+        require(g && (n == 0 || (ids && out && counts)), "null argument");
+        for (size_t i = 0; i < n; ++i) require(ids[i] < g->D, "edge id out of range");
+        HIP_OK(hipSetDevice(g->ctx->device));
+        graph_neighbors(g, ids, n, incoming, out, counts);
+    });
+}
+
+void mcaat_graph_free(mcaat_graph *g) { delete g; }
+
+void mcaat_cf_default_params(mcaat_cf_params *p) {
+    if (!p) return;
+    p->threshold_multiplicity = 20;
+    p->low_abundance = 1;
+    p->cycle_max_length = 77;
+    p->cycle_min_length = 27;
+    p->cluster_bound = 500;
+    p->step_cap = 10000000;
+}
+
+int mcaat_cycle_finder(mcaat_graph *g, const mcaat_cf_params *p, mcaat_cycles **out) {
+    return guarded([&] {
+        require(g && p && out, "null argument");
+        require(p->cycle_max_length >= 2 && p->cycle_max_length <= 250, "cycle_max_length must be in [2, 250]");
+        require(p->cluster_bound >= 1 && p->cluster_bound <= 65535, "cluster_bound must be in [1, 65535]");
+        require(p->step_cap >= 1, "step_cap must be positive");
+        HIP_OK(hipSetDevice(g->ctx->device));
+        auto *c = new mcaat_cycles;
+        try {
+            cycle_finder(g, *p, c);
+        } catch (...) {
+            delete c;
+            throw;
+        }
+        *out = c;
+    });
+}
+
+int mcaat_cycles_count(const mcaat_cycles *c, size_t *n) {
+    return guarded([&] {
+        require(c && n, "null argument");
+        *n = c->starts.size();
+    });
+}
+
+int mcaat_cycles_get(const mcaat_cycles *c, size_t i, uint64_t *start, const uint64_t **flat,
+                     const uint64_t **offsets, size_t *n_cycles) {
+    return guarded([&] {
+        require(c != nullptr, "null argument");
+        require(i < c->starts.size(), "entry index out of range");
+        if (start) *start = c->starts[i];
+        if (flat) *flat = c->flat[i].data();
+        if (offsets) *offsets = c->offsets[i].data();
+        if (n_cycles) *n_cycles = c->offsets[i].size() - 1;
+    });
+}
+
+int mcaat_cycles_stats(const mcaat_cycles *c, uint64_t *stats) {
+    return guarded([&] {
+        require(c && stats, "null argument");
+        for (int i = 0; i < 8; ++i) stats[i] = c->stats[i];
+    });
+}
+
+int mcaat_cycles_candidates(const mcaat_cycles *c, size_t *n, const uint64_t **ids, const int32_t **buckets) {
+    return guarded([&] {
+        require(c && n, "null argument");
+        *n = c->cand_ids.size();
+        if (ids) *ids = c->cand_ids.data();
+        if (buckets) *buckets = c->cand_bucket.data();
+    });
+}
+
+void mcaat_cycles_free(mcaat_cycles *c) { delete c; }
+
+int mcaat_stage_times(const mcaat_ctx *ctx, int max, const char **names, double *ms, int *n) {
+    return guarded([&] {
+        require(ctx && n, "null argument");
+        int m = 0;
+        for (auto &s : ctx->stages) {
+            if (m < max) {
+                if (names) names[m] = s.first;
+                if (ms) ms[m] = s.second;
+            }
+            ++m;
+        }
+        *n = m;
+    });
+}
+
+int mcaat_kernel_timing(const mcaat_ctx *ctx, const char *kernel, double *avg_ms, uint64_t *launches,
+                        double *bytes_per_launch) {
+    return guarded([&] {
+        require(ctx && kernel, "null argument");
+        auto it = ctx->kstats.find(kernel);
+        const KernelStat s = it == ctx->kstats.end() ? KernelStat{} : it->second;
+        if (avg_ms) *avg_ms = s.launches ? s.total_ms / s.launches : 0.0;
+        if (launches) *launches = s.launches;
+        if (bytes_per_launch) *bytes_per_launch = s.bytes_per_launch;
+    });
+}
+
+void mcaat_reset_timing(mcaat_ctx *ctx) {
+    if (ctx) ctx->kstats.clear();
+}
+
+}  // extern "C"

@@ -1,0 +1,986 @@
+// cycle_finder.hip — CycleFinder (reference cycle_finder.cpp:131-492) on gfx950.
+//
+// Stages:
+//   1. CollectTips (:346-357)                -> wave-ballot bitmap scan
+//   2. InvalidateMultiplicityOneNodes (:372) -> wave-ballot bitmap AND
+//   3. RecursiveReduction (:359-371)          -> parallel peel fixpoint: unary chains are
+//      resolved by ruler walks + pointer jumping (list ranking), branch nodes by a short
+//      iteration. Same result as the recursion (monotone least fixpoint).
+//   4. valid count / tips again (:443-452)   -> popcount scans
+//   5. ChunkStartNodes (:387-427)            -> filter kernel + one DLS thread per candidate
+//   6. bucket loop of FindCycle (:468-487)   -> speculative FindCycle, one thread per start
+//      against a `visited` snapshot, committed on the host in the reference's threads=1
+//      order; a start whose search read a node that an earlier commit marked visited is
+//      re-run (its footprint is its lock table).
+// The libstdc++ unordered_set iteration order of FindCycle's neighbour frames is emulated
+// exactly (13 buckets, identity hash; DESIGN.md "FindCycle frame order").
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <map>
+#include <unordered_set>
+
+#include "internal.h"
+
+namespace mcaat {
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr uint64_t kNone = ~0ULL;
+constexpr uint8_t kUnk = 0, kRem = 1, kSurv = 2;
+
+// ------------------------------- scans -------------------------------------
+// one wave per 64-edge bitmap word
+__global__ void __launch_bounds__(kBlock) k_tips(GraphView g, uint64_t *tip_bm, unsigned long long *count) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (g.D + 63) / 64;
+    const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nw; w += wstride) {
+        const uint64_t e = w * 64 + lane;
+        bool t = false;
+        if (e < g.D && bit_get(g.valid, e)) t = dev_outdeg(g, e) == 0;
+        const unsigned long long m = __ballot(t);
+        if (lane == 0) {
+            if (tip_bm) tip_bm[w] = m;
+            if (m) atomicAdd(count, (unsigned long long)__popcll(m));
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_mult_filter(GraphView g, unsigned long long *count) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (g.D + 63) / 64;
+    const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nw; w += wstride) {
+        const uint64_t e = w * 64 + lane;
+        const bool low = e < g.D && g.mult[e] <= 1;
+        const unsigned long long m = __ballot(low);
+        if (lane == 0) {
+            const uint64_t old = g.valid[w];
+            g.valid[w] = old & ~m;
+            if (m) atomicAdd(count, (unsigned long long)__popcll(m));  // reference counts every mult<=1 edge
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_popcount(const uint64_t *bm, uint64_t nw, unsigned long long *count) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    unsigned long long s = 0;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) s += __popcll(bm[w]);
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
+    if ((threadIdx.x & 63) == 0 && s) atomicAdd(count, s);
+}
+
+// ------------------------------- peel --------------------------------------
+struct PeelArrays {
+    uint8_t *od;      // valid out-degree, 0xFF = invalid edge
+    uint8_t *upred;   // 1: some unary node points here
+    uint8_t *ruler;   // 1: unary node chosen as ruler
+    uint8_t *st;      // kUnk / kRem / kSurv
+    uint64_t *nxt;    // sole successor of a unary node
+    uint64_t *owner;  // ruler whose walk passed this node (kNone: none)
+    uint64_t *jump;   // for rulers: terminal reached (kNone: cycle)
+    const uint64_t *seed;  // tips bitmap collected before the multiplicity filter
+};
+
+__global__ void __launch_bounds__(kBlock) k_peel_init(GraphView g, PeelArrays pa) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < g.D; e += stride) {
+        if (!bit_get(g.valid, e)) { pa.od[e] = 0xFF; continue; }
+        uint64_t out[4];
+        const int n = dev_outgoing(g, e, out);
+        pa.od[e] = (uint8_t)n;
+        if (n == 1) {
+            pa.nxt[e] = out[0];
+            pa.upred[out[0]] = 1;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_peel_rulers(uint64_t D, PeelArrays pa, uint64_t *list,
+                                                        unsigned long long *cursor) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const int lane = threadIdx.x & 63;
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < D; base += stride) {
+        const uint64_t e = base + threadIdx.x;
+        bool r = false;
+        if (e < D && pa.od[e] == 1) r = pa.upred[e] == 0 || (mix64(e ^ 0x5eed) & 63) == 0;
+        if (e < D) pa.ruler[e] = r;
+        const unsigned long long m = __ballot(r);
+        unsigned long long off = 0;
+        if (lane == 0 && m) off = atomicAdd(cursor, (unsigned long long)__popcll(m));
+        off = __shfl(off, 0);
+        if (r) list[off + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = e;
+    }
+}
+
+// each ruler walks its chain to the next ruler or non-unary node (Brent cycle check)
+__global__ void __launch_bounds__(kBlock) k_peel_walk(PeelArrays pa, const uint64_t *list, uint64_t nr) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nr; i += stride) {
+        const uint64_t r = list[i];
+        pa.owner[r] = r;
+        uint64_t y = pa.nxt[r], tort = r;
+        uint64_t power = 1, lam = 1;
+        uint64_t res = kNone;
+        for (;;) {
+            if (pa.od[y] != 1 || pa.ruler[y]) { res = y; break; }
+            if (y == tort) { res = kNone; break; }  // ruler-less unary cycle reached
+            pa.owner[y] = r;
+            if (power == lam) { tort = y; power <<= 1; lam = 0; }
+            y = pa.nxt[y];
+            ++lam;
+        }
+        pa.jump[r] = res;
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_peel_jump(PeelArrays pa, const uint64_t *list, uint64_t nr) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nr; i += stride) {
+        const uint64_t r = list[i];
+        const uint64_t j = pa.jump[r];
+        if (j != kNone && pa.od[j] == 1) pa.jump[r] = pa.jump[j];
+    }
+}
+
+__device__ __forceinline__ uint8_t peel_res(const PeelArrays &pa, uint64_t y) {
+    if (pa.od[y] != 1) return pa.st[y];
+    const uint64_t o = pa.ruler[y] ? y : pa.owner[y];
+    if (o == kNone) return kSurv;  // unary node on a ruler-less cycle
+    const uint64_t t = pa.jump[o];
+    if (t == kNone || pa.od[t] == 1) return kSurv;  // chain ends in a unary cycle
+    return pa.st[t];
+}
+
+__global__ void __launch_bounds__(kBlock) k_peel_term(uint64_t D, PeelArrays pa, uint64_t *blist,
+                                                      unsigned long long *cursor) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const int lane = threadIdx.x & 63;
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < D; base += stride) {
+        const uint64_t e = base + threadIdx.x;
+        bool br = false;
+        if (e < D) {
+            const uint8_t o = pa.od[e];
+            if (o == 0) pa.st[e] = bit_get(pa.seed, e) ? kRem : kSurv;
+            else pa.st[e] = kUnk;
+            br = (o != 0xFF && o >= 2);
+        }
+        const unsigned long long m = __ballot(br);
+        unsigned long long off = 0;
+        if (lane == 0 && m) off = atomicAdd(cursor, (unsigned long long)__popcll(m));
+        off = __shfl(off, 0);
+        if (br) blist[off + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = e;
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_peel_branch(GraphView g, PeelArrays pa, const uint64_t *blist,
+                                                        uint64_t nb, int *changed) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += stride) {
+        const uint64_t b = blist[i];
+        if (pa.st[b] != kUnk) continue;
+        uint64_t out[4];
+        const int n = dev_outgoing(g, b, out);
+        bool all_rem = true, any_surv = false;
+        for (int j = 0; j < n; ++j) {
+            const uint8_t r = peel_res(pa, out[j]);
+            if (r == kSurv) any_surv = true;
+            if (r != kRem) all_rem = false;
+        }
+        if (any_surv) { pa.st[b] = kSurv; *changed = 1; }
+        else if (all_rem) { pa.st[b] = kRem; *changed = 1; }
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_peel_apply(GraphView g, PeelArrays pa) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (g.D + 63) / 64;
+    const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nw; w += wstride) {
+        const uint64_t e = w * 64 + lane;
+        bool rem = false;
+        if (e < g.D && pa.od[e] != 0xFF) rem = peel_res(pa, e) == kRem;
+        const unsigned long long m = __ballot(rem);
+        if (lane == 0 && m) g.valid[w] &= ~m;
+    }
+}
+
+// --------------------------- start candidates --------------------------------
+__global__ void __launch_bounds__(kBlock) k_candidates(GraphView g, uint64_t thr, uint64_t *list,
+                                                       unsigned long long *cursor) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const int lane = threadIdx.x & 63;
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < g.D; base += stride) {
+        const uint64_t e = base + threadIdx.x;
+        bool c = false;
+        if (e < g.D && bit_get(g.valid, e) && (uint64_t)g.mult[e] > thr) {
+            uint64_t in[4];
+            const int n = dev_incoming(g, e, in);
+            if (n >= 2) {
+                c = true;
+                for (int j = 0; j < n; ++j)
+                    if (in[j] == e) c = false;  // _IncomingNotEqualToCurrentNode
+            }
+        }
+        const unsigned long long m = __ballot(c);
+        unsigned long long off = 0;
+        if (lane == 0 && m) off = atomicAdd(cursor, (unsigned long long)__popcll(m));
+        off = __shfl(off, 0);
+        if (c) list[off + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = e;
+    }
+}
+
+// ------------------------------ DLS ------------------------------------------
+// DepthLevelSearch(v, v, limit) (cycle_finder.cpp:248-343), one thread per candidate.
+// res: 1 found, 0 not found, -1 scratch overflow (re-run with larger caps)
+__device__ __forceinline__ bool set_insert(uint64_t *tab, uint32_t cap, uint64_t x, uint32_t &size, bool &over) {
+    uint32_t s = (uint32_t)(mix64(x) & (cap - 1));
+    for (;;) {
+        const uint64_t c = tab[s];
+        if (c == x) return false;
+        if (c == kNone) {
+            if (size + 1 > cap / 4 * 3) { over = true; return false; }
+            tab[s] = x;
+            ++size;
+            return true;
+        }
+        s = (s + 1) & (cap - 1);
+    }
+}
+__device__ __forceinline__ bool set_contains(const uint64_t *tab, uint32_t cap, uint64_t x) {
+    uint32_t s = (uint32_t)(mix64(x) & (cap - 1));
+    for (;;) {
+        const uint64_t c = tab[s];
+        if (c == x) return true;
+        if (c == kNone) return false;
+        s = (s + 1) & (cap - 1);
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_dls(GraphView g, const uint64_t *cand, uint64_t n, int limit,
+                                                uint64_t *stack_all, uint32_t cs, uint64_t *vis_all, uint32_t cv,
+                                                int8_t *res) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t *stk = stack_all + i * cs;
+    uint64_t *vis = vis_all + i * cv;
+    for (uint32_t j = 0; j < cv; ++j) vis[j] = kNone;
+    const uint64_t start = cand[i];
+    uint32_t sp = 0, vsize = 0;
+    bool over = false;
+    stk[sp++] = start << 8;  // (node << 8) | depth
+    int8_t found = 0;
+    while (sp > 0) {
+        const uint64_t top = stk[--sp];
+        const uint64_t v = top >> 8;
+        const int depth = (int)(top & 0xFF);
+        if (!bit_get(g.valid, v)) continue;
+        uint64_t nb[4];
+        const int od = dev_outgoing(g, v, nb);
+        if (od == 0) continue;  // EdgeOutdegreeZero
+        if (depth >= limit) continue;
+        for (int j = 0; j < od; ++j) {
+            const uint64_t x = nb[j];
+            const bool nv = !set_contains(vis, cv, x);
+            const bool sr = (x == start && depth > 0);
+            if (nv || sr) {
+                set_insert(vis, cv, x, vsize, over);
+                if (sp >= cs) over = true;
+                if (over) break;
+                stk[sp++] = (x << 8) | (uint64_t)(depth + 1);
+            }
+        }
+        if (over) break;
+        if (v == start && depth > 1) { found = 1; break; }
+    }
+    res[i] = over ? -1 : found;
+}
+
+// ---------------------------- FindCycle ----------------------------------------
+struct FcCaps {
+    uint32_t P;    // path/frames capacity (max_len + 2)
+    uint32_t CL;   // lock/footprint table (power of two)
+    uint32_t CR;   // relax stack
+    uint32_t CO;   // output nodes
+    uint32_t CC;   // output cycle count (cluster bound)
+};
+struct FcParams {
+    int maxl, minl, cluster;
+    int64_t step_cap;
+};
+struct FcScratch {
+    uint64_t *path;     // P
+    int32_t *bl;        // P
+    uint64_t *fr;       // 4P
+    uint8_t *frn;       // P
+    uint64_t *lk;       // CL keys
+    int32_t *lv;        // CL values
+    uint64_t *relax;    // CR
+    uint64_t *out;      // CO
+    uint16_t *olen;     // CC
+};
+struct FcStatus {
+    int32_t status;     // 0 ok, 1 lock table full, 2 relax stack full, 3 output full
+    int32_t ncyc;
+    uint32_t nnodes;
+    uint32_t pad;
+};
+
+struct FcThread {
+    const GraphView &g;
+    const uint64_t *visited;
+    FcScratch s;
+    FcCaps c;
+    uint32_t lsize = 0;
+    int32_t status = 0;
+
+    __device__ FcThread(const GraphView &gv, const uint64_t *vis, FcScratch sc, FcCaps cp)
+        : g(gv), visited(vis), s(sc), c(cp) {}
+
+    // lock.try_emplace(x, maxl): returns slot (inserting default), -1 on overflow
+    __device__ int lock_slot(uint64_t x, int dflt) {
+        uint32_t h = (uint32_t)(mix64(x) & (c.CL - 1));
+        for (;;) {
+            const uint64_t k = s.lk[h];
+            if (k == x) return (int)h;
+            if (k == kNone) {
+                if (lsize + 1 > c.CL / 4 * 3) { status = 1; return -1; }
+                s.lk[h] = x;
+                s.lv[h] = dflt;
+                ++lsize;
+                return (int)h;
+            }
+            h = (h + 1) & (c.CL - 1);
+        }
+    }
+    // _BackgroundCheck (cycle_finder.cpp:40-52); records x in the footprint
+    __device__ bool background(uint64_t node, uint64_t rm, uint64_t x, int maxl) {
+        if (lock_slot(x, maxl) < 0) return false;
+        const uint64_t nm = g.mult[x];
+        if (bit_get(visited, x)) return false;
+        if (rm / nm > 500) return false;
+        if (node == x) return false;
+        return true;
+    }
+    // _GetOutgoings(node, set, rm) + libstdc++ unordered_set insertion order
+    __device__ int get_outgoings(uint64_t node, uint64_t rm, uint64_t *f, int maxl) {
+        uint64_t nb[4];
+        const int od = dev_outgoing(g, node, nb);
+        int n = 0;
+        if (od == 0 || !bit_get(g.valid, node)) return 0;
+        for (int i = 0; i < od; ++i) {
+            const uint64_t x = nb[i];
+            if (background(node, rm, x, maxl) && bit_get(g.valid, x)) {
+                // 13 buckets, hash(x)=x: before the first element of x's bucket, else at front
+                int pos = 0;
+                for (int j = 0; j < n; ++j)
+                    if (f[j] % 13 == x % 13) { pos = j; break; }
+                for (int j = n; j > pos; --j) f[j] = f[j - 1];
+                f[pos] = x;
+                ++n;
+            }
+        }
+        return n;
+    }
+    __device__ int get_incomings(uint64_t node, uint64_t rm, uint64_t *f, int maxl) {
+        uint64_t in[4];
+        const int id = dev_incoming(g, node, in);
+        int n = 0;
+        if (id == 0 || !bit_get(g.valid, node)) return 0;
+        for (int i = 0; i < id; ++i)
+            if (background(node, rm, in[i], maxl) && bit_get(g.valid, in[i])) f[n++] = in[i];
+        return n;
+    }
+};
+
+__global__ void __launch_bounds__(64) k_findcycle(GraphView g, const uint64_t *visited, const uint64_t *starts,
+                                                  uint64_t n, FcCaps caps, FcParams prm, uint64_t *sbase,
+                                                  FcStatus *stat) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    // carve this thread's scratch
+    const uint64_t per = (uint64_t)caps.P * 8 + caps.P * 4 + caps.P * 32 + caps.P + (uint64_t)caps.CL * 12 +
+                         (uint64_t)caps.CR * 8 + (uint64_t)caps.CO * 8 + caps.CC * 2;
+    const uint64_t per_al = (per + 255) & ~255ULL;
+    uint8_t *base = (uint8_t *)sbase + i * per_al;
+    FcScratch s;
+    s.lk = (uint64_t *)base; base += (uint64_t)caps.CL * 8;
+    s.relax = (uint64_t *)base; base += (uint64_t)caps.CR * 8;
+    s.out = (uint64_t *)base; base += (uint64_t)caps.CO * 8;
+    s.path = (uint64_t *)base; base += (uint64_t)caps.P * 8;
+    s.fr = (uint64_t *)base; base += (uint64_t)caps.P * 32;
+    s.lv = (int32_t *)base; base += (uint64_t)caps.CL * 4;
+    s.bl = (int32_t *)base; base += (uint64_t)caps.P * 4;
+    s.olen = (uint16_t *)base; base += (uint64_t)caps.CC * 2;
+    s.frn = base;
+    for (uint32_t j = 0; j < caps.CL; ++j) s.lk[j] = kNone;
+
+    FcThread t(g, visited, s, caps);
+    const int maxl = prm.maxl, minl = prm.minl;
+    const uint64_t st = starts[i];
+    const uint64_t rm = g.mult[st];
+    uint32_t plen = 0, depth = 0, nnodes = 0;
+    int32_t ncyc = 0;
+    int64_t counter = 0, steps = 0;
+
+    // FindCycleUtil (cycle_finder.cpp:231-243)
+    s.path[plen++] = st;
+    {
+        const int sl = t.lock_slot(st, maxl);
+        if (sl >= 0) s.lv[sl] = 0;
+    }
+    s.frn[0] = (uint8_t)t.get_outgoings(st, rm, s.fr, maxl);
+    s.bl[0] = maxl;
+    depth = 1;
+
+    // FindCycle main loop (cycle_finder.cpp:147-212)
+    while (depth > 0 && t.status == 0) {
+        if (++steps > prm.step_cap) break;
+        const uint32_t top = depth - 1;
+        uint64_t N[4];
+        const int nN = s.frn[top];
+        for (int j = 0; j < nN; ++j) N[j] = s.fr[4 * top + j];
+        bool flag = true, pushed = false;
+        for (int j = 0; j < nN; ++j) {
+            const uint64_t x = N[j];
+            if (x == st) {
+                s.bl[top] = 1;
+                if ((int)plen > minl) {
+                    if (nnodes + plen > caps.CO || ncyc >= (int)caps.CC) { t.status = 3; break; }
+                    for (uint32_t q = 0; q < plen; ++q) s.out[nnodes + q] = s.path[q];
+                    nnodes += plen;
+                    s.olen[ncyc++] = (uint16_t)plen;
+                    counter += 1;
+                    if (counter >= prm.cluster) { ncyc = 0; nnodes = 0; flag = false; }
+                }
+            } else {
+                const int sl = t.lock_slot(x, maxl);
+                if (sl < 0) break;
+                if ((int)plen < s.lv[sl]) {
+                    // erase x from the top frame (order of the rest is kept)
+                    int m = s.frn[top], q = 0;
+                    for (int r = 0; r < m; ++r)
+                        if (s.fr[4 * top + r] != x) s.fr[4 * top + q++] = s.fr[4 * top + r];
+                    s.frn[top] = (uint8_t)q;
+                    s.path[plen++] = x;
+                    s.bl[depth] = maxl;
+                    s.lv[sl] = (int)plen;
+                    s.frn[depth] = (uint8_t)t.get_outgoings(x, rm, s.fr + 4 * depth, maxl);
+                    ++depth;
+                    flag = false;
+                    pushed = true;
+                    break;
+                }
+            }
+        }
+        if (t.status) break;
+        if (flag) {
+            --depth;
+            const uint64_t v = s.path[--plen];
+            const int b = s.bl[depth];
+            if (depth > 0) s.bl[depth - 1] = min(s.bl[depth - 1], b);
+            if (b < maxl) {
+                // lock relaxation (cycle_finder.cpp:191-209); its fixpoint does not depend on
+                // the processing order, so a plain stack is used.
+                uint32_t rs = 0;
+                s.relax[rs++] = (v << 16) | (uint64_t)b;
+                while (rs > 0 && t.status == 0) {
+                    const uint64_t e = s.relax[--rs];
+                    const int blv = (int)(e & 0xFFFF);
+                    const uint64_t u = e >> 16;
+                    const int sl = t.lock_slot(u, maxl);
+                    if (sl < 0) break;
+                    if (s.lv[sl] < maxl - blv + 1) {
+                        s.lv[sl] = maxl - blv + 1;
+                        uint64_t ins[4];
+                        const int ni = t.get_incomings(u, rm, ins, maxl);
+                        for (int j = 0; j < ni; ++j) {
+                            bool on_path = false;
+                            for (uint32_t q = 0; q < plen; ++q)
+                                if (s.path[q] == ins[j]) { on_path = true; break; }
+                            if (!on_path) {
+                                if (rs >= caps.CR) { t.status = 2; break; }
+                                s.relax[rs++] = (ins[j] << 16) | (uint64_t)(blv + 1);
+                            }
+                        }
+                    }
+                }
+            }
+        } else if (!pushed) {
+            // the cluster bound cleared the cycles and nothing was pushed: the state is a
+            // fixed point, the reference spins until the step cap and returns {}.
+            ncyc = 0;
+            nnodes = 0;
+            break;
+        }
+    }
+    FcStatus o;
+    o.status = t.status;
+    o.ncyc = ncyc;
+    o.nnodes = nnodes;
+    o.pad = 0;
+    stat[i] = o;
+}
+
+// gather thread outputs into one contiguous buffer
+__global__ void k_fc_gather(const uint64_t *sbase, uint64_t per_al, FcCaps caps, const uint64_t *sel,
+                            const uint64_t *node_off, const uint64_t *cyc_off, uint64_t *nodes, uint16_t *lens,
+                            uint64_t nsel) {
+    const uint64_t q = blockIdx.x;
+    if (q >= nsel) return;
+    const uint64_t i = sel[q];
+    const uint8_t *base = (const uint8_t *)sbase + i * per_al;
+    const uint64_t *out = (const uint64_t *)(base + (uint64_t)caps.CL * 8 + (uint64_t)caps.CR * 8);
+    const uint16_t *olen = (const uint16_t *)(base + (uint64_t)caps.CL * 8 + (uint64_t)caps.CR * 8 +
+                                              (uint64_t)caps.CO * 8 + (uint64_t)caps.P * 8 + (uint64_t)caps.P * 32 +
+                                              (uint64_t)caps.CL * 4 + (uint64_t)caps.P * 4);
+    const uint64_t nn = node_off[q + 1] - node_off[q];
+    const uint64_t nc = cyc_off[q + 1] - cyc_off[q];
+    for (uint64_t j = threadIdx.x; j < nn; j += blockDim.x) nodes[node_off[q] + j] = out[j];
+    for (uint64_t j = threadIdx.x; j < nc; j += blockDim.x) lens[cyc_off[q] + j] = olen[j];
+}
+
+// conflict[j] = 1 if a node first visited by tentative commit c < j is in j's footprint
+__global__ void k_fc_conflict(const uint64_t *sbase, uint64_t per_al, uint32_t CL, const uint64_t *newly,
+                              const uint32_t *newly_c, uint64_t n_newly, uint64_t W, int *conflict) {
+    const uint64_t tot = n_newly * W;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += stride) {
+        const uint64_t a = idx / W, j = idx - a * W;
+        if (j <= newly_c[a]) continue;
+        const uint64_t *lk = (const uint64_t *)((const uint8_t *)sbase + j * per_al);
+        if (set_contains(lk, CL, newly[a])) conflict[j] = 1;
+    }
+}
+
+__global__ void k_set_bits(uint64_t *bm, const uint64_t *ids, uint64_t n, int value) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t x = ids[i];
+        if (value) atomicOr((unsigned long long *)&bm[x >> 6], 1ull << (x & 63));
+        else atomicAnd((unsigned long long *)&bm[x >> 6], ~(1ull << (x & 63)));
+    }
+}
+
+__global__ void k_gather_mult(const uint16_t *mult, const uint64_t *ids, uint64_t n, uint16_t *out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = mult[ids[i]];
+}
+
+__global__ void k_neighbors(GraphView g, const uint64_t *ids, uint64_t n, int incoming, uint64_t *out,
+                            int32_t *counts) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint64_t t[4] = {kNone, kNone, kNone, kNone};
+    const int c = incoming ? dev_incoming(g, ids[i], t) : dev_outgoing(g, ids[i], t);
+    for (int j = 0; j < 4; ++j) out[4 * i + j] = t[j];
+    counts[i] = c;
+}
+
+__global__ void k_unpack_bits(const uint64_t *bm, uint64_t D, uint8_t *out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < D; e += stride) out[e] = bit_get(bm, e);
+}
+
+unsigned long long read_counter(mcaat_ctx *ctx, unsigned long long *d) {
+    unsigned long long h = 0;
+    HIP_OK(hipMemcpyAsync(&h, d, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    return h;
+}
+
+// host visited mirror: a dense bitmap of D bits
+struct HostBits {
+    std::vector<uint64_t> w;
+    explicit HostBits(uint64_t D) : w((D + 63) / 64, 0) {}
+    bool get(uint64_t x) const { return (w[x >> 6] >> (x & 63)) & 1; }
+    void set(uint64_t x) { w[x >> 6] |= 1ULL << (x & 63); }
+};
+
+}  // namespace
+
+// ------------------------------ peel driver -----------------------------------
+static void run_peel(mcaat_graph *g, const uint64_t *seed_bm) {
+    mcaat_ctx *ctx = g->ctx;
+    hipStream_t st = ctx->stream;
+    const uint64_t D = g->D;
+    if (!D) return;
+    GraphView v = g->view();
+    DevBuf<uint8_t> od(D), upred(D), ruler(D), stt(D);
+    DevBuf<uint64_t> nxt(D), owner(D), jump(D);
+    HIP_OK(hipMemsetAsync(upred.p, 0, D, st));
+    HIP_OK(hipMemsetAsync(owner.p, 0xFF, owner.bytes(), st));
+    PeelArrays pa{od.p, upred.p, ruler.p, stt.p, nxt.p, owner.p, jump.p, seed_bm};
+    hipLaunchKernelGGL(k_peel_init, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, v, pa);
+    LAUNCH_OK();
+    DevBuf<unsigned long long> cur(1);
+    HIP_OK(hipMemsetAsync(cur.p, 0, 8, st));
+    DevBuf<uint64_t> list(D);
+    hipLaunchKernelGGL(k_peel_rulers, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, D, pa, list.p, cur.p);
+    LAUNCH_OK();
+    const uint64_t nr = read_counter(ctx, cur.p);
+    if (nr) {
+        hipLaunchKernelGGL(k_peel_walk, dim3(grid_for(nr, kBlock)), dim3(kBlock), 0, st, pa, list.p, nr);
+        LAUNCH_OK();
+        int rounds = 2;
+        while ((1ULL << rounds) < nr + 1) ++rounds;
+        rounds += 1;
+        for (int r = 0; r < rounds; ++r) {
+            hipLaunchKernelGGL(k_peel_jump, dim3(grid_for(nr, kBlock)), dim3(kBlock), 0, st, pa, list.p, nr);
+            LAUNCH_OK();
+        }
+    }
+    HIP_OK(hipMemsetAsync(cur.p, 0, 8, st));
+    hipLaunchKernelGGL(k_peel_term, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, D, pa, list.p, cur.p);
+    LAUNCH_OK();
+    const uint64_t nb = read_counter(ctx, cur.p);
+    DevBuf<int> changed(1);
+    for (uint64_t it = 0; nb && it < D + 1; ++it) {
+        HIP_OK(hipMemsetAsync(changed.p, 0, 4, st));
+        hipLaunchKernelGGL(k_peel_branch, dim3(grid_for(nb, kBlock)), dim3(kBlock), 0, st, v, pa, list.p, nb,
+                           changed.p);
+        LAUNCH_OK();
+        int h = 0;
+        HIP_OK(hipMemcpyAsync(&h, changed.p, 4, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        if (!h) break;
+    }
+    hipLaunchKernelGGL(k_peel_apply, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, v, pa);
+    LAUNCH_OK();
+    HIP_OK(hipStreamSynchronize(st));
+}
+
+// ---------------------------- DLS driver -------------------------------------
+static std::vector<uint64_t> run_dls(mcaat_graph *g, const std::vector<uint64_t> &cand, int limit) {
+    mcaat_ctx *ctx = g->ctx;
+    hipStream_t st = ctx->stream;
+    std::vector<int8_t> res(cand.size(), -1);
+    std::vector<uint64_t> todo(cand.size());
+    for (size_t i = 0; i < cand.size(); ++i) todo[i] = i;
+    uint32_t cs = 1024, cv = 2048;
+    while (!todo.empty()) {
+        const uint64_t batch_cap = std::max<uint64_t>(64, (512ULL << 20) / (8ULL * (cs + cv)));
+        std::vector<uint64_t> next;
+        for (size_t b0 = 0; b0 < todo.size(); b0 += batch_cap) {
+            const uint64_t n = std::min<uint64_t>(batch_cap, todo.size() - b0);
+            std::vector<uint64_t> ids(n);
+            for (uint64_t j = 0; j < n; ++j) ids[j] = cand[todo[b0 + j]];
+            DevBuf<uint64_t> dids(n), dstk(n * cs), dvis(n * cv);
+            DevBuf<int8_t> dres(n);
+            HIP_OK(hipMemcpyAsync(dids.p, ids.data(), 8 * n, hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(k_dls, dim3(grid_for(n, 64)), dim3(64), 0, st, g->view(), dids.p, n, limit, dstk.p, cs,
+                               dvis.p, cv, dres.p);
+            LAUNCH_OK();
+            std::vector<int8_t> h(n);
+            HIP_OK(hipMemcpyAsync(h.data(), dres.p, n, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipStreamSynchronize(st));
+            for (uint64_t j = 0; j < n; ++j) {
+                if (h[j] < 0) next.push_back(todo[b0 + j]);
+                else res[todo[b0 + j]] = h[j];
+            }
+        }
+        todo.swap(next);
+        if (!todo.empty()) {
+            if (cs >= (1u << 26)) throw Error(MCAAT_E_CAPACITY, "DepthLevelSearch scratch exceeded 2^26 entries");
+            cs *= 8;
+            cv *= 8;
+        }
+    }
+    std::vector<uint64_t> pass;
+    for (size_t i = 0; i < cand.size(); ++i)
+        if (res[i] == 1) pass.push_back(cand[i]);
+    return pass;
+}
+
+// ---------------------------- FindCycle driver -----------------------------------
+struct FcRunner {
+    mcaat_graph *g;
+    FcParams prm;
+    FcCaps caps;
+    DevBuf<uint64_t> dvis;
+    HostBits hvis;
+    mcaat_cycles *out;
+    uint64_t rounds = 0, reruns = 0;
+
+    FcRunner(mcaat_graph *gr, const mcaat_cf_params &p, mcaat_cycles *o) : g(gr), hvis(gr->D), out(o) {
+        prm.maxl = p.cycle_max_length;
+        prm.minl = p.cycle_min_length;
+        prm.cluster = p.cluster_bound;
+        prm.step_cap = p.step_cap;
+        caps.P = (uint32_t)std::max(4, p.cycle_max_length + 2);
+        caps.CL = 4096;
+        caps.CR = 2048;
+        caps.CC = (uint32_t)std::max(1, p.cluster_bound);
+        caps.CO = (uint32_t)std::max<uint64_t>(caps.P, (uint64_t)caps.CC * (caps.P - 1));
+        dvis.alloc(gr->n_words());
+        HIP_OK(hipMemsetAsync(dvis.p, 0, dvis.bytes(), gr->ctx->stream));
+    }
+    uint64_t per_al() const {
+        const uint64_t per = (uint64_t)caps.P * 8 + caps.P * 4 + caps.P * 32 + caps.P + (uint64_t)caps.CL * 12 +
+                             (uint64_t)caps.CR * 8 + (uint64_t)caps.CO * 8 + caps.CC * 2;
+        return (per + 255) & ~255ULL;
+    }
+
+    void run_bucket(const std::vector<uint64_t> &bucket) {
+        hipStream_t st = g->ctx->stream;
+        std::vector<uint64_t> pending(bucket);
+        uint64_t window = 1024;
+        while (!pending.empty()) {
+            // starts already visited are skipped by the reference (:476) -> no entry
+            std::vector<uint64_t> keep;
+            keep.reserve(pending.size());
+            for (uint64_t s : pending)
+                if (!hvis.get(s)) keep.push_back(s);
+            pending.swap(keep);
+            if (pending.empty()) break;
+            ++rounds;
+            const uint64_t W = std::min<uint64_t>(window, pending.size());
+            const uint64_t pa = per_al();
+            DevBuf<uint64_t> dst(W);
+            DevBuf<uint8_t> scratch(W * pa);
+            DevBuf<FcStatus> dstat(W);
+            HIP_OK(hipMemcpyAsync(dst.p, pending.data(), 8 * W, hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(k_findcycle, dim3(grid_for(W, 64)), dim3(64), 0, st, g->view(), dvis.p, dst.p, W, caps,
+                               prm, (uint64_t *)scratch.p, dstat.p);
+            LAUNCH_OK();
+            std::vector<FcStatus> hs(W);
+            HIP_OK(hipMemcpyAsync(hs.data(), dstat.p, W * sizeof(FcStatus), hipMemcpyDeviceToHost, st));
+            HIP_OK(hipStreamSynchronize(st));
+            // outputs of every thread that finished (status 0) with cycles
+            std::vector<uint64_t> sel, noff{0}, coff{0};
+            std::vector<int64_t> sel_of(W, -1);
+            uint64_t first_bad = W;
+            for (uint64_t j = 0; j < W; ++j) {
+                if (hs[j].status != 0) { first_bad = j; break; }
+                if (hs[j].ncyc > 0) {
+                    sel_of[j] = (int64_t)sel.size();
+                    sel.push_back(j);
+                    noff.push_back(noff.back() + hs[j].nnodes);
+                    coff.push_back(coff.back() + hs[j].ncyc);
+                }
+            }
+            std::vector<uint64_t> nodes(noff.back());
+            std::vector<uint16_t> lens(coff.back());
+            if (!sel.empty()) {
+                DevBuf<uint64_t> dsel(sel.size()), dno(noff.size()), dco(coff.size()), dn(noff.back());
+                DevBuf<uint16_t> dl(coff.back());
+                HIP_OK(hipMemcpyAsync(dsel.p, sel.data(), 8 * sel.size(), hipMemcpyHostToDevice, st));
+                HIP_OK(hipMemcpyAsync(dno.p, noff.data(), 8 * noff.size(), hipMemcpyHostToDevice, st));
+                HIP_OK(hipMemcpyAsync(dco.p, coff.data(), 8 * coff.size(), hipMemcpyHostToDevice, st));
+                hipLaunchKernelGGL(k_fc_gather, dim3((unsigned)sel.size()), dim3(256), 0, st, (uint64_t *)scratch.p,
+                                   pa, caps, dsel.p, dno.p, dco.p, dn.p, dl.p, (uint64_t)sel.size());
+                LAUNCH_OK();
+                HIP_OK(hipMemcpyAsync(nodes.data(), dn.p, 8 * nodes.size(), hipMemcpyDeviceToHost, st));
+                HIP_OK(hipMemcpyAsync(lens.data(), dl.p, 2 * lens.size(), hipMemcpyDeviceToHost, st));
+                HIP_OK(hipStreamSynchronize(st));
+            }
+            // tentative sequential commit (threads=1 semantics)
+            std::unordered_set<uint64_t> tent;
+            std::vector<uint64_t> newly;
+            std::vector<uint32_t> newly_c;
+            std::vector<uint8_t> skip(W, 0);
+            for (uint64_t j = 0; j < first_bad; ++j) {
+                const uint64_t s = pending[j];
+                if (hvis.get(s) || tent.count(s)) { skip[j] = 1; continue; }
+                if (sel_of[j] >= 0) {
+                    const uint64_t q = (uint64_t)sel_of[j];
+                    for (uint64_t a = noff[q]; a < noff[q + 1]; ++a) {
+                        const uint64_t x = nodes[a];
+                        if (!hvis.get(x) && tent.insert(x).second) {
+                            newly.push_back(x);
+                            newly_c.push_back((uint32_t)j);
+                        }
+                    }
+                }
+            }
+            uint64_t f = first_bad;
+            if (!newly.empty() && first_bad > 1) {
+                DevBuf<uint64_t> dnw(newly.size());
+                DevBuf<uint32_t> dnc(newly.size());
+                DevBuf<int> dconf(W);
+                HIP_OK(hipMemsetAsync(dconf.p, 0, 4 * W, st));
+                HIP_OK(hipMemcpyAsync(dnw.p, newly.data(), 8 * newly.size(), hipMemcpyHostToDevice, st));
+                HIP_OK(hipMemcpyAsync(dnc.p, newly_c.data(), 4 * newly.size(), hipMemcpyHostToDevice, st));
+                hipLaunchKernelGGL(k_fc_conflict, dim3(grid_for((uint64_t)newly.size() * first_bad, kBlock)),
+                                   dim3(kBlock), 0, st, (uint64_t *)scratch.p, pa, caps.CL, dnw.p, dnc.p,
+                                   (uint64_t)newly.size(), first_bad, dconf.p);
+                LAUNCH_OK();
+                std::vector<int> conf(W);
+                HIP_OK(hipMemcpyAsync(conf.data(), dconf.p, 4 * W, hipMemcpyDeviceToHost, st));
+                HIP_OK(hipStreamSynchronize(st));
+                for (uint64_t j = 0; j < first_bad; ++j)
+                    if (!skip[j] && conf[j]) { f = j; break; }
+            }
+            // commit the prefix [0, f)
+            std::vector<uint64_t> setv;
+            for (uint64_t j = 0; j < f; ++j) {
+                if (skip[j]) continue;
+                out->starts.push_back(pending[j]);
+                std::vector<uint64_t> fl, of{0};
+                if (sel_of[j] >= 0) {
+                    const uint64_t q = (uint64_t)sel_of[j];
+                    fl.assign(nodes.begin() + noff[q], nodes.begin() + noff[q + 1]);
+                    for (uint64_t c = coff[q]; c < coff[q + 1]; ++c) of.push_back(of.back() + lens[c]);
+                }
+                out->stats[5] += of.size() - 1;
+                out->flat.push_back(std::move(fl));
+                out->offsets.push_back(std::move(of));
+            }
+            for (size_t a = 0; a < newly.size(); ++a)
+                if (newly_c[a] < f) { hvis.set(newly[a]); setv.push_back(newly[a]); }
+            if (!setv.empty()) {
+                DevBuf<uint64_t> ds(setv.size());
+                HIP_OK(hipMemcpyAsync(ds.p, setv.data(), 8 * setv.size(), hipMemcpyHostToDevice, st));
+                hipLaunchKernelGGL(k_set_bits, dim3(grid_for(setv.size(), kBlock)), dim3(kBlock), 0, st, dvis.p, ds.p,
+                                   (uint64_t)setv.size(), 1);
+                LAUNCH_OK();
+                HIP_OK(hipStreamSynchronize(st));
+            }
+            if (f < W) ++reruns;
+            if (f == first_bad && first_bad < W) {
+                // scratch overflow at position f: grow the exhausted structure and re-run
+                const int code = hs[f].status;
+                if (code == 1) caps.CL *= 4;
+                else if (code == 2) caps.CR *= 4;
+                else caps.CO *= 2;
+                if (caps.CL > (1u << 26) || caps.CR > (1u << 26) || caps.CO > (1u << 28))
+                    throw Error(MCAAT_E_CAPACITY, "FindCycle scratch exceeded its growth limit");
+            }
+            pending.erase(pending.begin(), pending.begin() + f);
+            // adapt the speculation window to the observed conflict rate
+            if (f < W / 4) window = std::max<uint64_t>(16, window / 2);
+            else if (f == W) window = std::min<uint64_t>(8192, window * 2);
+        }
+    }
+};
+
+void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out) {
+    mcaat_ctx *ctx = g->ctx;
+    hipStream_t st = ctx->stream;
+    const uint64_t D = g->D;
+    const uint64_t nw = g->n_words();
+    GraphView v = g->view();
+    StageTimer timer(ctx);
+    DevBuf<unsigned long long> cnt(1);
+    auto zero = [&]() { HIP_OK(hipMemsetAsync(cnt.p, 0, 8, st)); };
+    const unsigned wgrid = grid_for(nw * 64, kBlock);
+
+    // 1. CollectTips (before the multiplicity filter) -> seeds of the reduction
+    DevBuf<uint64_t> seeds(nw);
+    zero();
+    hipLaunchKernelGGL(k_tips, dim3(wgrid), dim3(kBlock), 0, st, v, seeds.p, cnt.p);
+    LAUNCH_OK();
+    out->stats[0] = read_counter(ctx, cnt.p);
+    timer.mark("collect_tips");
+    // 2. InvalidateMultiplicityOneNodes
+    zero();
+    hipLaunchKernelGGL(k_mult_filter, dim3(wgrid), dim3(kBlock), 0, st, v, cnt.p);
+    LAUNCH_OK();
+    out->stats[1] = read_counter(ctx, cnt.p);
+    timer.mark("mult_filter");
+    // 3. RecursiveReduction from every seed
+    run_peel(g, seeds.p);
+    seeds.release();
+    timer.mark("peel");
+    // 4. valid count + tips after pruning
+    zero();
+    hipLaunchKernelGGL(k_popcount, dim3(grid_for(nw, kBlock)), dim3(kBlock), 0, st, g->valid.p, nw, cnt.p);
+    LAUNCH_OK();
+    out->stats[2] = read_counter(ctx, cnt.p);
+    zero();
+    hipLaunchKernelGGL(k_tips, dim3(wgrid), dim3(kBlock), 0, st, v, (uint64_t *)nullptr, cnt.p);
+    LAUNCH_OK();
+    out->stats[3] = read_counter(ctx, cnt.p);
+    timer.mark("recount");
+    // 5. ChunkStartNodes
+    if (!p.low_abundance) {
+        zero();
+        hipLaunchKernelGGL(k_mult_filter, dim3(wgrid), dim3(kBlock), 0, st, v, cnt.p);
+        LAUNCH_OK();
+    }
+    std::vector<uint64_t> cand;
+    {
+        DevBuf<uint64_t> list(D ? D : 1);
+        zero();
+        hipLaunchKernelGGL(k_candidates, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, v, p.threshold_multiplicity,
+                           list.p, cnt.p);
+        LAUNCH_OK();
+        const uint64_t nc = read_counter(ctx, cnt.p);
+        cand.resize(nc);
+        if (nc) HIP_OK(hipMemcpy(cand.data(), list.p, 8 * nc, hipMemcpyDeviceToHost));
+    }
+    std::sort(cand.begin(), cand.end());
+    timer.mark("candidates");
+    std::vector<uint64_t> pass = run_dls(g, cand, p.cycle_max_length);
+    timer.mark("dls");
+    std::map<int, std::vector<uint64_t>, std::greater<int>> chunks;
+    if (!pass.empty()) {
+        DevBuf<uint64_t> ids(pass.size());
+        DevBuf<uint16_t> m(pass.size());
+        HIP_OK(hipMemcpyAsync(ids.p, pass.data(), 8 * pass.size(), hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_gather_mult, dim3(grid_for(pass.size(), kBlock)), dim3(kBlock), 0, st, g->mult.p, ids.p,
+                           (uint64_t)pass.size(), m.p);
+        LAUNCH_OK();
+        std::vector<uint16_t> hm(pass.size());
+        HIP_OK(hipMemcpyAsync(hm.data(), m.p, 2 * pass.size(), hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        for (size_t i = 0; i < pass.size(); ++i) {
+            const double l2 = std::ceil(std::log2(double(hm[i])));  // cycle_finder.cpp:414
+            chunks[(int)l2].push_back(pass[i]);
+        }
+    }
+    for (auto &kv : chunks)
+        for (uint64_t id : kv.second) { out->cand_ids.push_back(id); out->cand_bucket.push_back(kv.first); }
+    out->stats[4] = out->cand_ids.size();
+    // 6. bucket loop
+    FcRunner fr(g, p, out);
+    for (auto &kv : chunks) fr.run_bucket(kv.second);
+    out->stats[6] = fr.rounds;
+    out->stats[7] = fr.reruns;
+    timer.mark("find_cycle");
+    HIP_OK(hipStreamSynchronize(st));
+    timer.finish();
+}
+
+void graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, int incoming, uint64_t *out,
+                     int32_t *counts) {
+    if (!n) return;
+    hipStream_t st = g->ctx->stream;
+    DevBuf<uint64_t> di(n), dout(4 * n);
+    DevBuf<int32_t> dc(n);
+    HIP_OK(hipMemcpyAsync(di.p, ids, 8 * n, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_neighbors, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, g->view(), di.p, (uint64_t)n,
+                       incoming, dout.p, dc.p);
+    LAUNCH_OK();
+    HIP_OK(hipMemcpyAsync(out, dout.p, 32 * n, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(counts, dc.p, 4 * n, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+}
+
+void graph_set_valid(mcaat_graph *g, const uint64_t *ids, size_t n, int valid) {
+    if (!n) return;
+    for (size_t i = 0; i < n; ++i)
+        if (ids[i] >= g->D) throw Error(MCAAT_E_INVALID, "edge id out of range");
+    hipStream_t st = g->ctx->stream;
+    DevBuf<uint64_t> di(n);
+    HIP_OK(hipMemcpyAsync(di.p, ids, 8 * n, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_set_bits, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, g->valid.p, di.p, (uint64_t)n,
+                       valid);
+    LAUNCH_OK();
+    HIP_OK(hipStreamSynchronize(st));
+}
+
+void graph_download_valid(const mcaat_graph *g, uint8_t *valid) {
+    if (!g->D) return;
+    hipStream_t st = g->ctx->stream;
+    DevBuf<uint8_t> d(g->D);
+    hipLaunchKernelGGL(k_unpack_bits, dim3(grid_for(g->D, kBlock)), dim3(kBlock), 0, st, g->valid.p, g->D, d.p);
+    LAUNCH_OK();
+    HIP_OK(hipMemcpyAsync(valid, d.p, g->D, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+}
+
+}  // namespace mcaat

@@ -1,0 +1,201 @@
+// internal.h — library-private structures of libmcaat_gpu.so
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <map>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/mcaat_gpu.h"
+#include "common.h"
+
+namespace mcaat {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIP_OK(expr)                                                                              \
+    do {                                                                                          \
+        hipError_t e__ = (expr);                                                                  \
+        if (e__ != hipSuccess)                                                                    \
+            throw ::mcaat::Error(MCAAT_E_HIP, std::string(#expr " failed: ") + hipGetErrorString(e__) + \
+                                                  " at " + __FILE__ + ":" + std::to_string(__LINE__)); \
+    } while (0)
+
+#define LAUNCH_OK() HIP_OK(hipGetLastError())
+
+// owning device buffer
+template <class T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    DevBuf() = default;
+    explicit DevBuf(size_t count) { alloc(count); }
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    DevBuf(DevBuf &&o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+    DevBuf &operator=(DevBuf &&o) noexcept {
+        if (this != &o) { release(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; }
+        return *this;
+    }
+    ~DevBuf() { release(); }
+    void alloc(size_t count) {
+        release();
+        if (count == 0) count = 1;
+        hipError_t e = hipMalloc(&p, count * sizeof(T));
+        if (e != hipSuccess) {
+            p = nullptr;
+            (void)hipGetLastError();
+            throw Error(MCAAT_E_NOMEM, "hipMalloc of " + std::to_string(count * sizeof(T)) + " bytes failed: " +
+                                           hipGetErrorString(e));
+        }
+        n = count;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    size_t bytes() const { return n * sizeof(T); }
+};
+
+struct KernelStat {
+    double total_ms = 0;
+    uint64_t launches = 0;
+    double bytes_per_launch = 0;
+};
+
+}  // namespace mcaat
+
+struct mcaat_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::vector<std::pair<const char *, double>> stages;
+    std::map<std::string, mcaat::KernelStat> kstats;
+    bool timing = true;
+};
+
+struct mcaat_reads {
+    mcaat_ctx *ctx = nullptr;
+    mcaat::DevBuf<uint64_t> packed;
+    mcaat::DevBuf<uint64_t> offsets;
+    uint64_t n_reads = 0, n_bases = 0, n_words = 0;
+    uint64_t fixed_len = 0;  // >0 when every read has this length (offsets[i] = i*len)
+};
+
+struct mcaat_graph {
+    mcaat_ctx *ctx = nullptr;
+    int k = 0;
+    uint64_t D = 0;
+    mcaat::DevBuf<uint64_t> key;
+    mcaat::DevBuf<uint16_t> mult;
+    mcaat::DevBuf<uint64_t> out_info;
+    mcaat::DevBuf<uint64_t> in_info;
+    mcaat::DevBuf<uint64_t> valid;
+    mcaat::GraphView view() const {
+        return mcaat::GraphView{k, D, key.p, mult.p, out_info.p, in_info.p, valid.p};
+    }
+    uint64_t n_words() const { return (D + 63) / 64; }
+};
+
+struct mcaat_cycles {
+    std::vector<uint64_t> starts;
+    std::vector<std::vector<uint64_t>> flat;
+    std::vector<std::vector<uint64_t>> offsets;
+    std::vector<uint64_t> cand_ids;
+    std::vector<int32_t> cand_bucket;
+    uint64_t stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+};
+
+namespace mcaat {
+
+// event-bracketed stage timer on the ctx stream
+struct StageTimer {
+    mcaat_ctx *ctx;
+    std::vector<std::pair<const char *, hipEvent_t>> marks;
+    explicit StageTimer(mcaat_ctx *c) : ctx(c) { ctx->stages.clear(); mark("begin"); }
+    void mark(const char *name) {
+        hipEvent_t e;
+        HIP_OK(hipEventCreate(&e));
+        HIP_OK(hipEventRecord(e, ctx->stream));
+        marks.push_back({name, e});
+    }
+    // call after the stream is synchronised
+    void finish() {
+        for (size_t i = 1; i < marks.size(); ++i) {
+            float ms = 0;
+            HIP_OK(hipEventElapsedTime(&ms, marks[i - 1].second, marks[i].second));
+            ctx->stages.push_back({marks[i].first, (double)ms});
+        }
+        for (auto &m : marks) (void)hipEventDestroy(m.second);
+        marks.clear();
+    }
+    ~StageTimer() {
+        for (auto &m : marks) (void)hipEventDestroy(m.second);
+    }
+};
+
+// HIP-event timing of one kernel launch on the ctx stream
+struct KernelTimer {
+    mcaat_ctx *ctx;
+    const char *name;
+    double bytes;
+    hipEvent_t a = nullptr, b = nullptr;
+    KernelTimer(mcaat_ctx *c, const char *n, double algorithmic_bytes) : ctx(c), name(n), bytes(algorithmic_bytes) {
+        HIP_OK(hipEventCreate(&a));
+        HIP_OK(hipEventCreate(&b));
+        HIP_OK(hipEventRecord(a, ctx->stream));
+    }
+    void stop() {
+        HIP_OK(hipEventRecord(b, ctx->stream));
+        HIP_OK(hipEventSynchronize(b));
+        float ms = 0;
+        HIP_OK(hipEventElapsedTime(&ms, a, b));
+        auto &s = ctx->kstats[name];
+        s.total_ms += ms;
+        s.launches += 1;
+        s.bytes_per_launch = bytes;
+    }
+    ~KernelTimer() {
+        if (a) (void)hipEventDestroy(a);
+        if (b) (void)hipEventDestroy(b);
+    }
+};
+
+inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 65535u * 16) {
+    uint64_t g = (n + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > cap) g = cap;
+    return (unsigned)g;
+}
+
+inline uint64_t next_pow2(uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+}
+
+// stage entry points (implemented in the .hip files)
+struct CountResult {
+    DevBuf<uint64_t> keys;   // canonical lsb (k+1)-mers, unsorted unless requested
+    DevBuf<uint32_t> counts;
+    uint64_t n = 0;
+};
+void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out);
+void sort_counts(mcaat_ctx *ctx, CountResult &c, int k);
+void sdbg_build(mcaat_ctx *ctx, CountResult &c, int k, mcaat_graph *g);
+void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out);
+void synth_reads(mcaat_ctx *ctx, const mcaat_synth_spec &s, mcaat_reads *out);
+void synth_genome_host(const mcaat_synth_spec &s, std::vector<uint64_t> &genome);
+void graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, int incoming, uint64_t *out,
+                     int32_t *counts);
+void graph_set_valid(mcaat_graph *g, const uint64_t *ids, size_t n, int valid);
+void graph_download_valid(const mcaat_graph *g, uint8_t *valid);
+
+}  // namespace mcaat

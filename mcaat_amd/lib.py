@@ -1,0 +1,389 @@
+"""ctypes binding of libmcaat_gpu.so (include/mcaat_gpu.h)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmcaat_gpu.so")
+
+_u64p = C.POINTER(C.c_uint64)
+_u32p = C.POINTER(C.c_uint32)
+_u16p = C.POINTER(C.c_uint16)
+_u8p = C.POINTER(C.c_uint8)
+_i32p = C.POINTER(C.c_int32)
+
+
+class McaatError(RuntimeError):
+    """Raised for a negative mcaat_status (message from mcaat_last_error)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"mcaat error {code}: {msg}")
+        self.code = code
+
+
+class _SynthSpec(C.Structure):
+    _fields_ = [
+        ("seed", C.c_uint64),
+        ("n_genomes", C.c_uint32),
+        ("genome_len", C.c_uint64),
+        ("arrays_per_genome", C.c_uint32),
+        ("spacers_per_array", C.c_uint32),
+        ("repeat_len_min", C.c_uint32),
+        ("repeat_len_max", C.c_uint32),
+        ("spacer_len_min", C.c_uint32),
+        ("spacer_len_max", C.c_uint32),
+        ("read_len", C.c_uint32),
+        ("n_reads", C.c_uint64),
+        ("error_rate", C.c_double),
+        ("paired", C.c_int32),
+    ]
+
+
+class _CfParams(C.Structure):
+    _fields_ = [
+        ("threshold_multiplicity", C.c_uint64),
+        ("low_abundance", C.c_int32),
+        ("cycle_max_length", C.c_int32),
+        ("cycle_min_length", C.c_int32),
+        ("cluster_bound", C.c_int32),
+        ("step_cap", C.c_int64),
+    ]
+
+
+# every exported symbol and its ctypes signature (restype, argtypes)
+SIGNATURES = {
+    "mcaat_init": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    "mcaat_finalize": (None, [C.c_void_p]),
+    "mcaat_last_error": (C.c_char_p, []),
+    "mcaat_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "mcaat_reads_from_host": (C.c_int, [C.c_void_p, _u64p, C.c_uint64, _u64p, C.c_uint64, C.POINTER(C.c_void_p)]),
+    "mcaat_reads_from_fastx": (C.c_int, [C.c_void_p, C.POINTER(C.c_char_p), C.c_int, C.POINTER(C.c_void_p)]),
+    "mcaat_reads_info": (C.c_int, [C.c_void_p, _u64p, _u64p]),
+    "mcaat_reads_download": (C.c_int, [C.c_void_p, _u64p, _u64p]),
+    "mcaat_reads_free": (None, [C.c_void_p]),
+    "mcaat_reads_synth": (C.c_int, [C.c_void_p, C.POINTER(_SynthSpec), C.POINTER(C.c_void_p)]),
+    "mcaat_synth_host": (C.c_int, [C.POINTER(_SynthSpec), _u64p, _u64p]),
+    "mcaat_synth_genome_host": (C.c_int, [C.POINTER(_SynthSpec), _u64p]),
+    "mcaat_count_edges": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, _u64p, C.POINTER(_u64p), C.POINTER(_u32p)]),
+    "mcaat_free": (None, [C.c_void_p]),
+    "mcaat_build_graph": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
+    "mcaat_graph_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), _u64p]),
+    "mcaat_graph_download": (C.c_int, [C.c_void_p, _u64p, _u16p, _u8p]),
+    "mcaat_graph_set_valid": (C.c_int, [C.c_void_p, _u64p, C.c_size_t, C.c_int]),
+    "mcaat_graph_neighbors": (C.c_int, [C.c_void_p, _u64p, C.c_size_t, C.c_int, _u64p, _i32p]),
+    "mcaat_graph_free": (None, [C.c_void_p]),
+    "mcaat_cf_default_params": (None, [C.POINTER(_CfParams)]),
+    "mcaat_cycle_finder": (C.c_int, [C.c_void_p, C.POINTER(_CfParams), C.POINTER(C.c_void_p)]),
+    "mcaat_cycles_count": (C.c_int, [C.c_void_p, C.POINTER(C.c_size_t)]),
+    "mcaat_cycles_get": (
+        C.c_int,
+        [C.c_void_p, C.c_size_t, _u64p, C.POINTER(_u64p), C.POINTER(_u64p), C.POINTER(C.c_size_t)],
+    ),
+    "mcaat_cycles_stats": (C.c_int, [C.c_void_p, _u64p]),
+    "mcaat_cycles_candidates": (C.c_int, [C.c_void_p, C.POINTER(C.c_size_t), C.POINTER(_u64p), C.POINTER(_i32p)]),
+    "mcaat_cycles_free": (None, [C.c_void_p]),
+    "mcaat_stage_times": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(C.c_int)]),
+    "mcaat_kernel_timing": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_double), _u64p, C.POINTER(C.c_double)]),
+    "mcaat_reset_timing": (None, [C.c_void_p]),
+}
+
+_lib: Optional[C.CDLL] = None
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    """Load libmcaat_gpu.so (fails loudly: there is no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise McaatError(-1, f"{path} not built; run `make -C mcaat_amd` (or __graft_entry__.build())")
+    lib = C.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        msg = load_library().mcaat_last_error()
+        raise McaatError(rc, msg.decode() if msg else "")
+
+
+def _ptr(a: np.ndarray, t):
+    return a.ctypes.data_as(t)
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    _check(load_library().mcaat_device_count(C.byref(n)))
+    return n.value
+
+
+@dataclass
+class SynthSpec:
+    """Synthetic metagenome. Defaults: the C1 tiny config."""
+
+    seed: int = 1
+    n_genomes: int = 1
+    genome_len: int = 50_000
+    arrays_per_genome: int = 1
+    spacers_per_array: int = 12
+    repeat_len_min: int = 30
+    repeat_len_max: int = 30
+    spacer_len_min: int = 32
+    spacer_len_max: int = 32
+    read_len: int = 150
+    n_reads: int = 10_000
+    error_rate: float = 0.0
+    paired: bool = False
+
+    def to_c(self) -> _SynthSpec:
+        return _SynthSpec(
+            self.seed, self.n_genomes, self.genome_len, self.arrays_per_genome, self.spacers_per_array,
+            self.repeat_len_min, self.repeat_len_max, self.spacer_len_min, self.spacer_len_max,
+            self.read_len, self.n_reads, float(self.error_rate), int(self.paired),
+        )
+
+
+def synth_host(spec: SynthSpec) -> Tuple[np.ndarray, np.ndarray]:
+    """Host copy of the reads mcaat_reads_synth generates in HBM (packed words, offsets)."""
+    nb = spec.n_reads * spec.read_len
+    packed = np.zeros((nb + 31) // 32 + 1, dtype=np.uint64)
+    offsets = np.zeros(spec.n_reads + 1, dtype=np.uint64)
+    s = spec.to_c()
+    _check(load_library().mcaat_synth_host(C.byref(s), _ptr(packed, _u64p), _ptr(offsets, _u64p)))
+    return packed[: (nb + 31) // 32], offsets
+
+
+def synth_genome_host(spec: SynthSpec) -> np.ndarray:
+    total = spec.n_genomes * spec.genome_len
+    packed = np.zeros((total + 31) // 32 + 1, dtype=np.uint64)
+    s = spec.to_c()
+    _check(load_library().mcaat_synth_genome_host(C.byref(s), _ptr(packed, _u64p)))
+    return packed
+
+
+class Context:
+    """One GPU, one HIP stream (mcaat_ctx)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = load_library()
+        h = C.c_void_p()
+        _check(self._lib.mcaat_init(device, C.byref(h)))
+        self.h = h
+        self.device = device
+
+    def close(self) -> None:
+        if self.h:
+            self._lib.mcaat_finalize(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def stage_times(self) -> dict:
+        names = (C.c_char_p * 32)()
+        ms = (C.c_double * 32)()
+        n = C.c_int(0)
+        _check(self._lib.mcaat_stage_times(self.h, 32, names, ms, C.byref(n)))
+        return {names[i].decode(): ms[i] for i in range(min(n.value, 32))}
+
+    def kernel_timing(self, name: str) -> Tuple[float, int, float]:
+        avg = C.c_double(0)
+        n = C.c_uint64(0)
+        b = C.c_double(0)
+        _check(self._lib.mcaat_kernel_timing(self.h, name.encode(), C.byref(avg), C.byref(n), C.byref(b)))
+        return avg.value, n.value, b.value
+
+    def reset_timing(self) -> None:
+        self._lib.mcaat_reset_timing(self.h)
+
+
+class Reads:
+    """Packed 2-bit reads resident in HBM (mcaat_reads)."""
+
+    def __init__(self, ctx: Context, h):
+        self.ctx = ctx
+        self.h = h
+
+    @classmethod
+    def from_host(cls, ctx: Context, packed: np.ndarray, offsets: np.ndarray) -> "Reads":
+        packed = np.ascontiguousarray(packed, dtype=np.uint64)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        h = C.c_void_p()
+        _check(ctx._lib.mcaat_reads_from_host(ctx.h, _ptr(packed, _u64p), packed.size, _ptr(offsets, _u64p),
+                                              offsets.size - 1, C.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
+    def synth(cls, ctx: Context, spec: SynthSpec) -> "Reads":
+        h = C.c_void_p()
+        s = spec.to_c()
+        _check(ctx._lib.mcaat_reads_synth(ctx.h, C.byref(s), C.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
+    def from_fastx(cls, ctx: Context, files: Sequence[str]) -> "Reads":
+        arr = (C.c_char_p * len(files))(*[f.encode() for f in files])
+        h = C.c_void_p()
+        _check(ctx._lib.mcaat_reads_from_fastx(ctx.h, arr, len(files), C.byref(h)))
+        return cls(ctx, h)
+
+    def info(self) -> Tuple[int, int]:
+        n = C.c_uint64(0)
+        b = C.c_uint64(0)
+        _check(self.ctx._lib.mcaat_reads_info(self.h, C.byref(n), C.byref(b)))
+        return n.value, b.value
+
+    def download(self) -> Tuple[np.ndarray, np.ndarray]:
+        n, b = self.info()
+        packed = np.zeros((b + 31) // 32, dtype=np.uint64)
+        offsets = np.zeros(n + 1, dtype=np.uint64)
+        _check(self.ctx._lib.mcaat_reads_download(self.h, _ptr(packed, _u64p), _ptr(offsets, _u64p)))
+        return packed, offsets
+
+    def free(self) -> None:
+        if self.h:
+            self.ctx._lib.mcaat_reads_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def count_edges(ctx: Context, reads: Reads, k: int) -> Tuple[np.ndarray, np.ndarray]:
+    """node_counter: sorted canonical (k+1)-mers (LSB-first) and their counts."""
+    n = C.c_uint64(0)
+    kp = _u64p()
+    cp = _u32p()
+    _check(ctx._lib.mcaat_count_edges(ctx.h, reads.h, k, C.byref(n), C.byref(kp), C.byref(cp)))
+    try:
+        keys = np.ctypeslib.as_array(kp, shape=(max(n.value, 1),))[: n.value].copy()
+        counts = np.ctypeslib.as_array(cp, shape=(max(n.value, 1),))[: n.value].copy()
+    finally:
+        ctx._lib.mcaat_free(C.cast(kp, C.c_void_p))
+        ctx._lib.mcaat_free(C.cast(cp, C.c_void_p))
+    return keys, counts
+
+
+@dataclass
+class CfParams:
+    threshold_multiplicity: int = 20
+    low_abundance: bool = True
+    cycle_max_length: int = 77
+    cycle_min_length: int = 27
+    cluster_bound: int = 500
+    step_cap: int = 10_000_000
+
+    def to_c(self) -> _CfParams:
+        return _CfParams(self.threshold_multiplicity, int(self.low_abundance), self.cycle_max_length,
+                         self.cycle_min_length, self.cluster_bound, self.step_cap)
+
+
+@dataclass
+class CycleResult:
+    """CycleFinder::results in commit order: [(start, [cycle, ...]), ...]."""
+
+    entries: List[Tuple[int, List[List[int]]]] = field(default_factory=list)
+    stats: List[int] = field(default_factory=list)
+    candidates: List[int] = field(default_factory=list)
+    buckets: List[int] = field(default_factory=list)
+
+
+class Graph:
+    """Device-resident SDBG (mcaat_graph)."""
+
+    def __init__(self, ctx: Context, h):
+        self.ctx = ctx
+        self.h = h
+
+    @classmethod
+    def build(cls, ctx: Context, reads: Reads, k: int) -> "Graph":
+        h = C.c_void_p()
+        _check(ctx._lib.mcaat_build_graph(ctx.h, reads.h, k, C.byref(h)))
+        return cls(ctx, h)
+
+    def info(self) -> Tuple[int, int]:
+        k = C.c_int(0)
+        d = C.c_uint64(0)
+        _check(self.ctx._lib.mcaat_graph_info(self.h, C.byref(k), C.byref(d)))
+        return k.value, d.value
+
+    @property
+    def size(self) -> int:
+        return self.info()[1]
+
+    def download(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        _, d = self.info()
+        keys = np.zeros(max(d, 1), dtype=np.uint64)
+        mult = np.zeros(max(d, 1), dtype=np.uint16)
+        valid = np.zeros(max(d, 1), dtype=np.uint8)
+        _check(self.ctx._lib.mcaat_graph_download(self.h, _ptr(keys, _u64p), _ptr(mult, _u16p), _ptr(valid, _u8p)))
+        return keys[:d], mult[:d], valid[:d]
+
+    def neighbors(self, ids: np.ndarray, incoming: bool = False) -> Tuple[np.ndarray, np.ndarray]:
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        out = np.zeros(4 * max(ids.size, 1), dtype=np.uint64)
+        cnt = np.zeros(max(ids.size, 1), dtype=np.int32)
+        _check(self.ctx._lib.mcaat_graph_neighbors(self.h, _ptr(ids, _u64p), ids.size, int(incoming),
+                                                   _ptr(out, _u64p), _ptr(cnt, _i32p)))
+        return out[: 4 * ids.size].reshape(-1, 4), cnt[: ids.size]
+
+    def set_valid(self, ids: np.ndarray, valid: bool) -> None:
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        _check(self.ctx._lib.mcaat_graph_set_valid(self.h, _ptr(ids, _u64p), ids.size, int(valid)))
+
+    def cycle_finder(self, params: Optional[CfParams] = None) -> CycleResult:
+        p = (params or CfParams()).to_c()
+        h = C.c_void_p()
+        lib = self.ctx._lib
+        _check(lib.mcaat_cycle_finder(self.h, C.byref(p), C.byref(h)))
+        try:
+            res = CycleResult()
+            n = C.c_size_t(0)
+            _check(lib.mcaat_cycles_count(h, C.byref(n)))
+            for i in range(n.value):
+                s = C.c_uint64(0)
+                fl = _u64p()
+                of = _u64p()
+                nc = C.c_size_t(0)
+                _check(lib.mcaat_cycles_get(h, i, C.byref(s), C.byref(fl), C.byref(of), C.byref(nc)))
+                offs = [of[j] for j in range(nc.value + 1)]
+                cycles = [[fl[a] for a in range(offs[j], offs[j + 1])] for j in range(nc.value)]
+                res.entries.append((s.value, cycles))
+            st = (C.c_uint64 * 8)()
+            _check(lib.mcaat_cycles_stats(h, st))
+            res.stats = list(st)
+            nca = C.c_size_t(0)
+            ip = _u64p()
+            bp = _i32p()
+            _check(lib.mcaat_cycles_candidates(h, C.byref(nca), C.byref(ip), C.byref(bp)))
+            res.candidates = [ip[j] for j in range(nca.value)]
+            res.buckets = [bp[j] for j in range(nca.value)]
+            return res
+        finally:
+            lib.mcaat_cycles_free(h)
+
+    def free(self) -> None:
+        if self.h:
+            self.ctx._lib.mcaat_graph_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass

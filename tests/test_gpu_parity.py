@@ -1,0 +1,163 @@
+"""GPU parity: every stage of the HIP path against the CPU oracle on the same seeded inputs.
+
+Bar: bit-exact (integer/index work). Calls go through the C ABI (libmcaat_gpu.so).
+Oracle parity status: "parity unpinned"  — the oracle itself is
+checked by tests/test_oracle.py against brute-force restatements and analytic answers.
+"""
+import numpy as np
+import pytest
+
+import mcaat_amd as M
+import oracle as O
+from tests.helpers import pack_reads
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = {
+    # C1 tiny: one 50 kbp genome, one array (repeat 30, spacer 32, 12 copies)
+    "c1_k23": (M.SynthSpec(), 23, M.CfParams()),
+    "c1_k27": (M.SynthSpec(), 27, M.CfParams()),
+    # errors, several genomes/arrays, paired-end, ragged repeat/spacer lengths
+    "pe_err": (M.SynthSpec(seed=7, n_genomes=4, genome_len=20_000, arrays_per_genome=2, spacers_per_array=8,
+                           repeat_len_min=32, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
+                           n_reads=24_000, error_rate=0.002, paired=True), 23, M.CfParams(threshold_multiplicity=5)),
+    # low-abundance mode: threshold 2 -> many candidates and conflicting speculative starts
+    "low_thr": (M.SynthSpec(seed=11, n_genomes=3, genome_len=15_000, arrays_per_genome=2, spacers_per_array=10,
+                            repeat_len_min=30, repeat_len_max=34, spacer_len_min=30, spacer_len_max=34,
+                            n_reads=12_000, error_rate=0.004), 23,
+                M.CfParams(threshold_multiplicity=2, low_abundance=True)),
+    "low_abundance_false": (M.SynthSpec(seed=12, n_genomes=2, genome_len=12_000, arrays_per_genome=1,
+                                        spacers_per_array=6, n_reads=8_000, error_rate=0.003), 21,
+                            M.CfParams(threshold_multiplicity=3, low_abundance=False, cycle_min_length=20,
+                                       cycle_max_length=70)),
+}
+
+
+def _oracle_graph(packed, offs, k):
+    return O.OGraph.build(packed, offs, k, threads=4)
+
+
+@pytest.fixture(scope="module", params=sorted(CONFIGS))
+def case(request, gpu_ctx):
+    spec, k, prm = CONFIGS[request.param]
+    packed, offs = M.synth_host(spec)
+    reads = M.Reads.synth(gpu_ctx, spec)
+    return request.param, spec, k, prm, packed, offs, reads
+
+
+def test_synth_reads_device_equals_host(case):
+    _, spec, _, _, packed, offs, reads = case
+    dp, do = reads.download()
+    assert np.array_equal(do, offs)
+    assert np.array_equal(dp[: packed.size], packed)
+
+
+def test_node_counter_parity(case, gpu_ctx):
+    _, _, k, _, packed, offs, reads = case
+    gk, gc = M.count_edges(gpu_ctx, reads, k)
+    ok, oc = O.count_canonical(packed, offs, k, threads=4)
+    assert gk.size == ok.size
+    assert np.array_equal(gk, ok)
+    assert np.array_equal(gc, oc)
+
+
+def test_sdbg_build_parity(case, gpu_ctx):
+    _, _, k, _, packed, offs, reads = case
+    g = M.Graph.build(gpu_ctx, reads, k)
+    og = _oracle_graph(packed, offs, k)
+    keys, mult, valid = g.download()
+    okeys, omult = og.arrays()
+    assert g.size == og.size
+    assert np.array_equal(keys, okeys)
+    assert np.array_equal(mult, omult)
+    assert valid.all()
+    # neighbour queries (valid-only, DESCENDING out / ASCENDING in) on a sample of edges
+    rng = np.random.default_rng(0)
+    ids = rng.choice(g.size, size=min(g.size, 3000), replace=False).astype(np.uint64)
+    out, oc = g.neighbors(ids, incoming=False)
+    inn, ic = g.neighbors(ids, incoming=True)
+    for i, e in enumerate(ids):
+        assert list(out[i, : oc[i]]) == og.outgoing(int(e))
+        assert list(inn[i, : ic[i]]) == og.incoming(int(e))
+
+
+def test_cycle_finder_parity(case, gpu_ctx):
+    name, _, k, prm, packed, offs, reads = case
+    g = M.Graph.build(gpu_ctx, reads, k)
+    res = g.cycle_finder(prm)
+    og = _oracle_graph(packed, offs, k)
+    ores = og.cycle_finder(threshold_multiplicity=prm.threshold_multiplicity, low_abundance=prm.low_abundance,
+                           cycle_max_length=prm.cycle_max_length, cycle_min_length=prm.cycle_min_length, threads=1)
+    assert res.stats[:6] == ores["stats"], name
+    assert res.candidates == ores["candidates"]
+    assert res.buckets == ores["buckets"]
+    assert len(res.entries) == len(ores["entries"])
+    for (s, cyc), (os_, ocyc) in zip(res.entries, ores["entries"]):
+        assert s == os_
+        assert cyc == ocyc
+    # post-prune / post-search valid bits equal
+    _, _, valid = g.download()
+    assert np.array_equal(valid, og.valid())
+
+
+def test_fastx_reader_splits_on_n(gpu_ctx, tmp_path):
+    seqs = ["ACGTACGTTTGACCA" * 6, "GGGTTTAAACCC" * 5 + "N" + "ACGATCGATCGGATTAC" * 3, "ACGTNNACGT"]
+    fq = tmp_path / "r.fq"
+    with open(fq, "w") as f:
+        for i, s in enumerate(seqs):
+            f.write(f"@r{i}\n{s}\n+\n{'I' * len(s)}\n")
+    reads = M.Reads.from_fastx(gpu_ctx, [str(fq)])
+    parts = []
+    for s in seqs:
+        parts += [p for p in s.split("N") if p]
+    packed, offs = pack_reads(parts)
+    dp, do = reads.download()
+    assert np.array_equal(do, offs)
+    assert np.array_equal(dp[: packed.size], packed)
+    gk, gc = M.count_edges(gpu_ctx, reads, 11)
+    ok, oc = O.count_canonical(packed, offs, 11)
+    assert np.array_equal(gk, ok) and np.array_equal(gc, oc)
+
+
+def test_edge_cases_empty_and_short(gpu_ctx):
+    # reads shorter than k+1 contribute nothing; an all-short input gives an empty graph
+    packed, offs = pack_reads(["ACGT", "GATTACA", "A"])
+    reads = M.Reads.from_host(gpu_ctx, packed, offs)
+    g = M.Graph.build(gpu_ctx, reads, 9)
+    assert g.size == 0
+    res = g.cycle_finder(M.CfParams())
+    assert res.entries == [] and res.stats[:6] == [0, 0, 0, 0, 0, 0]
+
+
+def test_palindromes_and_homopolymers(gpu_ctx):
+    # palindromic (k+1)-mers (k+1 even) and a poly-A self-loop edge
+    pal = "ACGTACGT"  # rc(ACGTACGT) == ACGTACGT
+    seqs = [pal * 20, "A" * 60, "T" * 30 + pal + "GGCC" * 10]
+    packed, offs = pack_reads(seqs)
+    reads = M.Reads.from_host(gpu_ctx, packed, offs)
+    for k in (7, 9):
+        g = M.Graph.build(gpu_ctx, reads, k)
+        og = O.OGraph.build(packed, offs, k)
+        keys, mult, _ = g.download()
+        okeys, omult = og.arrays()
+        assert np.array_equal(keys, okeys) and np.array_equal(mult, omult)
+        res = g.cycle_finder(M.CfParams(threshold_multiplicity=1, cycle_min_length=1, cycle_max_length=20))
+        ores = og.cycle_finder(threshold_multiplicity=1, cycle_min_length=1, cycle_max_length=20)
+        assert res.entries == [tuple(e) for e in ores["entries"]]
+        assert res.stats[:6] == ores["stats"]
+
+
+def test_cluster_bound_and_step_cap(gpu_ctx):
+    # many spacers through one repeat: >= cluster_bound cycles -> empty entry (cycle_finder.cpp:162-165);
+    # a tiny step cap truncates the search (cycle_finder.cpp:148-151)
+    spec = M.SynthSpec(seed=21, n_genomes=1, genome_len=30_000, arrays_per_genome=1, spacers_per_array=40,
+                       repeat_len_min=30, repeat_len_max=30, spacer_len_min=30, spacer_len_max=34, n_reads=30_000)
+    packed, offs = M.synth_host(spec)
+    reads = M.Reads.synth(gpu_ctx, spec)
+    for bound, cap in ((5, 10_000_000), (500, 10_000_000), (500, 200), (3, 5000)):
+        g = M.Graph.build(gpu_ctx, reads, 23)
+        res = g.cycle_finder(M.CfParams(cluster_bound=bound, step_cap=cap))
+        og = O.OGraph.build(packed, offs, 23)
+        ores = og.cycle_finder(cluster_bound=bound, step_cap=cap)
+        assert res.stats[:6] == ores["stats"], (bound, cap)
+        assert [(s, c) for s, c in res.entries] == [tuple(e) for e in ores["entries"]], (bound, cap)
