@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""bench.py — k-mers/s through node_counter + sdbg_build + cycle_finder on MI355X.
+
+Metric (BASELINE.json): "k-mers/sec through sdbg_build+cycle_finder, 1B-node graph @ 1/2/4/8 GPUs".
+One step = one pass of the hot path over one synthetic metagenome resident in HBM:
+reads -> edge counting -> SDBG -> CycleFinder (results ready on the host).
+k-mers = N_occ = sum over reads of (L - k) edge occurrences.
+
+Workload (N=1): config C3 — ~300M x 150 bp reads, k=27, threshold_multiplicity=20,
+error rate tuned so the SDBG has ~1e9 edges (D). For N>1 every rank runs its own
+independent sample of the same size (weak scaling, no data-path collective;
+DESIGN.md §Multi-GPU); value = all ranks' k-mers / max-over-ranks step time.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|tiny]
+       N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import mcaat_amd as M  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # C3: 300 Mbp community (200 genomes x 1.5 Mbp, 2 arrays each), 300M SE reads, k=27
+    "c3": dict(spec=M.SynthSpec(seed=3, n_genomes=200, genome_len=1_500_000, arrays_per_genome=2,
+                                spacers_per_array=12, repeat_len_min=30, repeat_len_max=36, spacer_len_min=30,
+                                spacer_len_max=36, read_len=150, n_reads=300_000_000, error_rate=2.0e-4),
+               k=27, thr=20, name="C3 1B-node synthetic metagenome (300M x 150bp SE, k=27, thr=20)"),
+    # C2-shaped, smaller: 50M PE reads over a 400 Mbp community
+    "c2": dict(spec=M.SynthSpec(seed=2, n_genomes=200, genome_len=2_000_000, arrays_per_genome=2,
+                                spacers_per_array=12, repeat_len_min=30, repeat_len_max=36, spacer_len_min=30,
+                                spacer_len_max=36, read_len=150, n_reads=50_000_000, error_rate=5.0e-3, paired=True),
+               k=27, thr=20, name="C2 50M PE synthetic metagenome (k=27)"),
+    "tiny": dict(spec=M.SynthSpec(), k=27, thr=20, name="C1 tiny (10k x 150bp, 50 kbp genome, k=27)"),
+}
+
+
+def n_occ(spec: M.SynthSpec, k: int) -> int:
+    return spec.n_reads * max(0, spec.read_len - k)
+
+
+def cpu_baseline(cfg: dict, sample_reads: int, threads: int) -> dict:
+    """The oracle (CPU restatement, OpenMP) on a bounded sample of the same workload."""
+    import oracle as O
+
+    spec = M.SynthSpec(**{**cfg["spec"].__dict__, "n_reads": sample_reads})
+    packed, offs = M.synth_host(spec)
+    t0 = time.perf_counter()
+    g = O.OGraph.build(packed, offs, cfg["k"], threads=threads)
+    g.cycle_finder(threshold_multiplicity=cfg["thr"], threads=threads)
+    dt = time.perf_counter() - t0
+    kmers = n_occ(spec, cfg["k"])
+    return {
+        "value": kmers / dt,
+        "unit": "k-mers/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{sample_reads} reads of the same synthetic spec ({kmers} k-mers, D={g.size}), "
+                  f"oracle count+SDBG+CycleFinder, {dt:.2f} s",
+    }
+
+
+def traffic_from_profiles(kernel: str) -> float | None:
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary, if any."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return float(d[kernel]["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--reads", type=int, default=0, help="override n_reads")
+    ap.add_argument("--cpu-sample-reads", type=int, default=2_000_000)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist  # control plane only (barrier, max of times)
+
+        dist.init_process_group("gloo")
+    import torch
+
+    cfg = dict(CONFIGS[args.config])
+    spec = M.SynthSpec(**cfg["spec"].__dict__)
+    if args.reads:
+        spec.n_reads = args.reads
+    spec.seed = spec.seed * 1000 + rank  # independent sample per rank (weak scaling)
+    k, thr = cfg["k"], cfg["thr"]
+
+    ctx = M.Context(local)
+    reads = M.Reads.synth(ctx, spec)
+    prm = M.CfParams(threshold_multiplicity=thr)
+
+    def step():
+        g = M.Graph.build(ctx, reads, k)
+        st_build = ctx.stage_times()
+        d = g.size
+        res = g.cycle_finder(prm)
+        st_cf = ctx.stage_times()
+        g.free()
+        return d, res, {**st_build, **st_cf}
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+    ctx.reset_timing()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    D = 0
+    res = None
+    stages = {}
+    for _ in range(args.steps):
+        D, res, st = step()
+        for kk, vv in st.items():
+            stages[kk] = stages.get(kk, 0.0) + vv / args.steps
+    torch.cuda.synchronize()
+    barrier()
+    dt = (time.perf_counter() - t0) / max(1, args.steps)
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    avg_ms, launches, bytes_per_launch = ctx.kernel_timing("node_counter")
+    kmers_rank = n_occ(spec, k)
+    value = kmers_rank * world / dt
+    if rank == 0:
+        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        traffic = traffic_from_profiles("node_counter")
+        out = {
+            "metric": "k-mers/sec through sdbg_build+cycle_finder, 1B-node graph @ 1/2/4/8 GPUs",
+            "value": value,
+            "unit": "k-mers/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u64",
+            "data": "synthetic (counter-based RNG genomes with CRISPR arrays, reads generated in HBM)",
+            "config": {
+                "workload": cfg["name"],
+                "reads_per_gpu": spec.n_reads,
+                "read_len": spec.read_len,
+                "k": k,
+                "threshold_multiplicity": thr,
+                "error_rate": spec.error_rate,
+                "kmers_per_gpu": kmers_rank,
+                "sdbg_edges_D": D,
+                "parallelism": f"replicas{world}",
+                "cycle_entries": len(res.entries) if res else 0,
+                "cycles": res.stats[5] if res else 0,
+            },
+            "roofline": {
+                "kernel": "node_counter (k_count_fixed)",
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": PEAK_HBM_GBS,
+                "unit": "GB/s",
+                "frac": achieved / PEAK_HBM_GBS,
+                "traffic": traffic,
+                "avg_launch_ms": avg_ms,
+                "launches": launches,
+                "algorithmic_bytes_per_launch": bytes_per_launch,
+            },
+            "stages_ms": {kk: round(vv, 3) for kk, vv in stages.items()},
+            "cpu_baseline": None,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline(cfg, min(args.cpu_sample_reads, spec.n_reads), args.cpu_threads)
+            except Exception as e:  # reported, never fatal for the GPU number
+                out["cpu_baseline"] = {"error": str(e)}
+        print(json.dumps(out), flush=True)
+    reads.free()
+    ctx.close()
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -263,6 +263,7 @@ int mcaat_init(int device, mcaat_ctx **out) {
 void mcaat_finalize(mcaat_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
+    mcaat::dev_trim();
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

@@ -116,4 +116,18 @@ __device__ __forceinline__ int dev_indeg(const GraphView &g, uint64_t e) {
     return dev_incoming(g, e, t);
 }
 
+// block-wide sum, one atomic per block (blockDim.x must be a multiple of 64, <= 1024)
+__device__ __forceinline__ void block_add(unsigned long long *counter, unsigned long long v) {
+    __shared__ unsigned long long part[16];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) part[w] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += part[i];
+        if (t) atomicAdd(counter, t);
+    }
+}
+
 }  // namespace mcaat

@@ -37,6 +37,7 @@ __global__ void __launch_bounds__(kBlock) k_tips(GraphView g, uint64_t *tip_bm, 
     const int lane = threadIdx.x & 63;
     const uint64_t nw = (g.D + 63) / 64;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    unsigned long long acc = 0;
     for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nw; w += wstride) {
         const uint64_t e = w * 64 + lane;
         bool t = false;
@@ -44,15 +45,17 @@ __global__ void __launch_bounds__(kBlock) k_tips(GraphView g, uint64_t *tip_bm, 
         const unsigned long long m = __ballot(t);
         if (lane == 0) {
             if (tip_bm) tip_bm[w] = m;
-            if (m) atomicAdd(count, (unsigned long long)__popcll(m));
+            acc += __popcll(m);
         }
     }
+    block_add(count, acc);
 }
 
 __global__ void __launch_bounds__(kBlock) k_mult_filter(GraphView g, unsigned long long *count) {
     const int lane = threadIdx.x & 63;
     const uint64_t nw = (g.D + 63) / 64;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    unsigned long long acc = 0;
     for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nw; w += wstride) {
         const uint64_t e = w * 64 + lane;
         const bool low = e < g.D && g.mult[e] <= 1;
@@ -60,17 +63,17 @@ __global__ void __launch_bounds__(kBlock) k_mult_filter(GraphView g, unsigned lo
         if (lane == 0) {
             const uint64_t old = g.valid[w];
             g.valid[w] = old & ~m;
-            if (m) atomicAdd(count, (unsigned long long)__popcll(m));  // reference counts every mult<=1 edge
+            acc += __popcll(m);  // reference counts every mult<=1 edge
         }
     }
+    block_add(count, acc);
 }
 
 __global__ void __launch_bounds__(kBlock) k_popcount(const uint64_t *bm, uint64_t nw, unsigned long long *count) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     unsigned long long s = 0;
     for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) s += __popcll(bm[w]);
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o);
-    if ((threadIdx.x & 63) == 0 && s) atomicAdd(count, s);
+    block_add(count, s);
 }
 
 // ------------------------------- peel --------------------------------------
@@ -99,20 +102,12 @@ __global__ void __launch_bounds__(kBlock) k_peel_init(GraphView g, PeelArrays pa
     }
 }
 
-__global__ void __launch_bounds__(kBlock) k_peel_rulers(uint64_t D, PeelArrays pa, uint64_t *list,
-                                                        unsigned long long *cursor) {
+__global__ void __launch_bounds__(kBlock) k_peel_rulers(uint64_t D, PeelArrays pa) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    const int lane = threadIdx.x & 63;
-    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < D; base += stride) {
-        const uint64_t e = base + threadIdx.x;
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < D; e += stride) {
         bool r = false;
-        if (e < D && pa.od[e] == 1) r = pa.upred[e] == 0 || (mix64(e ^ 0x5eed) & 63) == 0;
-        if (e < D) pa.ruler[e] = r;
-        const unsigned long long m = __ballot(r);
-        unsigned long long off = 0;
-        if (lane == 0 && m) off = atomicAdd(cursor, (unsigned long long)__popcll(m));
-        off = __shfl(off, 0);
-        if (r) list[off + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = e;
+        if (pa.od[e] == 1) r = pa.upred[e] == 0 || (mix64(e ^ 0x5eed) & 63) == 0;
+        pa.ruler[e] = r;
     }
 }
 
@@ -592,6 +587,17 @@ unsigned long long read_counter(mcaat_ctx *ctx, unsigned long long *d) {
     return h;
 }
 
+// ids i in [0, n) with flags[i] != 0, in ascending order; returns the count
+uint64_t select_flagged(mcaat_ctx *ctx, const uint8_t *flags, uint64_t n, uint64_t *out, unsigned long long *d_num) {
+    hipcub::CountingInputIterator<uint64_t> it(0);
+    size_t tmp = 0;
+    HIP_OK(hipcub::DeviceSelect::Flagged(nullptr, tmp, it, flags, out, d_num, (size_t)n, ctx->stream));
+    DevBuf<uint8_t> t(tmp);
+    HIP_OK(hipcub::DeviceSelect::Flagged(t.p, tmp, it, flags, out, d_num, (size_t)n, ctx->stream));
+    return read_counter(ctx, d_num);
+}
+
+
 // host visited mirror: a dense bitmap of D bits
 struct HostBits {
     std::vector<uint64_t> w;
@@ -617,11 +623,10 @@ static void run_peel(mcaat_graph *g, const uint64_t *seed_bm) {
     hipLaunchKernelGGL(k_peel_init, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, v, pa);
     LAUNCH_OK();
     DevBuf<unsigned long long> cur(1);
-    HIP_OK(hipMemsetAsync(cur.p, 0, 8, st));
     DevBuf<uint64_t> list(D);
-    hipLaunchKernelGGL(k_peel_rulers, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, D, pa, list.p, cur.p);
+    hipLaunchKernelGGL(k_peel_rulers, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, D, pa);
     LAUNCH_OK();
-    const uint64_t nr = read_counter(ctx, cur.p);
+    const uint64_t nr = select_flagged(ctx, ruler.p, D, list.p, cur.p);
     if (nr) {
         hipLaunchKernelGGL(k_peel_walk, dim3(grid_for(nr, kBlock)), dim3(kBlock), 0, st, pa, list.p, nr);
         LAUNCH_OK();

@@ -30,37 +30,46 @@ struct Error : std::runtime_error {
 
 #define LAUNCH_OK() HIP_OK(hipGetLastError())
 
+// Caching device allocator: the hot path allocates the same multi-GB buffers every
+// step; hipMalloc/hipFree of such buffers costs 10-100s of ms each, so freed blocks are
+// kept per device and reused (best fit within 2x); on an allocation failure the cache
+// is trimmed and the allocation retried.
+void *dev_alloc(size_t bytes);
+void dev_free(void *p, size_t bytes);
+void dev_trim();
+
 // owning device buffer
 template <class T>
 struct DevBuf {
     T *p = nullptr;
     size_t n = 0;
+    size_t cap_bytes = 0;
     DevBuf() = default;
     explicit DevBuf(size_t count) { alloc(count); }
     DevBuf(const DevBuf &) = delete;
     DevBuf &operator=(const DevBuf &) = delete;
-    DevBuf(DevBuf &&o) noexcept : p(o.p), n(o.n) { o.p = nullptr; o.n = 0; }
+    DevBuf(DevBuf &&o) noexcept : p(o.p), n(o.n), cap_bytes(o.cap_bytes) { o.p = nullptr; o.n = 0; o.cap_bytes = 0; }
     DevBuf &operator=(DevBuf &&o) noexcept {
-        if (this != &o) { release(); p = o.p; n = o.n; o.p = nullptr; o.n = 0; }
+        if (this != &o) {
+            release();
+            p = o.p; n = o.n; cap_bytes = o.cap_bytes;
+            o.p = nullptr; o.n = 0; o.cap_bytes = 0;
+        }
         return *this;
     }
     ~DevBuf() { release(); }
     void alloc(size_t count) {
         release();
         if (count == 0) count = 1;
-        hipError_t e = hipMalloc(&p, count * sizeof(T));
-        if (e != hipSuccess) {
-            p = nullptr;
-            (void)hipGetLastError();
-            throw Error(MCAAT_E_NOMEM, "hipMalloc of " + std::to_string(count * sizeof(T)) + " bytes failed: " +
-                                           hipGetErrorString(e));
-        }
+        cap_bytes = (count * sizeof(T) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+        p = (T *)dev_alloc(cap_bytes);
         n = count;
     }
     void release() {
-        if (p) (void)hipFree(p);
+        if (p) dev_free(p, cap_bytes);
         p = nullptr;
         n = 0;
+        cap_bytes = 0;
     }
     size_t bytes() const { return n * sizeof(T); }
 };

@@ -19,27 +19,31 @@ namespace {
 constexpr int kBlock = 256;
 constexpr uint32_t kMaxProbe = 1u << 14;
 
-__device__ __forceinline__ void table_insert(uint64_t key, uint64_t *tkeys, uint32_t *tcnt, uint64_t mask,
-                                             unsigned long long *n_new, int *overflow) {
+// one 16-byte slot: key+1 (0 = empty, so a plain memset clears the table) and count,
+// in the same cache line so a hit costs one line
+struct __attribute__((aligned(16))) Slot {
+    unsigned long long key1;
+    unsigned int cnt;
+    unsigned int pad;
+};
+
+__device__ __forceinline__ void table_insert(uint64_t key, Slot *tab, uint64_t mask, unsigned long long *n_new,
+                                             int *overflow) {
+    const unsigned long long k1 = key + 1;
     uint64_t slot = mix64(key) & mask;
     for (uint32_t probe = 0; probe < kMaxProbe; ++probe) {
-        uint64_t cur = __hip_atomic_load(&tkeys[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (cur == key) {
-            atomicAdd(&tcnt[slot], 1u);
-            return;
-        }
-        if (cur == kEmpty) {
-            unsigned long long prev = atomicCAS((unsigned long long *)&tkeys[slot], (unsigned long long)kEmpty,
-                                                (unsigned long long)key);
-            if (prev == kEmpty) {
-                atomicAdd(&tcnt[slot], 1u);
+        unsigned long long cur = __hip_atomic_load(&tab[slot].key1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (cur == 0) {
+            cur = atomicCAS(&tab[slot].key1, 0ull, k1);
+            if (cur == 0) {
+                atomicAdd(&tab[slot].cnt, 1u);
                 atomicAdd(n_new, 1ull);
                 return;
             }
-            if (prev == key) {
-                atomicAdd(&tcnt[slot], 1u);
-                return;
-            }
+        }
+        if (cur == k1) {
+            atomicAdd(&tab[slot].cnt, 1u);
+            return;
         }
         slot = (slot + 1) & mask;
     }
@@ -48,8 +52,8 @@ __device__ __forceinline__ void table_insert(uint64_t key, uint64_t *tkeys, uint
 
 // fixed-length reads: thread i -> (read i / npos, position i % npos)
 __global__ void __launch_bounds__(kBlock) k_count_fixed(const uint64_t *__restrict__ packed, uint64_t n_reads,
-                                                        uint64_t L, int E, uint64_t *tkeys, uint32_t *tcnt,
-                                                        uint64_t mask, unsigned long long *n_new, int *overflow) {
+                                                        uint64_t L, int E, Slot *tab, uint64_t mask,
+                                                        unsigned long long *n_new, int *overflow) {
     const uint64_t npos = L - E + 1;
     const uint64_t total = n_reads * npos;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -57,15 +61,15 @@ __global__ void __launch_bounds__(kBlock) k_count_fixed(const uint64_t *__restri
         const uint64_t r = i / npos, p = i - r * npos;
         const uint64_t lsb = window_at(packed, r * L + p, E);
         const uint64_t rc = lsb_rc(lsb, E);
-        table_insert(lsb < rc ? lsb : rc, tkeys, tcnt, mask, n_new, overflow);
+        table_insert(lsb < rc ? lsb : rc, tab, mask, n_new, overflow);
     }
 }
 
 // variable-length reads: one wave per read, lanes stride over positions
 __global__ void __launch_bounds__(kBlock) k_count_var(const uint64_t *__restrict__ packed,
                                                       const uint64_t *__restrict__ offsets, uint64_t n_reads, int E,
-                                                      uint64_t *tkeys, uint32_t *tcnt, uint64_t mask,
-                                                      unsigned long long *n_new, int *overflow) {
+                                                      Slot *tab, uint64_t mask, unsigned long long *n_new,
+                                                      int *overflow) {
     const int lane = threadIdx.x & 63;
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
@@ -76,29 +80,21 @@ __global__ void __launch_bounds__(kBlock) k_count_var(const uint64_t *__restrict
         for (uint64_t p = lane; p < npos; p += 64) {
             const uint64_t lsb = window_at(packed, a + p, E);
             const uint64_t rc = lsb_rc(lsb, E);
-            table_insert(lsb < rc ? lsb : rc, tkeys, tcnt, mask, n_new, overflow);
+            table_insert(lsb < rc ? lsb : rc, tab, mask, n_new, overflow);
         }
     }
 }
 
-// compact occupied slots (wave-aggregated cursor; order is irrelevant, sorted later)
-__global__ void __launch_bounds__(kBlock) k_compact(const uint64_t *tkeys, const uint32_t *tcnt, uint64_t cap,
-                                                    uint64_t *okeys, uint32_t *ocnt, unsigned long long *cursor) {
+struct Occupied {
+    __device__ __forceinline__ bool operator()(const Slot &s) const { return s.key1 != 0; }
+};
+
+__global__ void __launch_bounds__(kBlock) k_split(const Slot *in, uint64_t n, uint64_t *keys, uint32_t *cnt) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    const int lane = threadIdx.x & 63;
-    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < cap; base += stride) {
-        const uint64_t i = base + threadIdx.x;
-        const bool occ = i < cap && tkeys[i] != kEmpty;
-        const unsigned long long m = __ballot(occ);
-        unsigned long long off = 0;
-        if (lane == 0 && m) off = atomicAdd(cursor, (unsigned long long)__popcll(m));
-        off = __shfl(off, 0);
-        if (occ) {
-            const unsigned long long below = m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane)));
-            const uint64_t o = off + __popcll(below);
-            okeys[o] = tkeys[i];
-            ocnt[o] = tcnt[i];
-        }
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const Slot s = in[i];
+        keys[i] = s.key1 - 1;
+        cnt[i] = s.cnt;
     }
 }
 
@@ -112,7 +108,8 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
         n_occ = r->fixed_len >= (uint64_t)E ? r->n_reads * (r->fixed_len - E + 1) : 0;
     } else {
         std::vector<uint64_t> off(r->n_reads + 1);
-        HIP_OK(hipMemcpy(off.data(), r->offsets.p, 8 * (r->n_reads + 1), hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpyAsync(off.data(), r->offsets.p, 8 * (r->n_reads + 1), hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
         for (uint64_t i = 0; i < r->n_reads; ++i)
             if (off[i + 1] - off[i] >= (uint64_t)E) n_occ += off[i + 1] - off[i] - E + 1;
     }
@@ -122,25 +119,20 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
 
     DevBuf<unsigned long long> dcnt(2);
     DevBuf<int> dover(1);
-    for (int attempt = 0;; ++attempt) {
-        DevBuf<uint64_t> tkeys(cap);
-        DevBuf<uint32_t> tcnt(cap);
-        HIP_OK(hipMemsetAsync(tkeys.p, 0xFF, tkeys.bytes(), st));
-        HIP_OK(hipMemsetAsync(tcnt.p, 0, tcnt.bytes(), st));
+    for (;;) {
+        DevBuf<Slot> tab(cap);
+        HIP_OK(hipMemsetAsync(tab.p, 0, tab.bytes(), st));
         HIP_OK(hipMemsetAsync(dcnt.p, 0, dcnt.bytes(), st));
         HIP_OK(hipMemsetAsync(dover.p, 0, dover.bytes(), st));
         {
             // algorithmic bytes per launch: 2-bit reads once + 16 B per occurrence
             KernelTimer kt(ctx, "node_counter", 0.25 * (double)r->n_bases + 16.0 * (double)n_occ);
             if (r->fixed_len) {
-                const uint64_t total = n_occ;
-                hipLaunchKernelGGL(k_count_fixed, dim3(grid_for(total, kBlock, 256 * 64)), dim3(kBlock), 0, st,
-                                   r->packed.p, r->n_reads, r->fixed_len, E, tkeys.p, tcnt.p, cap - 1, dcnt.p,
-                                   dover.p);
+                hipLaunchKernelGGL(k_count_fixed, dim3(grid_for(n_occ, kBlock, 256 * 64)), dim3(kBlock), 0, st,
+                                   r->packed.p, r->n_reads, r->fixed_len, E, tab.p, cap - 1, dcnt.p, dover.p);
             } else {
                 hipLaunchKernelGGL(k_count_var, dim3(grid_for(r->n_reads * 64, kBlock, 256 * 64)), dim3(kBlock), 0,
-                                   st, r->packed.p, r->offsets.p, r->n_reads, E, tkeys.p, tcnt.p, cap - 1, dcnt.p,
-                                   dover.p);
+                                   st, r->packed.p, r->offsets.p, r->n_reads, E, tab.p, cap - 1, dcnt.p, dover.p);
             }
             LAUNCH_OK();
             kt.stop();
@@ -155,12 +147,19 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
             cap <<= 2;
             continue;
         }
+        DevBuf<Slot> packed_slots(n_new);
+        size_t tmp = 0;
+        HIP_OK(hipcub::DeviceSelect::If(nullptr, tmp, tab.p, packed_slots.p, dcnt.p, (size_t)cap, Occupied(), st));
+        {
+            DevBuf<uint8_t> t(tmp);
+            HIP_OK(hipcub::DeviceSelect::If(t.p, tmp, tab.p, packed_slots.p, dcnt.p, (size_t)cap, Occupied(), st));
+        }
+        tab.release();
         out.n = n_new;
         out.keys.alloc(n_new);
         out.counts.alloc(n_new);
-        HIP_OK(hipMemsetAsync(dcnt.p, 0, 8, st));
-        hipLaunchKernelGGL(k_compact, dim3(grid_for(cap, kBlock, 256 * 64)), dim3(kBlock), 0, st, tkeys.p, tcnt.p,
-                           cap, out.keys.p, out.counts.p, dcnt.p);
+        hipLaunchKernelGGL(k_split, dim3(grid_for(n_new, kBlock)), dim3(kBlock), 0, st, packed_slots.p, n_new,
+                           out.keys.p, out.counts.p);
         LAUNCH_OK();
         HIP_OK(hipStreamSynchronize(st));
         break;
