@@ -80,6 +80,25 @@ def traffic_from_profiles(kernel: str) -> float | None:
         return None
 
 
+class _DryContext:
+    def kernel_timing(self, name):
+        return 0.0, 0, 0.0
+
+    def reset_timing(self):
+        pass
+
+    def stage_times(self):
+        return {}
+
+    def close(self):
+        pass
+
+
+class _DryReads:
+    def free(self):
+        pass
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -90,6 +109,8 @@ def main() -> int:
     ap.add_argument("--cpu-sample-reads", type=int, default=2_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU-only rehearsal of the control flow (ranks, barrier, max-reduce, JSON); no GPU work")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -109,11 +130,18 @@ def main() -> int:
     spec.seed = spec.seed * 1000 + rank  # independent sample per rank (weak scaling)
     k, thr = cfg["k"], cfg["thr"]
 
-    ctx = M.Context(local)
-    reads = M.Reads.synth(ctx, spec)
+    if args.dry_run:
+        ctx = _DryContext()
+        reads = _DryReads()
+    else:
+        ctx = M.Context(local)
+        reads = M.Reads.synth(ctx, spec)
     prm = M.CfParams(threshold_multiplicity=thr)
 
     def step():
+        if args.dry_run:
+            time.sleep(0.01 * (1 + rank))
+            return 0, None, {}
         g = M.Graph.build(ctx, reads, k)
         st_build = ctx.stage_times()
         d = g.size
@@ -129,8 +157,9 @@ def main() -> int:
     for _ in range(args.warmup):
         step()
     ctx.reset_timing()
+    sync = (lambda: None) if args.dry_run else torch.cuda.synchronize
     barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     D = 0
     res = None
@@ -139,7 +168,7 @@ def main() -> int:
         D, res, st = step()
         for kk, vv in st.items():
             stages[kk] = stages.get(kk, 0.0) + vv / args.steps
-    torch.cuda.synchronize()
+    sync()
     barrier()
     dt = (time.perf_counter() - t0) / max(1, args.steps)
     if dist is not None:
@@ -194,7 +223,7 @@ def main() -> int:
             "stages_ms": {kk: round(vv, 3) for kk, vv in stages.items()},
             "cpu_baseline": None,
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and not args.dry_run:
             try:
                 out["cpu_baseline"] = cpu_baseline(cfg, min(args.cpu_sample_reads, spec.n_reads), args.cpu_threads)
             except Exception as e:  # reported, never fatal for the GPU number

@@ -1,0 +1,251 @@
+"""CPU tests of the oracle (test infrastructure) — no GPU.
+
+The oracle is "parity unpinned" (the reference's MEGAHIT-backed path cannot be built
+here and ships no golden vectors). These tests pin it instead to:
+  * brute-force pure-Python restatements of the SDBG conventions,
+  * analytic known answers (a CRISPR array R S1 R ... Sn R yields exactly one cycle per
+    spacer whose edges are the (k+1)-mers of the circular string R+Si),
+  * a compiled libstdc++ probe of the unordered_set iteration order the GPU emulates,
+  * committed regression fixtures (tests/golden/, made by tests/golden/make_golden.py).
+"""
+import json
+import os
+import random
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle as O
+from tests.helpers import boss_key, brute_graph, brute_neighbors, lsb_value, pack_reads, rc
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def rand_seq(rng, n, alphabet="ACGT"):
+    return "".join(rng.choice(alphabet) for _ in range(n))
+
+
+@pytest.mark.parametrize("k", [5, 6, 7, 11])
+def test_count_canonical_matches_bruteforce(k):
+    rng = random.Random(k)
+    seqs = [rand_seq(rng, rng.randint(1, 60), "ACGT" if i % 3 else "AC") for i in range(80)]
+    packed, offs = pack_reads(seqs)
+    keys, counts = O.count_canonical(packed, offs, k)
+    E = k + 1
+    ref = {}
+    for s in seqs:
+        for i in range(len(s) - E + 1):
+            e = s[i:i + E]
+            c = min(lsb_value(e), lsb_value(rc(e)))
+            ref[c] = ref.get(c, 0) + 1
+    assert list(keys) == sorted(ref)
+    assert list(counts) == [ref[x] for x in sorted(ref)]
+
+
+@pytest.mark.parametrize("k", [4, 5, 7])
+def test_sdbg_arrays_and_neighbors_match_bruteforce(k):
+    rng = random.Random(100 + k)
+    seqs = [rand_seq(rng, rng.randint(10, 40), "ACGT" if i % 2 else "ACG") for i in range(60)]
+    seqs.append("ACGTACGT" * 3)  # palindromic edges for even k+1
+    packed, offs = pack_reads(seqs)
+    g = O.OGraph.build(packed, offs, k)
+    edges, mult = brute_graph(seqs, k)
+    keys, m = g.arrays()
+    assert list(keys) == [boss_key(e, k) for e in edges]
+    assert list(m) == [mult[e] for e in edges]
+    out, inc = brute_neighbors(edges, k)
+    for i in range(len(edges)):
+        assert g.outgoing(i) == out[i]
+        assert g.incoming(i) == inc[i]
+        # GetLabel: source-node label, symbols 1..4 (tmp_utils.cpp:83-89)
+        assert g.label(i) == ["ACGT".index(c) + 1 for c in edges[i][:k]]
+    # IndexBinarySearch: last edge of the node with that label, -1 when absent
+    for i, e in enumerate(edges):
+        lab = [("ACGT".index(c) + 1) for c in e[:k]]
+        j = g.index_binary_search(lab)
+        assert edges[j][:k] == e[:k] and (j + 1 == len(edges) or edges[j + 1][:k] != e[:k])
+    labels = {e[:k] for e in edges}
+    import itertools
+
+    missing = next(("".join(t) for t in itertools.product("ACGT", repeat=k) if "".join(t) not in labels), None)
+    if missing is not None:
+        assert g.index_binary_search(["ACGT".index(c) + 1 for c in missing]) == -1
+
+
+def test_valid_only_degrees():
+    seqs = ["ACGTTGCAAGGCTT" * 3, "ACGTTGCAAGGCTA" * 3]
+    packed, offs = pack_reads(seqs)
+    g = O.OGraph.build(packed, offs, 5)
+    for e in range(g.size):
+        outs = g.outgoing(e)
+        if not outs:
+            continue
+        v = g.valid().copy()
+        v[outs[0]] = 0
+        g.set_valid(v)
+        assert outs[0] not in g.outgoing(e)
+        v[outs[0]] = 1
+        g.set_valid(v)
+
+
+def _peel_levels(g, tips):
+    """Level-synchronous peel (the GPU's formulation): remove every valid seed tip with no
+    valid successor, then every valid parent of a removed node whose valid out-degree is
+    now zero, until nothing changes."""
+    v = g.valid().copy()
+    n = g.size
+    # static adjacency (valid-only queries would hide removed nodes' parents)
+    g.set_valid(np.ones(n, dtype=np.uint8))
+    succ = [g.outgoing(x) for x in range(n)]
+    pred = [g.incoming(x) for x in range(n)]
+    g.set_valid(v)
+    frontier = [t for t in range(n) if tips[t] and v[t] and not any(v[y] for y in succ[t])]
+    while frontier:
+        for t in frontier:
+            v[t] = 0
+        nxt = {p for t in frontier for p in pred[t] if v[p] and not any(v[y] for y in succ[p])}
+        frontier = sorted(nxt)
+    return v
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_recursive_reduction_is_order_independent_fixpoint(seed):
+    rng = random.Random(seed)
+    base = rand_seq(rng, 300)
+    seqs = []
+    for _ in range(120):
+        a = rng.randint(0, 260)
+        s = list(base[a:a + rng.randint(20, 40)])
+        for j in range(len(s)):
+            if rng.random() < 0.03:
+                s[j] = rng.choice("ACGT")
+        seqs.append("".join(s))
+    packed, offs = pack_reads(seqs)
+    g = O.OGraph.build(packed, offs, 7)
+    tips = g.collect_tips()
+    g.invalidate_mult_one()
+    g2 = O.OGraph.build(packed, offs, 7)
+    g2.invalidate_mult_one()
+    g.recursive_reduction(tips)
+    v_level = _peel_levels(g2, tips)
+    assert np.array_equal(g.valid(), v_level)
+
+
+def _array_genome(rng, rep_len, spacers, flank=400):
+    R = rand_seq(rng, rep_len)
+    S = [rand_seq(rng, rng.randint(30, 34)) for _ in range(spacers)]
+    arr = R + "".join(s + R for s in S)
+    return rand_seq(rng, flank) + arr + rand_seq(rng, flank), R, S
+
+
+@pytest.mark.parametrize("k", [21, 23])
+def test_known_answer_one_cycle_per_spacer(k):
+    rng = random.Random(k * 7)
+    genome, R, S = _array_genome(rng, 30, 7)
+    # perfect tiling reads, both strands, 60x
+    reads = []
+    for i in range(0, len(genome) - 100 + 1, 5):
+        reads.append(genome[i:i + 100])
+        reads.append(rc(genome[i:i + 100]))
+    packed, offs = pack_reads(reads)
+    g = O.OGraph.build(packed, offs, k)
+    keys, _ = g.arrays()
+    E = k + 1
+    res = g.cycle_finder(threshold_multiplicity=5)
+    assert res["stats"][5] == 2 * len(S)  # both strands
+    # expected cycle edge sets: (k+1)-mers of the circular strings R+Si and their rc
+    expected = set()
+    for sp in S:
+        circ = R + sp
+        ext = circ + circ[:E]
+        expected.add(frozenset(boss_key(ext[i:i + E], k) for i in range(len(circ))))
+        rcc = rc(circ)
+        ext = rcc + rcc[:E]
+        expected.add(frozenset(boss_key(ext[i:i + E], k) for i in range(len(rcc))))
+    got = set()
+    for start, cycles in res["entries"]:
+        for c in cycles:
+            assert c[0] == start
+            assert len(c) == len(set(c))
+            got.add(frozenset(int(keys[x]) for x in c))
+    assert got == expected
+
+
+def test_unordered_set_order_model_matches_libstdcxx(tmp_path):
+    """The GPU FindCycle emulates libstdc++ unordered_set<uint64_t> iteration order for
+    <= 4 elements (13 buckets, identity hash): a new element goes before the first element
+    of its bucket, or to the front when the bucket is empty; erase/copy keep the order."""
+    src = tmp_path / "probe.cpp"
+    src.write_text(r'''
+#include <unordered_set>
+#include <cstdio>
+#include <cstdint>
+int main(){ uint64_t v; int n;
+  while (scanf("%d", &n) == 1) { std::unordered_set<uint64_t> s;
+    for (int i = 0; i < n; ++i) { scanf("%lu", &v); s.insert(v); }
+    std::unordered_set<uint64_t> c = s; for (auto x : c) printf("%lu ", x); printf("\n"); } }''')
+    exe = tmp_path / "probe"
+    subprocess.run(["g++", "-O1", "-std=c++17", str(src), "-o", str(exe)], check=True)
+    rng = random.Random(5)
+    cases = []
+    for t in range(3000):
+        n = rng.randint(1, 4)
+        cases.append([rng.randrange(60) if t % 2 else rng.randrange(1 << 40) for _ in range(n)])
+    inp = "".join(f"{len(c)} " + " ".join(map(str, c)) + "\n" for c in cases)
+    out = subprocess.run([str(exe)], input=inp, capture_output=True, text=True, check=True).stdout.splitlines()
+
+    def model(ins):
+        L = []
+        for x in ins:
+            if x in L:
+                continue
+            pos = next((i for i, y in enumerate(L) if y % 13 == x % 13), 0)
+            L.insert(pos, x)
+        return L
+
+    for c, line in zip(cases, out):
+        assert [int(x) for x in line.split()] == model(c)
+
+
+def test_dls_requires_cycle_within_limit():
+    # a single cycle of length 40 edges through a branching node
+    rng = random.Random(9)
+    loop = rand_seq(rng, 40)
+    tail = rand_seq(rng, 30)
+    genome = tail + loop * 4 + rand_seq(rng, 30)
+    reads = [genome[i:i + 60] for i in range(0, len(genome) - 60 + 1, 2)]
+    reads += [rc(r) for r in reads]
+    packed, offs = pack_reads(reads)
+    g = O.OGraph.build(packed, offs, 9)
+    keys, mult = g.arrays()
+    branching = [e for e in range(g.size) if len(g.incoming(e)) >= 2]
+    assert branching
+    for e in branching:
+        assert g.dls(e, limit=77)          # the 40-edge loop is within the limit
+        assert not g.dls(e, limit=30)      # ... but not within 30
+
+
+GOLDEN = os.path.join(HERE, "golden")
+
+
+@pytest.mark.parametrize("name", sorted(f[:-5] for f in os.listdir(GOLDEN) if f.endswith(".json")))
+def test_golden_regression(name):
+    """Committed oracle outputs (regression pins of the restatement, not reference outputs)."""
+    import mcaat_amd as M
+
+    with open(os.path.join(GOLDEN, name + ".json")) as f:
+        gold = json.load(f)
+    spec = M.SynthSpec(**gold["spec"])
+    packed, offs = M.synth_host(spec)
+    g = O.OGraph.build(packed, offs, gold["k"], threads=2)
+    keys, mult = g.arrays()
+    assert g.size == gold["D"]
+    assert int(np.bitwise_xor.reduce(keys)) == gold["keys_xor"]
+    assert int(mult.astype(np.uint64).sum()) == gold["mult_sum"]
+    res = g.cycle_finder(**gold["params"])
+    assert res["stats"] == gold["stats"]
+    assert res["candidates"] == gold["candidates"]
+    assert res["buckets"] == gold["buckets"]
+    assert [[s, c] for s, c in res["entries"]] == gold["entries"]
+    assert res["map_order"] == gold["map_order"]
