@@ -598,12 +598,12 @@ uint64_t select_flagged(mcaat_ctx *ctx, const uint8_t *flags, uint64_t n, uint64
 }
 
 
-// host visited mirror: a dense bitmap of D bits
+// host visited mirror: only nodes of committed cycles are ever set, so a hash set
 struct HostBits {
-    std::vector<uint64_t> w;
-    explicit HostBits(uint64_t D) : w((D + 63) / 64, 0) {}
-    bool get(uint64_t x) const { return (w[x >> 6] >> (x & 63)) & 1; }
-    void set(uint64_t x) { w[x >> 6] |= 1ULL << (x & 63); }
+    std::unordered_set<uint64_t> s;
+    explicit HostBits(uint64_t) {}
+    bool get(uint64_t x) const { return s.count(x) != 0; }
+    void set(uint64_t x) { s.insert(x); }
 };
 
 }  // namespace

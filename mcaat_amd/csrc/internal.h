@@ -197,6 +197,7 @@ struct CountResult {
     uint64_t n = 0;
 };
 void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out);
+void verbose_mark(mcaat_ctx *ctx, const char *what);
 void sort_counts(mcaat_ctx *ctx, CountResult &c, int k);
 void sdbg_build(mcaat_ctx *ctx, CountResult &c, int k, mcaat_graph *g);
 void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out);

@@ -1,14 +1,27 @@
 // node_counter.hip — exact canonical (k+1)-mer (edge) multiplicity counting on gfx950.
 //
 // Replaces the counting inside MEGAHIT Read2SdbgS2::Run (reference sdbg_build.cpp:171-187,
-// "-m 1": every edge kept). Layout and roofline: DESIGN.md §node_counter.
+// "-m 1": every edge kept). Design and rooflines: DESIGN.md §node_counter.
 //
-// v1 design: one open-addressing table in HBM (keys u64 + counts u32, linear probing).
-// Each lane owns one (k+1)-mer position; the window is a funnel shift of two packed
-// words (coalesced: a wave reads ~40 consecutive bytes per 64 k-mers of a read).
-// Existing keys cost one load + one atomic add; new keys one CAS. The table is sized
-// from the occurrence count and regrown (x4) if the load factor passes 0.7.
+// Every occurrence of a canonical edge has the same canonical minimizer (the m-mer of its
+// window with the smallest hash), so edges are partitioned by minimizer hash and each
+// partition is counted in LDS:
+//   A  k_sk_scatter : reads -> super-k-mers (maximal runs of edges sharing a minimizer),
+//                     written as 16-byte descriptors carrying their bases inline, staged
+//                     in LDS and scattered to 256 L1 buckets (top 8 hash bits).
+//   B  k_l2_hist / k_l2_scan / k_l2_scatter : one LDS-staged radix pass per L1 bucket
+//                     on the next l2_bits hash bits -> 2^(8+l2_bits) fine partitions.
+//   C  k_lds_count  : one workgroup per fine partition; expands its super-k-mers and
+//                     counts canonical edges in an LDS open-addressing table; emits
+//                     (key, count). A partition whose distinct edges overflow the LDS
+//                     table is re-counted by the global-table fallback (k_fallback).
+// Output order is irrelevant: sdbg_build sorts by BOSS key.
 #include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <ctime>
 
 #include "internal.h"
 
@@ -17,12 +30,453 @@ namespace mcaat {
 namespace {
 
 constexpr int kBlock = 256;
+
+// ---- super-k-mer descriptor (16 B) ----------------------------------------------------
+// w0: bases [0,32); w1: bases [32,54) in bits 0..43 | n edges (6 bits) at 44 | 14 hash bits at 50
+constexpr int kDescBases = 54;
+constexpr int kNShift = 44;
+constexpr int kHShift = 50;
+constexpr int kHBits = 14;
+
+struct SkParams {
+    int E;        // edge length k+1
+    int m;        // minimizer length
+    int w;        // m-mers per edge window = E - m + 1
+    int nmax;     // max edges per descriptor = kDescBases - E + 1
+    int l2_bits;  // hash bits after the 8 L1 bits used for fine partitions
+    uint64_t salt;
+};
+
+__device__ __forceinline__ uint64_t desc_window(uint64_t w0, uint64_t w1, int i, int E) {
+    uint64_t v;
+    if (i == 0) v = w0;
+    else if (i < 32) v = (w0 >> (2 * i)) | (w1 << (64 - 2 * i));
+    else v = w1 >> (2 * (i - 32));
+    return v & mask_bits(2 * E);
+}
+
+// 32-bit helpers for m <= 16: reverse 2-bit groups, bijective mixer (lowbias32)
+__device__ __forceinline__ uint32_t rev2_32(uint32_t x) {
+    x = ((x >> 2) & 0x33333333u) | ((x & 0x33333333u) << 2);
+    x = ((x >> 4) & 0x0F0F0F0Fu) | ((x & 0x0F0F0F0Fu) << 4);
+    return __builtin_bswap32(x);
+}
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+__device__ __forceinline__ uint64_t canon_edge(uint64_t lsb, int E) {
+    const uint64_t rc = lsb_rc(lsb, E);
+    return lsb < rc ? lsb : rc;
+}
+
+// ---- A: super-k-mers -----------------------------------------------------------------
+constexpr int kAWaves = 8;
+constexpr int kAThreads = kAWaves * 64;
+constexpr int kItem = 128;               // edge positions per work item
+constexpr int kHB = kItem + 64;          // m-mer hashes per item (w <= 64)
+constexpr int kStage = 3584;             // staged descriptors per workgroup
+constexpr int kFlushAt = kStage - kAWaves * kItem;
+
+struct ItemSrc {
+    const uint64_t *offsets;
+    uint64_t n_reads;
+    uint64_t fixed_len;   // >0: items computed on the fly
+    uint64_t ipr;         // items per read (fixed)
+    const uint64_t *item_base;  // explicit items (variable-length reads)
+    const uint32_t *item_np;
+    uint64_t n_items;
+};
+
+__device__ __forceinline__ void get_item(const ItemSrc &s, int E, uint64_t it, uint64_t &base, int &np) {
+    if (s.fixed_len) {
+        const uint64_t r = it / s.ipr, c = it - r * s.ipr;
+        const uint64_t npos = s.fixed_len - E + 1;
+        base = r * s.fixed_len + c * kItem;
+        const uint64_t rem = npos - c * kItem;
+        np = (int)(rem < (uint64_t)kItem ? rem : kItem);
+    } else {
+        base = s.item_base[it];
+        np = (int)s.item_np[it];
+    }
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+constexpr uint32_t kMini = 1024;  // descriptors reserved per (workgroup, L1 bucket) grab
+
+__global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__restrict__ packed, ItemSrc src,
+                                                          SkParams P, uint4 *__restrict__ l1_data,
+                                                          const uint64_t *__restrict__ l1_base,
+                                                          const uint64_t *__restrict__ l1_cap,
+                                                          unsigned long long *l1_cursor) {
+    __shared__ uint4 stage[kStage];
+    __shared__ uint8_t stage_l1[kStage];
+    __shared__ uint32_t hb[kAWaves][kHB];
+    __shared__ uint32_t hist[256];
+    __shared__ unsigned long long rpos[256];  // next free slot of this workgroup's reservation
+    __shared__ uint32_t rleft[256];           // slots left in it
+    __shared__ uint32_t n_stage;
+
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (threadIdx.x == 0) n_stage = 0;
+    for (int b = threadIdx.x; b < 256; b += kAThreads) rleft[b] = 0;
+    __syncthreads();
+
+    // write one descriptor of bucket b; reservations are grabbed kMini slots at a time, so
+    // the 256 bucket cursors see ~1/kMini of the traffic
+    auto put = [&](int b, uint64_t pos, const uint4 &d) {
+        if (pos < l1_cap[b]) l1_data[l1_base[b] + pos] = d;
+    };
+
+    auto flush = [&]() {
+        const uint32_t ns = n_stage;
+        for (int i = threadIdx.x; i < 256; i += kAThreads) hist[i] = 0;
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < ns; i += kAThreads) atomicAdd(&hist[stage_l1[i]], 1u);
+        __syncthreads();
+        // thread b tops up bucket b's reservation; ranks below rleft go to the current
+        // reservation, the rest to a fresh contiguous grab (the old remainder is zero-filled)
+        for (int b = threadIdx.x; b < 256; b += kAThreads) {
+            const uint32_t need = hist[b];
+            if (need > rleft[b]) {
+                for (uint32_t z = 0; z < rleft[b]; ++z) put(b, rpos[b] + z, make_uint4(0, 0, 0, 0));
+                const uint32_t grab = ((need + kMini - 1) / kMini) * kMini;
+                rpos[b] = atomicAdd(&l1_cursor[b], (unsigned long long)grab);
+                rleft[b] = grab;
+            }
+            hist[b] = 0;
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < ns; i += kAThreads) {
+            const int b = stage_l1[i];
+            put(b, rpos[b] + atomicAdd(&hist[b], 1u), stage[i]);
+        }
+        __syncthreads();
+        for (int b = threadIdx.x; b < 256; b += kAThreads) {
+            rpos[b] += hist[b];
+            rleft[b] -= hist[b];
+        }
+        if (threadIdx.x == 0) n_stage = 0;
+        __syncthreads();
+    };
+
+    const uint64_t n_items = src.fixed_len ? src.n_reads * src.ipr : src.n_items;
+    const uint32_t mmask = (uint32_t)mask_bits(2 * P.m);
+    const int rsh = 32 - 2 * P.m;
+    const uint32_t salt32 = (uint32_t)P.salt;
+    for (uint64_t it0 = (uint64_t)blockIdx.x * kAWaves; it0 < n_items; it0 += (uint64_t)gridDim.x * kAWaves) {
+        const uint64_t it = it0 + wave;
+        if (it < n_items) {
+            uint64_t base;
+            int np;
+            get_item(src, P.E, it, base, np);
+            const int nm = np + P.w - 1;
+            // canonical m-mer (m <= 16, 32 bits) -> bijective 32-bit hash; the minimizer is
+            // the canonical m-mer of smallest hash (a function of the window's m-mer set,
+            // so an edge and its reverse complement get the same one)
+            for (int j = lane; j < nm; j += 64) {
+                const uint32_t mf = (uint32_t)window_at(packed, base + j, P.m);
+                const uint32_t mr = (rev2_32(mf) >> rsh) ^ mmask;
+                hb[wave][j] = mix32((mf < mr ? mf : mr) ^ salt32);
+            }
+            wave_sync_lds();
+            uint64_t hm[2];
+            bool st[2];
+            unsigned long long msk[2];
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const int i = lane + 64 * t;
+                uint32_t h = ~0u;
+                if (i < np)
+                    for (int q = 0; q < P.w; ++q) h = min(h, hb[wave][i + q]);
+                hm[t] = h;
+            }
+            wave_sync_lds();
+            // segment starts: position 0, or minimizer hash differs from the previous position
+            const uint64_t last0 = __shfl(hm[0], 63);
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const int i = lane + 64 * t;
+                uint64_t prev = __shfl_up(hm[t], 1);
+                if (lane == 0) prev = (t == 0) ? (hm[0] ^ 1) : last0;
+                st[t] = (i < np) && (i == 0 || hm[t] != prev);
+                msk[t] = __ballot(st[t]);
+            }
+            // pieces emitted by each segment start (segments longer than nmax are split)
+            int pieces = 0;
+            int seg_len[2] = {0, 0};
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const int i = lane + 64 * t;
+                if (st[t]) {
+                    int nxt = np;
+                    const int j = i + 1;
+                    if (j < 64) {
+                        const unsigned long long rest = msk[0] & (~0ULL << j);
+                        if (rest) nxt = __ffsll(rest) - 1;
+                        else if (msk[1]) nxt = 64 + __ffsll(msk[1]) - 1;
+                    } else if (j < 128) {
+                        const unsigned long long rest = msk[1] & (~0ULL << (j - 64));
+                        if (rest) nxt = 64 + __ffsll(rest) - 1;
+                    }
+                    if (nxt > np) nxt = np;
+                    seg_len[t] = nxt - i;
+                    pieces += (seg_len[t] + P.nmax - 1) / P.nmax;
+                }
+            }
+            int incl = pieces;
+            for (int o = 1; o < 64; o <<= 1) {
+                const int v = __shfl_up(incl, o);
+                if (lane >= o) incl += v;
+            }
+            const int total = __shfl(incl, 63);
+            uint32_t wbase = 0;
+            if (lane == 0 && total) wbase = atomicAdd(&n_stage, (uint32_t)total);
+            wbase = __shfl(wbase, 0);
+            uint32_t pos = wbase + incl - pieces;
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                if (!st[t]) continue;
+                const int i = lane + 64 * t;
+                // the minimum hash is biased towards 0: partition by a re-hash of it (a
+                // bijection of the minimizer), whose bits are uniform
+                const uint64_t h = mix64(hm[t] ^ 0x7061727469746eULL);
+                const uint32_t l1 = (uint32_t)(h >> 56);
+                const uint64_t h14 = (h >> (56 - kHBits)) & ((1u << kHBits) - 1);
+                for (int off = 0; off < seg_len[t]; off += P.nmax) {
+                    const int n = min(P.nmax, seg_len[t] - off);
+                    const uint64_t s0 = base + i + off;
+                    const uint64_t w0 = window_at(packed, s0, 32);
+                    uint64_t w1 = window_at(packed, s0 + 32, 22);
+                    w1 |= ((uint64_t)n << kNShift) | (h14 << kHShift);
+                    stage[pos] = make_uint4((unsigned)w0, (unsigned)(w0 >> 32), (unsigned)w1, (unsigned)(w1 >> 32));
+                    stage_l1[pos] = (uint8_t)l1;
+                    ++pos;
+                }
+            }
+        }
+        __syncthreads();
+        if (n_stage > (uint32_t)kFlushAt) flush();
+    }
+    __syncthreads();
+    if (n_stage) flush();
+    // zero-fill what is left of this workgroup's reservations (n = 0 descriptors are inert)
+    for (int b = 0; b < 256; ++b)
+        for (uint32_t z = threadIdx.x; z < rleft[b]; z += kAThreads) put(b, rpos[b] + z, make_uint4(0, 0, 0, 0));
+}
+
+// ---- B: radix pass on the next l2_bits hash bits, per L1 bucket -----------------------------
+// k_l2_hist adds each workgroup's LDS histogram into the per-(bucket, sub) totals; after an
+// exclusive scan those are the fine-partition bases, and k_l2_scatter reserves space per
+// (workgroup, sub) with one atomic on the fine cursor and ranks inside the workgroup in LDS.
+constexpr int kBThreads = 1024;
+constexpr uint32_t kChunk = 65536;
+
+__device__ __forceinline__ uint32_t desc_sub(const uint4 &d, int l2_bits) {
+    return (d.w >> (kHShift - 32)) >> (kHBits - l2_bits);
+}
+__device__ __forceinline__ bool desc_live(const uint4 &d) { return ((d.w >> (kNShift - 32)) & 63) != 0; }
+
+__global__ void __launch_bounds__(kBThreads) k_l2_hist(const uint4 *__restrict__ data, const uint64_t *chunk_start,
+                                                       const uint32_t *chunk_len, const uint32_t *chunk_bucket,
+                                                       int l2_bits, unsigned long long *tot) {
+    extern __shared__ uint32_t lh[];
+    const uint32_t S = 1u << l2_bits;
+    const uint64_t c = blockIdx.x;
+    for (uint32_t i = threadIdx.x; i < S; i += kBThreads) lh[i] = 0;
+    __syncthreads();
+    const uint64_t s0 = chunk_start[c];
+    const uint32_t n = chunk_len[c];
+    for (uint32_t i = threadIdx.x; i < n; i += kBThreads) {
+        const uint4 d = data[s0 + i];
+        if (desc_live(d)) atomicAdd(&lh[desc_sub(d, l2_bits)], 1u);
+    }
+    __syncthreads();
+    const uint64_t fb = (uint64_t)chunk_bucket[c] * S;
+    for (uint32_t i = threadIdx.x; i < S; i += kBThreads)
+        if (lh[i]) atomicAdd(&tot[fb + i], (unsigned long long)lh[i]);
+}
+
+__global__ void __launch_bounds__(kBThreads) k_l2_scatter(const uint4 *__restrict__ data, const uint64_t *chunk_start,
+                                                          const uint32_t *chunk_len, const uint32_t *chunk_bucket,
+                                                          int l2_bits, unsigned long long *cursor,
+                                                          uint4 *__restrict__ out) {
+    extern __shared__ unsigned long long lb[];  // [S] bases, then [S] u32 counters
+    const uint32_t S = 1u << l2_bits;
+    uint32_t *lc = (uint32_t *)(lb + S);
+    const uint64_t c = blockIdx.x;
+    for (uint32_t i = threadIdx.x; i < S; i += kBThreads) lc[i] = 0;
+    __syncthreads();
+    const uint64_t s0 = chunk_start[c];
+    const uint32_t n = chunk_len[c];
+    for (uint32_t i = threadIdx.x; i < n; i += kBThreads) {
+        const uint4 d = data[s0 + i];
+        if (desc_live(d)) atomicAdd(&lc[desc_sub(d, l2_bits)], 1u);
+    }
+    __syncthreads();
+    const uint64_t fb = (uint64_t)chunk_bucket[c] * S;
+    for (uint32_t i = threadIdx.x; i < S; i += kBThreads) {
+        lb[i] = lc[i] ? atomicAdd(&cursor[fb + i], (unsigned long long)lc[i]) : 0;
+        lc[i] = 0;
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += kBThreads) {
+        const uint4 d = data[s0 + i];
+        if (!desc_live(d)) continue;
+        const uint32_t s = desc_sub(d, l2_bits);
+        out[lb[s] + atomicAdd(&lc[s], 1u)] = d;
+    }
+}
+
+// ---- C: per-partition LDS counting ----------------------------------------------------
+constexpr int kCThreads = 512;
+constexpr int kCap = 4096;                          // LDS slots per workgroup
+constexpr int kCapMax = kCap * 85 / 100 - kCThreads;  // distinct edges before giving up
+
+__global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict__ data,
+                                                         const uint64_t *__restrict__ fine_base, uint64_t F, int E,
+                                                         uint64_t *out_keys, uint32_t *out_cnt, uint64_t out_cap,
+                                                         unsigned long long *out_cursor, uint32_t *ovf_list,
+                                                         unsigned long long *ovf_n) {
+    __shared__ unsigned long long keys[kCap];
+    __shared__ uint32_t cnt[kCap];
+    __shared__ uint32_t n_distinct;
+    __shared__ int ovf;
+    __shared__ uint32_t wsum[kCThreads / 64];
+    __shared__ unsigned long long obase;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+
+    for (uint64_t p = blockIdx.x; p < F; p += gridDim.x) {
+        for (int i = threadIdx.x; i < kCap; i += kCThreads) {
+            keys[i] = kEmpty;
+            cnt[i] = 0;
+        }
+        if (threadIdx.x == 0) {
+            n_distinct = 0;
+            ovf = 0;
+        }
+        __syncthreads();
+        const uint64_t beg = fine_base[p], end = fine_base[p + 1];
+        // each wave takes 64 descriptors at a time and spreads their edges over its lanes
+        for (uint64_t d0 = beg + (uint64_t)wave * 64; d0 < end; d0 += kCThreads) {
+            if (*(volatile int *)&ovf) break;
+            const uint64_t d = d0 + lane;
+            uint64_t w0 = 0, w1 = 0;
+            int n = 0;
+            if (d < end) {
+                const uint4 q = data[d];
+                w0 = (uint64_t)q.x | ((uint64_t)q.y << 32);
+                w1 = (uint64_t)q.z | ((uint64_t)q.w << 32);
+                n = (int)((w1 >> kNShift) & 63);
+            }
+            int incl = n;
+            for (int o = 1; o < 64; o <<= 1) {
+                const int v = __shfl_up(incl, o);
+                if (lane >= o) incl += v;
+            }
+            const int total = __shfl(incl, 63);
+            // all 64 lanes stay active through the shuffles (an inactive source lane reads 0)
+            for (int b0 = 0; b0 < total; b0 += 64) {
+                // checked every 64 edges (wave-uniform): after the flag is raised each wave
+                // inserts at most 64 more keys, so the table (kCapMax + kCThreads < kCap)
+                // always keeps a free slot and every probe terminates
+                if (*(volatile int *)&ovf) break;
+                const int idx = b0 + lane;
+                // owner lane: first lane whose inclusive prefix exceeds idx (6 uniform steps)
+                int lo = 0;
+#pragma unroll
+                for (int step = 32; step > 0; step >>= 1)
+                    if (__shfl(incl, lo + step - 1) <= idx) lo += step;
+                const int src = lo > 63 ? 63 : lo;
+                const int i = idx - (__shfl(incl, src) - __shfl(n, src));
+                const uint64_t a0 = __shfl(w0, src), a1 = __shfl(w1, src);
+                if (idx >= total) continue;
+                const uint64_t c = canon_edge(desc_window(a0, a1, i, E), E);
+                uint32_t h = (uint32_t)(mix64(c) >> 40) & (kCap - 1);
+                for (int probe = 0;; ++probe) {
+                    if (probe >= kCap) {  // defensive: never spin on a full table
+                        ovf = 1;
+                        break;
+                    }
+                    const unsigned long long cur = keys[h];
+                    if (cur == c) {
+                        atomicAdd(&cnt[h], 1u);
+                        break;
+                    }
+                    if (cur == kEmpty) {
+                        const unsigned long long prev = atomicCAS(&keys[h], kEmpty, (unsigned long long)c);
+                        if (prev == kEmpty) {
+                            atomicAdd(&cnt[h], 1u);
+                            if (atomicAdd(&n_distinct, 1u) + 1 > (uint32_t)kCapMax) ovf = 1;
+                            break;
+                        }
+                        if (prev == c) {
+                            atomicAdd(&cnt[h], 1u);
+                            break;
+                        }
+                    }
+                    h = (h + 1) & (kCap - 1);
+                }
+            }
+        }
+        __syncthreads();
+        if (ovf) {
+            if (threadIdx.x == 0) ovf_list[atomicAdd(ovf_n, 1ull)] = (uint32_t)p;
+            __syncthreads();
+            continue;
+        }
+        // block-wide compaction of the occupied slots
+        constexpr int per = kCap / kCThreads;
+        int mine = 0;
+        for (int j = 0; j < per; ++j) mine += keys[threadIdx.x * per + j] != kEmpty;
+        int incl = mine;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int v = __shfl_up(incl, o);
+            if (lane >= o) incl += v;
+        }
+        if (lane == 63) wsum[wave] = incl;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t t = 0;
+            for (int w = 0; w < kCThreads / 64; ++w) {
+                const uint32_t v = wsum[w];
+                wsum[w] = t;
+                t += v;
+            }
+            obase = t ? atomicAdd(out_cursor, (unsigned long long)t) : 0;
+        }
+        __syncthreads();
+        uint64_t o = obase + wsum[wave] + incl - mine;
+        for (int j = 0; j < per; ++j) {
+            const int s = threadIdx.x * per + j;
+            const unsigned long long kk = keys[s];
+            if (kk != kEmpty) {
+                if (o < out_cap) {
+                    out_keys[o] = kk;
+                    out_cnt[o] = cnt[s];
+                }
+                ++o;
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---- fallback: global open-addressing table for overflowing partitions ------------------
 constexpr uint32_t kMaxProbe = 1u << 14;
 
-// one 16-byte slot: key+1 (0 = empty, so a plain memset clears the table) and count,
-// in the same cache line so a hit costs one line
 struct __attribute__((aligned(16))) Slot {
-    unsigned long long key1;
+    unsigned long long key1;  // key + 1 (0 = empty)
     unsigned int cnt;
     unsigned int pad;
 };
@@ -50,119 +504,334 @@ __device__ __forceinline__ void table_insert(uint64_t key, Slot *tab, uint64_t m
     atomicExch(overflow, 1);
 }
 
-// fixed-length reads: thread i -> (read i / npos, position i % npos)
-__global__ void __launch_bounds__(kBlock) k_count_fixed(const uint64_t *__restrict__ packed, uint64_t n_reads,
-                                                        uint64_t L, int E, Slot *tab, uint64_t mask,
-                                                        unsigned long long *n_new, int *overflow) {
-    const uint64_t npos = L - E + 1;
-    const uint64_t total = n_reads * npos;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
-        const uint64_t r = i / npos, p = i - r * npos;
-        const uint64_t lsb = window_at(packed, r * L + p, E);
-        const uint64_t rc = lsb_rc(lsb, E);
-        table_insert(lsb < rc ? lsb : rc, tab, mask, n_new, overflow);
+__global__ void __launch_bounds__(kBlock) k_part_occ(const uint4 *data, const uint64_t *fine_base,
+                                                     const uint32_t *parts, uint64_t np, uint64_t *occ) {
+    for (uint64_t q = blockIdx.x; q < np; q += gridDim.x) {
+        const uint64_t p = parts[q];
+        unsigned long long acc = 0;
+        for (uint64_t d = fine_base[p] + threadIdx.x; d < fine_base[p + 1]; d += blockDim.x)
+            acc += (data[d].w >> (kNShift - 32)) & 63;
+        __shared__ unsigned long long s;
+        if (threadIdx.x == 0) s = 0;
+        __syncthreads();
+        block_add(&s, acc);
+        __syncthreads();
+        if (threadIdx.x == 0) occ[q] = s;
+        __syncthreads();
     }
 }
 
-// variable-length reads: one wave per read, lanes stride over positions
-__global__ void __launch_bounds__(kBlock) k_count_var(const uint64_t *__restrict__ packed,
-                                                      const uint64_t *__restrict__ offsets, uint64_t n_reads, int E,
-                                                      Slot *tab, uint64_t mask, unsigned long long *n_new,
-                                                      int *overflow) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t r = wave; r < n_reads; r += nwaves) {
-        const uint64_t a = offsets[r], b = offsets[r + 1];
-        if (b - a < (uint64_t)E) continue;
-        const uint64_t npos = b - a - E + 1;
-        for (uint64_t p = lane; p < npos; p += 64) {
-            const uint64_t lsb = window_at(packed, a + p, E);
-            const uint64_t rc = lsb_rc(lsb, E);
-            table_insert(lsb < rc ? lsb : rc, tab, mask, n_new, overflow);
+__global__ void __launch_bounds__(kBlock) k_fallback(const uint4 *data, const uint64_t *fine_base,
+                                                     const uint32_t *parts, uint64_t np, int E, Slot *tab,
+                                                     uint64_t mask, unsigned long long *n_new, int *overflow) {
+    for (uint64_t q = blockIdx.x; q < np; q += gridDim.x) {
+        const uint64_t p = parts[q];
+        for (uint64_t d = fine_base[p] + threadIdx.x; d < fine_base[p + 1]; d += blockDim.x) {
+            const uint4 x = data[d];
+            const uint64_t w0 = (uint64_t)x.x | ((uint64_t)x.y << 32);
+            const uint64_t w1 = (uint64_t)x.z | ((uint64_t)x.w << 32);
+            const int n = (int)((w1 >> kNShift) & 63);
+            for (int i = 0; i < n; ++i) table_insert(canon_edge(desc_window(w0, w1, i, E), E), tab, mask, n_new, overflow);
         }
     }
 }
 
-struct Occupied {
-    __device__ __forceinline__ bool operator()(const Slot &s) const { return s.key1 != 0; }
-};
-
-__global__ void __launch_bounds__(kBlock) k_split(const Slot *in, uint64_t n, uint64_t *keys, uint32_t *cnt) {
+__global__ void __launch_bounds__(kBlock) k_fallback_emit(const Slot *tab, uint64_t cap, uint64_t *out_keys,
+                                                          uint32_t *out_cnt, uint64_t out_cap,
+                                                          unsigned long long *out_cursor) {
+    const int lane = threadIdx.x & 63;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const Slot s = in[i];
-        keys[i] = s.key1 - 1;
-        cnt[i] = s.cnt;
+    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < cap; base += stride) {
+        const uint64_t i = base + threadIdx.x;
+        const bool occ = i < cap && tab[i].key1 != 0;
+        const unsigned long long m = __ballot(occ);
+        unsigned long long off = 0;
+        if (lane == 0 && m) off = atomicAdd(out_cursor, (unsigned long long)__popcll(m));
+        off = __shfl(off, 0);
+        if (occ) {
+            const uint64_t o = off + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+            if (o < out_cap) {
+                out_keys[o] = tab[i].key1 - 1;
+                out_cnt[o] = tab[i].cnt;
+            }
+        }
     }
+}
+
+__global__ void k_items_count(const uint64_t *offsets, uint64_t n_reads, int E, uint64_t *cnt) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_reads; r += stride) {
+        const uint64_t len = offsets[r + 1] - offsets[r];
+        cnt[r] = len >= (uint64_t)E ? (len - E + 1 + kItem - 1) / kItem : 0;
+    }
+}
+
+__global__ void k_items_fill(const uint64_t *offsets, uint64_t n_reads, int E, const uint64_t *start,
+                             uint64_t *item_base, uint32_t *item_np) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n_reads; r += stride) {
+        const uint64_t len = offsets[r + 1] - offsets[r];
+        if (len < (uint64_t)E) continue;
+        const uint64_t npos = len - E + 1;
+        uint64_t s = start[r];
+        for (uint64_t c = 0; c * kItem < npos; ++c, ++s) {
+            item_base[s] = offsets[r] + c * kItem;
+            const uint64_t rem = npos - c * kItem;
+            item_np[s] = (uint32_t)(rem < (uint64_t)kItem ? rem : kItem);
+        }
+    }
+}
+
+template <class T>
+void exclusive_scan(mcaat_ctx *ctx, const T *in, T *out, uint64_t n) {
+    size_t tmp = 0;
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, (size_t)n, ctx->stream));
+    DevBuf<uint8_t> t(tmp);
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(t.p, tmp, in, out, (size_t)n, ctx->stream));
 }
 
 }  // namespace
 
+// MCAAT_VERBOSE=1: host wall-clock marks of the sub-stages on stderr (stream-synchronised)
+void verbose_mark(mcaat_ctx *ctx, const char *what) {
+    static const bool on = getenv("MCAAT_VERBOSE") && getenv("MCAAT_VERBOSE")[0] == '1';
+    static double last = 0;
+    if (!on) return;
+    (void)hipStreamSynchronize(ctx->stream);
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    const double now = ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
+    fprintf(stderr, "[mcaat] %-28s %10.2f ms\n", what, last ? now - last : 0.0);
+    last = now;
+}
+
 void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out) {
+    verbose_mark(ctx, "node_counter.begin");
     const int E = k + 1;
     hipStream_t st = ctx->stream;
-    uint64_t n_occ = 0;
-    if (r->fixed_len) {
-        n_occ = r->fixed_len >= (uint64_t)E ? r->n_reads * (r->fixed_len - E + 1) : 0;
-    } else {
-        std::vector<uint64_t> off(r->n_reads + 1);
-        HIP_OK(hipMemcpyAsync(off.data(), r->offsets.p, 8 * (r->n_reads + 1), hipMemcpyDeviceToHost, st));
-        HIP_OK(hipStreamSynchronize(st));
-        for (uint64_t i = 0; i < r->n_reads; ++i)
-            if (off[i + 1] - off[i] >= (uint64_t)E) n_occ += off[i + 1] - off[i] - E + 1;
-    }
-    uint64_t cap = next_pow2(n_occ / 8 + 1);
-    if (cap < (1u << 16)) cap = 1u << 16;
-    if (cap > (1ull << 31)) cap = 1ull << 31;
+    SkParams P;
+    P.E = E;
+    // long minimizers (near-unique per genome locus) keep the per-partition load uniform;
+    // short ones (m=11) concentrate thousands of distinct edges on small-hash m-mers
+    P.m = std::max(3, std::min(16, E - 8));  // <= 16: the m-mer machinery is 32-bit
+    if (P.m > E) P.m = E;
+    P.w = E - P.m + 1;
+    P.nmax = kDescBases - E + 1;
+    P.salt = 0x6d696e696d697aULL;
 
-    DevBuf<unsigned long long> dcnt(2);
-    DevBuf<int> dover(1);
-    for (;;) {
-        DevBuf<Slot> tab(cap);
-        HIP_OK(hipMemsetAsync(tab.p, 0, tab.bytes(), st));
-        HIP_OK(hipMemsetAsync(dcnt.p, 0, dcnt.bytes(), st));
-        HIP_OK(hipMemsetAsync(dover.p, 0, dover.bytes(), st));
+    // work items (<= kItem edge positions each)
+    ItemSrc src{};
+    src.offsets = r->offsets.p;
+    src.n_reads = r->n_reads;
+    DevBuf<uint64_t> item_base;
+    DevBuf<uint32_t> item_np;
+    uint64_t n_occ = 0, n_items = 0;
+    if (r->fixed_len) {
+        src.fixed_len = r->fixed_len;
+        const uint64_t npos = r->fixed_len >= (uint64_t)E ? r->fixed_len - E + 1 : 0;
+        src.ipr = (npos + kItem - 1) / kItem;
+        n_items = r->n_reads * src.ipr;
+        n_occ = r->n_reads * npos;
+        if (!npos) {
+            src.fixed_len = 0;
+            src.n_items = 0;
+        }
+    } else if (r->n_reads) {
+        DevBuf<uint64_t> cnt(r->n_reads + 1), start(r->n_reads + 1);
+        HIP_OK(hipMemsetAsync(cnt.p, 0, cnt.bytes(), st));
+        hipLaunchKernelGGL(k_items_count, dim3(grid_for(r->n_reads, kBlock)), dim3(kBlock), 0, st, r->offsets.p,
+                           r->n_reads, E, cnt.p);
+        LAUNCH_OK();
+        exclusive_scan(ctx, cnt.p, start.p, r->n_reads + 1);
+        HIP_OK(hipMemcpyAsync(&n_items, start.p + r->n_reads, 8, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        item_base.alloc(n_items);
+        item_np.alloc(n_items);
+        hipLaunchKernelGGL(k_items_fill, dim3(grid_for(r->n_reads, kBlock)), dim3(kBlock), 0, st, r->offsets.p,
+                           r->n_reads, E, start.p, item_base.p, item_np.p);
+        LAUNCH_OK();
+        std::vector<uint32_t> hn(n_items);
+        HIP_OK(hipMemcpyAsync(hn.data(), item_np.p, 4 * n_items, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        for (uint32_t v : hn) n_occ += v;
+        src.item_base = item_base.p;
+        src.item_np = item_np.p;
+        src.n_items = n_items;
+    }
+    out.n = 0;
+    if (n_occ == 0) {
+        out.keys.alloc(1);
+        out.counts.alloc(1);
+        return;
+    }
+
+    // fine partitions: ~64K edge occurrences each, 8 L1 bits + l2_bits
+    int fine_bits = 0;
+    while ((1ULL << (fine_bits + 1)) * 65536ULL <= n_occ) ++fine_bits;
+    fine_bits = std::max(8, std::min(20, fine_bits));  // l2_bits <= 12: 48 KB of LDS in k_l2_scatter
+    P.l2_bits = fine_bits - 8;
+    const uint32_t S = 1u << P.l2_bits;
+    const uint64_t F = 256ull * S;
+
+    // ---- A ----
+    // expected descriptors: density 2/(w+1) per edge + one per item, with headroom
+    const double dens = 2.0 / (P.w + 1);
+    uint64_t est = (uint64_t)(1.08 * (dens * (double)n_occ + (double)n_items)) + 4096;
+    std::vector<uint64_t> cap(256), base(257);
+    // + one partially used reservation per (workgroup, bucket)
+    for (int b = 0; b < 256; ++b) cap[b] = est / 256 + 512ull * kMini;
+    DevBuf<uint64_t> dcap(256), dbase(257);
+    DevBuf<unsigned long long> dcur(256);
+    DevBuf<uint4> l1;
+    std::vector<unsigned long long> tot(256);
+    for (int attempt = 0;; ++attempt) {
+        base[0] = 0;
+        for (int b = 0; b < 256; ++b) base[b + 1] = base[b] + cap[b];
+        l1.alloc(base[256]);
+        HIP_OK(hipMemcpyAsync(dcap.p, cap.data(), 8 * 256, hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemcpyAsync(dbase.p, base.data(), 8 * 257, hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemsetAsync(dcur.p, 0, dcur.bytes(), st));
         {
-            // algorithmic bytes per launch: 2-bit reads once + 16 B per occurrence
-            KernelTimer kt(ctx, "node_counter", 0.25 * (double)r->n_bases + 16.0 * (double)n_occ);
-            if (r->fixed_len) {
-                hipLaunchKernelGGL(k_count_fixed, dim3(grid_for(n_occ, kBlock, 256 * 64)), dim3(kBlock), 0, st,
-                                   r->packed.p, r->n_reads, r->fixed_len, E, tab.p, cap - 1, dcnt.p, dover.p);
-            } else {
-                hipLaunchKernelGGL(k_count_var, dim3(grid_for(r->n_reads * 64, kBlock, 256 * 64)), dim3(kBlock), 0,
-                                   st, r->packed.p, r->offsets.p, r->n_reads, E, tab.p, cap - 1, dcnt.p, dover.p);
-            }
+            KernelTimer kt(ctx, "sk_scatter", 0.25 * (double)r->n_bases + 16.0 * (double)est / 1.25);
+            hipLaunchKernelGGL(k_sk_scatter, dim3(512), dim3(kAThreads), 0, st, r->packed.p, src, P, l1.p, dbase.p,
+                               dcap.p, dcur.p);
             LAUNCH_OK();
             kt.stop();
         }
-        unsigned long long n_new = 0;
-        int over = 0;
-        HIP_OK(hipMemcpyAsync(&n_new, dcnt.p, 8, hipMemcpyDeviceToHost, st));
-        HIP_OK(hipMemcpyAsync(&over, dover.p, 4, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipMemcpyAsync(tot.data(), dcur.p, 8 * 256, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
-        if (over || n_new > cap / 10 * 7) {
-            if (cap >= (1ull << 34)) throw Error(MCAAT_E_CAPACITY, "node_counter: hash table cannot grow further");
-            cap <<= 2;
-            continue;
+        bool ok = true;
+        for (int b = 0; b < 256; ++b)
+            if (tot[b] > cap[b]) ok = false;
+        if (ok) break;
+        if (attempt > 0) throw Error(MCAAT_E_CAPACITY, "node_counter: L1 bucket sizing failed");
+        for (int b = 0; b < 256; ++b) cap[b] = tot[b] + 1;  // exact on the second run (cursors count every grab)
+    }
+    uint64_t n_desc = 0;
+    for (int b = 0; b < 256; ++b) n_desc += tot[b];
+    verbose_mark(ctx, "node_counter.A");
+
+    // ---- B ----
+    std::vector<uint64_t> cstart;
+    std::vector<uint32_t> clen, cbucket;
+    for (int b = 0; b < 256; ++b)
+        for (uint64_t o = 0; o < tot[b]; o += kChunk) {
+            cstart.push_back(base[b] + o);
+            clen.push_back((uint32_t)std::min<uint64_t>(kChunk, tot[b] - o));
+            cbucket.push_back((uint32_t)b);
         }
-        DevBuf<Slot> packed_slots(n_new);
-        size_t tmp = 0;
-        HIP_OK(hipcub::DeviceSelect::If(nullptr, tmp, tab.p, packed_slots.p, dcnt.p, (size_t)cap, Occupied(), st));
+    const uint64_t nch = cstart.size();
+    DevBuf<uint64_t> dcs(nch), dfine(F + 1);
+    DevBuf<unsigned long long> dtot(F + 1), dcursor(F + 1);
+    DevBuf<uint32_t> dcl(nch), dcb(nch);
+    HIP_OK(hipMemcpyAsync(dcs.p, cstart.data(), 8 * nch, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(dcl.p, clen.data(), 4 * nch, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(dcb.p, cbucket.data(), 4 * nch, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemsetAsync(dtot.p, 0, dtot.bytes(), st));
+    uint64_t n_live = 0;
+    DevBuf<uint4> fine;
+    {
+        KernelTimer kt(ctx, "l2_partition", 3.0 * 16.0 * (double)n_desc);
+        if (nch) {
+            hipLaunchKernelGGL(k_l2_hist, dim3((unsigned)nch), dim3(kBThreads), 4 * S, st, l1.p, dcs.p, dcl.p, dcb.p,
+                               P.l2_bits, dtot.p);
+            LAUNCH_OK();
+        }
+        exclusive_scan(ctx, (const uint64_t *)dtot.p, dfine.p, F + 1);
+        HIP_OK(hipMemcpyAsync(&n_live, dfine.p + F, 8, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipMemcpyAsync(dcursor.p, dfine.p, 8 * (F + 1), hipMemcpyDeviceToDevice, st));
+        HIP_OK(hipStreamSynchronize(st));
+        fine.alloc(n_live);
+        if (nch) {
+            hipLaunchKernelGGL(k_l2_scatter, dim3((unsigned)nch), dim3(kBThreads), 12 * S, st, l1.p, dcs.p, dcl.p,
+                               dcb.p, P.l2_bits, dcursor.p, fine.p);
+            LAUNCH_OK();
+        }
+        kt.stop();
+    }
+    l1.release();
+    n_desc = n_live;
+    verbose_mark(ctx, "node_counter.B");
+
+    // ---- C ----
+    uint64_t out_cap = std::max<uint64_t>(n_occ / 32, 1u << 20);
+    DevBuf<unsigned long long> dcnt(4);
+    DevBuf<uint32_t> ovf_list(F);
+    for (int attempt = 0;; ++attempt) {
+        out.keys.alloc(out_cap);
+        out.counts.alloc(out_cap);
+        HIP_OK(hipMemsetAsync(dcnt.p, 0, dcnt.bytes(), st));
         {
-            DevBuf<uint8_t> t(tmp);
-            HIP_OK(hipcub::DeviceSelect::If(t.p, tmp, tab.p, packed_slots.p, dcnt.p, (size_t)cap, Occupied(), st));
+            KernelTimer kt(ctx, "lds_count", 16.0 * (double)n_desc);
+            hipLaunchKernelGGL(k_lds_count, dim3((unsigned)std::min<uint64_t>(F, 256 * 3 * 4)), dim3(kCThreads), 0, st,
+                               fine.p, dfine.p, F, E, out.keys.p, out.counts.p, out_cap, dcnt.p, ovf_list.p,
+                               dcnt.p + 1);
+            LAUNCH_OK();
+            kt.stop();
         }
-        tab.release();
-        out.n = n_new;
-        out.keys.alloc(n_new);
-        out.counts.alloc(n_new);
-        hipLaunchKernelGGL(k_split, dim3(grid_for(n_new, kBlock)), dim3(kBlock), 0, st, packed_slots.p, n_new,
-                           out.keys.p, out.counts.p);
-        LAUNCH_OK();
+        unsigned long long hc[2];
+        HIP_OK(hipMemcpyAsync(hc, dcnt.p, 16, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
-        break;
+        uint64_t n_out = hc[0];
+        const uint64_t n_ovf = hc[1];
+        // algorithmic bytes of the LDS count: descriptors read once + (key, count) written once
+        ctx->kstats["lds_count"].bytes_per_launch = 16.0 * (double)n_desc + 12.0 * (double)n_out;
+        ctx->kstats["lds_count_overflow_partitions"].launches = n_ovf;
+        if (n_ovf) {
+            // global-table fallback for the partitions whose distinct edges overflowed LDS,
+            // in batches whose table fits a fixed memory budget
+            DevBuf<uint64_t> occ(n_ovf);
+            hipLaunchKernelGGL(k_part_occ, dim3((unsigned)std::min<uint64_t>(n_ovf, 65536)), dim3(kBlock), 0, st,
+                               fine.p, dfine.p, ovf_list.p, n_ovf, occ.p);
+            LAUNCH_OK();
+            std::vector<uint64_t> occ_h(n_ovf);
+            std::vector<uint32_t> parts_h(n_ovf);
+            HIP_OK(hipMemcpyAsync(occ_h.data(), occ.p, 8 * n_ovf, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipMemcpyAsync(parts_h.data(), ovf_list.p, 4 * n_ovf, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipStreamSynchronize(st));
+            const uint64_t budget = 1ULL << 30;  // occurrences per batch (table <= 32 GB)
+            DevBuf<unsigned long long> nn(1);
+            DevBuf<int> dover(1);
+            DevBuf<uint32_t> dparts(n_ovf);
+            for (uint64_t q0 = 0; q0 < n_ovf;) {
+                uint64_t q1 = q0, occ_b = 0;
+                while (q1 < n_ovf && (q1 == q0 || occ_b + occ_h[q1] <= budget)) occ_b += occ_h[q1++];
+                HIP_OK(hipMemcpyAsync(dparts.p, parts_h.data() + q0, 4 * (q1 - q0), hipMemcpyHostToDevice, st));
+                uint64_t tcap = next_pow2(occ_b + occ_b / 2 + 1024);
+                for (;;) {
+                    DevBuf<Slot> tab(tcap);
+                    HIP_OK(hipMemsetAsync(tab.p, 0, tab.bytes(), st));
+                    HIP_OK(hipMemsetAsync(nn.p, 0, 8, st));
+                    HIP_OK(hipMemsetAsync(dover.p, 0, 4, st));
+                    hipLaunchKernelGGL(k_fallback, dim3((unsigned)std::min<uint64_t>(q1 - q0, 65536)), dim3(kBlock), 0,
+                                       st, fine.p, dfine.p, dparts.p, q1 - q0, E, tab.p, tcap - 1, nn.p, dover.p);
+                    LAUNCH_OK();
+                    int over = 0;
+                    HIP_OK(hipMemcpyAsync(&over, dover.p, 4, hipMemcpyDeviceToHost, st));
+                    HIP_OK(hipStreamSynchronize(st));
+                    if (over) {
+                        tcap <<= 1;
+                        continue;
+                    }
+                    hipLaunchKernelGGL(k_fallback_emit, dim3(grid_for(tcap, kBlock, 65536)), dim3(kBlock), 0, st,
+                                       tab.p, tcap, out.keys.p, out.counts.p, out_cap, dcnt.p);
+                    LAUNCH_OK();
+                    HIP_OK(hipStreamSynchronize(st));
+                    break;
+                }
+                q0 = q1;
+            }
+            HIP_OK(hipMemcpyAsync(hc, dcnt.p, 8, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipStreamSynchronize(st));
+            n_out = hc[0];
+        }
+        if (n_out <= out_cap) {
+            out.n = n_out;
+            verbose_mark(ctx, "node_counter.C");
+            break;
+        }
+        if (attempt > 0) throw Error(MCAAT_E_CAPACITY, "node_counter: output sizing failed");
+        out_cap = n_out;  // exact on the second run
     }
 }
 

@@ -161,3 +161,33 @@ def test_cluster_bound_and_step_cap(gpu_ctx):
         ores = og.cycle_finder(cluster_bound=bound, step_cap=cap)
         assert res.stats[:6] == ores["stats"], (bound, cap)
         assert [(s, c) for s, c in res.entries] == [tuple(e) for e in ores["entries"]], (bound, cap)
+
+
+def test_lds_overflow_fallback_low_coverage(gpu_ctx):
+    """Low coverage: almost every edge is distinct, every LDS partition overflows and the
+    global-table fallback counts it; results must still equal the oracle."""
+    spec = M.SynthSpec(seed=31, n_genomes=50, genome_len=1_000_000, arrays_per_genome=0, n_reads=60_000,
+                       error_rate=0.01)
+    packed, offs = M.synth_host(spec)
+    reads = M.Reads.synth(gpu_ctx, spec)
+    gk, gc = M.count_edges(gpu_ctx, reads, 27)
+    ok, oc = O.count_canonical(packed, offs, 27, threads=4)
+    assert np.array_equal(gk, ok) and np.array_equal(gc, oc)
+    assert gpu_ctx.kernel_timing("lds_count_overflow_partitions")[1] > 0
+
+
+def test_mixed_read_lengths(gpu_ctx):
+    """Variable-length reads, longer than one 128-position work item (items split reads)."""
+    rng = np.random.default_rng(4)
+    genome = "".join(rng.choice(list("ACGT"), size=20_000))
+    seqs = []
+    for i in range(3000):
+        L = int(rng.integers(20, 700))
+        a = int(rng.integers(0, len(genome) - L))
+        seqs.append(genome[a:a + L])
+    packed, offs = pack_reads(seqs)
+    reads = M.Reads.from_host(gpu_ctx, packed, offs)
+    for k in (15, 23, 30):
+        gk, gc = M.count_edges(gpu_ctx, reads, k)
+        ok, oc = O.count_canonical(packed, offs, k)
+        assert np.array_equal(gk, ok) and np.array_equal(gc, oc), k
