@@ -211,6 +211,8 @@ def main() -> int:
                 "parallelism": f"replicas{world}",
                 "cycle_entries": len(res.entries) if res else 0,
                 "cycles": res.stats[5] if res else 0,
+                "cf_stats": list(res.stats) if res else None,
+                "start_candidates": len(res.candidates) if res else 0,
             },
             "roofline": {
                 "kernel": kern,

@@ -75,7 +75,7 @@ void upload_reads(mcaat_ctx *ctx, const uint64_t *packed, uint64_t n_words, cons
         for (uint64_t i = 0; fixed && i <= n_reads; ++i) fixed = offsets[i] == i * L;
         if (fixed) r->fixed_len = L;
     }
-    r->packed.alloc(n_words + 8);
+    r->packed.alloc(n_words + 16);
     r->offsets.alloc(n_reads + 1);
     HIP_OK(hipMemsetAsync(r->packed.p, 0, r->packed.bytes(), ctx->stream));
     HIP_OK(hipMemcpyAsync(r->packed.p, packed, 8 * n_words, hipMemcpyHostToDevice, ctx->stream));
@@ -210,7 +210,7 @@ void synth_reads(mcaat_ctx *ctx, const mcaat_synth_spec &s, mcaat_reads *out) {
     out->n_bases = s.n_reads * s.read_len;
     out->n_words = (out->n_bases + 31) / 32;
     out->fixed_len = s.read_len;
-    out->packed.alloc(out->n_words + 8);
+    out->packed.alloc(out->n_words + 16);
     out->offsets.alloc(s.n_reads + 1);
     HIP_OK(hipMemsetAsync(out->packed.p, 0, out->packed.bytes(), st));
     hipLaunchKernelGGL(k_synth, dim3(grid_for(out->n_words, kBlock)), dim3(kBlock), 0, st, s, dg.p, out->packed.p,

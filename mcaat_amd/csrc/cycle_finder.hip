@@ -880,6 +880,7 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out) {
     LAUNCH_OK();
     out->stats[0] = read_counter(ctx, cnt.p);
     timer.mark("collect_tips");
+    verbose_mark(ctx, "cf.collect_tips");
     // 2. InvalidateMultiplicityOneNodes
     zero();
     hipLaunchKernelGGL(k_mult_filter, dim3(wgrid), dim3(kBlock), 0, st, v, cnt.p);
@@ -887,9 +888,11 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out) {
     out->stats[1] = read_counter(ctx, cnt.p);
     timer.mark("mult_filter");
     // 3. RecursiveReduction from every seed
+    verbose_mark(ctx, "cf.mult_filter");
     run_peel(g, seeds.p);
     seeds.release();
     timer.mark("peel");
+    verbose_mark(ctx, "cf.peel");
     // 4. valid count + tips after pruning
     zero();
     hipLaunchKernelGGL(k_popcount, dim3(grid_for(nw, kBlock)), dim3(kBlock), 0, st, g->valid.p, nw, cnt.p);
@@ -919,8 +922,10 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out) {
     }
     std::sort(cand.begin(), cand.end());
     timer.mark("candidates");
+    verbose_mark(ctx, "cf.candidates");
     std::vector<uint64_t> pass = run_dls(g, cand, p.cycle_max_length);
     timer.mark("dls");
+    verbose_mark(ctx, "cf.dls");
     std::map<int, std::vector<uint64_t>, std::greater<int>> chunks;
     if (!pass.empty()) {
         DevBuf<uint64_t> ids(pass.size());
@@ -946,6 +951,7 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out) {
     out->stats[6] = fr.rounds;
     out->stats[7] = fr.reruns;
     timer.mark("find_cycle");
+    verbose_mark(ctx, "cf.find_cycle");
     HIP_OK(hipStreamSynchronize(st));
     timer.finish();
 }

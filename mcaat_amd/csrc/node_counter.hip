@@ -80,8 +80,9 @@ constexpr int kAWaves = 8;
 constexpr int kAThreads = kAWaves * 64;
 constexpr int kItem = 128;               // edge positions per work item
 constexpr int kHB = kItem + 64;          // m-mer hashes per item (w <= 64)
-constexpr int kStage = 3584;             // staged descriptors per workgroup
-constexpr int kFlushAt = kStage - kAWaves * kItem;
+constexpr int kSeg = 256;                // per-wave stage segment (descriptors)
+constexpr int kWB = 10;                  // packed words per item window (<= 213 bases + 1 word)
+constexpr int kStage = kSeg * kAWaves;   // staged descriptors per workgroup
 
 struct ItemSrc {
     const uint64_t *offsets;
@@ -106,6 +107,15 @@ __device__ __forceinline__ void get_item(const ItemSrc &s, int E, uint64_t it, u
     }
 }
 
+// E-symbol window at relative base rel of a per-wave LDS copy of the packed stream
+__device__ __forceinline__ uint64_t window_lds(const uint64_t *wb, uint32_t rel, int E) {
+    const uint32_t w = rel >> 5;
+    const int s = 2 * (int)(rel & 31);
+    uint64_t v = wb[w] >> s;
+    if (s) v |= wb[w + 1] << (64 - s);
+    return v & mask_bits(2 * E);
+}
+
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -119,33 +129,36 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
                                                           const uint64_t *__restrict__ l1_base,
                                                           const uint64_t *__restrict__ l1_cap,
                                                           unsigned long long *l1_cursor) {
+    // Each wave owns a kSeg-descriptor segment of the stage and processes its own items
+    // until the segment cannot take a worst-case item (kItem descriptors); only then does
+    // the workgroup meet at a barrier and flush every segment to the L1 buckets.
     __shared__ uint4 stage[kStage];
     __shared__ uint8_t stage_l1[kStage];
     __shared__ uint32_t hb[kAWaves][kHB];
     __shared__ uint32_t hist[256];
     __shared__ unsigned long long rpos[256];  // next free slot of this workgroup's reservation
     __shared__ uint32_t rleft[256];           // slots left in it
-    __shared__ uint32_t n_stage;
+    __shared__ uint32_t seg_fill[kAWaves];
+    __shared__ uint64_t wb[kAWaves][kWB + 1];
+    __shared__ int any_left;
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    if (threadIdx.x == 0) n_stage = 0;
     for (int b = threadIdx.x; b < 256; b += kAThreads) rleft[b] = 0;
+    if (threadIdx.x < kAWaves) seg_fill[threadIdx.x] = 0;
     __syncthreads();
 
-    // write one descriptor of bucket b; reservations are grabbed kMini slots at a time, so
-    // the 256 bucket cursors see ~1/kMini of the traffic
     auto put = [&](int b, uint64_t pos, const uint4 &d) {
         if (pos < l1_cap[b]) l1_data[l1_base[b] + pos] = d;
     };
 
+    // reservations are grabbed kMini slots at a time, so the 256 bucket cursors see
+    // ~1/kMini of the traffic
     auto flush = [&]() {
-        const uint32_t ns = n_stage;
         for (int i = threadIdx.x; i < 256; i += kAThreads) hist[i] = 0;
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < ns; i += kAThreads) atomicAdd(&hist[stage_l1[i]], 1u);
+        for (uint32_t i = threadIdx.x; i < (uint32_t)kStage; i += kAThreads)
+            if ((i % kSeg) < seg_fill[i / kSeg]) atomicAdd(&hist[stage_l1[i]], 1u);
         __syncthreads();
-        // thread b tops up bucket b's reservation; ranks below rleft go to the current
-        // reservation, the rest to a fresh contiguous grab (the old remainder is zero-filled)
         for (int b = threadIdx.x; b < 256; b += kAThreads) {
             const uint32_t need = hist[b];
             if (need > rleft[b]) {
@@ -157,7 +170,8 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
             hist[b] = 0;
         }
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < ns; i += kAThreads) {
+        for (uint32_t i = threadIdx.x; i < (uint32_t)kStage; i += kAThreads) {
+            if ((i % kSeg) >= seg_fill[i / kSeg]) continue;
             const int b = stage_l1[i];
             put(b, rpos[b] + atomicAdd(&hist[b], 1u), stage[i]);
         }
@@ -166,7 +180,7 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
             rpos[b] += hist[b];
             rleft[b] -= hist[b];
         }
-        if (threadIdx.x == 0) n_stage = 0;
+        if (threadIdx.x < kAWaves) seg_fill[threadIdx.x] = 0;
         __syncthreads();
     };
 
@@ -174,18 +188,33 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
     const uint32_t mmask = (uint32_t)mask_bits(2 * P.m);
     const int rsh = 32 - 2 * P.m;
     const uint32_t salt32 = (uint32_t)P.salt;
-    for (uint64_t it0 = (uint64_t)blockIdx.x * kAWaves; it0 < n_items; it0 += (uint64_t)gridDim.x * kAWaves) {
-        const uint64_t it = it0 + wave;
-        if (it < n_items) {
-            uint64_t base;
-            int np;
-            get_item(src, P.E, it, base, np);
+    const uint64_t istride = (uint64_t)gridDim.x * kAWaves;
+    uint64_t it = (uint64_t)blockIdx.x * kAWaves + wave;  // this wave's next item
+    // the item's packed words are fetched once (lanes < kWB) one item ahead of their use
+    uint64_t nbase = 0, pre = 0;
+    int nnp = 0;
+    auto prefetch = [&](uint64_t item) {
+        if (item < n_items) {
+            get_item(src, P.E, item, nbase, nnp);
+            if (lane < kWB) pre = packed[(nbase >> 5) + lane];
+        }
+    };
+    prefetch(it);
+    for (;;) {
+        while (it < n_items && seg_fill[wave] + kItem <= (uint32_t)kSeg) {
+            const uint64_t base = nbase;
+            const int np = nnp;
+            if (lane < kWB) wb[wave][lane] = pre;
+            it += istride;
+            prefetch(it);
+            wave_sync_lds();
+            const uint32_t r0 = (uint32_t)(base & 31);  // item start relative to wb[wave][0]
             const int nm = np + P.w - 1;
             // canonical m-mer (m <= 16, 32 bits) -> bijective 32-bit hash; the minimizer is
             // the canonical m-mer of smallest hash (a function of the window's m-mer set,
             // so an edge and its reverse complement get the same one)
             for (int j = lane; j < nm; j += 64) {
-                const uint32_t mf = (uint32_t)window_at(packed, base + j, P.m);
+                const uint32_t mf = (uint32_t)window_lds(wb[wave], r0 + j, P.m);
                 const uint32_t mr = (rev2_32(mf) >> rsh) ^ mmask;
                 hb[wave][j] = mix32((mf < mr ? mf : mr) ^ salt32);
             }
@@ -202,7 +231,7 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
                 hm[t] = h;
             }
             wave_sync_lds();
-            // segment starts: position 0, or minimizer hash differs from the previous position
+            // segment starts: position 0, or minimizer differs from the previous position
             const uint64_t last0 = __shfl(hm[0], 63);
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
@@ -240,10 +269,7 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
                 if (lane >= o) incl += v;
             }
             const int total = __shfl(incl, 63);
-            uint32_t wbase = 0;
-            if (lane == 0 && total) wbase = atomicAdd(&n_stage, (uint32_t)total);
-            wbase = __shfl(wbase, 0);
-            uint32_t pos = wbase + incl - pieces;
+            uint32_t pos = (uint32_t)wave * kSeg + seg_fill[wave] + incl - pieces;
 #pragma unroll
             for (int t = 0; t < 2; ++t) {
                 if (!st[t]) continue;
@@ -255,24 +281,31 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
                 const uint64_t h14 = (h >> (56 - kHBits)) & ((1u << kHBits) - 1);
                 for (int off = 0; off < seg_len[t]; off += P.nmax) {
                     const int n = min(P.nmax, seg_len[t] - off);
-                    const uint64_t s0 = base + i + off;
-                    const uint64_t w0 = window_at(packed, s0, 32);
-                    uint64_t w1 = window_at(packed, s0 + 32, 22);
+                    const uint32_t s0 = r0 + i + off;
+                    const uint64_t w0 = window_lds(wb[wave], s0, 32);
+                    uint64_t w1 = window_lds(wb[wave], s0 + 32, 22);
                     w1 |= ((uint64_t)n << kNShift) | (h14 << kHShift);
                     stage[pos] = make_uint4((unsigned)w0, (unsigned)(w0 >> 32), (unsigned)w1, (unsigned)(w1 >> 32));
                     stage_l1[pos] = (uint8_t)l1;
                     ++pos;
                 }
             }
+            wave_sync_lds();
+            if (lane == 0) seg_fill[wave] += (uint32_t)total;
+            wave_sync_lds();
         }
+        if (threadIdx.x == 0) any_left = 0;
         __syncthreads();
-        if (n_stage > (uint32_t)kFlushAt) flush();
+        if (lane == 0 && it < n_items) any_left = 1;
+        __syncthreads();
+        const int more = any_left;
+        flush();
+        if (!more) break;
     }
-    __syncthreads();
-    if (n_stage) flush();
     // zero-fill what is left of this workgroup's reservations (n = 0 descriptors are inert)
     for (int b = 0; b < 256; ++b)
         for (uint32_t z = threadIdx.x; z < rleft[b]; z += kAThreads) put(b, rpos[b] + z, make_uint4(0, 0, 0, 0));
+    (void)packed;
 }
 
 // ---- B: radix pass on the next l2_bits hash bits, per L1 bucket -----------------------------
@@ -693,7 +726,7 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
         HIP_OK(hipMemsetAsync(dcur.p, 0, dcur.bytes(), st));
         {
             KernelTimer kt(ctx, "sk_scatter", 0.25 * (double)r->n_bases + 16.0 * (double)est / 1.25);
-            hipLaunchKernelGGL(k_sk_scatter, dim3(512), dim3(kAThreads), 0, st, r->packed.p, src, P, l1.p, dbase.p,
+            hipLaunchKernelGGL(k_sk_scatter, dim3(768), dim3(kAThreads), 0, st, r->packed.p, src, P, l1.p, dbase.p,
                                dcap.p, dcur.p);
             LAUNCH_OK();
             kt.stop();
