@@ -203,6 +203,66 @@ __global__ void __launch_bounds__(kBlock) k_peel_apply(GraphView g, PeelArrays p
     }
 }
 
+// ---- counter-driven peel (Kahn-style) ----
+// rem[e] = number of valid successors of a valid edge. Removing a child decrements each valid
+// parent; the thread whose decrement reaches zero owns that parent, removes it and keeps
+// walking, so every parent is removed exactly when its last valid child is (the reference's
+// recursion fixpoint) and chains are walked without a kernel per level.
+__global__ void __launch_bounds__(kBlock) k_kahn_init(GraphView g, const uint64_t *seed, uint32_t *rem, uint64_t *out,
+                                                      unsigned long long *cursor) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (g.D + 63) / 64;
+    const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nw; w += wstride) {
+        const uint64_t e = w * 64 + lane;
+        bool f = false;
+        if (e < g.D) {
+            uint32_t od = 0;
+            if (bit_get(g.valid, e)) od = (uint32_t)dev_outdeg(g, e);
+            rem[e] = od;
+            f = od == 0 && ((seed[w] & g.valid[w]) >> lane) & 1;
+        }
+        const unsigned long long m = __ballot(f);
+        unsigned long long off = 0;
+        if (lane == 0 && m) off = atomicAdd(cursor, (unsigned long long)__popcll(m));
+        off = __shfl(off, 0);
+        if (f) out[off + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = e;
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_kahn_walk(GraphView g, uint32_t *rem, const uint64_t *f, uint64_t n,
+                                                      uint64_t *next, unsigned long long *cursor, uint32_t budget,
+                                                      uint64_t *pend, unsigned long long *pend_n) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint64_t t = f[i];
+        for (uint32_t step = 0;; ++step) {
+            if (step == budget) {  // long chain: leave t (counter already zero, still valid) pending
+                pend[atomicAdd(pend_n, 1ull)] = t;
+                break;
+            }
+            // parents are read before t is invalidated (valid-only in-edges of t)
+            uint64_t in[4];
+            const int ni = dev_incoming(g, t, in);
+            atomicAnd((unsigned long long *)&g.valid[t >> 6], ~(1ull << (t & 63)));
+            uint64_t cont = kNone;
+            for (int j = 0; j < ni; ++j) {
+                if (atomicSub(&rem[in[j]], 1u) != 1u) continue;
+                if (cont == kNone) cont = in[j];
+                else next[atomicAdd(cursor, 1ull)] = in[j];
+            }
+            if (cont == kNone) break;
+            t = cont;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_ids_to_bits(const uint64_t *ids, uint64_t n, uint64_t *bm) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        atomicOr((unsigned long long *)&bm[ids[i] >> 6], 1ull << (ids[i] & 63));
+}
+
 // --------------------------- start candidates --------------------------------
 __global__ void __launch_bounds__(kBlock) k_candidates(GraphView g, uint64_t thr, uint64_t *list,
                                                        unsigned long long *cursor) {
@@ -538,16 +598,19 @@ __global__ void k_fc_gather(const uint64_t *sbase, uint64_t per_al, FcCaps caps,
     for (uint64_t j = threadIdx.x; j < nc; j += blockDim.x) lens[cyc_off[q] + j] = olen[j];
 }
 
-// conflict[j] = 1 if a node first visited by tentative commit c < j is in j's footprint
+// conflict[q] = 1 if a node first visited by a tentative commit c < jlist[q] is in the
+// footprint (lock table) of speculative start jlist[q]
 __global__ void k_fc_conflict(const uint64_t *sbase, uint64_t per_al, uint32_t CL, const uint64_t *newly,
-                              const uint32_t *newly_c, uint64_t n_newly, uint64_t W, int *conflict) {
-    const uint64_t tot = n_newly * W;
+                              const uint32_t *newly_c, uint64_t n_newly, const uint32_t *jlist, uint64_t nj,
+                              int *conflict) {
+    const uint64_t tot = n_newly * nj;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += stride) {
-        const uint64_t a = idx / W, j = idx - a * W;
-        if (j <= newly_c[a]) continue;
-        const uint64_t *lk = (const uint64_t *)((const uint8_t *)sbase + j * per_al);
-        if (set_contains(lk, CL, newly[a])) conflict[j] = 1;
+        const uint64_t a = idx / nj, q = idx - a * nj;
+        const uint32_t j = jlist[q];
+        if (j <= newly_c[a] || conflict[q]) continue;
+        const uint64_t *lk = (const uint64_t *)((const uint8_t *)sbase + (uint64_t)j * per_al);
+        if (set_contains(lk, CL, newly[a])) conflict[q] = 1;
     }
 }
 
@@ -598,18 +661,26 @@ uint64_t select_flagged(mcaat_ctx *ctx, const uint8_t *flags, uint64_t n, uint64
 }
 
 
-// host visited mirror: only nodes of committed cycles are ever set, so a hash set
+// host visited mirror: dense bitmap from calloc (pages are zero-filled lazily, so only the
+// pages holding visited nodes are ever touched)
 struct HostBits {
-    std::unordered_set<uint64_t> s;
-    explicit HostBits(uint64_t) {}
-    bool get(uint64_t x) const { return s.count(x) != 0; }
-    void set(uint64_t x) { s.insert(x); }
+    uint64_t *w = nullptr;
+    explicit HostBits(uint64_t D) {
+        w = (uint64_t *)calloc((D + 63) / 64 + 1, 8);
+        if (!w) throw std::bad_alloc();
+    }
+    ~HostBits() { free(w); }
+    HostBits(const HostBits &) = delete;
+    HostBits &operator=(const HostBits &) = delete;
+    bool get(uint64_t x) const { return (w[x >> 6] >> (x & 63)) & 1; }
+    void set(uint64_t x) { w[x >> 6] |= 1ULL << (x & 63); }
+    void clear(uint64_t x) { w[x >> 6] &= ~(1ULL << (x & 63)); }
 };
 
 }  // namespace
 
 // ------------------------------ peel driver -----------------------------------
-static void run_peel(mcaat_graph *g, const uint64_t *seed_bm) {
+static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm) {
     mcaat_ctx *ctx = g->ctx;
     hipStream_t st = ctx->stream;
     const uint64_t D = g->D;
@@ -655,6 +726,44 @@ static void run_peel(mcaat_graph *g, const uint64_t *seed_bm) {
     }
     hipLaunchKernelGGL(k_peel_apply, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, v, pa);
     LAUNCH_OK();
+    HIP_OK(hipStreamSynchronize(st));
+}
+
+// RecursiveReduction from every seed: counter-driven walks (work proportional to what is
+// removed) with a per-thread step budget; if chains are longer than that, the pending
+// frontier seeds the parallel ruler/list-ranking peel, whose fixpoint from this state is
+// the same (every pending node is valid, has no valid successor and must be removed).
+static void run_peel(mcaat_graph *g, const uint64_t *seed_bm) {
+    constexpr uint32_t kBudget = 512;
+    mcaat_ctx *ctx = g->ctx;
+    hipStream_t st = ctx->stream;
+    const uint64_t D = g->D, nw = g->n_words();
+    if (!D) return;
+    GraphView v = g->view();
+    DevBuf<unsigned long long> cur(2);
+    DevBuf<uint32_t> rem(D);
+    DevBuf<uint64_t> fa(D), fb(D), pend(D);
+    HIP_OK(hipMemsetAsync(cur.p, 0, 16, st));
+    hipLaunchKernelGGL(k_kahn_init, dim3(grid_for(nw * 64, kBlock)), dim3(kBlock), 0, st, v, seed_bm, rem.p, fa.p,
+                       cur.p);
+    LAUNCH_OK();
+    uint64_t n = read_counter(ctx, cur.p);
+    while (n) {
+        HIP_OK(hipMemsetAsync(cur.p, 0, 8, st));
+        hipLaunchKernelGGL(k_kahn_walk, dim3(grid_for(n, 64)), dim3(64), 0, st, v, rem.p, fa.p, n, fb.p, cur.p,
+                           kBudget, pend.p, cur.p + 1);
+        LAUNCH_OK();
+        n = read_counter(ctx, cur.p);
+        std::swap(fa, fb);
+    }
+    const uint64_t np = read_counter(ctx, cur.p + 1);
+    if (np) {
+        DevBuf<uint64_t> bm(nw);
+        HIP_OK(hipMemsetAsync(bm.p, 0, bm.bytes(), st));
+        hipLaunchKernelGGL(k_ids_to_bits, dim3(grid_for(np, kBlock)), dim3(kBlock), 0, st, pend.p, np, bm.p);
+        LAUNCH_OK();
+        run_peel_rulers(g, bm.p);
+    }
     HIP_OK(hipStreamSynchronize(st));
 }
 
@@ -782,19 +891,20 @@ struct FcRunner {
                 HIP_OK(hipMemcpyAsync(lens.data(), dl.p, 2 * lens.size(), hipMemcpyDeviceToHost, st));
                 HIP_OK(hipStreamSynchronize(st));
             }
-            // tentative sequential commit (threads=1 semantics)
-            std::unordered_set<uint64_t> tent;
+            // tentative sequential commit (threads=1 semantics), applied directly to the
+            // host visited bitmap and rolled back past the first conflicting start
             std::vector<uint64_t> newly;
             std::vector<uint32_t> newly_c;
             std::vector<uint8_t> skip(W, 0);
             for (uint64_t j = 0; j < first_bad; ++j) {
                 const uint64_t s = pending[j];
-                if (hvis.get(s) || tent.count(s)) { skip[j] = 1; continue; }
+                if (hvis.get(s)) { skip[j] = 1; continue; }
                 if (sel_of[j] >= 0) {
                     const uint64_t q = (uint64_t)sel_of[j];
                     for (uint64_t a = noff[q]; a < noff[q + 1]; ++a) {
                         const uint64_t x = nodes[a];
-                        if (!hvis.get(x) && tent.insert(x).second) {
+                        if (!hvis.get(x)) {
+                            hvis.set(x);
                             newly.push_back(x);
                             newly_c.push_back((uint32_t)j);
                         }
@@ -802,22 +912,31 @@ struct FcRunner {
                 }
             }
             uint64_t f = first_bad;
-            if (!newly.empty() && first_bad > 1) {
+            // only starts that would commit after some tentative commit can conflict
+            std::vector<uint32_t> jl;
+            bool seen_commit = false;
+            for (uint64_t j = 0; j < first_bad; ++j) {
+                if (skip[j]) continue;
+                if (seen_commit) jl.push_back((uint32_t)j);
+                seen_commit = true;
+            }
+            if (!newly.empty() && !jl.empty()) {
                 DevBuf<uint64_t> dnw(newly.size());
-                DevBuf<uint32_t> dnc(newly.size());
-                DevBuf<int> dconf(W);
-                HIP_OK(hipMemsetAsync(dconf.p, 0, 4 * W, st));
+                DevBuf<uint32_t> dnc(newly.size()), djl(jl.size());
+                DevBuf<int> dconf(jl.size());
+                HIP_OK(hipMemsetAsync(dconf.p, 0, 4 * jl.size(), st));
                 HIP_OK(hipMemcpyAsync(dnw.p, newly.data(), 8 * newly.size(), hipMemcpyHostToDevice, st));
                 HIP_OK(hipMemcpyAsync(dnc.p, newly_c.data(), 4 * newly.size(), hipMemcpyHostToDevice, st));
-                hipLaunchKernelGGL(k_fc_conflict, dim3(grid_for((uint64_t)newly.size() * first_bad, kBlock)),
+                HIP_OK(hipMemcpyAsync(djl.p, jl.data(), 4 * jl.size(), hipMemcpyHostToDevice, st));
+                hipLaunchKernelGGL(k_fc_conflict, dim3(grid_for((uint64_t)newly.size() * jl.size(), kBlock)),
                                    dim3(kBlock), 0, st, (uint64_t *)scratch.p, pa, caps.CL, dnw.p, dnc.p,
-                                   (uint64_t)newly.size(), first_bad, dconf.p);
+                                   (uint64_t)newly.size(), djl.p, (uint64_t)jl.size(), dconf.p);
                 LAUNCH_OK();
-                std::vector<int> conf(W);
-                HIP_OK(hipMemcpyAsync(conf.data(), dconf.p, 4 * W, hipMemcpyDeviceToHost, st));
+                std::vector<int> conf(jl.size());
+                HIP_OK(hipMemcpyAsync(conf.data(), dconf.p, 4 * jl.size(), hipMemcpyDeviceToHost, st));
                 HIP_OK(hipStreamSynchronize(st));
-                for (uint64_t j = 0; j < first_bad; ++j)
-                    if (!skip[j] && conf[j]) { f = j; break; }
+                for (size_t q = 0; q < jl.size(); ++q)
+                    if (conf[q]) { f = jl[q]; break; }
             }
             // commit the prefix [0, f)
             std::vector<uint64_t> setv;
@@ -834,8 +953,10 @@ struct FcRunner {
                 out->flat.push_back(std::move(fl));
                 out->offsets.push_back(std::move(of));
             }
-            for (size_t a = 0; a < newly.size(); ++a)
-                if (newly_c[a] < f) { hvis.set(newly[a]); setv.push_back(newly[a]); }
+            for (size_t a = 0; a < newly.size(); ++a) {
+                if (newly_c[a] < f) setv.push_back(newly[a]);
+                else hvis.clear(newly[a]);  // roll back tentative marks past the commit prefix
+            }
             if (!setv.empty()) {
                 DevBuf<uint64_t> ds(setv.size());
                 HIP_OK(hipMemcpyAsync(ds.p, setv.data(), 8 * setv.size(), hipMemcpyHostToDevice, st));

@@ -361,8 +361,9 @@ class Graph:
                 of = _u64p()
                 nc = C.c_size_t(0)
                 _check(lib.mcaat_cycles_get(h, i, C.byref(s), C.byref(fl), C.byref(of), C.byref(nc)))
-                offs = [of[j] for j in range(nc.value + 1)]
-                cycles = [[fl[a] for a in range(offs[j], offs[j + 1])] for j in range(nc.value)]
+                offs = np.ctypeslib.as_array(of, shape=(nc.value + 1,)).tolist()
+                flat = np.ctypeslib.as_array(fl, shape=(max(offs[-1], 1),))[: offs[-1]].tolist() if offs[-1] else []
+                cycles = [flat[offs[j]:offs[j + 1]] for j in range(nc.value)]
                 res.entries.append((s.value, cycles))
             st = (C.c_uint64 * 8)()
             _check(lib.mcaat_cycles_stats(h, st))

@@ -191,3 +191,27 @@ def test_mixed_read_lengths(gpu_ctx):
         gk, gc = M.count_edges(gpu_ctx, reads, k)
         ok, oc = O.count_canonical(packed, offs, k)
         assert np.array_equal(gk, ok) and np.array_equal(gc, oc), k
+
+
+@pytest.mark.parametrize("glen", [400, 6000])
+def test_long_peel_chains(gpu_ctx, glen):
+    """Reads tiling a linear genome end to end (both strands, >= 2x at the ends): the seed tips
+    survive the multiplicity filter and the reduction peels back along the whole genome; 6000
+    bases exceed the frontier level cap and exercise the ruler/list-ranking fallback."""
+    rng = np.random.default_rng(glen)
+    genome = "".join(rng.choice(list("ACGT"), size=glen))
+    from tests.helpers import rc
+
+    seqs = []
+    for i in range(0, glen - 100 + 1):
+        seqs += [genome[i:i + 100], rc(genome[i:i + 100])]
+    packed, offs = pack_reads(seqs)
+    reads = M.Reads.from_host(gpu_ctx, packed, offs)
+    g = M.Graph.build(gpu_ctx, reads, 23)
+    res = g.cycle_finder(M.CfParams(threshold_multiplicity=2))
+    og = O.OGraph.build(packed, offs, 23)
+    ores = og.cycle_finder(threshold_multiplicity=2)
+    assert res.stats[:6] == ores["stats"]
+    _, _, valid = g.download()
+    assert np.array_equal(valid, og.valid())
+    assert ores["stats"][2] < og.size // 2  # most of the genome was peeled
