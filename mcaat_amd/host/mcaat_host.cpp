@@ -1,0 +1,195 @@
+// mcaat_host.cpp — SDBGBuild / SDBG / CycleFinder over the C ABI (see mcaat_host.h).
+#include "mcaat_host.h"
+
+#include <algorithm>
+#include <filesystem>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+
+namespace fs = std::filesystem;
+
+void mcaat_check(int rc, const char *what) {
+    if (rc != MCAAT_OK) throw std::runtime_error(std::string(what) + ": " + mcaat_last_error());
+}
+
+mcaat_ctx *mcaat_host_ctx(int device) {
+    static mcaat_ctx *ctx = nullptr;
+    static int dev = -1;
+    if (ctx && dev != device) {
+        mcaat_finalize(ctx);
+        ctx = nullptr;
+    }
+    if (!ctx) {
+        mcaat_check(mcaat_init(device, &ctx), "mcaat_init");
+        dev = device;
+    }
+    return ctx;
+}
+
+// ---------------------------------------------------------------- SDBGBuild
+SDBGBuild::SDBGBuild(Settings s) : settings(s) {
+    BuildLib();
+    BuildSDBG();
+}
+
+SDBGBuild::~SDBGBuild() {
+    if (graph_) mcaat_graph_free(graph_);
+    if (reads_) mcaat_reads_free(reads_);
+}
+
+// sdbg_build.cpp:25-75: "<graph>/data.lib" = comment line + "se"|"pe" + input files
+std::string SDBGBuild::WriteLibFile() {
+    std::cout << "\n-----------------------------------------\n" << std::endl;
+    std::cout << "2. Building the SDBG: " << std::endl;
+    fs::path dir(settings.graph_folder);
+    try {
+        if (!fs::exists(dir)) fs::create_directories(dir);
+    } catch (const fs::filesystem_error &e) {
+        std::cerr << "Error creating directories: " << e.what() << std::endl;
+        return "";
+    }
+    fs::path lib = dir / "data.lib";
+    std::ofstream f(lib, std::ios::out | std::ios::trunc);
+    if (!f) {
+        std::cerr << "Error creating file: " << lib << std::endl;
+        return "";
+    }
+    std::istringstream iss(settings.input_files);
+    std::vector<std::string> tok;
+    std::string t;
+    while (iss >> t) tok.push_back(t);
+    f << "#lib file for the SDBG from " + settings.input_files + "\n";
+    f << std::string(tok.size() > 1 ? "pe" : "se") + " " + settings.input_files;
+    return lib.string();
+}
+
+void SDBGBuild::BuildLib() {
+    WriteLibFile();
+    std::istringstream iss(settings.input_files);
+    std::vector<std::string> files;
+    std::string t;
+    while (iss >> t) files.push_back(t);
+    std::vector<const char *> cf;
+    for (auto &x : files) cf.push_back(x.c_str());
+    mcaat_ctx *ctx = mcaat_host_ctx(settings.gpu);
+    mcaat_check(mcaat_reads_from_fastx(ctx, cf.data(), (int)cf.size(), &reads_), "reading input files");
+}
+
+void SDBGBuild::BuildSDBG() {
+    mcaat_ctx *ctx = mcaat_host_ctx(settings.gpu);
+    mcaat_check(mcaat_build_graph(ctx, reads_, settings.kmer_k, &graph_), "building the SDBG");
+    mcaat_reads_free(reads_);
+    reads_ = nullptr;
+    std::cout << "\n-----------------------------------------\n" << std::endl;
+}
+
+// ---------------------------------------------------------------- SDBG
+SDBG::~SDBG() {
+    if (g_) mcaat_graph_free(g_);
+}
+
+void SDBG::LoadFromDevice(mcaat_graph *g) {
+    if (g_ && g_ != g) mcaat_graph_free(g_);
+    g_ = g;
+    uint64_t D = 0;
+    mcaat_check(mcaat_graph_info(g_, &k_, &D), "mcaat_graph_info");
+    key_.resize(D);
+    mult_.resize(D);
+    valid_.resize(D);
+    mcaat_check(mcaat_graph_download(g_, key_.data(), mult_.data(), valid_.data()), "mcaat_graph_download");
+}
+
+void SDBG::SyncFromDevice() {
+    mcaat_check(mcaat_graph_download(g_, nullptr, nullptr, valid_.data()), "mcaat_graph_download");
+}
+
+void SDBG::SetInvalidEdge(uint64_t e) {
+    valid_[e] = 0;
+    mcaat_check(mcaat_graph_set_valid(g_, &e, 1, 0), "mcaat_graph_set_valid");
+}
+
+void SDBG::SetValidEdge(uint64_t e) {
+    valid_[e] = 1;
+    mcaat_check(mcaat_graph_set_valid(g_, &e, 1, 1), "mcaat_graph_set_valid");
+}
+
+uint64_t SDBG::lower(uint64_t q) const { return std::lower_bound(key_.begin(), key_.end(), q) - key_.begin(); }
+
+int SDBG::OutgoingEdges(uint64_t e, uint64_t *out) const {
+    const uint64_t K = key_[e], W = K & 3, R = K >> 2;
+    const uint64_t Rt = (W << (2 * (k_ - 1))) | (R >> 2);
+    uint64_t tmp[4];
+    int n = 0;
+    for (uint64_t i = lower(Rt << 2); i < size() && (key_[i] >> 2) == Rt; ++i)
+        if (valid_[i]) tmp[n++] = i;
+    for (int i = 0; i < n; ++i) out[i] = tmp[n - 1 - i];
+    return n;
+}
+
+int SDBG::IncomingEdges(uint64_t e, uint64_t *in) const {
+    const uint64_t K = key_[e];
+    const uint64_t c = (K >> (2 * k_)) & 3;
+    const uint64_t G = (K >> 2) & ((1ULL << (2 * (k_ - 1))) - 1);
+    int n = 0;
+    for (uint64_t i = lower(G << 4); i < size() && (key_[i] >> 4) == G; ++i)
+        if ((key_[i] & 3) == c && valid_[i]) in[n++] = i;
+    return n;
+}
+
+uint32_t SDBG::GetLabel(uint64_t e, uint8_t *seq) const {
+    const uint64_t R = key_[e] >> 2;
+    for (int i = 0; i < k_; ++i) seq[i] = (uint8_t)(((R >> (2 * i)) & 3) + 1);
+    return (uint32_t)k_;
+}
+
+int64_t SDBG::IndexBinarySearch(const uint8_t *seq) const {
+    uint64_t R = 0;
+    for (int i = 0; i < k_; ++i) R |= (uint64_t)((seq[i] - 1) & 3) << (2 * i);
+    int64_t last = -1;
+    for (uint64_t i = lower(R << 2); i < size() && (key_[i] >> 2) == R; ++i) last = (int64_t)i;
+    return last;
+}
+
+// ---------------------------------------------------------------- CycleFinder
+CycleFinder::CycleFinder(Settings &s) : settings(s) {
+    if (settings.sdbg == nullptr)  // cycle_finder.cpp:134-136
+        throw std::runtime_error("CycleFinder requires settings.sdbg to be set to a valid SDBG instance");
+    mcaat_cf_params p;
+    mcaat_cf_default_params(&p);
+    p.threshold_multiplicity = settings.cycle_finder_settings.threshold_multiplicity;
+    p.low_abundance = settings.cycle_finder_settings.low_abundance ? 1 : 0;
+    p.cycle_max_length = settings.cycle_finder_settings.cycle_max_length;
+    p.cycle_min_length = settings.cycle_finder_settings.cycle_min_length;
+    mcaat_cycles *c = nullptr;
+    mcaat_check(mcaat_cycle_finder(settings.sdbg->device(), &p, &c), "CycleFinder");
+    size_t n = 0;
+    mcaat_cycles_count(c, &n);
+    mcaat_cycles_stats(c, stats);
+    std::cout << "Graph size: " << settings.sdbg->size() << " nodes; gathered tips: " << stats[0] << std::endl;
+    std::cout << "Pre-filter: invalidated " << stats[1] << " node(s) with multiplicity <= 1." << std::endl;
+    std::cout << "After pruning, tips: " << stats[3] << ", valid edges: " << stats[2] << std::endl;
+    std::cout << "Start nodes found in chunks: " << stats[4] << std::endl;
+    for (size_t i = 0; i < n; ++i) {
+        uint64_t start = 0;
+        const uint64_t *flat = nullptr, *off = nullptr;
+        size_t nc = 0;
+        mcaat_cycles_get(c, i, &start, &flat, &off, &nc);
+        std::vector<std::vector<uint64_t>> cycles(nc);
+        for (size_t j = 0; j < nc; ++j) cycles[j].assign(flat + off[j], flat + off[j + 1]);
+        results[start] = std::move(cycles);  // commit order == reference insertion order
+        commit_order.push_back(start);
+    }
+    mcaat_cycles_free(c);
+    settings.sdbg->SyncFromDevice();  // the reference mutates the SDBG's valid bits
+    std::cout << "Cycle enumeration completed: total cycles=" << stats[5] << ", result nodes=" << results.size()
+              << std::endl;
+}
+
+std::vector<std::vector<uint64_t>> cycles_map_to_cycles(
+    const std::unordered_map<uint64_t, std::vector<std::vector<uint64_t>>> &cycles_map) {
+    std::vector<std::vector<uint64_t>> cycles;
+    for (const auto &[_, inner] : cycles_map)
+        for (const auto &c : inner) cycles.push_back(c);
+    return cycles;
+}

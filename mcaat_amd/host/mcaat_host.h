@@ -1,0 +1,105 @@
+// mcaat_host.h — the reference's hot-path classes (SDBGBuild, SDBG, CycleFinder) over the
+// C ABI of libmcaat_gpu.so. Same names, constructor signatures, public members and error
+// behaviour as reference include/sdbg_build.h:21-33, MEGAHIT sdbg/sdbg.h (API subset used
+// by mcaat) and include/cycle_finder.h:25-85, so `main` reads the same.
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mcaat_gpu.h"
+#include "settings.h"
+
+// throws std::runtime_error(mcaat_last_error()) for a negative status
+void mcaat_check(int rc, const char *what);
+
+// One GPU context per process (one process per GPU).
+mcaat_ctx *mcaat_host_ctx(int device);
+
+// Reference: SDBGBuild(Settings) writes <graph>/data.lib (sdbg_build.cpp:25-75), builds the
+// read library and the SDBG (MEGAHIT). Here: the same data.lib, FASTQ/FASTA(.gz) -> packed
+// reads in HBM -> node_counter -> sdbg_build; the graph stays resident on the GPU.
+class SDBGBuild {
+   public:
+    explicit SDBGBuild(Settings settings);
+    ~SDBGBuild();
+    mcaat_graph *graph() const { return graph_; }
+    mcaat_graph *release_graph() {
+        mcaat_graph *g = graph_;
+        graph_ = nullptr;
+        return g;
+    }
+
+   private:
+    std::string WriteLibFile();
+    void BuildLib();
+    void BuildSDBG();
+    Settings settings;
+    mcaat_reads *reads_ = nullptr;
+    mcaat_graph *graph_ = nullptr;
+};
+
+// MEGAHIT SDBG API subset, valid-only neighbour semantics (DESIGN.md "SDBG conventions").
+// Queries run on a host mirror of the device arrays; SetInvalidEdge/SetValidEdge update both.
+class SDBG {
+   public:
+    SDBG() = default;
+    ~SDBG();
+    SDBG(const SDBG &) = delete;
+    SDBG &operator=(const SDBG &) = delete;
+    // adopt a device graph (replaces SDBG::LoadFromFile of the on-disk MEGAHIT graph)
+    void LoadFromDevice(mcaat_graph *g);
+    // refresh the host mirror after device-side mutation (CycleFinder)
+    void SyncFromDevice();
+    mcaat_graph *device() const { return g_; }
+
+    uint64_t size() const { return key_.size(); }
+    int k() const { return k_; }
+    bool IsValidEdge(uint64_t e) const { return valid_[e] != 0; }
+    void SetInvalidEdge(uint64_t e);
+    void SetValidEdge(uint64_t e);
+    uint16_t EdgeMultiplicity(uint64_t e) const { return mult_[e]; }
+    int OutgoingEdges(uint64_t e, uint64_t *out) const;  // descending ids
+    int IncomingEdges(uint64_t e, uint64_t *in) const;   // ascending ids
+    int EdgeOutdegree(uint64_t e) const {
+        uint64_t t[4];
+        return OutgoingEdges(e, t);
+    }
+    int EdgeIndegree(uint64_t e) const {
+        uint64_t t[4];
+        return IncomingEdges(e, t);
+    }
+    bool EdgeOutdegreeZero(uint64_t e) const { return EdgeOutdegree(e) == 0; }
+    uint32_t GetLabel(uint64_t e, uint8_t *seq) const;      // symbols 1..4 = ACGT
+    int64_t IndexBinarySearch(const uint8_t *seq) const;    // -1 if absent
+    static constexpr uint64_t kNullID = ~0ULL;
+
+   private:
+    uint64_t lower(uint64_t q) const;
+    mcaat_graph *g_ = nullptr;
+    int k_ = 0;
+    std::vector<uint64_t> key_;
+    std::vector<uint16_t> mult_;
+    std::vector<uint8_t> valid_;
+};
+
+// Reference: CycleFinder(Settings&) runs FindApproximateCRISPRArrays in the constructor and
+// leaves `results` (cycle_finder.cpp:131-138, cycle_finder.h:60). Results are inserted in the
+// reference's threads=1 commit order, so the unordered_map iteration order is the reference's.
+class CycleFinder {
+   public:
+    explicit CycleFinder(Settings &settings);
+    std::unordered_map<uint64_t, std::vector<std::vector<uint64_t>>> results;
+    std::vector<uint64_t> commit_order;  // start nodes in commit order
+    uint64_t stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+
+   private:
+    Settings &settings;
+};
+
+// tmp_utils.cpp:26-38
+std::vector<std::vector<uint64_t>> cycles_map_to_cycles(
+    const std::unordered_map<uint64_t, std::vector<std::vector<uint64_t>>> &cycles_map);
