@@ -251,6 +251,9 @@ int mcaat_init(int device, mcaat_ctx **out) {
         HIP_OK(hipSetDevice(device));
         auto *ctx = new mcaat_ctx;
         ctx->device = device;
+        int ncu = 0;
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && ncu > 0)
+            ctx->n_cu = ncu;
         hipError_t se = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
         if (se != hipSuccess) {
             delete ctx;

@@ -84,6 +84,7 @@ struct KernelStat {
 
 struct mcaat_ctx {
     int device = 0;
+    int n_cu = 256;  // compute units (persistent-grid sizing)
     hipStream_t stream = nullptr;
     std::vector<std::pair<const char *, double>> stages;
     std::map<std::string, mcaat::KernelStat> kstats;

@@ -76,13 +76,21 @@ __device__ __forceinline__ uint64_t canon_edge(uint64_t lsb, int E) {
 }
 
 // ---- A: super-k-mers -----------------------------------------------------------------
+// One lane scans one work item (<= kItem edge positions of one read) left to right, kCk
+// positions per step: a step hashes kCk new m-mers out of one 32-base window (forward and
+// reverse-complement m-mers are funnel shifts of the window and of its reverse complement),
+// takes the sliding minimum over the W = E-m+1 m-mers of each edge with compile-time
+// register indices, and closes the open super-k-mer where the minimum changes (or it
+// reaches nmax edges). Closed super-k-mers are appended to the wave's stage segment by
+// ballot compaction as {first base, n edges, minimizer hash}; when a segment runs low on
+// room the wave fills in the bases of its entries and the workgroup scatters all segments
+// to the 256 L1 buckets.
 constexpr int kAWaves = 8;
 constexpr int kAThreads = kAWaves * 64;
-constexpr int kItem = 128;               // edge positions per work item
-constexpr int kHB = kItem + 64;          // m-mer hashes per item (w <= 64)
-constexpr int kSeg = 256;                // per-wave stage segment (descriptors)
-constexpr int kWB = 10;                  // packed words per item window (<= 213 bases + 1 word)
-constexpr int kStage = kSeg * kAWaves;   // staged descriptors per workgroup
+constexpr int kItem = 127;              // edge positions per work item (the close at np fits 16 steps)
+constexpr int kCk = 8;                  // positions per step
+constexpr int kSeg = 1024;              // per-wave stage segment (entries); a step appends <= 64*kCk
+constexpr int kStage = kSeg * kAWaves;  // 128 KB of LDS
 
 struct ItemSrc {
     const uint64_t *offsets;
@@ -107,58 +115,187 @@ __device__ __forceinline__ void get_item(const ItemSrc &s, int E, uint64_t it, u
     }
 }
 
-// E-symbol window at relative base rel of a per-wave LDS copy of the packed stream
-__device__ __forceinline__ uint64_t window_lds(const uint64_t *wb, uint32_t rel, int E) {
-    const uint32_t w = rel >> 5;
-    const int s = 2 * (int)(rel & 31);
-    uint64_t v = wb[w] >> s;
-    if (s) v |= wb[w + 1] << (64 - s);
-    return v & mask_bits(2 * E);
+// 2-bit-group reversal by the hardware bit reverse
+__device__ __forceinline__ uint64_t rev2_dev(uint64_t x) {
+    const uint64_t y = __builtin_bitreverse64(x);
+    return ((y >> 1) & 0x5555555555555555ULL) | ((y & 0x5555555555555555ULL) << 1);
 }
 
-__device__ __forceinline__ void wave_sync_lds() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+// 32 bases starting at absolute base B of the packed stream, from its two words
+__device__ __forceinline__ uint64_t win32(uint64_t a, uint64_t b, uint64_t B) {
+    const int sh = 2 * (int)(B & 31);
+    return sh ? (a >> sh) | (b << (64 - sh)) : a;
+}
+
+// hashes of the kCk canonical m-mers starting at the bases 0..kCk-1 of win (m <= 16)
+__device__ __forceinline__ void hash_step(uint64_t win, int m, uint32_t mmask, uint32_t salt, uint32_t *h) {
+    const uint64_t R = (rev2_dev(win) ^ ~0ULL) >> (2 * (25 - m));  // rc, aligned for t = 7
+    const uint32_t wl = (uint32_t)win, wh = (uint32_t)(win >> 32);
+    const uint32_t rl = (uint32_t)R, rh = (uint32_t)(R >> 32);
+#pragma unroll
+    for (int t = 0; t < kCk; ++t) {
+        const uint32_t f = __builtin_amdgcn_alignbit(wh, wl, 2 * t) & mmask;
+        const uint32_t r = __builtin_amdgcn_alignbit(rh, rl, 2 * (kCk - 1 - t)) & mmask;
+        h[t] = mix32(min(f, r) ^ salt);
+    }
+}
+
+// minimum over H[t .. t+W-1] for t < kCk (H holds 2*kCk + kCk = 24 hashes; W <= 16)
+template <int W>
+__device__ __forceinline__ void window_min(const uint32_t *H, uint32_t *hm) {
+    if constexpr (W > kCk) {
+        // suffix minima of H[t..kCk-1] and prefix minima of H[kCk..kCk+u]
+        uint32_t S[kCk], Pm[W - 1];
+        S[kCk - 1] = H[kCk - 1];
+#pragma unroll
+        for (int t = kCk - 2; t >= 0; --t) S[t] = min(H[t], S[t + 1]);
+        Pm[0] = H[kCk];
+#pragma unroll
+        for (int u = 1; u < W - 1; ++u) Pm[u] = min(Pm[u - 1], H[kCk + u]);
+#pragma unroll
+        for (int t = 0; t < kCk; ++t) hm[t] = min(S[t], Pm[t + W - 1 - kCk]);
+    } else {
+#pragma unroll
+        for (int t = 0; t < kCk; ++t) {
+            uint32_t v = H[t];
+#pragma unroll
+            for (int q = 1; q < W; ++q) v = min(v, H[t + q]);
+            hm[t] = v;
+        }
+    }
 }
 
 constexpr uint32_t kMini = 1024;  // descriptors reserved per (workgroup, L1 bucket) grab
 
+template <int W>
 __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__restrict__ packed, ItemSrc src,
                                                           SkParams P, uint4 *__restrict__ l1_data,
                                                           const uint64_t *__restrict__ l1_base,
                                                           const uint64_t *__restrict__ l1_cap,
                                                           unsigned long long *l1_cursor) {
-    // Each wave owns a kSeg-descriptor segment of the stage and processes its own items
-    // until the segment cannot take a worst-case item (kItem descriptors); only then does
-    // the workgroup meet at a barrier and flush every segment to the L1 buckets.
     __shared__ uint4 stage[kStage];
     __shared__ uint8_t stage_l1[kStage];
-    __shared__ uint32_t hb[kAWaves][kHB];
     __shared__ uint32_t hist[256];
     __shared__ unsigned long long rpos[256];  // next free slot of this workgroup's reservation
     __shared__ uint32_t rleft[256];           // slots left in it
-    __shared__ uint32_t seg_fill[kAWaves];
-    __shared__ uint64_t wb[kAWaves][kWB + 1];
-    __shared__ int any_left;
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int b = threadIdx.x; b < 256; b += kAThreads) rleft[b] = 0;
-    if (threadIdx.x < kAWaves) seg_fill[threadIdx.x] = 0;
+    for (int b = threadIdx.x; b < 256; b += kAThreads) {
+        rleft[b] = 0;
+        hist[b] = 0;
+    }
     __syncthreads();
+    uint4 *seg = stage + wave * kSeg;
+    uint8_t *seg_l1 = stage_l1 + wave * kSeg;
 
     auto put = [&](int b, uint64_t pos, const uint4 &d) {
         if (pos < l1_cap[b]) l1_data[l1_base[b] + pos] = d;
     };
 
-    // reservations are grabbed kMini slots at a time, so the 256 bucket cursors see
-    // ~1/kMini of the traffic
-    auto flush = [&]() {
-        for (int i = threadIdx.x; i < 256; i += kAThreads) hist[i] = 0;
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < (uint32_t)kStage; i += kAThreads)
-            if ((i % kSeg) < seg_fill[i / kSeg]) atomicAdd(&hist[stage_l1[i]], 1u);
-        __syncthreads();
+    const uint64_t n_items = src.fixed_len ? src.n_reads * src.ipr : src.n_items;
+    const uint64_t n_batches = (n_items + 63) / 64;
+    const uint64_t bstride = (uint64_t)gridDim.x * kAWaves;
+    uint64_t batch = (uint64_t)blockIdx.x * kAWaves + wave;
+    const uint32_t mmask = (uint32_t)mask_bits(2 * P.m);
+    const uint32_t salt32 = (uint32_t)P.salt;
+    const int nmax = P.nmax;
+
+    // per-lane scan state (wave-uniform: active, c, nck, fill)
+    uint32_t H[3 * kCk];
+    uint64_t s = 0, pa = 0, pb = 0;
+    int np = 0, p_open = 0, c = 0, nck = 0;
+    uint32_t prev_hm = 0, h_open = 0, fill = 0;
+    bool active = false;
+
+    for (;;) {
+        for (;;) {
+            if (!active) {
+                if (batch >= n_batches) break;
+                const uint64_t item = batch * 64 + lane;
+                s = 0;
+                np = 0;
+                if (item < n_items) get_item(src, P.E, item, s, np);
+                int mx = np;
+#pragma unroll
+                for (int o = 32; o; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+                nck = mx / kCk + 1;  // steps covering positions 0..max np (the last close)
+                {
+                    const uint64_t q0 = s >> 5;
+                    const uint64_t a0 = packed[q0], a1 = packed[q0 + 1];
+                    const uint64_t q1 = (s + kCk) >> 5;
+                    const uint64_t b0 = packed[q1], b1 = packed[q1 + 1];
+                    hash_step(win32(a0, a1, s), P.m, mmask, salt32, H);
+                    hash_step(win32(b0, b1, s + kCk), P.m, mmask, salt32, H + kCk);
+                    const uint64_t q2 = (s + 2 * kCk) >> 5;
+                    pa = packed[q2];
+                    pb = packed[q2 + 1];
+                }
+                c = 0;
+                active = true;
+            }
+            if (fill + 64 * kCk > (uint32_t)kSeg) break;
+            // ---- one step: positions 8c .. 8c+7 ----
+            const uint64_t Bw = s + (uint64_t)kCk * c + 2 * kCk;
+            const uint64_t win = win32(pa, pb, Bw);
+            {
+                const uint64_t qn = (Bw + kCk) >> 5;  // next step's window words
+                pa = packed[qn];
+                pb = packed[qn + 1];
+            }
+            hash_step(win, P.m, mmask, salt32, H + 2 * kCk);
+            uint32_t hm[kCk];
+            window_min<W>(H, hm);
+            if (c == 0) {
+                prev_hm = hm[0];
+                h_open = hm[0];
+                p_open = 0;
+            }
+#pragma unroll
+            for (int t = 0; t < kCk; ++t) {
+                const int i = kCk * c + t;
+                const bool cl = i > 0 && i <= np && (i == np || hm[t] != prev_hm || i - p_open >= nmax);
+                const unsigned long long bm = __ballot(cl);
+                if (bm) {
+                    if (cl) {
+                        const uint32_t idx =
+                            fill + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0));
+                        const uint64_t B0 = s + (uint64_t)p_open;
+                        seg[idx] = make_uint4((uint32_t)B0, (uint32_t)(B0 >> 32) | ((uint32_t)(i - p_open) << 16), h_open, 0u);
+                        p_open = i;
+                        h_open = hm[t];
+                    }
+                    fill += (uint32_t)__popcll(bm);
+                }
+                prev_hm = hm[t];
+            }
+#pragma unroll
+            for (int t = 0; t < 2 * kCk; ++t) H[t] = H[t + kCk];
+            if (++c == nck) {
+                active = false;
+                batch += bstride;
+            }
+        }
+        // fill in the bases of this wave's entries and count them per L1 bucket; the minimum
+        // hash is biased towards 0, so buckets come from a re-hash of it (a bijection)
+        for (uint32_t e = lane; e < fill; e += 64) {
+            const uint4 q = seg[e];
+            const uint64_t B0 = (uint64_t)q.x | ((uint64_t)(q.y & 0xffffu) << 32);
+            const uint32_t n = q.y >> 16;
+            const uint64_t w = B0 >> 5;
+            const uint64_t x0 = packed[w], x1 = packed[w + 1], x2 = packed[w + 2];
+            const int sh = 2 * (int)(B0 & 31);
+            const uint64_t w0 = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
+            uint64_t w1 = (sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1) & mask_bits(2 * (kDescBases - 32));
+            const uint64_t h = mix64((uint64_t)q.z ^ 0x7061727469746eULL);
+            const uint32_t l1 = (uint32_t)(h >> 56);
+            w1 |= ((uint64_t)n << kNShift) | (((h >> (56 - kHBits)) & ((1u << kHBits) - 1)) << kHShift);
+            seg[e] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+            seg_l1[e] = (uint8_t)l1;
+            atomicAdd(&hist[l1], 1u);
+        }
+        const int more = __syncthreads_or(active || batch < n_batches);
+        // reservations are grabbed kMini slots at a time, so the 256 bucket cursors see
+        // ~1/kMini of the traffic
         for (int b = threadIdx.x; b < 256; b += kAThreads) {
             const uint32_t need = hist[b];
             if (need > rleft[b]) {
@@ -170,142 +307,37 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
             hist[b] = 0;
         }
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < (uint32_t)kStage; i += kAThreads) {
-            if ((i % kSeg) >= seg_fill[i / kSeg]) continue;
-            const int b = stage_l1[i];
-            put(b, rpos[b] + atomicAdd(&hist[b], 1u), stage[i]);
+        for (uint32_t e = lane; e < fill; e += 64) {
+            const int b = seg_l1[e];
+            put(b, rpos[b] + atomicAdd(&hist[b], 1u), seg[e]);
         }
         __syncthreads();
         for (int b = threadIdx.x; b < 256; b += kAThreads) {
             rpos[b] += hist[b];
             rleft[b] -= hist[b];
+            hist[b] = 0;
         }
-        if (threadIdx.x < kAWaves) seg_fill[threadIdx.x] = 0;
+        fill = 0;
         __syncthreads();
-    };
-
-    const uint64_t n_items = src.fixed_len ? src.n_reads * src.ipr : src.n_items;
-    const uint32_t mmask = (uint32_t)mask_bits(2 * P.m);
-    const int rsh = 32 - 2 * P.m;
-    const uint32_t salt32 = (uint32_t)P.salt;
-    const uint64_t istride = (uint64_t)gridDim.x * kAWaves;
-    uint64_t it = (uint64_t)blockIdx.x * kAWaves + wave;  // this wave's next item
-    // the item's packed words are fetched once (lanes < kWB) one item ahead of their use
-    uint64_t nbase = 0, pre = 0;
-    int nnp = 0;
-    auto prefetch = [&](uint64_t item) {
-        if (item < n_items) {
-            get_item(src, P.E, item, nbase, nnp);
-            if (lane < kWB) pre = packed[(nbase >> 5) + lane];
-        }
-    };
-    prefetch(it);
-    for (;;) {
-        while (it < n_items && seg_fill[wave] + kItem <= (uint32_t)kSeg) {
-            const uint64_t base = nbase;
-            const int np = nnp;
-            if (lane < kWB) wb[wave][lane] = pre;
-            it += istride;
-            prefetch(it);
-            wave_sync_lds();
-            const uint32_t r0 = (uint32_t)(base & 31);  // item start relative to wb[wave][0]
-            const int nm = np + P.w - 1;
-            // canonical m-mer (m <= 16, 32 bits) -> bijective 32-bit hash; the minimizer is
-            // the canonical m-mer of smallest hash (a function of the window's m-mer set,
-            // so an edge and its reverse complement get the same one)
-            for (int j = lane; j < nm; j += 64) {
-                const uint32_t mf = (uint32_t)window_lds(wb[wave], r0 + j, P.m);
-                const uint32_t mr = (rev2_32(mf) >> rsh) ^ mmask;
-                hb[wave][j] = mix32((mf < mr ? mf : mr) ^ salt32);
-            }
-            wave_sync_lds();
-            uint64_t hm[2];
-            bool st[2];
-            unsigned long long msk[2];
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const int i = lane + 64 * t;
-                uint32_t h = ~0u;
-                if (i < np)
-                    for (int q = 0; q < P.w; ++q) h = min(h, hb[wave][i + q]);
-                hm[t] = h;
-            }
-            wave_sync_lds();
-            // segment starts: position 0, or minimizer differs from the previous position
-            const uint64_t last0 = __shfl(hm[0], 63);
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const int i = lane + 64 * t;
-                uint64_t prev = __shfl_up(hm[t], 1);
-                if (lane == 0) prev = (t == 0) ? (hm[0] ^ 1) : last0;
-                st[t] = (i < np) && (i == 0 || hm[t] != prev);
-                msk[t] = __ballot(st[t]);
-            }
-            // pieces emitted by each segment start (segments longer than nmax are split)
-            int pieces = 0;
-            int seg_len[2] = {0, 0};
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const int i = lane + 64 * t;
-                if (st[t]) {
-                    int nxt = np;
-                    const int j = i + 1;
-                    if (j < 64) {
-                        const unsigned long long rest = msk[0] & (~0ULL << j);
-                        if (rest) nxt = __ffsll(rest) - 1;
-                        else if (msk[1]) nxt = 64 + __ffsll(msk[1]) - 1;
-                    } else if (j < 128) {
-                        const unsigned long long rest = msk[1] & (~0ULL << (j - 64));
-                        if (rest) nxt = 64 + __ffsll(rest) - 1;
-                    }
-                    if (nxt > np) nxt = np;
-                    seg_len[t] = nxt - i;
-                    pieces += (seg_len[t] + P.nmax - 1) / P.nmax;
-                }
-            }
-            int incl = pieces;
-            for (int o = 1; o < 64; o <<= 1) {
-                const int v = __shfl_up(incl, o);
-                if (lane >= o) incl += v;
-            }
-            const int total = __shfl(incl, 63);
-            uint32_t pos = (uint32_t)wave * kSeg + seg_fill[wave] + incl - pieces;
-#pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                if (!st[t]) continue;
-                const int i = lane + 64 * t;
-                // the minimum hash is biased towards 0: partition by a re-hash of it (a
-                // bijection of the minimizer), whose bits are uniform
-                const uint64_t h = mix64(hm[t] ^ 0x7061727469746eULL);
-                const uint32_t l1 = (uint32_t)(h >> 56);
-                const uint64_t h14 = (h >> (56 - kHBits)) & ((1u << kHBits) - 1);
-                for (int off = 0; off < seg_len[t]; off += P.nmax) {
-                    const int n = min(P.nmax, seg_len[t] - off);
-                    const uint32_t s0 = r0 + i + off;
-                    const uint64_t w0 = window_lds(wb[wave], s0, 32);
-                    uint64_t w1 = window_lds(wb[wave], s0 + 32, 22);
-                    w1 |= ((uint64_t)n << kNShift) | (h14 << kHShift);
-                    stage[pos] = make_uint4((unsigned)w0, (unsigned)(w0 >> 32), (unsigned)w1, (unsigned)(w1 >> 32));
-                    stage_l1[pos] = (uint8_t)l1;
-                    ++pos;
-                }
-            }
-            wave_sync_lds();
-            if (lane == 0) seg_fill[wave] += (uint32_t)total;
-            wave_sync_lds();
-        }
-        if (threadIdx.x == 0) any_left = 0;
-        __syncthreads();
-        if (lane == 0 && it < n_items) any_left = 1;
-        __syncthreads();
-        const int more = any_left;
-        flush();
         if (!more) break;
     }
     // zero-fill what is left of this workgroup's reservations (n = 0 descriptors are inert)
     for (int b = 0; b < 256; ++b)
         for (uint32_t z = threadIdx.x; z < rleft[b]; z += kAThreads) put(b, rpos[b] + z, make_uint4(0, 0, 0, 0));
-    (void)packed;
+}
+
+typedef void (*SkKernel)(const uint64_t *, ItemSrc, SkParams, uint4 *, const uint64_t *, const uint64_t *,
+                         unsigned long long *);
+SkKernel sk_kernel(int w) {
+    switch (w) {
+#define MCAAT_SK(W) \
+    case W:         \
+        return k_sk_scatter<W>;
+        MCAAT_SK(1) MCAAT_SK(2) MCAAT_SK(3) MCAAT_SK(4) MCAAT_SK(5) MCAAT_SK(6) MCAAT_SK(7) MCAAT_SK(8)
+        MCAAT_SK(9) MCAAT_SK(10) MCAAT_SK(11) MCAAT_SK(12) MCAAT_SK(13) MCAAT_SK(14) MCAAT_SK(15) MCAAT_SK(16)
+#undef MCAAT_SK
+    }
+    throw Error(MCAAT_E_INVALID, "node_counter: minimizer window out of range");
 }
 
 // ---- B: radix pass on the next l2_bits hash bits, per L1 bucket -----------------------------
@@ -726,8 +758,8 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
         HIP_OK(hipMemsetAsync(dcur.p, 0, dcur.bytes(), st));
         {
             KernelTimer kt(ctx, "sk_scatter", 0.25 * (double)r->n_bases + 16.0 * (double)est / 1.25);
-            hipLaunchKernelGGL(k_sk_scatter, dim3(768), dim3(kAThreads), 0, st, r->packed.p, src, P, l1.p, dbase.p,
-                               dcap.p, dcur.p);
+            hipLaunchKernelGGL(sk_kernel(P.w), dim3(ctx->n_cu), dim3(kAThreads), 0, st, r->packed.p, src, P, l1.p,
+                               dbase.p, dcap.p, dcur.p);
             LAUNCH_OK();
             kt.stop();
         }
