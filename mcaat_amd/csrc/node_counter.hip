@@ -89,8 +89,8 @@ constexpr int kAWaves = 8;
 constexpr int kAThreads = kAWaves * 64;
 constexpr int kItem = 127;              // edge positions per work item (the close at np fits 16 steps)
 constexpr int kCk = 8;                  // positions per step
-constexpr int kSeg = 1024;              // per-wave stage segment (entries); a step appends <= 64*kCk
-constexpr int kStage = kSeg * kAWaves;  // 128 KB of LDS
+constexpr int kSeg = 960;               // per-wave stage segment (entries); a step appends <= 64*kCk
+constexpr int kStage = kSeg * kAWaves;  // 120 KB of LDS
 
 struct ItemSrc {
     const uint64_t *offsets;
@@ -167,29 +167,54 @@ __device__ __forceinline__ void window_min(const uint32_t *H, uint32_t *hm) {
 
 constexpr uint32_t kMini = 1024;  // descriptors reserved per (workgroup, L1 bucket) grab
 
+// workgroup barrier for LDS hand-offs only: __syncthreads() also drains every outstanding
+// global store and atomic (vmcnt(0)), which would expose the bucket writes and the
+// reservation prefetch at every flush
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+constexpr int kFB = 2;  // fill batch (entries per lane per round)
+
 template <int W>
 __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__restrict__ packed, ItemSrc src,
                                                           SkParams P, uint4 *__restrict__ l1_data,
                                                           const uint64_t *__restrict__ l1_base,
                                                           const uint64_t *__restrict__ l1_cap,
-                                                          unsigned long long *l1_cursor) {
+                                                          unsigned long long *l1_cursor, unsigned long long *prof) {
     __shared__ uint4 stage[kStage];
     __shared__ uint8_t stage_l1[kStage];
-    __shared__ uint32_t hist[256];
-    __shared__ unsigned long long rpos[256];  // next free slot of this workgroup's reservation
+    __shared__ uint16_t perm[kStage];         // stage entries in bucket order
+    __shared__ uint32_t hist[256];            // entries per bucket in this flush
+    __shared__ uint32_t boff[256];            // exclusive scan of hist
+    __shared__ uint32_t bcur[256];            // rank cursors
+    __shared__ unsigned long long rpos[256];  // next free slot of this workgroup's reservation (absolute)
+    __shared__ unsigned long long rlim[256];  // end of the bucket's region (absolute)
     __shared__ uint32_t rleft[256];           // slots left in it
+    __shared__ uint32_t wtot[kAWaves];
+    __shared__ int more_flag[2];  // alternating per flush: set, barrier, read; reset a flush later
 
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int b = threadIdx.x; b < 256; b += kAThreads) {
-        rleft[b] = 0;
-        hist[b] = 0;
+    const int tb = threadIdx.x;  // threads < 256 own bucket tb through every flush
+    // each bucket holds its current reservation and, in a register of its owner thread,
+    // the next one, requested a flush ahead so the cursor atomic's latency is hidden
+    unsigned long long my_next = 0;
+    uint32_t prev_need = 0;  // applied to rpos/rleft at the next flush (after its barrier)
+    if (tb < 256) {
+        rleft[tb] = 0;
+        hist[tb] = 0;
+        bcur[tb] = 0;
+        rlim[tb] = l1_base[tb] + l1_cap[tb];
+        my_next = l1_base[tb] + atomicAdd(&l1_cursor[tb], (unsigned long long)kMini);
     }
+    if (threadIdx.x == 0) more_flag[0] = more_flag[1] = 0;
     __syncthreads();
     uint4 *seg = stage + wave * kSeg;
     uint8_t *seg_l1 = stage_l1 + wave * kSeg;
+    uint32_t nflush = 0;
 
+    // absolute slot; a bucket whose region is exhausted drops the write (its cursor keeps
+    // counting, so the host re-sizes and re-runs)
     auto put = [&](int b, uint64_t pos, const uint4 &d) {
-        if (pos < l1_cap[b]) l1_data[l1_base[b] + pos] = d;
+        if (pos < rlim[b]) l1_data[pos] = d;
     };
 
     const uint64_t n_items = src.fixed_len ? src.n_reads * src.ipr : src.n_items;
@@ -202,43 +227,58 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
 
     // per-lane scan state (wave-uniform: active, c, nck, fill)
     uint32_t H[3 * kCk];
-    uint64_t s = 0, pa = 0, pb = 0;
+    uint64_t cw[3], pa = 0, pb = 0;  // the item's first words; the next step's window words
+    uint64_t s = 0;
     int np = 0, p_open = 0, c = 0, nck = 0;
     uint32_t prev_hm = 0, h_open = 0, fill = 0;
     bool active = false;
+    auto fetch = [&](uint64_t bt, uint64_t &sb, int &n, uint64_t *w) {
+        const uint64_t item = bt * 64 + lane;
+        sb = 0;
+        n = 0;
+        if (bt < n_batches && item < n_items) get_item(src, P.E, item, sb, n);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) w[k] = packed[(sb >> 5) + k];
+    };
+
+    // MCAAT_PROF_A=1: 100-MHz real-time ticks per phase, summed over waves
+    unsigned long long tp[5] = {0, 0, 0, 0, 0}, t0 = prof ? __builtin_amdgcn_s_memrealtime() : 0;
+    auto tick = [&](int ph) {
+        if (prof) {
+            const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+            tp[ph] += t1 - t0;
+            t0 = t1;
+        }
+    };
 
     for (;;) {
         for (;;) {
             if (!active) {
                 if (batch >= n_batches) break;
-                const uint64_t item = batch * 64 + lane;
-                s = 0;
-                np = 0;
-                if (item < n_items) get_item(src, P.E, item, s, np);
-                int mx = np;
-#pragma unroll
-                for (int o = 32; o; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
-                nck = mx / kCk + 1;  // steps covering positions 0..max np (the last close)
+                fetch(batch, s, np, cw);
                 {
-                    const uint64_t q0 = s >> 5;
-                    const uint64_t a0 = packed[q0], a1 = packed[q0 + 1];
-                    const uint64_t q1 = (s + kCk) >> 5;
-                    const uint64_t b0 = packed[q1], b1 = packed[q1 + 1];
-                    hash_step(win32(a0, a1, s), P.m, mmask, salt32, H);
-                    hash_step(win32(b0, b1, s + kCk), P.m, mmask, salt32, H + kCk);
                     const uint64_t q2 = (s + 2 * kCk) >> 5;
                     pa = packed[q2];
                     pb = packed[q2 + 1];
                 }
+                int mx = np;
+#pragma unroll
+                for (int o = 32; o; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+                nck = mx / kCk + 1;  // steps covering positions 0..max np (the last close)
+                const int o8 = (int)(s & 31) + kCk;
+                hash_step(win32(cw[0], cw[1], s), P.m, mmask, salt32, H);
+                hash_step(o8 >= 32 ? win32(cw[1], cw[2], s + kCk) : win32(cw[0], cw[1], s + kCk), P.m, mmask,
+                          salt32, H + kCk);
                 c = 0;
                 active = true;
             }
+            // a wave short of room for a worst-case step goes to the flush
             if (fill + 64 * kCk > (uint32_t)kSeg) break;
-            // ---- one step: positions 8c .. 8c+7 ----
-            const uint64_t Bw = s + (uint64_t)kCk * c + 2 * kCk;
-            const uint64_t win = win32(pa, pb, Bw);
+            // ---- one step: positions 8c .. 8c+7; window bases from 8c+16 ----
+            const int rb = 8 * c + 2 * kCk;
+            const uint64_t win = win32(pa, pb, s + rb);
             {
-                const uint64_t qn = (Bw + kCk) >> 5;  // next step's window words
+                const uint64_t qn = (s + rb + kCk) >> 5;  // next step's window words
                 pa = packed[qn];
                 pb = packed[qn + 1];
             }
@@ -275,59 +315,123 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
                 batch += bstride;
             }
         }
+        tick(0);
         // fill in the bases of this wave's entries and count them per L1 bucket; the minimum
-        // hash is biased towards 0, so buckets come from a re-hash of it (a bijection)
-        for (uint32_t e = lane; e < fill; e += 64) {
-            const uint4 q = seg[e];
-            const uint64_t B0 = (uint64_t)q.x | ((uint64_t)(q.y & 0xffffu) << 32);
-            const uint32_t n = q.y >> 16;
-            const uint64_t w = B0 >> 5;
-            const uint64_t x0 = packed[w], x1 = packed[w + 1], x2 = packed[w + 2];
-            const int sh = 2 * (int)(B0 & 31);
-            const uint64_t w0 = sh ? (x0 >> sh) | (x1 << (64 - sh)) : x0;
-            uint64_t w1 = (sh ? (x1 >> sh) | (x2 << (64 - sh)) : x1) & mask_bits(2 * (kDescBases - 32));
-            const uint64_t h = mix64((uint64_t)q.z ^ 0x7061727469746eULL);
-            const uint32_t l1 = (uint32_t)(h >> 56);
-            w1 |= ((uint64_t)n << kNShift) | (((h >> (56 - kHBits)) & ((1u << kHBits) - 1)) << kHShift);
-            seg[e] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
-            seg_l1[e] = (uint8_t)l1;
-            atomicAdd(&hist[l1], 1u);
-        }
-        const int more = __syncthreads_or(active || batch < n_batches);
-        // reservations are grabbed kMini slots at a time, so the 256 bucket cursors see
-        // ~1/kMini of the traffic
-        for (int b = threadIdx.x; b < 256; b += kAThreads) {
-            const uint32_t need = hist[b];
-            if (need > rleft[b]) {
-                for (uint32_t z = 0; z < rleft[b]; ++z) put(b, rpos[b] + z, make_uint4(0, 0, 0, 0));
-                const uint32_t grab = ((need + kMini - 1) / kMini) * kMini;
-                rpos[b] = atomicAdd(&l1_cursor[b], (unsigned long long)grab);
-                rleft[b] = grab;
+        // hash is biased towards 0, so buckets come from a re-hash of it (a bijection).
+        // kFB entries per lane per round keep 3*kFB loads in flight.
+        for (uint32_t e0 = 0; e0 < fill; e0 += 64 * kFB) {
+            uint4 q[kFB];
+            uint64_t x[kFB][3];
+#pragma unroll
+            for (int k = 0; k < kFB; ++k) {
+                const uint32_t e = e0 + 64 * k + lane;
+                q[k] = e < fill ? seg[e] : make_uint4(0, 0, 0, 0);
+                const uint64_t B0 = (uint64_t)q[k].x | ((uint64_t)(q[k].y & 0xffffu) << 32);
+#pragma unroll
+                for (int j = 0; j < 3; ++j) x[k][j] = packed[(B0 >> 5) + j];
             }
-            hist[b] = 0;
+#pragma unroll
+            for (int k = 0; k < kFB; ++k) {
+                const uint32_t e = e0 + 64 * k + lane;
+                if (e >= fill) continue;
+                const uint64_t B0 = (uint64_t)q[k].x | ((uint64_t)(q[k].y & 0xffffu) << 32);
+                const uint32_t n = q[k].y >> 16;
+                const int sh = 2 * (int)(B0 & 31);
+                const uint64_t w0 = sh ? (x[k][0] >> sh) | (x[k][1] << (64 - sh)) : x[k][0];
+                uint64_t w1 = (sh ? (x[k][1] >> sh) | (x[k][2] << (64 - sh)) : x[k][1]) & mask_bits(2 * (kDescBases - 32));
+                const uint64_t h = mix64((uint64_t)q[k].z ^ 0x7061727469746eULL);
+                const uint32_t l1 = (uint32_t)(h >> 56);
+                w1 |= ((uint64_t)n << kNShift) | (((h >> (56 - kHBits)) & ((1u << kHBits) - 1)) << kHShift);
+                seg[e] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+                seg_l1[e] = (uint8_t)l1;
+                atomicAdd(&hist[l1], 1u);
+            }
         }
-        __syncthreads();
+        tick(1);
+        if (lane == 0) wtot[wave] = fill;
+        if (lane == 0 && (active || batch < n_batches)) more_flag[nflush & 1] = 1;
+        lds_barrier();  // A: stage, hist, wtot complete
+        const int more = more_flag[nflush & 1];
+        if (threadIdx.x == 0) more_flag[(nflush + 1) & 1] = 0;
+        ++nflush;
+        tick(2);
+        // reservations (threads < 256, one bucket each) and the bucket offsets (wave 0)
+        if (tb < 256) {
+            rpos[tb] += prev_need;
+            rleft[tb] -= prev_need;
+            const uint32_t need = hist[tb];
+            if (need > rleft[tb]) {
+                for (uint32_t z = 0; z < rleft[tb]; ++z) put(tb, rpos[tb] + z, make_uint4(0, 0, 0, 0));
+                if (need <= kMini) {
+                    rpos[tb] = my_next;
+                    rleft[tb] = kMini;
+                    my_next = l1_base[tb] + atomicAdd(&l1_cursor[tb], (unsigned long long)kMini);
+                } else {  // more than a reservation in one flush: grab synchronously
+                    const uint32_t grab = ((need + kMini - 1) / kMini) * kMini;
+                    rpos[tb] = l1_base[tb] + atomicAdd(&l1_cursor[tb], (unsigned long long)grab);
+                    rleft[tb] = grab;
+                }
+            }
+            prev_need = need;
+        }
+        if (wave == 0) {
+            const uint4 hv = *(const uint4 *)&hist[4 * lane];
+            const uint32_t sum4 = hv.x + hv.y + hv.z + hv.w;
+            uint32_t incl = sum4;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t v = __shfl_up(incl, o);
+                if (lane >= o) incl += v;
+            }
+            const uint32_t ex = incl - sum4;
+            *(uint4 *)&boff[4 * lane] = make_uint4(ex, ex + hv.x, ex + hv.x + hv.y, ex + hv.x + hv.y + hv.z);
+        }
+        lds_barrier();  // B: boff, rpos ready; hist consumed
+        if (tb < 256) hist[tb] = 0;
+        tick(3);
         for (uint32_t e = lane; e < fill; e += 64) {
             const int b = seg_l1[e];
-            put(b, rpos[b] + atomicAdd(&hist[b], 1u), seg[e]);
+            perm[boff[b] + atomicAdd(&bcur[b], 1u)] = (uint16_t)(wave * kSeg + e);
         }
-        __syncthreads();
-        for (int b = threadIdx.x; b < 256; b += kAThreads) {
-            rpos[b] += hist[b];
-            rleft[b] -= hist[b];
-            hist[b] = 0;
+        lds_barrier();  // C: perm ready
+        // consecutive threads write consecutive slots of a bucket's run
+        uint32_t total = 0;
+#pragma unroll
+        for (int w = 0; w < kAWaves; ++w) total += wtot[w];
+        for (uint32_t j = threadIdx.x; j < total; j += kAThreads) {
+            const uint32_t i = perm[j];
+            const int b = stage_l1[i];
+            put(b, rpos[b] + (j - boff[b]), stage[i]);
         }
+        if (tb < 256) bcur[tb] = 0;
         fill = 0;
-        __syncthreads();
+        lds_barrier();  // D: stage free again
+        tick(4);
         if (!more) break;
     }
-    // zero-fill what is left of this workgroup's reservations (n = 0 descriptors are inert)
-    for (int b = 0; b < 256; ++b)
-        for (uint32_t z = threadIdx.x; z < rleft[b]; z += kAThreads) put(b, rpos[b] + z, make_uint4(0, 0, 0, 0));
+    // zero-fill what is left of this workgroup's reservations, the current and the
+    // prefetched one (n = 0 descriptors are inert)
+    if (tb < 256) {
+        rpos[tb] += prev_need;
+        rleft[tb] -= prev_need;
+    }
+    __syncthreads();
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int b = 0; b < 256; ++b)
+            for (uint32_t z = threadIdx.x; z < rleft[b]; z += kAThreads) put(b, rpos[b] + z, make_uint4(0, 0, 0, 0));
+        __syncthreads();
+        if (tb < 256) {
+            rpos[tb] = my_next;
+            rleft[tb] = kMini;
+        }
+        __syncthreads();
+    }
+    if (prof && lane == 0)
+        for (int i = 0; i < 5; ++i) atomicAdd(&prof[i], tp[i]);
 }
 
 typedef void (*SkKernel)(const uint64_t *, ItemSrc, SkParams, uint4 *, const uint64_t *, const uint64_t *,
-                         unsigned long long *);
+                         unsigned long long *, unsigned long long *);
 SkKernel sk_kernel(int w) {
     switch (w) {
 #define MCAAT_SK(W) \
@@ -749,6 +853,9 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     DevBuf<unsigned long long> dcur(256);
     DevBuf<uint4> l1;
     std::vector<unsigned long long> tot(256);
+    static const bool prof_a = getenv("MCAAT_PROF_A") && getenv("MCAAT_PROF_A")[0] == '1';
+    DevBuf<unsigned long long> dprof(prof_a ? 8 : 1);
+    if (prof_a) HIP_OK(hipMemsetAsync(dprof.p, 0, dprof.bytes(), st));
     for (int attempt = 0;; ++attempt) {
         base[0] = 0;
         for (int b = 0; b < 256; ++b) base[b + 1] = base[b] + cap[b];
@@ -759,7 +866,7 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
         {
             KernelTimer kt(ctx, "sk_scatter", 0.25 * (double)r->n_bases + 16.0 * (double)est / 1.25);
             hipLaunchKernelGGL(sk_kernel(P.w), dim3(ctx->n_cu), dim3(kAThreads), 0, st, r->packed.p, src, P, l1.p,
-                               dbase.p, dcap.p, dcur.p);
+                               dbase.p, dcap.p, dcur.p, prof_a ? dprof.p : nullptr);
             LAUNCH_OK();
             kt.stop();
         }
@@ -774,6 +881,13 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     }
     uint64_t n_desc = 0;
     for (int b = 0; b < 256; ++b) n_desc += tot[b];
+    if (prof_a) {
+        unsigned long long hp[8];
+        HIP_OK(hipMemcpy(hp, dprof.p, 64, hipMemcpyDeviceToHost));
+        const double waves = (double)ctx->n_cu * kAWaves;
+        fprintf(stderr, "[mcaat] pass A per-wave ms (100 MHz clock): scan %.1f fill %.1f wait %.1f reserve %.1f scatter %.1f\n",
+                hp[0] / waves / 1e5, hp[1] / waves / 1e5, hp[2] / waves / 1e5, hp[3] / waves / 1e5, hp[4] / waves / 1e5);
+    }
     verbose_mark(ctx, "node_counter.A");
 
     // ---- B ----

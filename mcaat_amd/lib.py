@@ -8,7 +8,8 @@ from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmcaat_gpu.so")
+# MCAAT_LIB: load another build of the same library (A/B experiments)
+LIB_PATH = os.environ.get("MCAAT_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libmcaat_gpu.so")
 
 _u64p = C.POINTER(C.c_uint64)
 _u32p = C.POINTER(C.c_uint32)
