@@ -70,8 +70,12 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
     return x;
 }
 
+// canonical (smaller of the edge and its reverse complement); 2-bit reversal by the
+// hardware bit reverse plus one swap of adjacent bits
 __device__ __forceinline__ uint64_t canon_edge(uint64_t lsb, int E) {
-    const uint64_t rc = lsb_rc(lsb, E);
+    const uint64_t y = __builtin_bitreverse64(lsb);
+    const uint64_t r2 = ((y >> 1) & 0x5555555555555555ULL) | ((y & 0x5555555555555555ULL) << 1);
+    const uint64_t rc = (r2 >> (64 - 2 * E)) ^ mask_bits(2 * E);
     return lsb < rc ? lsb : rc;
 }
 
@@ -337,8 +341,11 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
                 const uint64_t B0 = (uint64_t)q[k].x | ((uint64_t)(q[k].y & 0xffffu) << 32);
                 const uint32_t n = q[k].y >> 16;
                 const int sh = 2 * (int)(B0 & 31);
-                const uint64_t w0 = sh ? (x[k][0] >> sh) | (x[k][1] << (64 - sh)) : x[k][0];
-                uint64_t w1 = (sh ? (x[k][1] >> sh) | (x[k][2] << (64 - sh)) : x[k][1]) & mask_bits(2 * (kDescBases - 32));
+                // bases past the last edge are zeroed, so every copy of a super-k-mer is the
+                // same 128-bit descriptor whatever follows it in its read
+                const int L = (int)n + P.E - 1;
+                const uint64_t w0 = (sh ? (x[k][0] >> sh) | (x[k][1] << (64 - sh)) : x[k][0]) & mask_bits(2 * L);
+                uint64_t w1 = (sh ? (x[k][1] >> sh) | (x[k][2] << (64 - sh)) : x[k][1]) & mask_bits(L > 32 ? 2 * (L - 32) : 0);
                 const uint64_t h = mix64((uint64_t)q[k].z ^ 0x7061727469746eULL);
                 const uint32_t l1 = (uint32_t)(h >> 56);
                 w1 |= ((uint64_t)n << kNShift) | (((h >> (56 - kHBits)) & ((1u << kHBits) - 1)) << kHShift);
@@ -508,46 +515,158 @@ __global__ void __launch_bounds__(kBThreads) k_l2_scatter(const uint4 *__restric
 }
 
 // ---- C: per-partition LDS counting ----------------------------------------------------
-constexpr int kCThreads = 512;
-constexpr int kCap = 4096;                          // LDS slots per workgroup
-constexpr int kCapMax = kCap * 85 / 100 - kCThreads;  // distinct edges before giving up
+// Deep coverage repeats every interior super-k-mer of a locus once per covering read, so a
+// partition first collapses identical descriptors (LDS table keyed by all 128 bits), then
+// expands each distinct one once, adding its multiplicity to every edge it holds. A
+// partition with too many distinct descriptors (shallow data) is expanded from the raw
+// descriptor stream instead; one with too many distinct edges for LDS goes to the
+// global-table fallback.
+constexpr int kCThreads = 1024;
+constexpr int kCWaves = kCThreads / 64;
+constexpr int kCap = 4096;                                 // edge slots
+constexpr int kCapMax = kCap * 85 / 100 - kCWaves * 64;    // distinct edges before giving up
+constexpr int kDCap = 2048;                                // descriptor slots
+constexpr int kDMax = kDCap * 3 / 4;                       // distinct descriptors before going raw
+constexpr int kDProbe = 128;                               // probe bound of the descriptor table
+constexpr int kCB = 8;                                     // descriptor loads in flight per thread
+
+__device__ __forceinline__ uint32_t edge_slot(uint64_t c) {
+    return (((uint32_t)c ^ (uint32_t)(c >> 32)) * 0x9E3779B1u) >> (32 - 12);
+}
+static_assert(kCap == 4096, "edge_slot yields 12 bits");
+__device__ __forceinline__ uint32_t desc_slot(uint64_t w0, uint64_t w1) {
+    const uint64_t x = (w0 ^ (w1 * 0x9E3779B97F4A7C15ULL)) * 0xD6E8FEB86659FD93ULL;
+    return (uint32_t)(x >> (64 - 11));
+}
+static_assert(kDCap == 2048, "desc_slot yields 11 bits");
 
 __global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict__ data,
                                                          const uint64_t *__restrict__ fine_base, uint64_t F, int E,
                                                          uint64_t *out_keys, uint32_t *out_cnt, uint64_t out_cap,
                                                          unsigned long long *out_cursor, uint32_t *ovf_list,
-                                                         unsigned long long *ovf_n) {
+                                                         unsigned long long *ovf_n, unsigned long long *prof) {
     __shared__ unsigned long long keys[kCap];
     __shared__ uint32_t cnt[kCap];
-    __shared__ uint32_t n_distinct;
-    __shared__ int ovf;
-    __shared__ uint32_t wsum[kCThreads / 64];
+    __shared__ unsigned long long dk0[kDCap], dk1[kDCap];
+    __shared__ uint32_t dcnt[kDCap];  // > 0: the slot holds a descriptor
+    __shared__ uint32_t n_distinct, n_ddistinct;
+    __shared__ int ovf, dovf;
+    __shared__ uint32_t wsum[kCWaves];
     __shared__ unsigned long long obase;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // MCAAT_PROF_C=1: 100-MHz ticks per phase (clear, collapse, expand, emit) and counts of
+    // partitions expanded raw
+    unsigned long long tp[5] = {0, 0, 0, 0, 0}, t0 = prof ? __builtin_amdgcn_s_memrealtime() : 0;
+    auto tick = [&](int ph) {
+        if (prof) {
+            const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+            tp[ph] += t1 - t0;
+            t0 = t1;
+        }
+    };
+
+    // add weight to canonical edge c; false once the table has overflowed
+    auto insert = [&](uint64_t c, uint32_t weight) {
+        uint32_t h = edge_slot(c);
+        for (int probe = 0; probe < kCap; ++probe) {
+            const unsigned long long cur = keys[h];
+            if (cur == c) {
+                atomicAdd(&cnt[h], weight);
+                return;
+            }
+            if (cur == kEmpty) {
+                const unsigned long long prev = atomicCAS(&keys[h], kEmpty, (unsigned long long)c);
+                if (prev == kEmpty) {
+                    atomicAdd(&cnt[h], weight);
+                    if (atomicAdd(&n_distinct, 1u) + 1 > (uint32_t)kCapMax) ovf = 1;
+                    return;
+                }
+                if (prev == c) {
+                    atomicAdd(&cnt[h], weight);
+                    return;
+                }
+            }
+            h = (h + 1) & (kCap - 1);
+        }
+        ovf = 1;  // defensive: never spin on a full table
+    };
 
     for (uint64_t p = blockIdx.x; p < F; p += gridDim.x) {
         for (int i = threadIdx.x; i < kCap; i += kCThreads) {
             keys[i] = kEmpty;
             cnt[i] = 0;
         }
+        for (int i = threadIdx.x; i < kDCap; i += kCThreads) {
+            dk0[i] = dk1[i] = kEmpty;
+            dcnt[i] = 0;
+        }
         if (threadIdx.x == 0) {
-            n_distinct = 0;
-            ovf = 0;
+            n_distinct = n_ddistinct = 0;
+            ovf = dovf = 0;
         }
         __syncthreads();
+        tick(0);
         const uint64_t beg = fine_base[p], end = fine_base[p + 1];
-        // each wave takes 64 descriptors at a time and spreads their edges over its lanes
-        for (uint64_t d0 = beg + (uint64_t)wave * 64; d0 < end; d0 += kCThreads) {
-            if (*(volatile int *)&ovf) break;
-            const uint64_t d = d0 + lane;
-            uint64_t w0 = 0, w1 = 0;
-            int n = 0;
-            if (d < end) {
-                const uint4 q = data[d];
-                w0 = (uint64_t)q.x | ((uint64_t)q.y << 32);
-                w1 = (uint64_t)q.z | ((uint64_t)q.w << 32);
-                n = (int)((w1 >> kNShift) & 63);
+
+        // ---- 1: collapse identical descriptors ----
+        // wait-free: the two key words are claimed separately, each by a CAS from empty; a
+        // lane moves on as soon as either word holds another value, so no lane ever waits on
+        // another (a descriptor whose first word is the empty marker is expanded directly)
+        auto collapse = [&](uint64_t w0, uint64_t w1) {
+            if (w0 == kEmpty) {
+                const int n = (int)((w1 >> kNShift) & 63);
+                for (int i = 0; i < n; ++i) insert(canon_edge(desc_window(w0, w1, i, E), E), 1u);
+                return;
             }
+            uint32_t h = desc_slot(w0, w1);
+            for (int probe = 0; probe < kDProbe; ++probe, h = (h + 1) & (kDCap - 1)) {
+                unsigned long long k1 = dk1[h];
+                if (k1 == kEmpty) {
+                    k1 = atomicCAS(&dk1[h], kEmpty, (unsigned long long)w1);
+                    if (k1 == kEmpty) {
+                        k1 = w1;
+                        if (atomicAdd(&n_ddistinct, 1u) + 1 > (uint32_t)kDMax) dovf = 1;
+                    }
+                }
+                if (k1 != w1) continue;
+                unsigned long long k0 = dk0[h];
+                if (k0 == kEmpty) {
+                    k0 = atomicCAS(&dk0[h], kEmpty, (unsigned long long)w0);
+                    if (k0 == kEmpty) k0 = w0;
+                }
+                if (k0 != w0) continue;
+                atomicAdd(&dcnt[h], 1u);
+                return;
+            }
+            dovf = 1;
+            if (prof) atomicAdd(&prof[5], 1ull);
+        };
+        // kCB descriptors per thread per round: their loads are all in flight together
+        for (uint64_t d0 = beg + threadIdx.x; d0 < end; d0 += (uint64_t)kCThreads * kCB) {
+            if (__hip_atomic_load(&dovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+            uint4 q[kCB];
+#pragma unroll
+            for (int k = 0; k < kCB; ++k) {
+                const uint64_t d = d0 + (uint64_t)k * kCThreads;
+                q[k] = d < end ? data[d] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int k = 0; k < kCB; ++k)
+                if (d0 + (uint64_t)k * kCThreads < end)
+                    collapse((uint64_t)q[k].x | ((uint64_t)q[k].y << 32), (uint64_t)q[k].z | ((uint64_t)q[k].w << 32));
+        }
+        __syncthreads();
+        tick(1);
+        if (prof && threadIdx.x == 0) {
+            if (dovf) tp[4]++;
+            atomicAdd(&prof[6], (unsigned long long)n_ddistinct);
+            atomicAdd(&prof[7], (unsigned long long)(end - beg));
+        }
+
+        // ---- 2: expand into canonical edges ----
+        // wave-level: the edges of the wave's 64 descriptors are spread over its lanes, each
+        // added with its descriptor's multiplicity
+        auto spread = [&](uint64_t w0, uint64_t w1, int n, uint32_t wgt) {
             int incl = n;
             for (int o = 1; o < 64; o <<= 1) {
                 const int v = __shfl_up(incl, o);
@@ -559,7 +678,7 @@ __global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict
                 // checked every 64 edges (wave-uniform): after the flag is raised each wave
                 // inserts at most 64 more keys, so the table (kCapMax + kCThreads < kCap)
                 // always keeps a free slot and every probe terminates
-                if (*(volatile int *)&ovf) break;
+                if (__hip_atomic_load(&ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
                 const int idx = b0 + lane;
                 // owner lane: first lane whose inclusive prefix exceeds idx (6 uniform steps)
                 int lo = 0;
@@ -569,42 +688,39 @@ __global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict
                 const int src = lo > 63 ? 63 : lo;
                 const int i = idx - (__shfl(incl, src) - __shfl(n, src));
                 const uint64_t a0 = __shfl(w0, src), a1 = __shfl(w1, src);
+                const uint32_t wt = __shfl(wgt, src);
                 if (idx >= total) continue;
-                const uint64_t c = canon_edge(desc_window(a0, a1, i, E), E);
-                uint32_t h = (uint32_t)(mix64(c) >> 40) & (kCap - 1);
-                for (int probe = 0;; ++probe) {
-                    if (probe >= kCap) {  // defensive: never spin on a full table
-                        ovf = 1;
-                        break;
-                    }
-                    const unsigned long long cur = keys[h];
-                    if (cur == c) {
-                        atomicAdd(&cnt[h], 1u);
-                        break;
-                    }
-                    if (cur == kEmpty) {
-                        const unsigned long long prev = atomicCAS(&keys[h], kEmpty, (unsigned long long)c);
-                        if (prev == kEmpty) {
-                            atomicAdd(&cnt[h], 1u);
-                            if (atomicAdd(&n_distinct, 1u) + 1 > (uint32_t)kCapMax) ovf = 1;
-                            break;
-                        }
-                        if (prev == c) {
-                            atomicAdd(&cnt[h], 1u);
-                            break;
-                        }
-                    }
-                    h = (h + 1) & (kCap - 1);
+                insert(canon_edge(desc_window(a0, a1, i, E), E), wt);
+            }
+        };
+        if (!dovf) {
+            for (int i0 = wave * 64; i0 < kDCap; i0 += kCThreads) {
+                const int i = i0 + lane;
+                const bool live = dcnt[i] != 0;
+                const uint64_t w1 = live ? dk1[i] : 0;
+                spread(live ? dk0[i] : 0, w1, (int)((w1 >> kNShift) & 63), live ? dcnt[i] : 0);
+            }
+        } else {
+            for (uint64_t d0 = beg + (uint64_t)wave * 64; d0 < end; d0 += kCThreads) {
+                if (__hip_atomic_load(&ovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+                const uint64_t d = d0 + lane;
+                uint64_t w0 = 0, w1 = 0;
+                if (d < end) {
+                    const uint4 q = data[d];
+                    w0 = (uint64_t)q.x | ((uint64_t)q.y << 32);
+                    w1 = (uint64_t)q.z | ((uint64_t)q.w << 32);
                 }
+                spread(w0, w1, (int)((w1 >> kNShift) & 63), 1u);
             }
         }
         __syncthreads();
+        tick(2);
         if (ovf) {
             if (threadIdx.x == 0) ovf_list[atomicAdd(ovf_n, 1ull)] = (uint32_t)p;
             __syncthreads();
             continue;
         }
-        // block-wide compaction of the occupied slots
+        // ---- 3: block-wide compaction of the occupied slots ----
         constexpr int per = kCap / kCThreads;
         int mine = 0;
         for (int j = 0; j < per; ++j) mine += keys[threadIdx.x * per + j] != kEmpty;
@@ -617,7 +733,7 @@ __global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict
         __syncthreads();
         if (threadIdx.x == 0) {
             uint32_t t = 0;
-            for (int w = 0; w < kCThreads / 64; ++w) {
+            for (int w = 0; w < kCWaves; ++w) {
                 const uint32_t v = wsum[w];
                 wsum[w] = t;
                 t += v;
@@ -638,7 +754,10 @@ __global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict
             }
         }
         __syncthreads();
+        tick(3);
     }
+    if (prof && (threadIdx.x & 63) == 0)
+        for (int i = 0; i < 5; ++i) atomicAdd(&prof[i], tp[i]);
 }
 
 // ---- fallback: global open-addressing table for overflowing partitions ------------------
@@ -854,7 +973,7 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     DevBuf<uint4> l1;
     std::vector<unsigned long long> tot(256);
     static const bool prof_a = getenv("MCAAT_PROF_A") && getenv("MCAAT_PROF_A")[0] == '1';
-    DevBuf<unsigned long long> dprof(prof_a ? 8 : 1);
+    DevBuf<unsigned long long> dprof(8);
     if (prof_a) HIP_OK(hipMemsetAsync(dprof.p, 0, dprof.bytes(), st));
     for (int attempt = 0;; ++attempt) {
         base[0] = 0;
@@ -936,17 +1055,26 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     uint64_t out_cap = std::max<uint64_t>(n_occ / 32, 1u << 20);
     DevBuf<unsigned long long> dcnt(4);
     DevBuf<uint32_t> ovf_list(F);
+    static const bool prof_c = getenv("MCAAT_PROF_C") && getenv("MCAAT_PROF_C")[0] == '1';
     for (int attempt = 0;; ++attempt) {
+        if (prof_c) HIP_OK(hipMemsetAsync(dprof.p, 0, dprof.bytes(), st));
         out.keys.alloc(out_cap);
         out.counts.alloc(out_cap);
         HIP_OK(hipMemsetAsync(dcnt.p, 0, dcnt.bytes(), st));
         {
             KernelTimer kt(ctx, "lds_count", 16.0 * (double)n_desc);
-            hipLaunchKernelGGL(k_lds_count, dim3((unsigned)std::min<uint64_t>(F, 256 * 3 * 4)), dim3(kCThreads), 0, st,
+            hipLaunchKernelGGL(k_lds_count, dim3((unsigned)std::min<uint64_t>(F, (uint64_t)ctx->n_cu)), dim3(kCThreads), 0, st,
                                fine.p, dfine.p, F, E, out.keys.p, out.counts.p, out_cap, dcnt.p, ovf_list.p,
-                               dcnt.p + 1);
+                               dcnt.p + 1, prof_c ? dprof.p : nullptr);
             LAUNCH_OK();
             kt.stop();
+        }
+        if (prof_c) {
+            unsigned long long hp[8];
+            HIP_OK(hipMemcpy(hp, dprof.p, 64, hipMemcpyDeviceToHost));
+            const double waves = (double)std::min<uint64_t>(F, (uint64_t)ctx->n_cu) * kCWaves;
+            fprintf(stderr, "[mcaat] pass C per-wave ms: clear %.1f collapse %.1f expand %.1f emit %.1f; raw partitions %.0f (probe fails %llu), distinct descriptors %llu of %llu\n",
+                    hp[0] / waves / 1e5, hp[1] / waves / 1e5, hp[2] / waves / 1e5, hp[3] / waves / 1e5, (double)hp[4], hp[5], hp[6], hp[7]);
         }
         unsigned long long hc[2];
         HIP_OK(hipMemcpyAsync(hc, dcnt.p, 16, hipMemcpyDeviceToHost, st));

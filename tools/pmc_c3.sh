@@ -9,6 +9,8 @@ for g in $G; do
     w) run w WRITE_SIZE ;;
     s1) run s1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_BUSY_CYCLES ;;
     s2) run s2 SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY ;;
+    s3) run s3 SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS ;;
+    s4) run s4 SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH ;;
   esac || exit $?
 done
 echo exit=0
