@@ -170,6 +170,7 @@ __device__ __forceinline__ void window_min(const uint32_t *H, uint32_t *hm) {
 }
 
 constexpr uint32_t kMini = 1024;  // descriptors reserved per (workgroup, L1 bucket) grab
+constexpr uint16_t kDeadSub = 0xffff;  // sub-partition mark of an inert (n = 0) slot
 
 // workgroup barrier for LDS hand-offs only: __syncthreads() also drains every outstanding
 // global store and atomic (vmcnt(0)), which would expose the bucket writes and the
@@ -183,7 +184,8 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
                                                           SkParams P, uint4 *__restrict__ l1_data,
                                                           const uint64_t *__restrict__ l1_base,
                                                           const uint64_t *__restrict__ l1_cap,
-                                                          unsigned long long *l1_cursor, unsigned long long *prof) {
+                                                          unsigned long long *l1_cursor, uint16_t *__restrict__ l1_sub,
+                                                          unsigned long long *prof) {
     __shared__ uint4 stage[kStage];
     __shared__ uint8_t stage_l1[kStage];
     __shared__ uint16_t perm[kStage];         // stage entries in bucket order
@@ -216,9 +218,15 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
     uint32_t nflush = 0;
 
     // absolute slot; a bucket whose region is exhausted drops the write (its cursor keeps
-    // counting, so the host re-sizes and re-runs)
+    // counting, so the host re-sizes and re-runs). Beside each descriptor goes its fine
+    // sub-partition (kDeadSub for padding), so pass B's counting passes read 2 bytes, not 16.
+    const int sub_shift = kHShift + kHBits - P.l2_bits;
     auto put = [&](int b, uint64_t pos, const uint4 &d) {
-        if (pos < rlim[b]) l1_data[pos] = d;
+        if (pos < rlim[b]) {
+            l1_data[pos] = d;
+            const uint64_t hi = (uint64_t)d.w << 32;
+            l1_sub[pos] = ((d.w >> (kNShift - 32)) & 63) ? (uint16_t)(sub_shift < 64 ? hi >> sub_shift : 0) : kDeadSub;
+        }
     };
 
     const uint64_t n_items = src.fixed_len ? src.n_reads * src.ipr : src.n_items;
@@ -438,7 +446,7 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
 }
 
 typedef void (*SkKernel)(const uint64_t *, ItemSrc, SkParams, uint4 *, const uint64_t *, const uint64_t *,
-                         unsigned long long *, unsigned long long *);
+                         unsigned long long *, uint16_t *, unsigned long long *);
 SkKernel sk_kernel(int w) {
     switch (w) {
 #define MCAAT_SK(W) \
@@ -458,12 +466,37 @@ SkKernel sk_kernel(int w) {
 constexpr int kBThreads = 1024;
 constexpr uint32_t kChunk = 65536;
 
-__device__ __forceinline__ uint32_t desc_sub(const uint4 &d, int l2_bits) {
-    return (d.w >> (kHShift - 32)) >> (kHBits - l2_bits);
-}
-__device__ __forceinline__ bool desc_live(const uint4 &d) { return ((d.w >> (kNShift - 32)) & 63) != 0; }
 
-__global__ void __launch_bounds__(kBThreads) k_l2_hist(const uint4 *__restrict__ data, const uint64_t *chunk_start,
+// Every (chunk, sub) run is rounded up to a multiple of 4 descriptors (64 B) and padded
+// with inert ones, so each 64-B line of the fine partitions is written by one workgroup.
+__device__ __forceinline__ uint32_t round4(uint32_t x) { return (x + 3) & ~3u; }
+
+// LDS histogram of one chunk's sub rows (16-B aligned: 8 rows per load, all loads of a
+// thread in flight together)
+__device__ __forceinline__ void chunk_hist(const uint16_t *__restrict__ sub, uint64_t s0, uint32_t n, uint32_t *lh) {
+    const uint4 *v = (const uint4 *)(sub + s0);
+    const uint32_t n8 = n / 8;
+    for (uint32_t i0 = threadIdx.x; i0 < n8; i0 += 4 * kBThreads) {
+        uint4 q[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[k] = i0 + k * kBThreads < n8 ? v[i0 + k * kBThreads] : make_uint4(~0u, ~0u, ~0u, ~0u);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t w[4] = {q[k].x, q[k].y, q[k].z, q[k].w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if ((w[j] & 0xffff) != kDeadSub) atomicAdd(&lh[w[j] & 0xffff], 1u);
+                if ((w[j] >> 16) != kDeadSub) atomicAdd(&lh[w[j] >> 16], 1u);
+            }
+        }
+    }
+    for (uint32_t i = 8 * n8 + threadIdx.x; i < n; i += kBThreads) {
+        const uint32_t x = sub[s0 + i];
+        if (x != kDeadSub) atomicAdd(&lh[x], 1u);
+    }
+}
+
+__global__ void __launch_bounds__(kBThreads) k_l2_hist(const uint16_t *__restrict__ sub, const uint64_t *chunk_start,
                                                        const uint32_t *chunk_len, const uint32_t *chunk_bucket,
                                                        int l2_bits, unsigned long long *tot) {
     extern __shared__ uint32_t lh[];
@@ -471,46 +504,89 @@ __global__ void __launch_bounds__(kBThreads) k_l2_hist(const uint4 *__restrict__
     const uint64_t c = blockIdx.x;
     for (uint32_t i = threadIdx.x; i < S; i += kBThreads) lh[i] = 0;
     __syncthreads();
-    const uint64_t s0 = chunk_start[c];
-    const uint32_t n = chunk_len[c];
-    for (uint32_t i = threadIdx.x; i < n; i += kBThreads) {
-        const uint4 d = data[s0 + i];
-        if (desc_live(d)) atomicAdd(&lh[desc_sub(d, l2_bits)], 1u);
-    }
+    chunk_hist(sub, chunk_start[c], chunk_len[c], lh);
     __syncthreads();
     const uint64_t fb = (uint64_t)chunk_bucket[c] * S;
     for (uint32_t i = threadIdx.x; i < S; i += kBThreads)
-        if (lh[i]) atomicAdd(&tot[fb + i], (unsigned long long)lh[i]);
+        if (lh[i]) atomicAdd(&tot[fb + i], (unsigned long long)round4(lh[i]));
 }
 
-__global__ void __launch_bounds__(kBThreads) k_l2_scatter(const uint4 *__restrict__ data, const uint64_t *chunk_start,
-                                                          const uint32_t *chunk_len, const uint32_t *chunk_bucket,
-                                                          int l2_bits, unsigned long long *cursor,
-                                                          uint4 *__restrict__ out) {
-    extern __shared__ unsigned long long lb[];  // [S] bases, then [S] u32 counters
+// Each sub keeps one 64-B line (4 descriptors) of its run in LDS; the lane that completes
+// the line writes it out whole, so HBM sees full-line writes instead of 16-B pieces. Runs
+// start on line boundaries (round4), so no line is shared by two workgroups. A sub that gets
+// more descriptors in one round than its buffered line holds writes the excess directly
+// (rare), and copies the ones that belong to its new partial line into the buffer once the
+// old line has been written.
+constexpr int kLG = 4;          // descriptors per line
+constexpr int kMaxSub = 2048;   // l2_bits <= 11: 128 KB of line buffers
+
+__global__ void __launch_bounds__(kBThreads) k_l2_scatter(const uint4 *__restrict__ data,
+                                                          const uint16_t *__restrict__ sub,
+                                                          const uint64_t *chunk_start, const uint32_t *chunk_len,
+                                                          const uint32_t *chunk_bucket, int l2_bits,
+                                                          unsigned long long *cursor, uint4 *__restrict__ out) {
+    __shared__ uint4 buf[kMaxSub * kLG];
+    __shared__ uint32_t lb[kMaxSub];  // this workgroup's run of each sub, in lines
+    __shared__ uint32_t lc[kMaxSub];  // descriptors per sub: counted, then placed
+    __shared__ uint32_t bl[kMaxSub];  // line of the run held in buf
     const uint32_t S = 1u << l2_bits;
-    uint32_t *lc = (uint32_t *)(lb + S);
     const uint64_t c = blockIdx.x;
     for (uint32_t i = threadIdx.x; i < S; i += kBThreads) lc[i] = 0;
     __syncthreads();
     const uint64_t s0 = chunk_start[c];
     const uint32_t n = chunk_len[c];
-    for (uint32_t i = threadIdx.x; i < n; i += kBThreads) {
-        const uint4 d = data[s0 + i];
-        if (desc_live(d)) atomicAdd(&lc[desc_sub(d, l2_bits)], 1u);
-    }
+    chunk_hist(sub, s0, n, lc);
     __syncthreads();
     const uint64_t fb = (uint64_t)chunk_bucket[c] * S;
     for (uint32_t i = threadIdx.x; i < S; i += kBThreads) {
-        lb[i] = lc[i] ? atomicAdd(&cursor[fb + i], (unsigned long long)lc[i]) : 0;
+        const uint32_t k = lc[i];
+        lb[i] = k ? (uint32_t)(atomicAdd(&cursor[fb + i], (unsigned long long)round4(k)) / kLG) : 0;
         lc[i] = 0;
+        bl[i] = 0;
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < n; i += kBThreads) {
-        const uint4 d = data[s0 + i];
-        if (!desc_live(d)) continue;
-        const uint32_t s = desc_sub(d, l2_bits);
-        out[lb[s] + atomicAdd(&lc[s], 1u)] = d;
+    // one descriptor per thread per round, the next round's already in flight
+    uint32_t v = threadIdx.x < n ? sub[s0 + threadIdx.x] : kDeadSub;
+    uint4 d = threadIdx.x < n ? data[s0 + threadIdx.x] : make_uint4(0, 0, 0, 0);
+    for (uint32_t i0 = 0; i0 < n; i0 += kBThreads) {
+        const uint32_t cv = v;
+        const uint4 cd = d;
+        const uint32_t ni = i0 + kBThreads + threadIdx.x;
+        v = ni < n ? sub[s0 + ni] : kDeadSub;
+        if (ni < n) d = data[s0 + ni];
+        const bool live = cv != kDeadSub;
+        uint32_t r = 0, line = 0;
+        bool buffered = false;
+        if (live) {
+            r = atomicAdd(&lc[cv], 1u);
+            line = bl[cv];
+            buffered = r / kLG == line;
+            if (buffered) buf[cv * kLG + (r & (kLG - 1))] = cd;
+            else out[(uint64_t)lb[cv] * kLG + r] = cd;
+        }
+        lds_barrier();
+        uint32_t nline = 0;
+        if (live) {
+            if (buffered && (r & (kLG - 1)) == kLG - 1) {
+                uint4 *o = out + ((uint64_t)lb[cv] + line) * kLG;
+#pragma unroll
+                for (int z = 0; z < kLG; ++z) o[z] = buf[cv * kLG + z];
+            }
+            nline = lc[cv] / kLG;
+            bl[cv] = nline;  // every writer stores the same value
+        }
+        lds_barrier();
+        if (live && !buffered && r / kLG == nline) buf[cv * kLG + (r & (kLG - 1))] = cd;
+    }
+    lds_barrier();
+    // the last, partly filled line of each run, padded with inert descriptors
+    for (uint32_t i = threadIdx.x; i < S; i += kBThreads) {
+        const uint32_t k = lc[i];
+        if (k & (kLG - 1)) {
+            uint4 *o = out + ((uint64_t)lb[i] + k / kLG) * kLG;
+#pragma unroll
+            for (uint32_t z = 0; z < kLG; ++z) o[z] = z < (k & (kLG - 1)) ? buf[i * kLG + z] : make_uint4(0, 0, 0, 0);
+        }
     }
 }
 
@@ -613,6 +689,7 @@ __global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict
         // lane moves on as soon as either word holds another value, so no lane ever waits on
         // another (a descriptor whose first word is the empty marker is expanded directly)
         auto collapse = [&](uint64_t w0, uint64_t w1) {
+            if (((w1 >> kNShift) & 63) == 0) return;  // padding
             if (w0 == kEmpty) {
                 const int n = (int)((w1 >> kNShift) & 63);
                 for (int i = 0; i < n; ++i) insert(canon_edge(desc_window(w0, w1, i, E), E), 1u);
@@ -956,7 +1033,7 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     // fine partitions: ~64K edge occurrences each, 8 L1 bits + l2_bits
     int fine_bits = 0;
     while ((1ULL << (fine_bits + 1)) * 65536ULL <= n_occ) ++fine_bits;
-    fine_bits = std::max(8, std::min(20, fine_bits));  // l2_bits <= 12: 48 KB of LDS in k_l2_scatter
+    fine_bits = std::max(8, std::min(19, fine_bits));  // l2_bits <= 11: k_l2_scatter's line buffers
     P.l2_bits = fine_bits - 8;
     const uint32_t S = 1u << P.l2_bits;
     const uint64_t F = 256ull * S;
@@ -967,10 +1044,11 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     uint64_t est = (uint64_t)(1.08 * (dens * (double)n_occ + (double)n_items)) + 4096;
     std::vector<uint64_t> cap(256), base(257);
     // + one partially used reservation per (workgroup, bucket)
-    for (int b = 0; b < 256; ++b) cap[b] = est / 256 + 512ull * kMini;
+    for (int b = 0; b < 256; ++b) cap[b] = (est / 256 + 512ull * kMini + 7) & ~7ull;  // 16-B aligned sub rows
     DevBuf<uint64_t> dcap(256), dbase(257);
     DevBuf<unsigned long long> dcur(256);
     DevBuf<uint4> l1;
+    DevBuf<uint16_t> l1s;
     std::vector<unsigned long long> tot(256);
     static const bool prof_a = getenv("MCAAT_PROF_A") && getenv("MCAAT_PROF_A")[0] == '1';
     DevBuf<unsigned long long> dprof(8);
@@ -979,13 +1057,14 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
         base[0] = 0;
         for (int b = 0; b < 256; ++b) base[b + 1] = base[b] + cap[b];
         l1.alloc(base[256]);
+        l1s.alloc(base[256]);
         HIP_OK(hipMemcpyAsync(dcap.p, cap.data(), 8 * 256, hipMemcpyHostToDevice, st));
         HIP_OK(hipMemcpyAsync(dbase.p, base.data(), 8 * 257, hipMemcpyHostToDevice, st));
         HIP_OK(hipMemsetAsync(dcur.p, 0, dcur.bytes(), st));
         {
             KernelTimer kt(ctx, "sk_scatter", 0.25 * (double)r->n_bases + 16.0 * (double)est / 1.25);
             hipLaunchKernelGGL(sk_kernel(P.w), dim3(ctx->n_cu), dim3(kAThreads), 0, st, r->packed.p, src, P, l1.p,
-                               dbase.p, dcap.p, dcur.p, prof_a ? dprof.p : nullptr);
+                               dbase.p, dcap.p, dcur.p, l1s.p, prof_a ? dprof.p : nullptr);
             LAUNCH_OK();
             kt.stop();
         }
@@ -996,7 +1075,7 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
             if (tot[b] > cap[b]) ok = false;
         if (ok) break;
         if (attempt > 0) throw Error(MCAAT_E_CAPACITY, "node_counter: L1 bucket sizing failed");
-        for (int b = 0; b < 256; ++b) cap[b] = tot[b] + 1;  // exact on the second run (cursors count every grab)
+        for (int b = 0; b < 256; ++b) cap[b] = (tot[b] + 8) & ~7ull;  // exact on the second run (cursors count every grab)
     }
     uint64_t n_desc = 0;
     for (int b = 0; b < 256; ++b) n_desc += tot[b];
@@ -1029,9 +1108,9 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     uint64_t n_live = 0;
     DevBuf<uint4> fine;
     {
-        KernelTimer kt(ctx, "l2_partition", 3.0 * 16.0 * (double)n_desc);
+        KernelTimer kt(ctx, "l2_partition", 36.0 * (double)n_desc);  // sub rows read twice, descriptors moved once
         if (nch) {
-            hipLaunchKernelGGL(k_l2_hist, dim3((unsigned)nch), dim3(kBThreads), 4 * S, st, l1.p, dcs.p, dcl.p, dcb.p,
+            hipLaunchKernelGGL(k_l2_hist, dim3((unsigned)nch), dim3(kBThreads), 4 * S, st, l1s.p, dcs.p, dcl.p, dcb.p,
                                P.l2_bits, dtot.p);
             LAUNCH_OK();
         }
@@ -1041,13 +1120,14 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
         HIP_OK(hipStreamSynchronize(st));
         fine.alloc(n_live);
         if (nch) {
-            hipLaunchKernelGGL(k_l2_scatter, dim3((unsigned)nch), dim3(kBThreads), 12 * S, st, l1.p, dcs.p, dcl.p,
-                               dcb.p, P.l2_bits, dcursor.p, fine.p);
+            hipLaunchKernelGGL(k_l2_scatter, dim3((unsigned)nch), dim3(kBThreads), 0, st, l1.p, l1s.p, dcs.p,
+                               dcl.p, dcb.p, P.l2_bits, dcursor.p, fine.p);
             LAUNCH_OK();
         }
         kt.stop();
     }
     l1.release();
+    l1s.release();
     n_desc = n_live;
     verbose_mark(ctx, "node_counter.B");
 
