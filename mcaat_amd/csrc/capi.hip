@@ -532,7 +532,7 @@ int mcaat_kernel_timing(const mcaat_ctx *ctx, const char *kernel, double *avg_ms
         const KernelStat s = it == ctx->kstats.end() ? KernelStat{} : it->second;
         if (avg_ms) *avg_ms = s.launches ? s.total_ms / s.launches : 0.0;
         if (launches) *launches = s.launches;
-        if (bytes_per_launch) *bytes_per_launch = s.bytes_per_launch;
+        if (bytes_per_launch) *bytes_per_launch = s.launches ? s.total_bytes / s.launches : 0.0;
     });
 }
 

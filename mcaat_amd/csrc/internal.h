@@ -77,7 +77,7 @@ struct DevBuf {
 struct KernelStat {
     double total_ms = 0;
     uint64_t launches = 0;
-    double bytes_per_launch = 0;
+    double total_bytes = 0;  // algorithmic bytes over all launches
 };
 
 }  // namespace mcaat
@@ -170,7 +170,7 @@ struct KernelTimer {
         auto &s = ctx->kstats[name];
         s.total_ms += ms;
         s.launches += 1;
-        s.bytes_per_launch = bytes;
+        s.total_bytes += bytes;
     }
     ~KernelTimer() {
         if (a) (void)hipEventDestroy(a);

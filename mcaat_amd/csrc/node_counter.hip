@@ -524,7 +524,8 @@ __global__ void __launch_bounds__(kBThreads) k_l2_scatter(const uint4 *__restric
                                                           const uint16_t *__restrict__ sub,
                                                           const uint64_t *chunk_start, const uint32_t *chunk_len,
                                                           const uint32_t *chunk_bucket, int l2_bits,
-                                                          unsigned long long *cursor, uint4 *__restrict__ out) {
+                                                          unsigned long long *cursor, uint4 *__restrict__ out,
+                                                          uint64_t gbase) {
     __shared__ uint4 buf[kMaxSub * kLG];
     __shared__ uint32_t lb[kMaxSub];  // this workgroup's run of each sub, in lines
     __shared__ uint32_t lc[kMaxSub];  // descriptors per sub: counted, then placed
@@ -562,13 +563,13 @@ __global__ void __launch_bounds__(kBThreads) k_l2_scatter(const uint4 *__restric
             line = bl[cv];
             buffered = r / kLG == line;
             if (buffered) buf[cv * kLG + (r & (kLG - 1))] = cd;
-            else out[(uint64_t)lb[cv] * kLG + r] = cd;
+            else out[(uint64_t)lb[cv] * kLG + r - gbase] = cd;
         }
         lds_barrier();
         uint32_t nline = 0;
         if (live) {
             if (buffered && (r & (kLG - 1)) == kLG - 1) {
-                uint4 *o = out + ((uint64_t)lb[cv] + line) * kLG;
+                uint4 *o = out + (((uint64_t)lb[cv] + line) * kLG - gbase);
 #pragma unroll
                 for (int z = 0; z < kLG; ++z) o[z] = buf[cv * kLG + z];
             }
@@ -583,7 +584,7 @@ __global__ void __launch_bounds__(kBThreads) k_l2_scatter(const uint4 *__restric
     for (uint32_t i = threadIdx.x; i < S; i += kBThreads) {
         const uint32_t k = lc[i];
         if (k & (kLG - 1)) {
-            uint4 *o = out + ((uint64_t)lb[i] + k / kLG) * kLG;
+            uint4 *o = out + (((uint64_t)lb[i] + k / kLG) * kLG - gbase);
 #pragma unroll
             for (uint32_t z = 0; z < kLG; ++z) o[z] = z < (k & (kLG - 1)) ? buf[i * kLG + z] : make_uint4(0, 0, 0, 0);
         }
@@ -616,8 +617,9 @@ __device__ __forceinline__ uint32_t desc_slot(uint64_t w0, uint64_t w1) {
 }
 static_assert(kDCap == 2048, "desc_slot yields 11 bits");
 
-__global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict__ data,
-                                                         const uint64_t *__restrict__ fine_base, uint64_t F, int E,
+__global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict__ data, uint64_t gbase,
+                                                         const uint64_t *__restrict__ fine_base, uint64_t p0,
+                                                         uint64_t F, int E,
                                                          uint64_t *out_keys, uint32_t *out_cnt, uint64_t out_cap,
                                                          unsigned long long *out_cursor, uint32_t *ovf_list,
                                                          unsigned long long *ovf_n, unsigned long long *prof) {
@@ -667,7 +669,7 @@ __global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict
         ovf = 1;  // defensive: never spin on a full table
     };
 
-    for (uint64_t p = blockIdx.x; p < F; p += gridDim.x) {
+    for (uint64_t p = p0 + blockIdx.x; p < F; p += gridDim.x) {
         for (int i = threadIdx.x; i < kCap; i += kCThreads) {
             keys[i] = kEmpty;
             cnt[i] = 0;
@@ -682,7 +684,7 @@ __global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict
         }
         __syncthreads();
         tick(0);
-        const uint64_t beg = fine_base[p], end = fine_base[p + 1];
+        const uint64_t beg = fine_base[p] - gbase, end = fine_base[p + 1] - gbase;
 
         // ---- 1: collapse identical descriptors ----
         // wait-free: the two key words are claimed separately, each by a CAS from empty; a
@@ -869,12 +871,12 @@ __device__ __forceinline__ void table_insert(uint64_t key, Slot *tab, uint64_t m
     atomicExch(overflow, 1);
 }
 
-__global__ void __launch_bounds__(kBlock) k_part_occ(const uint4 *data, const uint64_t *fine_base,
+__global__ void __launch_bounds__(kBlock) k_part_occ(const uint4 *data, uint64_t gbase, const uint64_t *fine_base,
                                                      const uint32_t *parts, uint64_t np, uint64_t *occ) {
     for (uint64_t q = blockIdx.x; q < np; q += gridDim.x) {
         const uint64_t p = parts[q];
         unsigned long long acc = 0;
-        for (uint64_t d = fine_base[p] + threadIdx.x; d < fine_base[p + 1]; d += blockDim.x)
+        for (uint64_t d = fine_base[p] - gbase + threadIdx.x; d < fine_base[p + 1] - gbase; d += blockDim.x)
             acc += (data[d].w >> (kNShift - 32)) & 63;
         __shared__ unsigned long long s;
         if (threadIdx.x == 0) s = 0;
@@ -886,12 +888,12 @@ __global__ void __launch_bounds__(kBlock) k_part_occ(const uint4 *data, const ui
     }
 }
 
-__global__ void __launch_bounds__(kBlock) k_fallback(const uint4 *data, const uint64_t *fine_base,
+__global__ void __launch_bounds__(kBlock) k_fallback(const uint4 *data, uint64_t gbase, const uint64_t *fine_base,
                                                      const uint32_t *parts, uint64_t np, int E, Slot *tab,
                                                      uint64_t mask, unsigned long long *n_new, int *overflow) {
     for (uint64_t q = blockIdx.x; q < np; q += gridDim.x) {
         const uint64_t p = parts[q];
-        for (uint64_t d = fine_base[p] + threadIdx.x; d < fine_base[p + 1]; d += blockDim.x) {
+        for (uint64_t d = fine_base[p] - gbase + threadIdx.x; d < fine_base[p + 1] - gbase; d += blockDim.x) {
             const uint4 x = data[d];
             const uint64_t w0 = (uint64_t)x.x | ((uint64_t)x.y << 32);
             const uint64_t w1 = (uint64_t)x.z | ((uint64_t)x.w << 32);
@@ -1088,138 +1090,168 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     }
     verbose_mark(ctx, "node_counter.A");
 
-    // ---- B ----
+    // ---- B + C, over groups of L1 buckets whose fine partitions fit a memory budget ----
+    // The sub histogram of every chunk gives all fine-partition offsets at once; each group
+    // then scatters its buckets into a buffer of its own and counts them, so the peak
+    // footprint is the L1 buckets plus one group's fine partitions.
     std::vector<uint64_t> cstart;
     std::vector<uint32_t> clen, cbucket;
-    for (int b = 0; b < 256; ++b)
+    std::vector<uint64_t> bchunk(257, 0);  // first chunk of each bucket
+    for (int b = 0; b < 256; ++b) {
+        bchunk[b] = cstart.size();
         for (uint64_t o = 0; o < tot[b]; o += kChunk) {
             cstart.push_back(base[b] + o);
             clen.push_back((uint32_t)std::min<uint64_t>(kChunk, tot[b] - o));
             cbucket.push_back((uint32_t)b);
         }
+    }
+    bchunk[256] = cstart.size();
     const uint64_t nch = cstart.size();
-    DevBuf<uint64_t> dcs(nch), dfine(F + 1);
+    DevBuf<uint64_t> dcs(nch ? nch : 1), dfine(F + 1);
     DevBuf<unsigned long long> dtot(F + 1), dcursor(F + 1);
-    DevBuf<uint32_t> dcl(nch), dcb(nch);
+    DevBuf<uint32_t> dcl(nch ? nch : 1), dcb(nch ? nch : 1);
     HIP_OK(hipMemcpyAsync(dcs.p, cstart.data(), 8 * nch, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(dcl.p, clen.data(), 4 * nch, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(dcb.p, cbucket.data(), 4 * nch, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemsetAsync(dtot.p, 0, dtot.bytes(), st));
-    uint64_t n_live = 0;
-    DevBuf<uint4> fine;
+    std::vector<uint64_t> hfine(F + 1);
     {
-        KernelTimer kt(ctx, "l2_partition", 36.0 * (double)n_desc);  // sub rows read twice, descriptors moved once
+        KernelTimer kt(ctx, "l2_hist", 2.0 * (double)n_desc);
         if (nch) {
             hipLaunchKernelGGL(k_l2_hist, dim3((unsigned)nch), dim3(kBThreads), 4 * S, st, l1s.p, dcs.p, dcl.p, dcb.p,
                                P.l2_bits, dtot.p);
             LAUNCH_OK();
         }
         exclusive_scan(ctx, (const uint64_t *)dtot.p, dfine.p, F + 1);
-        HIP_OK(hipMemcpyAsync(&n_live, dfine.p + F, 8, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipMemcpyAsync(hfine.data(), dfine.p, 8 * (F + 1), hipMemcpyDeviceToHost, st));
         HIP_OK(hipMemcpyAsync(dcursor.p, dfine.p, 8 * (F + 1), hipMemcpyDeviceToDevice, st));
-        HIP_OK(hipStreamSynchronize(st));
-        fine.alloc(n_live);
-        if (nch) {
-            hipLaunchKernelGGL(k_l2_scatter, dim3((unsigned)nch), dim3(kBThreads), 0, st, l1.p, l1s.p, dcs.p,
-                               dcl.p, dcb.p, P.l2_bits, dcursor.p, fine.p);
-            LAUNCH_OK();
-        }
         kt.stop();
+    }
+    const uint64_t n_live = hfine[F];
+    verbose_mark(ctx, "node_counter.B_hist");
+
+    uint64_t out_cap = std::max<uint64_t>(n_occ / 32, 1u << 20);
+    out.keys.alloc(out_cap);
+    out.counts.alloc(out_cap);
+    DevBuf<unsigned long long> dcnt(4);
+    HIP_OK(hipMemsetAsync(dcnt.p, 0, dcnt.bytes(), st));
+    DevBuf<uint32_t> ovf_list(F);
+    static const bool prof_c = getenv("MCAAT_PROF_C") && getenv("MCAAT_PROF_C")[0] == '1';
+    if (prof_c) HIP_OK(hipMemsetAsync(dprof.p, 0, dprof.bytes(), st));
+    const uint64_t group_budget = std::max<uint64_t>(n_live / 4 + 1, 1ULL << 28);  // descriptors per group
+    uint64_t n_out = 0;
+    for (int b0 = 0; b0 < 256;) {
+        int b1 = b0 + 1;
+        while (b1 < 256 && hfine[(uint64_t)(b1 + 1) * S] - hfine[(uint64_t)b0 * S] <= group_budget) ++b1;
+        const uint64_t p0 = (uint64_t)b0 * S, p1 = (uint64_t)b1 * S;
+        const uint64_t gbase = hfine[p0], gn = hfine[p1] - gbase;
+        const uint64_t c0 = bchunk[b0], c1 = bchunk[b1];
+        DevBuf<uint4> fine(gn ? gn : 1);
+        {
+            KernelTimer kt(ctx, "l2_partition", 34.0 * (double)gn);  // sub rows + descriptors read, descriptors written
+            if (c1 > c0) {
+                hipLaunchKernelGGL(k_l2_scatter, dim3((unsigned)(c1 - c0)), dim3(kBThreads), 0, st, l1.p, l1s.p,
+                                   dcs.p + c0, dcl.p + c0, dcb.p + c0, P.l2_bits, dcursor.p, fine.p, gbase);
+                LAUNCH_OK();
+            }
+            kt.stop();
+        }
+        // C; a group whose output overflows the key buffers is counted again after they grow
+        for (int attempt = 0;; ++attempt) {
+            HIP_OK(hipMemsetAsync(dcnt.p + 1, 0, 8, st));
+            {
+                KernelTimer kt(ctx, "lds_count", 16.0 * (double)gn);
+                hipLaunchKernelGGL(k_lds_count, dim3((unsigned)std::min<uint64_t>(p1 - p0, (uint64_t)ctx->n_cu)),
+                                   dim3(kCThreads), 0, st, fine.p, gbase, dfine.p, p0, p1, E, out.keys.p, out.counts.p,
+                                   out_cap, dcnt.p, ovf_list.p, dcnt.p + 1, prof_c ? dprof.p : nullptr);
+                LAUNCH_OK();
+                kt.stop();
+            }
+            unsigned long long hc[2];
+            HIP_OK(hipMemcpyAsync(hc, dcnt.p, 16, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipStreamSynchronize(st));
+            const uint64_t n_ovf = hc[1];
+            ctx->kstats["lds_count_overflow_partitions"].launches += n_ovf;
+            if (n_ovf) {
+                // global-table fallback for the partitions whose distinct edges overflowed LDS,
+                // in batches whose table fits a fixed memory budget
+                DevBuf<uint64_t> occ(n_ovf);
+                hipLaunchKernelGGL(k_part_occ, dim3((unsigned)std::min<uint64_t>(n_ovf, 65536)), dim3(kBlock), 0, st,
+                                   fine.p, gbase, dfine.p, ovf_list.p, n_ovf, occ.p);
+                LAUNCH_OK();
+                std::vector<uint64_t> occ_h(n_ovf);
+                std::vector<uint32_t> parts_h(n_ovf);
+                HIP_OK(hipMemcpyAsync(occ_h.data(), occ.p, 8 * n_ovf, hipMemcpyDeviceToHost, st));
+                HIP_OK(hipMemcpyAsync(parts_h.data(), ovf_list.p, 4 * n_ovf, hipMemcpyDeviceToHost, st));
+                HIP_OK(hipStreamSynchronize(st));
+                const uint64_t budget = 1ULL << 30;  // occurrences per batch (table <= 32 GB)
+                DevBuf<unsigned long long> nn(1);
+                DevBuf<int> dover(1);
+                DevBuf<uint32_t> dparts(n_ovf);
+                for (uint64_t q0 = 0; q0 < n_ovf;) {
+                    uint64_t q1 = q0, occ_b = 0;
+                    while (q1 < n_ovf && (q1 == q0 || occ_b + occ_h[q1] <= budget)) occ_b += occ_h[q1++];
+                    HIP_OK(hipMemcpyAsync(dparts.p, parts_h.data() + q0, 4 * (q1 - q0), hipMemcpyHostToDevice, st));
+                    uint64_t tcap = next_pow2(occ_b + occ_b / 2 + 1024);
+                    for (;;) {
+                        DevBuf<Slot> tab(tcap);
+                        HIP_OK(hipMemsetAsync(tab.p, 0, tab.bytes(), st));
+                        HIP_OK(hipMemsetAsync(nn.p, 0, 8, st));
+                        HIP_OK(hipMemsetAsync(dover.p, 0, 4, st));
+                        hipLaunchKernelGGL(k_fallback, dim3((unsigned)std::min<uint64_t>(q1 - q0, 65536)), dim3(kBlock),
+                                           0, st, fine.p, gbase, dfine.p, dparts.p, q1 - q0, E, tab.p, tcap - 1, nn.p,
+                                           dover.p);
+                        LAUNCH_OK();
+                        int over = 0;
+                        HIP_OK(hipMemcpyAsync(&over, dover.p, 4, hipMemcpyDeviceToHost, st));
+                        HIP_OK(hipStreamSynchronize(st));
+                        if (over) {
+                            tcap <<= 1;
+                            continue;
+                        }
+                        hipLaunchKernelGGL(k_fallback_emit, dim3(grid_for(tcap, kBlock, 65536)), dim3(kBlock), 0, st,
+                                           tab.p, tcap, out.keys.p, out.counts.p, out_cap, dcnt.p);
+                        LAUNCH_OK();
+                        HIP_OK(hipStreamSynchronize(st));
+                        break;
+                    }
+                    q0 = q1;
+                }
+                HIP_OK(hipMemcpyAsync(hc, dcnt.p, 8, hipMemcpyDeviceToHost, st));
+                HIP_OK(hipStreamSynchronize(st));
+            }
+            const uint64_t total = hc[0];
+            ctx->kstats["lds_count"].total_bytes += 12.0 * (double)(std::min(total, out_cap) - std::min(n_out, out_cap));
+            if (total <= out_cap) {
+                n_out = total;
+                break;
+            }
+            if (attempt > 0) throw Error(MCAAT_E_CAPACITY, "node_counter: output sizing failed");
+            // grow (keeping the groups already counted) and count this group again
+            const uint64_t ncap = total + (total - n_out) * (uint64_t)(256 - b1) / (uint64_t)(b1 - b0) + (1u << 20);
+            DevBuf<uint64_t> k2(ncap);
+            DevBuf<uint32_t> c2(ncap);
+            HIP_OK(hipMemcpyAsync(k2.p, out.keys.p, 8 * n_out, hipMemcpyDeviceToDevice, st));
+            HIP_OK(hipMemcpyAsync(c2.p, out.counts.p, 4 * n_out, hipMemcpyDeviceToDevice, st));
+            out.keys = std::move(k2);
+            out.counts = std::move(c2);
+            out_cap = ncap;
+            const unsigned long long keep = n_out;
+            HIP_OK(hipMemcpyAsync(dcnt.p, &keep, 8, hipMemcpyHostToDevice, st));
+        }
+        b0 = b1;
+    }
+    if (prof_c) {
+        unsigned long long hp[8];
+        HIP_OK(hipMemcpy(hp, dprof.p, 64, hipMemcpyDeviceToHost));
+        const double waves = (double)ctx->n_cu * kCWaves;
+        fprintf(stderr, "[mcaat] pass C per-wave ms: clear %.1f collapse %.1f expand %.1f emit %.1f; raw partitions %.0f (probe fails %llu), distinct descriptors %llu of %llu\n",
+                hp[0] / waves / 1e5, hp[1] / waves / 1e5, hp[2] / waves / 1e5, hp[3] / waves / 1e5, (double)hp[4], hp[5], hp[6], hp[7]);
     }
     l1.release();
     l1s.release();
-    n_desc = n_live;
-    verbose_mark(ctx, "node_counter.B");
-
-    // ---- C ----
-    uint64_t out_cap = std::max<uint64_t>(n_occ / 32, 1u << 20);
-    DevBuf<unsigned long long> dcnt(4);
-    DevBuf<uint32_t> ovf_list(F);
-    static const bool prof_c = getenv("MCAAT_PROF_C") && getenv("MCAAT_PROF_C")[0] == '1';
-    for (int attempt = 0;; ++attempt) {
-        if (prof_c) HIP_OK(hipMemsetAsync(dprof.p, 0, dprof.bytes(), st));
-        out.keys.alloc(out_cap);
-        out.counts.alloc(out_cap);
-        HIP_OK(hipMemsetAsync(dcnt.p, 0, dcnt.bytes(), st));
-        {
-            KernelTimer kt(ctx, "lds_count", 16.0 * (double)n_desc);
-            hipLaunchKernelGGL(k_lds_count, dim3((unsigned)std::min<uint64_t>(F, (uint64_t)ctx->n_cu)), dim3(kCThreads), 0, st,
-                               fine.p, dfine.p, F, E, out.keys.p, out.counts.p, out_cap, dcnt.p, ovf_list.p,
-                               dcnt.p + 1, prof_c ? dprof.p : nullptr);
-            LAUNCH_OK();
-            kt.stop();
-        }
-        if (prof_c) {
-            unsigned long long hp[8];
-            HIP_OK(hipMemcpy(hp, dprof.p, 64, hipMemcpyDeviceToHost));
-            const double waves = (double)std::min<uint64_t>(F, (uint64_t)ctx->n_cu) * kCWaves;
-            fprintf(stderr, "[mcaat] pass C per-wave ms: clear %.1f collapse %.1f expand %.1f emit %.1f; raw partitions %.0f (probe fails %llu), distinct descriptors %llu of %llu\n",
-                    hp[0] / waves / 1e5, hp[1] / waves / 1e5, hp[2] / waves / 1e5, hp[3] / waves / 1e5, (double)hp[4], hp[5], hp[6], hp[7]);
-        }
-        unsigned long long hc[2];
-        HIP_OK(hipMemcpyAsync(hc, dcnt.p, 16, hipMemcpyDeviceToHost, st));
-        HIP_OK(hipStreamSynchronize(st));
-        uint64_t n_out = hc[0];
-        const uint64_t n_ovf = hc[1];
-        // algorithmic bytes of the LDS count: descriptors read once + (key, count) written once
-        ctx->kstats["lds_count"].bytes_per_launch = 16.0 * (double)n_desc + 12.0 * (double)n_out;
-        ctx->kstats["lds_count_overflow_partitions"].launches = n_ovf;
-        if (n_ovf) {
-            // global-table fallback for the partitions whose distinct edges overflowed LDS,
-            // in batches whose table fits a fixed memory budget
-            DevBuf<uint64_t> occ(n_ovf);
-            hipLaunchKernelGGL(k_part_occ, dim3((unsigned)std::min<uint64_t>(n_ovf, 65536)), dim3(kBlock), 0, st,
-                               fine.p, dfine.p, ovf_list.p, n_ovf, occ.p);
-            LAUNCH_OK();
-            std::vector<uint64_t> occ_h(n_ovf);
-            std::vector<uint32_t> parts_h(n_ovf);
-            HIP_OK(hipMemcpyAsync(occ_h.data(), occ.p, 8 * n_ovf, hipMemcpyDeviceToHost, st));
-            HIP_OK(hipMemcpyAsync(parts_h.data(), ovf_list.p, 4 * n_ovf, hipMemcpyDeviceToHost, st));
-            HIP_OK(hipStreamSynchronize(st));
-            const uint64_t budget = 1ULL << 30;  // occurrences per batch (table <= 32 GB)
-            DevBuf<unsigned long long> nn(1);
-            DevBuf<int> dover(1);
-            DevBuf<uint32_t> dparts(n_ovf);
-            for (uint64_t q0 = 0; q0 < n_ovf;) {
-                uint64_t q1 = q0, occ_b = 0;
-                while (q1 < n_ovf && (q1 == q0 || occ_b + occ_h[q1] <= budget)) occ_b += occ_h[q1++];
-                HIP_OK(hipMemcpyAsync(dparts.p, parts_h.data() + q0, 4 * (q1 - q0), hipMemcpyHostToDevice, st));
-                uint64_t tcap = next_pow2(occ_b + occ_b / 2 + 1024);
-                for (;;) {
-                    DevBuf<Slot> tab(tcap);
-                    HIP_OK(hipMemsetAsync(tab.p, 0, tab.bytes(), st));
-                    HIP_OK(hipMemsetAsync(nn.p, 0, 8, st));
-                    HIP_OK(hipMemsetAsync(dover.p, 0, 4, st));
-                    hipLaunchKernelGGL(k_fallback, dim3((unsigned)std::min<uint64_t>(q1 - q0, 65536)), dim3(kBlock), 0,
-                                       st, fine.p, dfine.p, dparts.p, q1 - q0, E, tab.p, tcap - 1, nn.p, dover.p);
-                    LAUNCH_OK();
-                    int over = 0;
-                    HIP_OK(hipMemcpyAsync(&over, dover.p, 4, hipMemcpyDeviceToHost, st));
-                    HIP_OK(hipStreamSynchronize(st));
-                    if (over) {
-                        tcap <<= 1;
-                        continue;
-                    }
-                    hipLaunchKernelGGL(k_fallback_emit, dim3(grid_for(tcap, kBlock, 65536)), dim3(kBlock), 0, st,
-                                       tab.p, tcap, out.keys.p, out.counts.p, out_cap, dcnt.p);
-                    LAUNCH_OK();
-                    HIP_OK(hipStreamSynchronize(st));
-                    break;
-                }
-                q0 = q1;
-            }
-            HIP_OK(hipMemcpyAsync(hc, dcnt.p, 8, hipMemcpyDeviceToHost, st));
-            HIP_OK(hipStreamSynchronize(st));
-            n_out = hc[0];
-        }
-        if (n_out <= out_cap) {
-            out.n = n_out;
-            verbose_mark(ctx, "node_counter.C");
-            break;
-        }
-        if (attempt > 0) throw Error(MCAAT_E_CAPACITY, "node_counter: output sizing failed");
-        out_cap = n_out;  // exact on the second run
-    }
+    out.n = n_out;
+    verbose_mark(ctx, "node_counter.C");
 }
 
 void sort_counts(mcaat_ctx *ctx, CountResult &c, int k) {
