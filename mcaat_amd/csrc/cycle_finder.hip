@@ -77,12 +77,19 @@ __global__ void __launch_bounds__(kBlock) k_popcount(const uint64_t *bm, uint64_
 }
 
 // ------------------------------- peel --------------------------------------
+// kind[e]: 0x7F invalid edge, else valid out-degree (0..4) | 0x80 when e is a ruler.
+// nxk[e] (unary e): its sole successor in bits 0..55 and the successor's kind in 56..63, so a
+// ruler walk pays one dependent load per step.
+constexpr uint8_t kInvalid = 0x7F, kRulerBit = 0x80;
+constexpr uint64_t kNodeMask = (1ULL << 56) - 1;
+__device__ __forceinline__ int kind_od(uint8_t k) { return k & 0x7F; }
+__device__ __forceinline__ bool kind_chain(uint8_t k) { return k == 1; }  // unary, not a ruler
+
 struct PeelArrays {
-    uint8_t *od;      // valid out-degree, 0xFF = invalid edge
+    uint8_t *kind;
     uint8_t *upred;   // 1: some unary node points here
-    uint8_t *ruler;   // 1: unary node chosen as ruler
-    uint8_t *st;      // kUnk / kRem / kSurv
-    uint64_t *nxt;    // sole successor of a unary node
+    uint8_t *st;      // kUnk / kRem / kSurv (non-unary nodes)
+    uint64_t *nxk;    // successor | successor kind << 56 (unary nodes)
     uint64_t *owner;  // ruler whose walk passed this node (kNone: none)
     uint64_t *jump;   // for rulers: terminal reached (kNone: cycle)
     const uint64_t *seed;  // tips bitmap collected before the multiplicity filter
@@ -91,24 +98,70 @@ struct PeelArrays {
 __global__ void __launch_bounds__(kBlock) k_peel_init(GraphView g, PeelArrays pa) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < g.D; e += stride) {
-        if (!bit_get(g.valid, e)) { pa.od[e] = 0xFF; continue; }
+        if (!bit_get(g.valid, e)) { pa.kind[e] = kInvalid; continue; }
         uint64_t out[4];
         const int n = dev_outgoing(g, e, out);
-        pa.od[e] = (uint8_t)n;
+        pa.kind[e] = (uint8_t)n;
         if (n == 1) {
-            pa.nxt[e] = out[0];
+            pa.nxk[e] = out[0];
             pa.upred[out[0]] = 1;
         }
     }
 }
 
-__global__ void __launch_bounds__(kBlock) k_peel_rulers(uint64_t D, PeelArrays pa) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < D; e += stride) {
-        bool r = false;
-        if (pa.od[e] == 1) r = pa.upred[e] == 0 || (mix64(e ^ 0x5eed) & 63) == 0;
-        pa.ruler[e] = r;
+// rulers: unary nodes without a unary predecessor (chain heads) plus 1/64 of the others;
+// compacted into list by wave ballots, one cursor atomic per 4096-edge tile
+constexpr int kTileJ = 16;  // 64-edge words per wave per tile
+__global__ void __launch_bounds__(kBlock) k_peel_rulers(uint64_t D, PeelArrays pa, uint64_t *list,
+                                                        unsigned long long *cursor) {
+    __shared__ uint32_t wcnt[kBlock / 64];
+    __shared__ unsigned long long tbase;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t tile = (uint64_t)kBlock * kTileJ;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * tile; t0 < D; t0 += (uint64_t)gridDim.x * tile) {
+        unsigned long long m[kTileJ];
+        uint32_t c = 0;
+#pragma unroll
+        for (int j = 0; j < kTileJ; ++j) {
+            const uint64_t e = t0 + (uint64_t)j * kBlock + threadIdx.x;
+            bool r = false;
+            if (e < D && pa.kind[e] == 1) {
+                r = pa.upred[e] == 0 || (mix64(e ^ 0x5eed) & 63) == 0;
+                if (r) pa.kind[e] = 1 | kRulerBit;
+            }
+            m[j] = __ballot(r);
+            c += __popcll(m[j]);
+        }
+        if (lane == 0) wcnt[wave] = c;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t t = 0;
+            for (int w = 0; w < kBlock / 64; ++w) {
+                const uint32_t x = wcnt[w];
+                wcnt[w] = t;
+                t += x;
+            }
+            tbase = t ? atomicAdd(cursor, (unsigned long long)t) : 0;
+        }
+        __syncthreads();
+        uint64_t off = tbase + wcnt[wave];
+        const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+#pragma unroll
+        for (int j = 0; j < kTileJ; ++j) {
+            if ((m[j] >> lane) & 1) list[off + __popcll(m[j] & lt)] = t0 + (uint64_t)j * kBlock + threadIdx.x;
+            off += __popcll(m[j]);
+        }
+        __syncthreads();
     }
+}
+
+__global__ void __launch_bounds__(kBlock) k_peel_pack(uint64_t D, PeelArrays pa) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < D; e += stride)
+        if (kind_od(pa.kind[e]) == 1) {
+            const uint64_t y = pa.nxk[e];
+            pa.nxk[e] = y | ((uint64_t)pa.kind[y] << 56);
+        }
 }
 
 // each ruler walks its chain to the next ruler or non-unary node (Brent cycle check)
@@ -117,15 +170,16 @@ __global__ void __launch_bounds__(kBlock) k_peel_walk(PeelArrays pa, const uint6
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nr; i += stride) {
         const uint64_t r = list[i];
         pa.owner[r] = r;
-        uint64_t y = pa.nxt[r], tort = r;
+        uint64_t w = pa.nxk[r], tort = r;
         uint64_t power = 1, lam = 1;
         uint64_t res = kNone;
         for (;;) {
-            if (pa.od[y] != 1 || pa.ruler[y]) { res = y; break; }
+            const uint64_t y = w & kNodeMask;
+            if (!kind_chain((uint8_t)(w >> 56))) { res = y; break; }
             if (y == tort) { res = kNone; break; }  // ruler-less unary cycle reached
             pa.owner[y] = r;
             if (power == lam) { tort = y; power <<= 1; lam = 0; }
-            y = pa.nxt[y];
+            w = pa.nxk[y];
             ++lam;
         }
         pa.jump[r] = res;
@@ -137,19 +191,22 @@ __global__ void __launch_bounds__(kBlock) k_peel_jump(PeelArrays pa, const uint6
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nr; i += stride) {
         const uint64_t r = list[i];
         const uint64_t j = pa.jump[r];
-        if (j != kNone && pa.od[j] == 1) pa.jump[r] = pa.jump[j];
+        if (j != kNone && kind_od(pa.kind[j]) == 1) pa.jump[r] = pa.jump[j];
     }
 }
 
 __device__ __forceinline__ uint8_t peel_res(const PeelArrays &pa, uint64_t y) {
-    if (pa.od[y] != 1) return pa.st[y];
-    const uint64_t o = pa.ruler[y] ? y : pa.owner[y];
+    const uint8_t k = pa.kind[y];
+    if (kind_od(k) != 1) return pa.st[y];
+    const uint64_t o = (k & kRulerBit) ? y : pa.owner[y];
     if (o == kNone) return kSurv;  // unary node on a ruler-less cycle
     const uint64_t t = pa.jump[o];
-    if (t == kNone || pa.od[t] == 1) return kSurv;  // chain ends in a unary cycle
+    if (t == kNone || kind_od(pa.kind[t]) == 1) return kSurv;  // chain ends in a unary cycle
     return pa.st[t];
 }
 
+// non-unary valid nodes: seeds without successors are removed, the rest wait for their
+// successors; branch nodes (out-degree >= 2) and removed seeds are listed
 __global__ void __launch_bounds__(kBlock) k_peel_term(uint64_t D, PeelArrays pa, uint64_t *blist,
                                                       unsigned long long *cursor) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -158,10 +215,15 @@ __global__ void __launch_bounds__(kBlock) k_peel_term(uint64_t D, PeelArrays pa,
         const uint64_t e = base + threadIdx.x;
         bool br = false;
         if (e < D) {
-            const uint8_t o = pa.od[e];
-            if (o == 0) pa.st[e] = bit_get(pa.seed, e) ? kRem : kSurv;
-            else pa.st[e] = kUnk;
-            br = (o != 0xFF && o >= 2);
+            const uint8_t o = pa.kind[e];
+            if (o == 0) {
+                const bool rm = bit_get(pa.seed, e);
+                pa.st[e] = rm ? kRem : kSurv;
+                br = rm;
+            } else {
+                pa.st[e] = kUnk;
+                br = o != kInvalid && kind_od(o) >= 2;
+            }
         }
         const unsigned long long m = __ballot(br);
         unsigned long long off = 0;
@@ -190,16 +252,28 @@ __global__ void __launch_bounds__(kBlock) k_peel_branch(GraphView g, PeelArrays 
     }
 }
 
-__global__ void __launch_bounds__(kBlock) k_peel_apply(GraphView g, PeelArrays pa) {
-    const int lane = threadIdx.x & 63;
-    const uint64_t nw = (g.D + 63) / 64;
-    const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nw; w += wstride) {
-        const uint64_t e = w * 64 + lane;
-        bool rem = false;
-        if (e < g.D && pa.od[e] != 0xFF) rem = peel_res(pa, e) == kRem;
-        const unsigned long long m = __ballot(rem);
-        if (lane == 0 && m) g.valid[w] &= ~m;
+__device__ __forceinline__ void clear_valid(GraphView &g, uint64_t e) {
+    atomicAnd((unsigned long long *)&g.valid[e >> 6], ~(1ull << (e & 63)));
+}
+
+// removal: listed non-unary nodes resolved kRem, and the chain segments of rulers whose
+// terminal was removed (each segment re-walked; only removed ones are visited)
+__global__ void __launch_bounds__(kBlock) k_peel_apply_list(GraphView g, PeelArrays pa, const uint64_t *blist,
+                                                            uint64_t nb) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += stride)
+        if (pa.st[blist[i]] == kRem) clear_valid(g, blist[i]);
+}
+
+__global__ void __launch_bounds__(kBlock) k_peel_apply_rulers(GraphView g, PeelArrays pa, const uint64_t *list,
+                                                              uint64_t nr) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nr; i += stride) {
+        const uint64_t r = list[i];
+        if (peel_res(pa, r) != kRem) continue;  // a removed chain ends at a non-unary node: no cycle
+        clear_valid(g, r);
+        for (uint64_t w = pa.nxk[r]; kind_chain((uint8_t)(w >> 56)); w = pa.nxk[w & kNodeMask])
+            clear_valid(g, w & kNodeMask);
     }
 }
 
@@ -686,18 +760,21 @@ static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm) {
     const uint64_t D = g->D;
     if (!D) return;
     GraphView v = g->view();
-    DevBuf<uint8_t> od(D), upred(D), ruler(D), stt(D);
-    DevBuf<uint64_t> nxt(D), owner(D), jump(D);
+    DevBuf<uint8_t> kind(D), upred(D), stt(D);
+    DevBuf<uint64_t> nxk(D), owner(D), jump(D);
     HIP_OK(hipMemsetAsync(upred.p, 0, D, st));
     HIP_OK(hipMemsetAsync(owner.p, 0xFF, owner.bytes(), st));
-    PeelArrays pa{od.p, upred.p, ruler.p, stt.p, nxt.p, owner.p, jump.p, seed_bm};
+    PeelArrays pa{kind.p, upred.p, stt.p, nxk.p, owner.p, jump.p, seed_bm};
     hipLaunchKernelGGL(k_peel_init, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, v, pa);
     LAUNCH_OK();
     DevBuf<unsigned long long> cur(1);
     DevBuf<uint64_t> list(D);
-    hipLaunchKernelGGL(k_peel_rulers, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, D, pa);
+    HIP_OK(hipMemsetAsync(cur.p, 0, 8, st));
+    hipLaunchKernelGGL(k_peel_rulers, dim3(grid_for(D, kBlock * kTileJ)), dim3(kBlock), 0, st, D, pa, list.p, cur.p);
     LAUNCH_OK();
-    const uint64_t nr = select_flagged(ctx, ruler.p, D, list.p, cur.p);
+    hipLaunchKernelGGL(k_peel_pack, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, D, pa);
+    LAUNCH_OK();
+    const uint64_t nr = read_counter(ctx, cur.p);
     if (nr) {
         hipLaunchKernelGGL(k_peel_walk, dim3(grid_for(nr, kBlock)), dim3(kBlock), 0, st, pa, list.p, nr);
         LAUNCH_OK();
@@ -709,14 +786,15 @@ static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm) {
             LAUNCH_OK();
         }
     }
+    DevBuf<uint64_t> blist(D);
     HIP_OK(hipMemsetAsync(cur.p, 0, 8, st));
-    hipLaunchKernelGGL(k_peel_term, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, D, pa, list.p, cur.p);
+    hipLaunchKernelGGL(k_peel_term, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, D, pa, blist.p, cur.p);
     LAUNCH_OK();
     const uint64_t nb = read_counter(ctx, cur.p);
     DevBuf<int> changed(1);
     for (uint64_t it = 0; nb && it < D + 1; ++it) {
         HIP_OK(hipMemsetAsync(changed.p, 0, 4, st));
-        hipLaunchKernelGGL(k_peel_branch, dim3(grid_for(nb, kBlock)), dim3(kBlock), 0, st, v, pa, list.p, nb,
+        hipLaunchKernelGGL(k_peel_branch, dim3(grid_for(nb, kBlock)), dim3(kBlock), 0, st, v, pa, blist.p, nb,
                            changed.p);
         LAUNCH_OK();
         int h = 0;
@@ -724,8 +802,15 @@ static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm) {
         HIP_OK(hipStreamSynchronize(st));
         if (!h) break;
     }
-    hipLaunchKernelGGL(k_peel_apply, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, v, pa);
-    LAUNCH_OK();
+    // resolution reads valid bits (dev_outgoing), so removal waits until it is complete
+    if (nb) {
+        hipLaunchKernelGGL(k_peel_apply_list, dim3(grid_for(nb, kBlock)), dim3(kBlock), 0, st, v, pa, blist.p, nb);
+        LAUNCH_OK();
+    }
+    if (nr) {
+        hipLaunchKernelGGL(k_peel_apply_rulers, dim3(grid_for(nr, kBlock)), dim3(kBlock), 0, st, v, pa, list.p, nr);
+        LAUNCH_OK();
+    }
     HIP_OK(hipStreamSynchronize(st));
 }
 
@@ -748,7 +833,9 @@ static void run_peel(mcaat_graph *g, const uint64_t *seed_bm) {
                        cur.p);
     LAUNCH_OK();
     uint64_t n = read_counter(ctx, cur.p);
+    static const bool verbose = getenv("MCAAT_VERBOSE") && getenv("MCAAT_VERBOSE")[0] == '1';
     while (n) {
+        if (verbose) fprintf(stderr, "[mcaat] peel: kahn frontier %llu\n", (unsigned long long)n);
         HIP_OK(hipMemsetAsync(cur.p, 0, 8, st));
         hipLaunchKernelGGL(k_kahn_walk, dim3(grid_for(n, 64)), dim3(64), 0, st, v, rem.p, fa.p, n, fb.p, cur.p,
                            kBudget, pend.p, cur.p + 1);
@@ -757,6 +844,7 @@ static void run_peel(mcaat_graph *g, const uint64_t *seed_bm) {
         std::swap(fa, fb);
     }
     const uint64_t np = read_counter(ctx, cur.p + 1);
+    if (verbose) fprintf(stderr, "[mcaat] peel: pending after kahn walks %llu\n", (unsigned long long)np);
     if (np) {
         DevBuf<uint64_t> bm(nw);
         HIP_OK(hipMemsetAsync(bm.p, 0, bm.bytes(), st));
@@ -992,7 +1080,9 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out) {
     StageTimer timer(ctx);
     DevBuf<unsigned long long> cnt(1);
     auto zero = [&]() { HIP_OK(hipMemsetAsync(cnt.p, 0, 8, st)); };
-    const unsigned wgrid = grid_for(nw * 64, kBlock);
+    // grid-stride scans whose per-block totals meet in one counter: a capped grid keeps that
+    // counter's atomics to a few thousand
+    const unsigned wgrid = grid_for(nw * 64, kBlock, (unsigned)ctx->n_cu * 16);
 
     // 1. CollectTips (before the multiplicity filter) -> seeds of the reduction
     DevBuf<uint64_t> seeds(nw);
@@ -1016,7 +1106,8 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out) {
     verbose_mark(ctx, "cf.peel");
     // 4. valid count + tips after pruning
     zero();
-    hipLaunchKernelGGL(k_popcount, dim3(grid_for(nw, kBlock)), dim3(kBlock), 0, st, g->valid.p, nw, cnt.p);
+    hipLaunchKernelGGL(k_popcount, dim3(grid_for(nw, kBlock, (unsigned)ctx->n_cu * 16)), dim3(kBlock), 0, st,
+                       g->valid.p, nw, cnt.p);
     LAUNCH_OK();
     out->stats[2] = read_counter(ctx, cnt.p);
     zero();
