@@ -391,8 +391,10 @@ __device__ __forceinline__ bool set_contains(const uint64_t *tab, uint32_t cap, 
 
 __global__ void __launch_bounds__(kBlock) k_dls(GraphView g, const uint64_t *cand, uint64_t n, int limit,
                                                 uint64_t *stack_all, uint32_t cs, uint64_t *vis_all, uint32_t cv,
-                                                int8_t *res) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                                int8_t *res, int lpw) {
+    // lpw searches per wave (divergent searches serialise each other's branches)
+    if ((int)(threadIdx.x & 63) >= lpw) return;
+    const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64 * lpw + (threadIdx.x & 63);
     if (i >= n) return;
     uint64_t *stk = stack_all + i * cs;
     uint64_t *vis = vis_all + i * cv;
@@ -525,10 +527,13 @@ struct FcThread {
     }
 };
 
+// lpw searches per wave: each search is a divergent pointer-chasing state machine, so lanes
+// of one wave serialise each other's branches; few lanes per wave keep searches independent
 __global__ void __launch_bounds__(64) k_findcycle(GraphView g, const uint64_t *visited, const uint64_t *starts,
                                                   uint64_t n, FcCaps caps, FcParams prm, uint64_t *sbase,
-                                                  FcStatus *stat) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                                  FcStatus *stat, int lpw) {
+    if ((int)threadIdx.x >= lpw) return;
+    const uint64_t i = (uint64_t)blockIdx.x * lpw + threadIdx.x;
     if (i >= n) return;
     // carve this thread's scratch
     const uint64_t per = (uint64_t)caps.P * 8 + caps.P * 4 + caps.P * 32 + caps.P + (uint64_t)caps.CL * 12 +
@@ -735,19 +740,26 @@ uint64_t select_flagged(mcaat_ctx *ctx, const uint8_t *flags, uint64_t n, uint64
 }
 
 
-// host visited mirror: dense bitmap from calloc (pages are zero-filled lazily, so only the
-// pages holding visited nodes are ever touched)
+// host visited mirror: a dense bitmap in the context's pool (faulted in on first use only);
+// the words touched are recorded and zeroed again when the mirror goes away
 struct HostBits {
-    uint64_t *w = nullptr;
-    explicit HostBits(uint64_t D) {
-        w = (uint64_t *)calloc((D + 63) / 64 + 1, 8);
-        if (!w) throw std::bad_alloc();
+    uint64_t *w;
+    std::vector<uint64_t> touched;
+    HostBits(mcaat_ctx *ctx, uint64_t D) {
+        ctx->host_bits.ensure((D + 63) / 64 + 1);
+        w = ctx->host_bits.p;
     }
-    ~HostBits() { free(w); }
+    ~HostBits() {
+        for (uint64_t i : touched) w[i] = 0;
+    }
     HostBits(const HostBits &) = delete;
     HostBits &operator=(const HostBits &) = delete;
     bool get(uint64_t x) const { return (w[x >> 6] >> (x & 63)) & 1; }
-    void set(uint64_t x) { w[x >> 6] |= 1ULL << (x & 63); }
+    void set(uint64_t x) {
+        uint64_t &v = w[x >> 6];
+        if (!v) touched.push_back(x >> 6);
+        v |= 1ULL << (x & 63);
+    }
     void clear(uint64_t x) { w[x >> 6] &= ~(1ULL << (x & 63)); }
 };
 
@@ -873,8 +885,9 @@ static std::vector<uint64_t> run_dls(mcaat_graph *g, const std::vector<uint64_t>
             DevBuf<uint64_t> dids(n), dstk(n * cs), dvis(n * cv);
             DevBuf<int8_t> dres(n);
             HIP_OK(hipMemcpyAsync(dids.p, ids.data(), 8 * n, hipMemcpyHostToDevice, st));
-            hipLaunchKernelGGL(k_dls, dim3(grid_for(n, 64)), dim3(64), 0, st, g->view(), dids.p, n, limit, dstk.p, cs,
-                               dvis.p, cv, dres.p);
+            constexpr int kDlsLanes = 4;
+            hipLaunchKernelGGL(k_dls, dim3(grid_for(n, kDlsLanes)), dim3(64), 0, st, g->view(), dids.p, n, limit, dstk.p,
+                               cs, dvis.p, cv, dres.p, kDlsLanes);
             LAUNCH_OK();
             std::vector<int8_t> h(n);
             HIP_OK(hipMemcpyAsync(h.data(), dres.p, n, hipMemcpyDeviceToHost, st));
@@ -907,7 +920,7 @@ struct FcRunner {
     mcaat_cycles *out;
     uint64_t rounds = 0, reruns = 0;
 
-    FcRunner(mcaat_graph *gr, const mcaat_cf_params &p, mcaat_cycles *o) : g(gr), hvis(gr->D), out(o) {
+    FcRunner(mcaat_graph *gr, const mcaat_cf_params &p, mcaat_cycles *o) : g(gr), hvis(gr->ctx, gr->D), out(o) {
         prm.maxl = p.cycle_max_length;
         prm.minl = p.cycle_min_length;
         prm.cluster = p.cluster_bound;
@@ -929,7 +942,7 @@ struct FcRunner {
     void run_bucket(const std::vector<uint64_t> &bucket) {
         hipStream_t st = g->ctx->stream;
         std::vector<uint64_t> pending(bucket);
-        uint64_t window = 1024;
+        uint64_t window = 8192;
         while (!pending.empty()) {
             // starts already visited are skipped by the reference (:476) -> no entry
             std::vector<uint64_t> keep;
@@ -945,12 +958,14 @@ struct FcRunner {
             DevBuf<uint8_t> scratch(W * pa);
             DevBuf<FcStatus> dstat(W);
             HIP_OK(hipMemcpyAsync(dst.p, pending.data(), 8 * W, hipMemcpyHostToDevice, st));
-            hipLaunchKernelGGL(k_findcycle, dim3(grid_for(W, 64)), dim3(64), 0, st, g->view(), dvis.p, dst.p, W, caps,
-                               prm, (uint64_t *)scratch.p, dstat.p);
+            static const int lpw = getenv("MCAAT_FC_LPW") ? atoi(getenv("MCAAT_FC_LPW")) : 1;  // measured: 64 lanes 93 ms, 16: 44, 4: 30, 1: 23 (C3)
+            hipLaunchKernelGGL(k_findcycle, dim3(grid_for(W, (unsigned)lpw)), dim3(64), 0, st, g->view(), dvis.p, dst.p,
+                               W, caps, prm, (uint64_t *)scratch.p, dstat.p, lpw);
             LAUNCH_OK();
             std::vector<FcStatus> hs(W);
             HIP_OK(hipMemcpyAsync(hs.data(), dstat.p, W * sizeof(FcStatus), hipMemcpyDeviceToHost, st));
             HIP_OK(hipStreamSynchronize(st));
+            verbose_mark(g->ctx, "fc.round_kernel");
             // outputs of every thread that finished (status 0) with cycles
             std::vector<uint64_t> sel, noff{0}, coff{0};
             std::vector<int64_t> sel_of(W, -1);
@@ -979,6 +994,7 @@ struct FcRunner {
                 HIP_OK(hipMemcpyAsync(lens.data(), dl.p, 2 * lens.size(), hipMemcpyDeviceToHost, st));
                 HIP_OK(hipStreamSynchronize(st));
             }
+            verbose_mark(g->ctx, "fc.round_gather");
             // tentative sequential commit (threads=1 semantics), applied directly to the
             // host visited bitmap and rolled back past the first conflicting start
             std::vector<uint64_t> newly;
@@ -1053,6 +1069,7 @@ struct FcRunner {
                 LAUNCH_OK();
                 HIP_OK(hipStreamSynchronize(st));
             }
+            verbose_mark(g->ctx, "fc.round_commit");
             if (f < W) ++reruns;
             if (f == first_bad && first_bad < W) {
                 // scratch overflow at position f: grow the exhausted structure and re-run
@@ -1158,8 +1175,12 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out) {
         for (uint64_t id : kv.second) { out->cand_ids.push_back(id); out->cand_bucket.push_back(kv.first); }
     out->stats[4] = out->cand_ids.size();
     // 6. bucket loop
+    verbose_mark(ctx, "cf.chunks");
     FcRunner fr(g, p, out);
-    for (auto &kv : chunks) fr.run_bucket(kv.second);
+    verbose_mark(ctx, "cf.fc_setup");
+    // with threads=1 the reference's bucket loop is one ordered sequence of starts, so the
+    // speculative windows run across bucket boundaries
+    fr.run_bucket(out->cand_ids);
     out->stats[6] = fr.rounds;
     out->stats[7] = fr.reruns;
     timer.mark("find_cycle");

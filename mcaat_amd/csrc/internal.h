@@ -9,6 +9,10 @@
 #include <string>
 #include <utility>
 #include <vector>
+#include <sys/mman.h>
+#include <cstring>
+#include <cstdlib>
+#include <new>
 
 #include "../../include/mcaat_gpu.h"
 #include "common.h"
@@ -80,6 +84,28 @@ struct KernelStat {
     double total_bytes = 0;  // algorithmic bytes over all launches
 };
 
+struct HostPool {
+    uint64_t *p = nullptr;
+    size_t n = 0;  // words
+    HostPool() = default;
+    HostPool(const HostPool &) = delete;
+    HostPool &operator=(const HostPool &) = delete;
+    ~HostPool() { free(p); }
+    void ensure(size_t words) {
+        if (words <= n) return;
+        free(p);
+        p = nullptr;
+        n = 0;
+        const size_t huge = 2u << 20, bytes = (words * 8 + huge - 1) / huge * huge;
+        void *q = nullptr;
+        if (posix_memalign(&q, huge, bytes) != 0) throw std::bad_alloc();
+        madvise(q, bytes, MADV_HUGEPAGE);
+        memset(q, 0, bytes);
+        p = (uint64_t *)q;
+        n = bytes / 8;
+    }
+};
+
 }  // namespace mcaat
 
 struct mcaat_ctx {
@@ -89,6 +115,10 @@ struct mcaat_ctx {
     std::vector<std::pair<const char *, double>> stages;
     std::map<std::string, mcaat::KernelStat> kstats;
     bool timing = true;
+    // host bitmap pool reused by every CycleFinder call: 2-MB aligned and advised for huge
+    // pages (random bit probes over ~D/8 bytes), faulted in once; each call zeroes only the
+    // words it touched
+    mcaat::HostPool host_bits;
 };
 
 struct mcaat_reads {
