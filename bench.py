@@ -7,11 +7,16 @@ reads -> edge counting -> SDBG -> CycleFinder (results ready on the host).
 k-mers = N_occ = sum over reads of (L - k) edge occurrences.
 
 Workload (N=1): config C3 — ~300M x 150 bp reads, k=27, threshold_multiplicity=20,
-error rate tuned so the SDBG has ~1e9 edges (D). For N>1 every rank runs its own
-independent sample of the same size (weak scaling, no data-path collective;
-DESIGN.md §Multi-GPU); value = all ranks' k-mers / max-over-ranks step time.
+error rate tuned so the SDBG has ~1e9 edges (D).
+N>1, default --mode shard (config C4): the SAME C3 dataset is split over
+the ranks; each counts its slice, the oriented edges are routed to their owner rank by a
+hash(BOSS-key)-range all-to-all over RCCL (torch.distributed "nccl"), owners sort and sum,
+an all-gather in rank order gives every rank the single-GPU graph, and CycleFinder runs on
+it (scaling "strong": total work fixed). --mode replicas: every rank runs its own
+independent C3-sized sample, no collective on the data path (scaling "weak").
+value = all k-mers processed / max-over-ranks step time.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|tiny]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|tiny] [--mode shard|replicas]
        N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
 """
 from __future__ import annotations
@@ -111,6 +116,8 @@ def main() -> int:
     ap.add_argument("--cpu-sample-reads", type=int, default=2_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--mode", default="shard", choices=["shard", "replicas"],
+                    help="N>1: one dataset hash-range sharded over the ranks, or one dataset per rank")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU-only rehearsal of the control flow (ranks, barrier, max-reduce, JSON); no GPU work")
     args = ap.parse_args()
@@ -118,34 +125,56 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # control plane only (barrier, max of times)
-
-        dist.init_process_group("gloo")
+    sharded = world > 1 and args.mode == "shard"
     import torch
+
+    dist = None
+    cdev = torch.device("cpu")
+    if world > 1:
+        import torch.distributed as dist
+
+        if sharded and not args.dry_run and os.environ.get("MCAAT_COMM_BACKEND", "nccl") == "nccl":
+            # data path: RCCL all-to-all / all-gather of device tensors (MCAAT_COMM_BACKEND=gloo
+            # stages them through host memory instead: a rehearsal with ranks sharing one GPU)
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl")
+            cdev = torch.device("cuda", local)
+        else:  # control plane only (barrier, max of times)
+            dist.init_process_group("gloo")
 
     cfg = dict(CONFIGS[args.config])
     spec = M.SynthSpec(**cfg["spec"].__dict__)
     if args.reads:
         spec.n_reads = args.reads
-    spec.seed = spec.seed * 1000 + rank  # independent sample per rank (weak scaling)
+    if world > 1 and not sharded:
+        spec.seed = spec.seed * 1000 + rank  # independent sample per rank (weak scaling)
+    first = rank * spec.n_reads // world if sharded else 0
+    count = ((rank + 1) * spec.n_reads // world - first) if sharded else spec.n_reads
     k, thr = cfg["k"], cfg["thr"]
 
     if args.dry_run:
         ctx = _DryContext()
         reads = _DryReads()
     else:
+        if sharded:
+            local = local % max(1, torch.cuda.device_count())
+            torch.cuda.set_device(local)
         ctx = M.Context(local)
-        reads = M.Reads.synth(ctx, spec)
+        reads = M.Reads.synth_range(ctx, spec, first, count) if sharded else M.Reads.synth(ctx, spec)
     prm = M.CfParams(threshold_multiplicity=thr)
 
     def step():
         if args.dry_run:
             time.sleep(0.01 * (1 + rank))
             return 0, None, {}
-        g = M.Graph.build(ctx, reads, k)
-        st_build = ctx.stage_times()
+        if sharded:
+            from mcaat_amd import shard
+
+            st_build = {}
+            g = shard.sharded_build(shard.DeviceOps(ctx, k), reads, times=st_build)
+        else:
+            g = M.Graph.build(ctx, reads, k)
+            st_build = ctx.stage_times()
         d = g.size
         res = g.cycle_finder(prm)
         st_cf = ctx.stage_times()
@@ -174,7 +203,7 @@ def main() -> int:
     barrier()
     dt = (time.perf_counter() - t0) / max(1, args.steps)
     if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64)
+        t = torch.tensor([dt], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
@@ -185,8 +214,9 @@ def main() -> int:
         return a * l / max(1, args.steps)
     kern = max(HOT_KERNELS, key=per_step_ms)
     avg_ms, launches, bytes_per_launch = ctx.kernel_timing(kern)
-    kmers_rank = n_occ(spec, k)
-    value = kmers_rank * world / dt
+    kmers_rank = count * max(0, spec.read_len - k)
+    kmers_total = n_occ(spec, k) if sharded else kmers_rank * world
+    value = kmers_total / dt
     if rank == 0:
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         traffic = traffic_from_profiles(kern)
@@ -199,20 +229,23 @@ def main() -> int:
             "warmup": args.warmup,
             "ms_per_step": dt * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if sharded else "weak",
             "vs_baseline": None,
             "dtype": "u64",
             "data": "synthetic (counter-based RNG genomes with CRISPR arrays, reads generated in HBM)",
             "config": {
-                "workload": cfg["name"],
-                "reads_per_gpu": spec.n_reads,
+                "workload": (cfg["name"] + f", hash-range sharded over {world} GPUs (C4)") if sharded else cfg["name"],
+                "reads_per_gpu": count,
+                "reads_total": spec.n_reads if sharded else spec.n_reads * world,
                 "read_len": spec.read_len,
                 "k": k,
                 "threshold_multiplicity": thr,
                 "error_rate": spec.error_rate,
                 "kmers_per_gpu": kmers_rank,
+                "kmers_total": kmers_total,
                 "sdbg_edges_D": D,
-                "parallelism": f"replicas{world}",
+                "parallelism": (f"shard{world} (BOSS-key-range all-to-all + all-gather over RCCL)" if sharded
+                                else f"replicas{world}"),
                 "cycle_entries": len(res.entries) if res else 0,
                 "cycles": res.stats[5] if res else 0,
                 "cf_stats": list(res.stats) if res else None,

@@ -36,6 +36,7 @@ typedef struct mcaat_ctx mcaat_ctx;
 typedef struct mcaat_reads mcaat_reads;
 typedef struct mcaat_graph mcaat_graph;
 typedef struct mcaat_cycles mcaat_cycles;
+typedef struct mcaat_counts mcaat_counts;
 
 /* ---- context ------------------------------------------------------------- */
 /* Replaces: nothing in the reference (single process, OpenMP). Binds one GPU. */
@@ -73,6 +74,9 @@ typedef struct {
     int32_t paired; /* 1: pairs (fragment 300+-30, R2 = reverse complement of fragment end) */
 } mcaat_synth_spec;
 int mcaat_reads_synth(mcaat_ctx *ctx, const mcaat_synth_spec *spec, mcaat_reads **out);
+/* reads [first, first+count) of the same stream: a rank's slice of one dataset */
+int mcaat_reads_synth_range(mcaat_ctx *ctx, const mcaat_synth_spec *spec, uint64_t first, uint64_t count,
+                            mcaat_reads **out);
 /* host-side generator of the same reads (for tests and FASTQ fixtures) */
 int mcaat_synth_host(const mcaat_synth_spec *spec, uint64_t *packed, uint64_t *offsets);
 /* the genome sequences (n_genomes*genome_len bases, packed) and array truth */
@@ -104,6 +108,33 @@ int mcaat_graph_set_valid(mcaat_graph *g, const uint64_t *ids, size_t n, int val
 int mcaat_graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, int incoming,
                           uint64_t *out, int32_t *counts);
 void mcaat_graph_free(mcaat_graph *g);
+
+/* ---- multi-GPU build (one process per GPU) ---------------------
+ * Replaces: the single-process Read2SdbgS2::Run of sdbg_build.cpp:171-187 when the reads
+ * are split over ranks. Each rank counts its reads (mcaat_count_local), the ranks agree on
+ * owner ranges of the BOSS key from the summed histogram (mcaat_counts_histogram), each
+ * rank groups its oriented (BOSS key, partial count) pairs by owner
+ * (mcaat_counts_partition), the caller exchanges them (all-to-all over RCCL), each owner
+ * sorts and sums its pairs (mcaat_edges_reduce), the caller all-gathers the owners' arrays
+ * in rank order, and every rank builds the graph from them (mcaat_graph_from_sorted).
+ * Device pointers (_dev) are caller-owned device memory on this ctx's GPU. */
+int mcaat_count_local(mcaat_ctx *ctx, const mcaat_reads *r, int k, mcaat_counts **out);
+int mcaat_counts_info(const mcaat_counts *c, uint64_t *n_canonical);
+/* hist[2^bits] (host): oriented edges per value of the top `bits` of the 2(k+1)-bit BOSS key */
+int mcaat_counts_histogram(const mcaat_counts *c, int bits, uint64_t *hist);
+/* owner o takes BOSS keys in [splits[o-1], splits[o]) (splits ascending, n_owners-1 of them);
+ * writes the pairs owner-major into keys_dev/counts_dev (cap entries, >= 2 * n_canonical)
+ * and sizes[o] (host). Palindromes contribute one pair with twice the count. */
+int mcaat_counts_partition(const mcaat_counts *c, int n_owners, const uint64_t *splits, uint64_t *sizes,
+                           uint64_t *keys_dev, uint32_t *counts_dev, uint64_t cap);
+void mcaat_counts_free(mcaat_counts *c);
+/* sorts n received pairs by key and sums the counts of equal keys (saturating at 65535):
+ * *n_out unique keys ascending in keys_out_dev, multiplicities in mult_out_dev (n entries) */
+int mcaat_edges_reduce(mcaat_ctx *ctx, int k, const uint64_t *keys_dev, const uint32_t *counts_dev, uint64_t n,
+                       uint64_t *keys_out_dev, uint16_t *mult_out_dev, uint64_t *n_out);
+/* graph from D ascending unique BOSS keys and their multiplicities (copied) */
+int mcaat_graph_from_sorted(mcaat_ctx *ctx, int k, const uint64_t *keys_dev, const uint16_t *mult_dev, uint64_t D,
+                            mcaat_graph **out);
 
 /* ---- cycle_finder ------------------------------------------------------------
  * Replaces: CycleFinder::CycleFinder(Settings&) -> FindApproximateCRISPRArrays

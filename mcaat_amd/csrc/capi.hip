@@ -39,10 +39,11 @@ void require(bool c, const char *msg) {
 
 constexpr int kBlock = 256;
 
-__global__ void k_synth(mcaat_synth_spec s, const uint64_t *genome, uint64_t *packed, uint64_t n_words) {
+__global__ void k_synth(mcaat_synth_spec s, const uint64_t *genome, uint64_t *packed, uint64_t n_words,
+                        uint64_t first, uint64_t count) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < n_words; w += stride)
-        packed[w] = synth_word(s, genome, w);
+        packed[w] = synth_word(s, genome, w, first, count);
 }
 
 __global__ void k_fixed_offsets(uint64_t *off, uint64_t n, uint64_t L) {
@@ -199,25 +200,25 @@ void synth_genome_host(const mcaat_synth_spec &s, std::vector<uint64_t> &genome)
     }
 }
 
-void synth_reads(mcaat_ctx *ctx, const mcaat_synth_spec &s, mcaat_reads *out) {
+void synth_reads(mcaat_ctx *ctx, const mcaat_synth_spec &s, mcaat_reads *out, uint64_t first, uint64_t count) {
     std::vector<uint64_t> genome;
     synth_genome_host(s, genome);
     hipStream_t st = ctx->stream;
     DevBuf<uint64_t> dg(genome.size());
     HIP_OK(hipMemcpyAsync(dg.p, genome.data(), 8 * genome.size(), hipMemcpyHostToDevice, st));
     out->ctx = ctx;
-    out->n_reads = s.n_reads;
-    out->n_bases = s.n_reads * s.read_len;
+    out->n_reads = count;
+    out->n_bases = count * s.read_len;
     out->n_words = (out->n_bases + 31) / 32;
     out->fixed_len = s.read_len;
     out->packed.alloc(out->n_words + 16);
     out->offsets.alloc(s.n_reads + 1);
     HIP_OK(hipMemsetAsync(out->packed.p, 0, out->packed.bytes(), st));
     hipLaunchKernelGGL(k_synth, dim3(grid_for(out->n_words, kBlock)), dim3(kBlock), 0, st, s, dg.p, out->packed.p,
-                       out->n_words);
+                       out->n_words, first, count);
     LAUNCH_OK();
-    hipLaunchKernelGGL(k_fixed_offsets, dim3(grid_for(s.n_reads + 1, kBlock)), dim3(kBlock), 0, st,
-                       out->offsets.p, s.n_reads, (uint64_t)s.read_len);
+    hipLaunchKernelGGL(k_fixed_offsets, dim3(grid_for(count + 1, kBlock)), dim3(kBlock), 0, st,
+                       out->offsets.p, count, (uint64_t)s.read_len);
     LAUNCH_OK();
     HIP_OK(hipStreamSynchronize(st));
 }
@@ -330,7 +331,25 @@ int mcaat_reads_synth(mcaat_ctx *ctx, const mcaat_synth_spec *spec, mcaat_reads 
         HIP_OK(hipSetDevice(ctx->device));
         auto *r = new mcaat_reads;
         try {
-            synth_reads(ctx, *spec, r);
+            synth_reads(ctx, *spec, r, 0, spec->n_reads);
+        } catch (...) {
+            delete r;
+            throw;
+        }
+        *out = r;
+    });
+}
+
+int mcaat_reads_synth_range(mcaat_ctx *ctx, const mcaat_synth_spec *spec, uint64_t first, uint64_t count,
+                            mcaat_reads **out) {
+    return guarded([&] {
+        require(ctx && spec && out, "null argument");
+        check_spec(*spec);
+        require(first <= spec->n_reads && count <= spec->n_reads - first, "read range outside the spec");
+        HIP_OK(hipSetDevice(ctx->device));
+        auto *r = new mcaat_reads;
+        try {
+            synth_reads(ctx, *spec, r, first, count);
         } catch (...) {
             delete r;
             throw;
@@ -397,6 +416,91 @@ int mcaat_build_graph(mcaat_ctx *ctx, const mcaat_reads *r, int k, mcaat_graph *
             sdbg_build(ctx, c, k, g);
             timer.mark("sdbg_build");
             HIP_OK(hipStreamSynchronize(ctx->stream));
+            timer.finish();
+        } catch (...) {
+            delete g;
+            throw;
+        }
+        *out = g;
+    });
+}
+
+int mcaat_count_local(mcaat_ctx *ctx, const mcaat_reads *r, int k, mcaat_counts **out) {
+    return guarded([&] {
+        require(ctx && r && out, "null argument");
+        require(k >= 2 && k <= kMaxK, "k must be in [2, 30]");
+        HIP_OK(hipSetDevice(ctx->device));
+        auto *c = new mcaat_counts;
+        c->ctx = ctx;
+        c->k = k;
+        try {
+            StageTimer timer(ctx);
+            node_counter(ctx, r, k, c->c);
+            timer.mark("node_counter");
+            timer.finish();
+        } catch (...) {
+            delete c;
+            throw;
+        }
+        *out = c;
+    });
+}
+
+int mcaat_counts_info(const mcaat_counts *c, uint64_t *n_canonical) {
+    return guarded([&] {
+        require(c && n_canonical, "null argument");
+        *n_canonical = c->c.n;
+    });
+}
+
+int mcaat_counts_histogram(const mcaat_counts *c, int bits, uint64_t *hist) {
+    return guarded([&] {
+        require(c && hist, "null argument");
+        require(bits >= 1 && bits <= 13 && bits <= 2 * (c->k + 1), "histogram bits must be in [1, min(13, 2(k+1))]");
+        HIP_OK(hipSetDevice(c->ctx->device));
+        counts_histogram(c->ctx, c->c, c->k, bits, hist);
+    });
+}
+
+int mcaat_counts_partition(const mcaat_counts *c, int n_owners, const uint64_t *splits, uint64_t *sizes,
+                           uint64_t *keys_dev, uint32_t *counts_dev, uint64_t cap) {
+    return guarded([&] {
+        require(c && sizes && (n_owners == 1 || splits), "null argument");
+        require(n_owners >= 1 && n_owners <= 64, "n_owners must be in [1, 64]");
+        for (int i = 1; i + 1 < n_owners; ++i) require(splits[i - 1] <= splits[i], "splits must be ascending");
+        HIP_OK(hipSetDevice(c->ctx->device));
+        counts_partition(c->ctx, c->c, c->k, n_owners, splits, sizes, keys_dev, counts_dev, cap);
+    });
+}
+
+void mcaat_counts_free(mcaat_counts *c) {
+    if (!c) return;
+    (void)hipSetDevice(c->ctx->device);
+    delete c;
+}
+
+int mcaat_edges_reduce(mcaat_ctx *ctx, int k, const uint64_t *keys_dev, const uint32_t *counts_dev, uint64_t n,
+                       uint64_t *keys_out_dev, uint16_t *mult_out_dev, uint64_t *n_out) {
+    return guarded([&] {
+        require(ctx && n_out && (n == 0 || (keys_dev && counts_dev && keys_out_dev && mult_out_dev)), "null argument");
+        require(k >= 2 && k <= kMaxK, "k must be in [2, 30]");
+        HIP_OK(hipSetDevice(ctx->device));
+        *n_out = edges_reduce(ctx, k, keys_dev, counts_dev, n, keys_out_dev, mult_out_dev);
+    });
+}
+
+int mcaat_graph_from_sorted(mcaat_ctx *ctx, int k, const uint64_t *keys_dev, const uint16_t *mult_dev, uint64_t D,
+                            mcaat_graph **out) {
+    return guarded([&] {
+        require(ctx && out && (D == 0 || (keys_dev && mult_dev)), "null argument");
+        require(k >= 2 && k <= kMaxK, "k must be in [2, 30]");
+        HIP_OK(hipSetDevice(ctx->device));
+        auto *g = new mcaat_graph;
+        g->ctx = ctx;
+        try {
+            StageTimer timer(ctx);
+            graph_from_sorted(ctx, k, keys_dev, mult_dev, D, g);
+            timer.mark("sdbg_build");
             timer.finish();
         } catch (...) {
             delete g;

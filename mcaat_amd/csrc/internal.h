@@ -231,8 +231,16 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
 void verbose_mark(mcaat_ctx *ctx, const char *what);
 void sort_counts(mcaat_ctx *ctx, CountResult &c, int k);
 void sdbg_build(mcaat_ctx *ctx, CountResult &c, int k, mcaat_graph *g);
+void sdbg_finish(mcaat_ctx *ctx, mcaat_graph *g);
+// multi-GPU build pieces (shard.hip)
+void counts_histogram(mcaat_ctx *ctx, const CountResult &c, int k, int bits, uint64_t *hist_host);
+void counts_partition(mcaat_ctx *ctx, const CountResult &c, int k, int n_owners, const uint64_t *splits_host,
+                      uint64_t *sizes_host, uint64_t *okeys, uint32_t *ocnt, uint64_t cap);
+uint64_t edges_reduce(mcaat_ctx *ctx, int k, const uint64_t *keys, const uint32_t *cnt, uint64_t n, uint64_t *keys_out,
+                      uint16_t *mult_out);
+void graph_from_sorted(mcaat_ctx *ctx, int k, const uint64_t *keys, const uint16_t *mult, uint64_t D, mcaat_graph *g);
 void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out);
-void synth_reads(mcaat_ctx *ctx, const mcaat_synth_spec &s, mcaat_reads *out);
+void synth_reads(mcaat_ctx *ctx, const mcaat_synth_spec &s, mcaat_reads *out, uint64_t first, uint64_t count);
 void synth_genome_host(const mcaat_synth_spec &s, std::vector<uint64_t> &genome);
 void graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, int incoming, uint64_t *out,
                      int32_t *counts);
@@ -240,3 +248,10 @@ void graph_set_valid(mcaat_graph *g, const uint64_t *ids, size_t n, int valid);
 void graph_download_valid(const mcaat_graph *g, uint8_t *valid);
 
 }  // namespace mcaat
+
+struct mcaat_counts {  // device-resident canonical counts of one rank
+    mcaat_ctx *ctx = nullptr;
+    int k = 0;
+    mcaat::CountResult c;
+};
+

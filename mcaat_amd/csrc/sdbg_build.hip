@@ -141,8 +141,15 @@ void sdbg_build(mcaat_ctx *ctx, CountResult &c, int k, mcaat_graph *g) {
     HIP_OK(hipStreamSynchronize(st));
     ek.release();
     em.release();
-    const uint64_t D = n2 - n_pal;
-    g->D = D;
+    g->D = n2 - n_pal;
+    sdbg_finish(ctx, g);
+}
+
+// sorted unique (key, mult) in g -> directory, adjacency words, valid bitmap
+void sdbg_finish(mcaat_ctx *ctx, mcaat_graph *g) {
+    hipStream_t st = ctx->stream;
+    const int k = g->k, E = k + 1;
+    const uint64_t D = g->D;
 
     // radix directory: B top bits of the 2E-bit key, ~8-16 edges per bucket
     int lg = 0;

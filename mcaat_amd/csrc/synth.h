@@ -59,22 +59,28 @@ MCAAT_HD int synth_base(const mcaat_synth_spec &s, const uint64_t *genome, const
     return b;
 }
 
-// packed word w of the read stream (reads are fixed length, read r = bases [r*L, r*L+L))
-MCAAT_HD uint64_t synth_word(const mcaat_synth_spec &s, const uint64_t *genome, uint64_t w) {
-    const uint64_t L = s.read_len, total = s.n_reads * L;
+// packed word w of the stream of reads [first, first + count) (fixed length L: the slice's
+// read i = bases [i*L, i*L+L)); read indices stay global, so a rank's slice is exactly that
+// part of the single-stream reads
+MCAAT_HD uint64_t synth_word(const mcaat_synth_spec &s, const uint64_t *genome, uint64_t w, uint64_t first,
+                             uint64_t count) {
+    const uint64_t L = s.read_len, total = count * L;
     uint64_t v = 0;
     uint64_t j = w * 32;
     uint64_t r = j / L, pos = j - r * L;
-    ReadPlace p = synth_place(s, r);
+    ReadPlace p = synth_place(s, first + r);
     for (int i = 0; i < 32 && j < total; ++i, ++j) {
-        v |= (uint64_t)synth_base(s, genome, p, r, pos) << (2 * i);
+        v |= (uint64_t)synth_base(s, genome, p, first + r, pos) << (2 * i);
         if (++pos == L) {
             pos = 0;
             ++r;
-            if (r < s.n_reads) p = synth_place(s, r);
+            if (r < count) p = synth_place(s, first + r);
         }
     }
     return v;
+}
+MCAAT_HD uint64_t synth_word(const mcaat_synth_spec &s, const uint64_t *genome, uint64_t w) {
+    return synth_word(s, genome, w, 0, s.n_reads);
 }
 
 }  // namespace mcaat

@@ -90,6 +90,17 @@ SIGNATURES = {
     "mcaat_stage_times": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(C.c_int)]),
     "mcaat_kernel_timing": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_double), _u64p, C.POINTER(C.c_double)]),
     "mcaat_reset_timing": (None, [C.c_void_p]),
+    "mcaat_reads_synth_range": (C.c_int, [C.c_void_p, C.POINTER(_SynthSpec), C.c_uint64, C.c_uint64,
+                                          C.POINTER(C.c_void_p)]),
+    "mcaat_count_local": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
+    "mcaat_counts_info": (C.c_int, [C.c_void_p, _u64p]),
+    "mcaat_counts_histogram": (C.c_int, [C.c_void_p, C.c_int, _u64p]),
+    "mcaat_counts_partition": (C.c_int, [C.c_void_p, C.c_int, _u64p, _u64p, C.c_void_p, C.c_void_p, C.c_uint64]),
+    "mcaat_counts_free": (None, [C.c_void_p]),
+    "mcaat_edges_reduce": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p,
+                                     _u64p]),
+    "mcaat_graph_from_sorted": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64,
+                                          C.POINTER(C.c_void_p)]),
 }
 
 _lib: Optional[C.CDLL] = None
@@ -234,6 +245,14 @@ class Reads:
         return cls(ctx, h)
 
     @classmethod
+    def synth_range(cls, ctx: Context, spec: SynthSpec, first: int, count: int) -> "Reads":
+        """Reads [first, first+count) of the stream `synth` generates (a rank's slice)."""
+        h = C.c_void_p()
+        s = spec.to_c()
+        _check(ctx._lib.mcaat_reads_synth_range(ctx.h, C.byref(s), first, count, C.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
     def from_fastx(cls, ctx: Context, files: Sequence[str]) -> "Reads":
         arr = (C.c_char_p * len(files))(*[f.encode() for f in files])
         h = C.c_void_p()
@@ -280,6 +299,61 @@ def count_edges(ctx: Context, reads: Reads, k: int) -> Tuple[np.ndarray, np.ndar
     return keys, counts
 
 
+class Counts:
+    """Device-resident canonical counts of one rank (mcaat_counts; multi-GPU build)."""
+
+    def __init__(self, ctx: Context, h, k: int):
+        self.ctx = ctx
+        self.h = h
+        self.k = k
+
+    @classmethod
+    def count(cls, ctx: Context, reads: Reads, k: int) -> "Counts":
+        h = C.c_void_p()
+        _check(ctx._lib.mcaat_count_local(ctx.h, reads.h, k, C.byref(h)))
+        return cls(ctx, h, k)
+
+    @property
+    def n(self) -> int:
+        n = C.c_uint64(0)
+        _check(self.ctx._lib.mcaat_counts_info(self.h, C.byref(n)))
+        return n.value
+
+    def histogram(self, bits: int) -> np.ndarray:
+        h = np.zeros(1 << bits, dtype=np.uint64)
+        _check(self.ctx._lib.mcaat_counts_histogram(self.h, bits, _ptr(h, _u64p)))
+        return h
+
+    def partition(self, splits: np.ndarray, keys_dev: int, counts_dev: int, cap: int) -> np.ndarray:
+        """Owner-major oriented (BOSS key, count) pairs into device memory; returns sizes."""
+        splits = np.ascontiguousarray(splits, dtype=np.uint64)
+        sizes = np.zeros(len(splits) + 1, dtype=np.uint64)
+        sp = _ptr(splits, _u64p) if len(splits) else None
+        _check(self.ctx._lib.mcaat_counts_partition(self.h, len(splits) + 1, sp, _ptr(sizes, _u64p),
+                                                    C.c_void_p(keys_dev), C.c_void_p(counts_dev), cap))
+        return sizes
+
+    def free(self) -> None:
+        if self.h:
+            self.ctx._lib.mcaat_counts_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def edges_reduce(ctx: Context, k: int, keys_dev: int, counts_dev: int, n: int, keys_out_dev: int,
+                 mult_out_dev: int) -> int:
+    """Sort received (BOSS key, count) pairs and sum equal keys (device memory); returns #unique."""
+    out = C.c_uint64(0)
+    _check(ctx._lib.mcaat_edges_reduce(ctx.h, k, C.c_void_p(keys_dev), C.c_void_p(counts_dev), n,
+                                       C.c_void_p(keys_out_dev), C.c_void_p(mult_out_dev), C.byref(out)))
+    return out.value
+
+
 @dataclass
 class CfParams:
     threshold_multiplicity: int = 20
@@ -315,6 +389,13 @@ class Graph:
     def build(cls, ctx: Context, reads: Reads, k: int) -> "Graph":
         h = C.c_void_p()
         _check(ctx._lib.mcaat_build_graph(ctx.h, reads.h, k, C.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
+    def from_sorted(cls, ctx: Context, k: int, keys_dev: int, mult_dev: int, D: int) -> "Graph":
+        """Graph from ascending unique BOSS keys and multiplicities in device memory."""
+        h = C.c_void_p()
+        _check(ctx._lib.mcaat_graph_from_sorted(ctx.h, k, C.c_void_p(keys_dev), C.c_void_p(mult_dev), D, C.byref(h)))
         return cls(ctx, h)
 
     def info(self) -> Tuple[int, int]:

@@ -89,18 +89,24 @@ def test_synth_paired_reads_and_errors():
     assert diff > 0
 
 
-def test_bench_two_ranks_gloo_dry_run():
+@pytest.mark.parametrize("mode,port", [("replicas", 29561), ("shard", 29562)])
+def test_bench_two_ranks_gloo_dry_run(mode, port):
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", "--master-port=29561", os.path.join(ROOT, "bench.py"),
-           "--gpus", "2", "--steps", "2", "--warmup", "1", "--config", "tiny", "--dry-run"]
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "2", "--warmup", "1", "--config", "tiny", "--dry-run", "--mode", mode]
     out = subprocess.run(cmd, capture_output=True, text=True, env=env, timeout=300)
     assert out.returncode == 0, out.stderr[-2000:]
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1  # rank 0 only
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1 and d["scaling"] == "weak"
-    # value = all ranks' k-mers / max-over-ranks step time (rank 1 sleeps longer)
-    kmers = d["config"]["kmers_per_gpu"]
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["warmup"] == 1
+    # value = all k-mers processed / max-over-ranks step time (rank 1 sleeps longer)
     assert d["ms_per_step"] >= 19.0
-    assert abs(d["value"] - 2 * kmers / (d["ms_per_step"] / 1e3)) / d["value"] < 1e-6
+    total = d["config"]["kmers_total"]
+    assert abs(d["value"] - total / (d["ms_per_step"] / 1e3)) / d["value"] < 1e-6
+    if mode == "replicas":
+        assert d["scaling"] == "weak" and total == 2 * d["config"]["kmers_per_gpu"]
+    else:  # one dataset split over the ranks
+        assert d["scaling"] == "strong" and total == 2 * d["config"]["kmers_per_gpu"]
+        assert d["config"]["reads_total"] == 10_000
