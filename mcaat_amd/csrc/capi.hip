@@ -437,6 +437,7 @@ int mcaat_count_local(mcaat_ctx *ctx, const mcaat_reads *r, int k, mcaat_counts 
             StageTimer timer(ctx);
             node_counter(ctx, r, k, c->c);
             timer.mark("node_counter");
+            HIP_OK(hipStreamSynchronize(ctx->stream));
             timer.finish();
         } catch (...) {
             delete c;
@@ -501,6 +502,7 @@ int mcaat_graph_from_sorted(mcaat_ctx *ctx, int k, const uint64_t *keys_dev, con
             StageTimer timer(ctx);
             graph_from_sorted(ctx, k, keys_dev, mult_dev, D, g);
             timer.mark("sdbg_build");
+            HIP_OK(hipStreamSynchronize(ctx->stream));
             timer.finish();
         } catch (...) {
             delete g;

@@ -168,6 +168,7 @@ struct StageTimer {
     }
     // call after the stream is synchronised
     void finish() {
+        if (!marks.empty()) HIP_OK(hipEventSynchronize(marks.back().second));
         for (size_t i = 1; i < marks.size(); ++i) {
             float ms = 0;
             HIP_OK(hipEventElapsedTime(&ms, marks[i - 1].second, marks[i].second));

@@ -1032,9 +1032,12 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
         return;
     }
 
-    // fine partitions: ~64K edge occurrences each, 8 L1 bits + l2_bits
+    // fine partitions: ~8K edge occurrences each (8 L1 bits + l2_bits), so that even at
+    // ~5x coverage (a rank's share of a sharded dataset) a partition's distinct edges fit
+    // the LDS table; deep data reaches the 2^19 cap long before (C3: 70K occurrences each,
+    // ~1K distinct descriptors after the collapse)
     int fine_bits = 0;
-    while ((1ULL << (fine_bits + 1)) * 65536ULL <= n_occ) ++fine_bits;
+    while ((1ULL << (fine_bits + 1)) * 8192ULL <= n_occ) ++fine_bits;
     fine_bits = std::max(8, std::min(19, fine_bits));  // l2_bits <= 11: k_l2_scatter's line buffers
     P.l2_bits = fine_bits - 8;
     const uint32_t S = 1u << P.l2_bits;
