@@ -77,13 +77,15 @@ __global__ void __launch_bounds__(kBlock) k_popcount(const uint64_t *bm, uint64_
 }
 
 // ------------------------------- peel --------------------------------------
-// kind[e]: 0x7F invalid edge, else valid out-degree (0..4) | 0x80 when e is a ruler.
+// kind[e]: low 6 bits the valid out-degree (0..4; 0x3F invalid edge), 0x80 when e is a
+// ruler, 0x40 when e is a successor of a branch node (only those nodes' owners are ever
+// read, so a walk stores no other owner: the walk is one random read per step).
 // nxk[e] (unary e): its sole successor in bits 0..55 and the successor's kind in 56..63, so a
 // ruler walk pays one dependent load per step.
-constexpr uint8_t kInvalid = 0x7F, kRulerBit = 0x80;
+constexpr uint8_t kInvalid = 0x3F, kRulerBit = 0x80, kBranchSucc = 0x40;
 constexpr uint64_t kNodeMask = (1ULL << 56) - 1;
-__device__ __forceinline__ int kind_od(uint8_t k) { return k & 0x7F; }
-__device__ __forceinline__ bool kind_chain(uint8_t k) { return k == 1; }  // unary, not a ruler
+__device__ __forceinline__ int kind_od(uint8_t k) { return k & 0x3F; }
+__device__ __forceinline__ bool kind_chain(uint8_t k) { return (k & 0xBF) == 1; }  // unary, not a ruler
 
 struct PeelArrays {
     uint8_t *kind;
@@ -109,6 +111,20 @@ __global__ void __launch_bounds__(kBlock) k_peel_init(GraphView g, PeelArrays pa
     }
 }
 
+__global__ void __launch_bounds__(kBlock) k_peel_mark(GraphView g, PeelArrays pa) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < g.D; e += stride) {
+        const int od = kind_od(pa.kind[e]);
+        if (od < 2 || od == kInvalid) continue;
+        uint64_t out[4];
+        const int n = dev_outgoing(g, e, out);
+        for (int j = 0; j < n; ++j) {
+            const uint64_t y = out[j];
+            atomicOr((unsigned int *)(pa.kind + (y & ~3ULL)), (unsigned)kBranchSucc << (8 * (y & 3)));
+        }
+    }
+}
+
 // rulers: unary nodes without a unary predecessor (chain heads) plus 1/64 of the others;
 // compacted into list by wave ballots, one cursor atomic per 4096-edge tile
 constexpr int kTileJ = 16;  // 64-edge words per wave per tile
@@ -125,9 +141,9 @@ __global__ void __launch_bounds__(kBlock) k_peel_rulers(uint64_t D, PeelArrays p
         for (int j = 0; j < kTileJ; ++j) {
             const uint64_t e = t0 + (uint64_t)j * kBlock + threadIdx.x;
             bool r = false;
-            if (e < D && pa.kind[e] == 1) {
+            if (e < D && kind_chain(pa.kind[e])) {
                 r = pa.upred[e] == 0 || (mix64(e ^ 0x5eed) & 63) == 0;
-                if (r) pa.kind[e] = 1 | kRulerBit;
+                if (r) pa.kind[e] |= kRulerBit;
             }
             m[j] = __ballot(r);
             c += __popcll(m[j]);
@@ -169,7 +185,6 @@ __global__ void __launch_bounds__(kBlock) k_peel_walk(PeelArrays pa, const uint6
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nr; i += stride) {
         const uint64_t r = list[i];
-        pa.owner[r] = r;
         uint64_t w = pa.nxk[r], tort = r;
         uint64_t power = 1, lam = 1;
         uint64_t res = kNone;
@@ -177,7 +192,7 @@ __global__ void __launch_bounds__(kBlock) k_peel_walk(PeelArrays pa, const uint6
             const uint64_t y = w & kNodeMask;
             if (!kind_chain((uint8_t)(w >> 56))) { res = y; break; }
             if (y == tort) { res = kNone; break; }  // ruler-less unary cycle reached
-            pa.owner[y] = r;
+            if ((w >> 56) & kBranchSucc) pa.owner[y] = r;
             if (power == lam) { tort = y; power <<= 1; lam = 0; }
             w = pa.nxk[y];
             ++lam;
@@ -216,13 +231,13 @@ __global__ void __launch_bounds__(kBlock) k_peel_term(uint64_t D, PeelArrays pa,
         bool br = false;
         if (e < D) {
             const uint8_t o = pa.kind[e];
-            if (o == 0) {
+            if (kind_od(o) == 0) {
                 const bool rm = bit_get(pa.seed, e);
                 pa.st[e] = rm ? kRem : kSurv;
                 br = rm;
             } else {
                 pa.st[e] = kUnk;
-                br = o != kInvalid && kind_od(o) >= 2;
+                br = kind_od(o) != kInvalid && kind_od(o) >= 2;
             }
         }
         const unsigned long long m = __ballot(br);
@@ -778,6 +793,8 @@ static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm) {
     HIP_OK(hipMemsetAsync(owner.p, 0xFF, owner.bytes(), st));
     PeelArrays pa{kind.p, upred.p, stt.p, nxk.p, owner.p, jump.p, seed_bm};
     hipLaunchKernelGGL(k_peel_init, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, v, pa);
+    LAUNCH_OK();
+    hipLaunchKernelGGL(k_peel_mark, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, v, pa);
     LAUNCH_OK();
     DevBuf<unsigned long long> cur(1);
     DevBuf<uint64_t> list(D);
