@@ -1032,6 +1032,7 @@ struct FcRunner {
                     }
                 }
             }
+            verbose_mark(g->ctx, "fc.commit_tentative");
             uint64_t f = first_bad;
             // only starts that would commit after some tentative commit can conflict
             std::vector<uint32_t> jl;
@@ -1059,6 +1060,7 @@ struct FcRunner {
                 for (size_t q = 0; q < jl.size(); ++q)
                     if (conf[q]) { f = jl[q]; break; }
             }
+            verbose_mark(g->ctx, "fc.commit_conflicts");
             // commit the prefix [0, f)
             std::vector<uint64_t> setv;
             for (uint64_t j = 0; j < f; ++j) {
@@ -1078,6 +1080,7 @@ struct FcRunner {
                 if (newly_c[a] < f) setv.push_back(newly[a]);
                 else hvis.clear(newly[a]);  // roll back tentative marks past the commit prefix
             }
+            verbose_mark(g->ctx, "fc.commit_results");
             if (!setv.empty()) {
                 DevBuf<uint64_t> ds(setv.size());
                 HIP_OK(hipMemcpyAsync(ds.p, setv.data(), 8 * setv.size(), hipMemcpyHostToDevice, st));
