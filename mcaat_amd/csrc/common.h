@@ -130,4 +130,8 @@ __device__ __forceinline__ void block_add(unsigned long long *counter, unsigned 
     }
 }
 
+// workgroup barrier for LDS hand-offs only: __syncthreads() also drains every outstanding
+// global store and atomic (vmcnt(0))
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 }  // namespace mcaat

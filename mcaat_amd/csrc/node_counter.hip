@@ -172,10 +172,6 @@ __device__ __forceinline__ void window_min(const uint32_t *H, uint32_t *hm) {
 constexpr uint32_t kMini = 1024;  // descriptors reserved per (workgroup, L1 bucket) grab
 constexpr uint16_t kDeadSub = 0xffff;  // sub-partition mark of an inert (n = 0) slot
 
-// workgroup barrier for LDS hand-offs only: __syncthreads() also drains every outstanding
-// global store and atomic (vmcnt(0)), which would expose the bucket writes and the
-// reservation prefetch at every flush
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 constexpr int kFB = 2;  // fill batch (entries per lane per round)
 

@@ -44,6 +44,15 @@ __global__ void __launch_bounds__(kBlock) k_expand(const uint64_t *ckeys, const 
     }
 }
 
+__global__ void __launch_bounds__(kBlock) k_count_pal(const uint64_t *ckeys, uint64_t n, int k, unsigned long long *n_pal) {
+    const int E = k + 1;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    unsigned long long c = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        c += ckeys[i] == lsb_rc(ckeys[i], E);
+    block_add(n_pal, c);
+}
+
 // dir[p] = first index whose key prefix (top B of 2E bits) >= p, p in [0, 2^B]
 __global__ void __launch_bounds__(kBlock) k_dir(const uint64_t *key, uint64_t D, int shift, uint64_t nprefix,
                                                 uint64_t *dir) {
@@ -107,6 +116,385 @@ __global__ void __launch_bounds__(kBlock) k_valid_init(uint64_t *valid, uint64_t
     }
 }
 
+// ---- MSD edge sort (k <= 28) ------------------------------------------------------------
+// Oriented edges are items (key remainder << 16 | mult): level 1 scatters them by the top 11
+// key bits into 2048 buckets, level 2 by the next 11 bits into 2048 sub-buckets each, both
+// with per-chunk runs aligned to 64-B lines and LDS line buffers (whole-line HBM writes);
+// level 3 sorts each ~D/4M-item bucket in LDS (bitonic, one wave per bucket; a workgroup
+// for large ones) and writes keys and multiplicities. Padding items are ~0 (sort last).
+constexpr int kMB = 11;               // bits per MSD level
+constexpr int kMS = 1 << kMB;         // buckets per level
+constexpr int kIL = 8;                // items per 64-B line
+constexpr uint64_t kPad = ~0ULL;
+constexpr uint32_t kCh1 = 32768;      // canonical entries per level-1 chunk (<= 2 items each)
+constexpr uint32_t kCh2 = 65536;      // items per level-2 chunk
+constexpr int kWaveSort = 512;        // largest level-3 bucket sorted by one wave
+constexpr int kBlockSort = 16384;     // largest sorted by a 1024-thread workgroup (128 KB)
+
+__device__ __forceinline__ uint32_t round8(uint32_t x) { return (x + kIL - 1) & ~(uint32_t)(kIL - 1); }
+
+// oriented items of a canonical count: top-11-bit bucket and the item word
+__device__ __forceinline__ int msd_items(uint64_t a, uint32_t c, int k, uint32_t *bk, uint64_t *it) {
+    const int E = k + 1, rb = 2 * E - kMB;
+    const uint64_t b = lsb_rc(a, E);
+    const uint64_t m = a == b ? 2ull * c : (uint64_t)c;
+    const uint64_t mult = m > 65535 ? 65535 : m;
+    const uint64_t K0 = boss_key(a, k);
+    bk[0] = (uint32_t)(K0 >> rb);
+    it[0] = ((K0 & mask_bits(rb)) << 16) | mult;
+    if (a == b) return 1;
+    const uint64_t K1 = boss_key(b, k);
+    bk[1] = (uint32_t)(K1 >> rb);
+    it[1] = ((K1 & mask_bits(rb)) << 16) | mult;
+    return 2;
+}
+
+// level-1 per-chunk bucket counts, rounded to lines, summed per bucket
+__global__ void __launch_bounds__(kBlock) k_msd1_hist(const uint64_t *ckeys, const uint32_t *ccnt, uint64_t n, int k,
+                                                      unsigned long long *tot) {
+    __shared__ uint32_t lc[kMS];
+    const uint64_t c0 = (uint64_t)blockIdx.x * kCh1, c1 = c0 + kCh1 < n ? c0 + kCh1 : n;
+    for (int i = threadIdx.x; i < kMS; i += kBlock) lc[i] = 0;
+    __syncthreads();
+    for (uint64_t i = c0 + threadIdx.x; i < c1; i += kBlock) {
+        uint32_t bk[2];
+        uint64_t it[2];
+        const int no = msd_items(ckeys[i], ccnt[i], k, bk, it);
+        for (int j = 0; j < no; ++j) atomicAdd(&lc[bk[j]], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kMS; i += kBlock)
+        if (lc[i]) atomicAdd(&tot[i], (unsigned long long)round8(lc[i]));
+}
+
+// line-buffered placement of one item (see k_l2_scatter in node_counter.hip): the lane that
+// completes a buffered line writes it whole; the excess of a round goes directly and is
+// copied into the new partial line after the round's flush
+struct LinePlace {
+    uint64_t *buf;  // [kMS][kIL]
+    uint32_t *lb, *lc, *bl;
+    uint64_t *out;
+    uint64_t gbase;
+    __device__ __forceinline__ void put(uint32_t b, uint64_t it, uint32_t &r, uint32_t &line, bool &buffered) {
+        r = atomicAdd(&lc[b], 1u);
+        line = bl[b];
+        buffered = r / kIL == line;
+        if (buffered) buf[b * kIL + (r & (kIL - 1))] = it;
+        else out[(uint64_t)lb[b] * kIL + r - gbase] = it;
+    }
+    __device__ __forceinline__ void flush(uint32_t b, uint32_t r, uint32_t line, bool buffered, uint32_t &nline) {
+        if (buffered && (r & (kIL - 1)) == kIL - 1) {
+            uint64_t *o = out + (((uint64_t)lb[b] + line) * kIL - gbase);
+#pragma unroll
+            for (int z = 0; z < kIL; ++z) o[z] = buf[b * kIL + z];
+        }
+        nline = lc[b] / kIL;
+        bl[b] = nline;
+    }
+    __device__ __forceinline__ void backfill(uint32_t b, uint64_t it, uint32_t r, bool buffered, uint32_t nline) {
+        if (!buffered && r / kIL == nline) buf[b * kIL + (r & (kIL - 1))] = it;
+    }
+    __device__ __forceinline__ void tails(int nb) {
+        for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+            const uint32_t c = lc[i];
+            if (c & (kIL - 1)) {
+                uint64_t *o = out + (((uint64_t)lb[i] + c / kIL) * kIL - gbase);
+                for (uint32_t z = 0; z < kIL; ++z) o[z] = z < (c & (kIL - 1)) ? buf[i * kIL + z] : kPad;
+            }
+        }
+    }
+};
+
+constexpr int kSBlock = 1024;
+
+__global__ void __launch_bounds__(kSBlock) k_msd1_scatter(const uint64_t *ckeys, const uint32_t *ccnt, uint64_t n,
+                                                          int k, unsigned long long *cursor, uint64_t *out) {
+    __shared__ uint64_t buf[kMS * kIL];
+    __shared__ uint32_t lb[kMS], lc[kMS], bl[kMS];
+    const uint64_t c0 = (uint64_t)blockIdx.x * kCh1, c1 = c0 + kCh1 < n ? c0 + kCh1 : n;
+    for (int i = threadIdx.x; i < kMS; i += kSBlock) lc[i] = 0;
+    __syncthreads();
+    for (uint64_t i = c0 + threadIdx.x; i < c1; i += kSBlock) {
+        uint32_t bk[2];
+        uint64_t it[2];
+        const int no = msd_items(ckeys[i], ccnt[i], k, bk, it);
+        for (int j = 0; j < no; ++j) atomicAdd(&lc[bk[j]], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kMS; i += kSBlock) {
+        const uint32_t c = lc[i];
+        lb[i] = c ? (uint32_t)(atomicAdd(&cursor[i], (unsigned long long)round8(c)) / kIL) : 0;
+        lc[i] = 0;
+        bl[i] = 0;
+    }
+    __syncthreads();
+    LinePlace lp{buf, lb, lc, bl, out, 0};
+    for (uint64_t i0 = c0; i0 < c1; i0 += kSBlock) {
+        const uint64_t i = i0 + threadIdx.x;
+        uint32_t bk[2] = {0, 0}, r[2] = {0, 0}, line[2] = {0, 0}, nl[2] = {0, 0};
+        uint64_t it[2] = {0, 0};
+        bool bf[2] = {false, false};
+        int no = 0;
+        if (i < c1) no = msd_items(ckeys[i], ccnt[i], k, bk, it);
+        for (int j = 0; j < no; ++j) lp.put(bk[j], it[j], r[j], line[j], bf[j]);
+        lds_barrier();
+        for (int j = 0; j < no; ++j) lp.flush(bk[j], r[j], line[j], bf[j], nl[j]);
+        lds_barrier();
+        for (int j = 0; j < no; ++j) lp.backfill(bk[j], it[j], r[j], bf[j], nl[j]);
+    }
+    lds_barrier();
+    lp.tails(kMS);
+}
+
+// level-2 chunks: [start, start+len) of one level-1 bucket
+__device__ __forceinline__ uint32_t msd_sub(uint64_t it, int k) {
+    const int E = k + 1;
+    return (uint32_t)(it >> (16 + 2 * E - 2 * kMB)) & (kMS - 1);
+}
+
+__global__ void __launch_bounds__(kBlock) k_msd2_hist(const uint64_t *in, const uint64_t *cstart, const uint32_t *clen,
+                                                      const uint32_t *cbucket, int k, unsigned long long *tot,
+                                                      unsigned long long *real) {
+    __shared__ uint32_t lc[kMS];
+    const uint64_t c = blockIdx.x;
+    for (int i = threadIdx.x; i < kMS; i += kBlock) lc[i] = 0;
+    __syncthreads();
+    const uint64_t s0 = cstart[c];
+    const uint32_t n = clen[c];
+    for (uint32_t i = threadIdx.x; i < n; i += kBlock) {
+        const uint64_t it = in[s0 + i];
+        if (it != kPad) atomicAdd(&lc[msd_sub(it, k)], 1u);
+    }
+    __syncthreads();
+    const uint64_t fb = (uint64_t)cbucket[c] * kMS;
+    for (int i = threadIdx.x; i < kMS; i += kBlock)
+        if (lc[i]) {
+            atomicAdd(&tot[fb + i], (unsigned long long)round8(lc[i]));
+            atomicAdd(&real[fb + i], (unsigned long long)lc[i]);
+        }
+}
+
+__global__ void __launch_bounds__(kSBlock) k_msd2_scatter(const uint64_t *in, const uint64_t *cstart,
+                                                          const uint32_t *clen, const uint32_t *cbucket, int k,
+                                                          unsigned long long *cursor, uint64_t *out) {
+    __shared__ uint64_t buf[kMS * kIL];
+    __shared__ uint32_t lb[kMS], lc[kMS], bl[kMS];
+    const uint64_t c = blockIdx.x;
+    for (int i = threadIdx.x; i < kMS; i += kSBlock) lc[i] = 0;
+    __syncthreads();
+    const uint64_t s0 = cstart[c];
+    const uint32_t n = clen[c];
+    for (uint32_t i = threadIdx.x; i < n; i += kSBlock) {
+        const uint64_t it = in[s0 + i];
+        if (it != kPad) atomicAdd(&lc[msd_sub(it, k)], 1u);
+    }
+    __syncthreads();
+    const uint64_t fb = (uint64_t)cbucket[c] * kMS;
+    for (int i = threadIdx.x; i < kMS; i += kSBlock) {
+        const uint32_t x = lc[i];
+        lb[i] = x ? (uint32_t)(atomicAdd(&cursor[fb + i], (unsigned long long)round8(x)) / kIL) : 0;
+        lc[i] = 0;
+        bl[i] = 0;
+    }
+    __syncthreads();
+    LinePlace lp{buf, lb, lc, bl, out, 0};
+    uint64_t nxt = threadIdx.x < n ? in[s0 + threadIdx.x] : kPad;
+    for (uint32_t i0 = 0; i0 < n; i0 += kSBlock) {
+        const uint64_t it = nxt;
+        const uint32_t ni = i0 + kSBlock + threadIdx.x;
+        nxt = ni < n ? in[s0 + ni] : kPad;
+        const bool live = it != kPad;
+        uint32_t b = 0, r = 0, line = 0, nl = 0;
+        bool bf = false;
+        if (live) {
+            b = msd_sub(it, k);
+            lp.put(b, it, r, line, bf);
+        }
+        lds_barrier();
+        if (live) lp.flush(b, r, line, bf, nl);
+        lds_barrier();
+        if (live) lp.backfill(b, it, r, bf, nl);
+    }
+    lds_barrier();
+    lp.tails(kMS);
+}
+
+// bitonic sort of P (power of two) items in LDS by `nth` threads starting at thread t0
+__device__ __forceinline__ void lds_bitonic(uint64_t *s, uint32_t P, uint32_t t, uint32_t nth, bool wave_only) {
+    for (uint32_t kk = 2; kk <= P; kk <<= 1)
+        for (uint32_t j = kk >> 1; j > 0; j >>= 1) {
+            for (uint32_t q = t; q < P / 2; q += nth) {
+                const uint32_t i = ((q & ~(j - 1)) << 1) | (q & (j - 1)), l = i + j;
+                const uint64_t a = s[i], b = s[l];
+                if ((a > b) == ((i & kk) == 0)) {
+                    s[i] = b;
+                    s[l] = a;
+                }
+            }
+            if (wave_only) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            } else {
+                lds_barrier();
+            }
+        }
+}
+
+__device__ __forceinline__ void msd_emit(const uint64_t *s, uint32_t nreal, uint32_t t, uint32_t nth, uint64_t hi,
+                                         uint64_t *key, uint16_t *mult, uint64_t base) {
+    for (uint32_t i = t; i < nreal; i += nth) {
+        const uint64_t it = s[i];
+        key[base + i] = hi | (it >> 16);
+        mult[base + i] = (uint16_t)(it & 0xFFFF);
+    }
+}
+
+// one wave per level-2 bucket of <= kWaveSort items; larger ones are listed
+constexpr int kL3Waves = 4;
+__global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in, const uint64_t *off2,
+                                                             const uint64_t *real2, const uint64_t *base3, int k,
+                                                             uint64_t *key, uint16_t *mult, uint32_t *big,
+                                                             unsigned long long *nbig) {
+    __shared__ uint64_t sm[kL3Waves][kWaveSort];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint64_t *s = sm[wave];
+    const int E = k + 1;
+    const uint64_t nb = (uint64_t)kMS * kMS;
+    for (uint64_t b = (uint64_t)blockIdx.x * kL3Waves + wave; b < nb; b += (uint64_t)gridDim.x * kL3Waves) {
+        const uint64_t lo = off2[b], n = off2[b + 1] - lo;
+        if (n == 0) continue;
+        if (n > (uint64_t)kWaveSort) {
+            if (lane == 0) big[atomicAdd(nbig, 1ull)] = (uint32_t)b;
+            continue;
+        }
+        uint32_t P = 8;
+        while (P < n) P <<= 1;
+        for (uint32_t i = lane; i < P; i += 64) s[i] = i < n ? in[lo + i] : kPad;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        lds_bitonic(s, P, lane, 64, true);
+        const uint64_t hi = (b >> kMB) << (2 * E - kMB);
+        msd_emit(s, (uint32_t)real2[b], lane, 64, hi, key, mult, base3[b]);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_msd3_block(const uint64_t *in, const uint64_t *off2, const uint64_t *real2,
+                                                     const uint64_t *base3, int k, const uint32_t *big, uint64_t nbig,
+                                                     uint64_t *key, uint16_t *mult, int *too_big) {
+    __shared__ uint64_t s[kBlockSort];
+    const int E = k + 1;
+    for (uint64_t q = blockIdx.x; q < nbig; q += gridDim.x) {
+        const uint64_t b = big[q], lo = off2[b], n = off2[b + 1] - lo;
+        if (n > (uint64_t)kBlockSort) {
+            if (threadIdx.x == 0) *too_big = 1;
+            continue;
+        }
+        uint32_t P = 8;
+        while (P < n) P <<= 1;
+        for (uint32_t i = threadIdx.x; i < P; i += 1024) s[i] = i < n ? in[lo + i] : kPad;
+        __syncthreads();
+        lds_bitonic(s, P, threadIdx.x, 1024, false);
+        const uint64_t hi = (b >> kMB) << (2 * E - kMB);
+        msd_emit(s, (uint32_t)real2[b], threadIdx.x, 1024, hi, key, mult, base3[b]);
+        __syncthreads();
+    }
+}
+
+template <class T>
+void excl_scan(hipStream_t st, const T *in, T *out, uint64_t n) {
+    size_t tmp = 0;
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, in, out, (size_t)n, st));
+    DevBuf<uint8_t> t(tmp);
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(t.p, tmp, in, out, (size_t)n, st));
+}
+
+// returns false (nothing written) if a bucket exceeds the LDS sorts: caller uses the radix sort
+bool msd_sort(mcaat_ctx *ctx, const uint64_t *ckeys, const uint32_t *ccnt, uint64_t n, int k, uint64_t D,
+              uint64_t *key, uint16_t *mult) {
+    hipStream_t st = ctx->stream;
+    const uint64_t nch1 = (n + kCh1 - 1) / kCh1;
+    // level 1
+    DevBuf<unsigned long long> tot1(kMS + 1), cur1(kMS + 1);
+    HIP_OK(hipMemsetAsync(tot1.p, 0, tot1.bytes(), st));
+    hipLaunchKernelGGL(k_msd1_hist, dim3((unsigned)nch1), dim3(kBlock), 0, st, ckeys, ccnt, n, k, tot1.p);
+    LAUNCH_OK();
+    excl_scan(st, (const uint64_t *)tot1.p, (uint64_t *)cur1.p, kMS + 1);
+    std::vector<uint64_t> off1(kMS + 1);
+    HIP_OK(hipMemcpyAsync(off1.data(), cur1.p, 8 * (kMS + 1), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    DevBuf<uint64_t> l1(off1[kMS] ? off1[kMS] : 1);
+    hipLaunchKernelGGL(k_msd1_scatter, dim3((unsigned)nch1), dim3(kSBlock), 0, st, ckeys, ccnt, n, k, cur1.p, l1.p);
+    LAUNCH_OK();
+    // level 2
+    std::vector<uint64_t> cstart;
+    std::vector<uint32_t> clen, cbk;
+    for (int b = 0; b < kMS; ++b)
+        for (uint64_t o = off1[b]; o < off1[b + 1]; o += kCh2) {
+            cstart.push_back(o);
+            clen.push_back((uint32_t)std::min<uint64_t>(kCh2, off1[b + 1] - o));
+            cbk.push_back((uint32_t)b);
+        }
+    const uint64_t nch2 = cstart.size(), NB = (uint64_t)kMS * kMS;
+    DevBuf<uint64_t> dcs(nch2 ? nch2 : 1);
+    DevBuf<uint32_t> dcl(nch2 ? nch2 : 1), dcb(nch2 ? nch2 : 1);
+    DevBuf<unsigned long long> tot2(NB + 1), real2(NB + 1), cur2(NB + 1), base3(NB + 1);
+    HIP_OK(hipMemcpyAsync(dcs.p, cstart.data(), 8 * nch2, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(dcl.p, clen.data(), 4 * nch2, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(dcb.p, cbk.data(), 4 * nch2, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemsetAsync(tot2.p, 0, tot2.bytes(), st));
+    HIP_OK(hipMemsetAsync(real2.p, 0, real2.bytes(), st));
+    if (nch2) {
+        hipLaunchKernelGGL(k_msd2_hist, dim3((unsigned)nch2), dim3(kBlock), 0, st, l1.p, dcs.p, dcl.p, dcb.p, k,
+                           tot2.p, real2.p);
+        LAUNCH_OK();
+    }
+    excl_scan(st, (const uint64_t *)tot2.p, (uint64_t *)cur2.p, NB + 1);
+    excl_scan(st, (const uint64_t *)real2.p, (uint64_t *)base3.p, NB + 1);
+    uint64_t n2 = 0, nreal = 0;
+    HIP_OK(hipMemcpyAsync(&n2, cur2.p + NB, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(&nreal, base3.p + NB, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (nreal != D) throw Error(MCAAT_E_CAPACITY, "msd_sort: item count mismatch");
+    DevBuf<uint64_t> off2(NB + 1);
+    HIP_OK(hipMemcpyAsync(off2.p, cur2.p, 8 * (NB + 1), hipMemcpyDeviceToDevice, st));
+    DevBuf<uint64_t> l2(n2 ? n2 : 1);
+    if (nch2) {
+        hipLaunchKernelGGL(k_msd2_scatter, dim3((unsigned)nch2), dim3(kSBlock), 0, st, l1.p, dcs.p, dcl.p, dcb.p, k,
+                           cur2.p, l2.p);
+        LAUNCH_OK();
+    }
+    l1.release();
+    // level 3
+    DevBuf<uint32_t> big(NB);
+    DevBuf<unsigned long long> nbig(1);
+    DevBuf<int> too(1);
+    HIP_OK(hipMemsetAsync(nbig.p, 0, 8, st));
+    HIP_OK(hipMemsetAsync(too.p, 0, 4, st));
+    hipLaunchKernelGGL(k_msd3_wave, dim3((unsigned)ctx->n_cu * 16), dim3(kL3Waves * 64), 0, st, l2.p, off2.p,
+                       (const uint64_t *)real2.p, (const uint64_t *)base3.p, k, key, mult, big.p, nbig.p);
+    LAUNCH_OK();
+    unsigned long long hb = 0;
+    HIP_OK(hipMemcpyAsync(&hb, nbig.p, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (hb) {
+        hipLaunchKernelGGL(k_msd3_block, dim3((unsigned)std::min<uint64_t>(hb, (uint64_t)ctx->n_cu)), dim3(1024), 0, st,
+                           l2.p, off2.p, (const uint64_t *)real2.p, (const uint64_t *)base3.p, k, big.p, (uint64_t)hb,
+                           key, mult, too.p);
+        LAUNCH_OK();
+        int h = 0;
+        HIP_OK(hipMemcpyAsync(&h, too.p, 4, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        if (h) return false;
+    }
+    HIP_OK(hipStreamSynchronize(st));
+    return true;
+}
+
 }  // namespace
 
 void sdbg_build(mcaat_ctx *ctx, CountResult &c, int k, mcaat_graph *g) {
@@ -116,32 +504,48 @@ void sdbg_build(mcaat_ctx *ctx, CountResult &c, int k, mcaat_graph *g) {
     g->k = k;
     DevBuf<unsigned long long> npal(1);
     HIP_OK(hipMemsetAsync(npal.p, 0, 8, st));
-    DevBuf<uint64_t> ek(n2);
-    DevBuf<uint16_t> em(n2);
     if (c.n) {
+        hipLaunchKernelGGL(k_count_pal, dim3(grid_for(c.n, kBlock, (unsigned)ctx->n_cu * 16)), dim3(kBlock), 0, st,
+                           c.keys.p, c.n, k, npal.p);
+        LAUNCH_OK();
+    }
+    unsigned long long n_pal = 0;
+    HIP_OK(hipMemcpyAsync(&n_pal, npal.p, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    const uint64_t D = n2 - n_pal;
+    g->D = D;
+    g->key.alloc(D ? D : 1);
+    g->mult.alloc(D ? D : 1);
+    // MSD sort with LDS bucket sorts (k <= 28: key remainder and mult share one word);
+    // the radix sort otherwise, or when a bucket is too skewed for LDS
+    bool done = false;
+    if (k <= 28 && D >= (1u << 16)) {
+        KernelTimer kt(ctx, "edge_sort", 64.0 * (double)D);
+        done = msd_sort(ctx, c.keys.p, c.counts.p, c.n, k, D, g->key.p, g->mult.p);
+        kt.stop();
+    }
+    if (!done && n2) {
+        DevBuf<uint64_t> ek(n2);
+        DevBuf<uint16_t> em(n2);
+        HIP_OK(hipMemsetAsync(npal.p, 0, 8, st));
         hipLaunchKernelGGL(k_expand, dim3(grid_for(c.n, kBlock)), dim3(kBlock), 0, st, c.keys.p, c.counts.p, c.n, k,
                            ek.p, em.p, npal.p);
         LAUNCH_OK();
+        DevBuf<uint64_t> sk(n2);
+        DevBuf<uint16_t> sm(n2);
+        size_t tmp = 0;
+        HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, ek.p, sk.p, em.p, sm.p, (size_t)n2, 0, 2 * E + 1, st));
+        DevBuf<uint8_t> t(tmp);
+        HIP_OK(hipcub::DeviceRadixSort::SortPairs(t.p, tmp, ek.p, sk.p, em.p, sm.p, (size_t)n2, 0, 2 * E + 1, st));
+        // palindromes left sentinels (1 << 2E) at the end
+        if (D) {
+            HIP_OK(hipMemcpyAsync(g->key.p, sk.p, 8 * D, hipMemcpyDeviceToDevice, st));
+            HIP_OK(hipMemcpyAsync(g->mult.p, sm.p, 2 * D, hipMemcpyDeviceToDevice, st));
+        }
+        HIP_OK(hipStreamSynchronize(st));
     }
-    // release the counting table output before sorting
     c.keys.release();
     c.counts.release();
-    unsigned long long n_pal = 0;
-    HIP_OK(hipMemcpyAsync(&n_pal, npal.p, 8, hipMemcpyDeviceToHost, st));
-    g->key.alloc(n2);
-    g->mult.alloc(n2);
-    if (n2) {
-        size_t tmp = 0;
-        HIP_OK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, ek.p, g->key.p, em.p, g->mult.p, (size_t)n2, 0,
-                                                  2 * E + 1, st));
-        DevBuf<uint8_t> t(tmp);
-        HIP_OK(hipcub::DeviceRadixSort::SortPairs(t.p, tmp, ek.p, g->key.p, em.p, g->mult.p, (size_t)n2, 0, 2 * E + 1,
-                                                  st));
-    }
-    HIP_OK(hipStreamSynchronize(st));
-    ek.release();
-    em.release();
-    g->D = n2 - n_pal;
     sdbg_finish(ctx, g);
 }
 
