@@ -361,22 +361,57 @@ __global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in,
     uint64_t *s = sm[wave];
     const int E = k + 1;
     const uint64_t nb = (uint64_t)kMS * kMS;
-    for (uint64_t b = (uint64_t)blockIdx.x * kL3Waves + wave; b < nb; b += (uint64_t)gridDim.x * kL3Waves) {
-        const uint64_t lo = off2[b], n = off2[b + 1] - lo;
+    const uint64_t bstride = (uint64_t)gridDim.x * kL3Waves;
+    constexpr int NL = 10;  // loads per lane: buckets of up to 640 padded items
+    uint64_t b = (uint64_t)blockIdx.x * kL3Waves + wave;
+    // bucket metadata one bucket ahead
+    uint64_t m_lo = 0, m_hi = 0, m_real = 0, m_base = 0;
+    if (b < nb) {
+        m_lo = off2[b];
+        m_hi = off2[b + 1];
+        m_real = real2[b];
+        m_base = base3[b];
+    }
+    for (; b < nb; b += bstride) {
+        const uint64_t lo = m_lo, n = m_hi - m_lo, nr64 = m_real, base = m_base;
+        const uint64_t bn = b + bstride;
+        if (bn < nb) {
+            m_lo = off2[bn];
+            m_hi = off2[bn + 1];
+            m_real = real2[bn];
+            m_base = base3[bn];
+        }
         if (n == 0) continue;
-        if (n > (uint64_t)kWaveSort) {
+        if (nr64 > (uint64_t)kWaveSort || n > (uint64_t)NL * 64) {
             if (lane == 0) big[atomicAdd(nbig, 1ull)] = (uint32_t)b;
             continue;
         }
+        // load the bucket (all loads in flight together), compacted: line padding dropped, so
+        // the network is sized by the real items
+        const uint32_t nreal = (uint32_t)nr64;
+        uint64_t v[NL];
+#pragma unroll
+        for (int t = 0; t < NL; ++t) {
+            const uint32_t i = t * 64 + lane;
+            v[t] = i < n ? in[lo + i] : kPad;
+        }
         uint32_t P = 8;
-        while (P < n) P <<= 1;
-        for (uint32_t i = lane; i < P; i += 64) s[i] = i < n ? in[lo + i] : kPad;
+        while (P < nreal) P <<= 1;
+        uint32_t fill = 0;
+#pragma unroll
+        for (int t = 0; t < NL; ++t) {
+            const unsigned long long m = __ballot(v[t] != kPad);
+            if (v[t] != kPad)
+                s[fill + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = v[t];
+            fill += (uint32_t)__popcll(m);
+        }
+        for (uint32_t i = nreal + lane; i < P; i += 64) s[i] = kPad;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         lds_bitonic(s, P, lane, 64, true);
         const uint64_t hi = (b >> kMB) << (2 * E - kMB);
-        msd_emit(s, (uint32_t)real2[b], lane, 64, hi, key, mult, base3[b]);
+        msd_emit(s, nreal, lane, 64, hi, key, mult, base);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
