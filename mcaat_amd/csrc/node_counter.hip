@@ -93,8 +93,8 @@ constexpr int kAWaves = 8;
 constexpr int kAThreads = kAWaves * 64;
 constexpr int kItem = 127;              // edge positions per work item (the close at np fits 16 steps)
 constexpr int kCk = 8;                  // positions per step
-constexpr int kSeg = 960;               // per-wave stage segment (entries); a step appends <= 64*kCk
-constexpr int kStage = kSeg * kAWaves;  // 120 KB of LDS
+constexpr int kSeg = 1600;              // per-wave stage segment (entries); a step appends <= 64*kCk
+constexpr int kStage = kSeg * kAWaves;  // 8-B pre-entries: 100 KB of LDS
 
 struct ItemSrc {
     const uint64_t *offsets;
@@ -173,7 +173,15 @@ constexpr uint32_t kMini = 1024;  // descriptors reserved per (workgroup, L1 buc
 constexpr uint16_t kDeadSub = 0xffff;  // sub-partition mark of an inert (n = 0) slot
 
 
-constexpr int kFB = 2;  // fill batch (entries per lane per round)
+constexpr int kWB = 4;  // write batch (entries per thread per round: 12 loads in flight)
+
+// 8-byte pre-entry of a closed super-k-mer: minimizer hash (32 bits), n edges (6), first
+// position in its item (7), batch parity (1), lane (6). The item's first base comes from
+// the wave's table of the current and previous batch (sbase), so the pre-entry is half a
+// descriptor and the stage holds 1600 per wave; bases are fetched when the entry is written.
+__device__ __forceinline__ uint64_t pre_entry(uint32_t h, uint32_t n, uint32_t p, uint32_t par, uint32_t lane) {
+    return (uint64_t)h | ((uint64_t)n << 32) | ((uint64_t)p << 38) | ((uint64_t)par << 45) | ((uint64_t)lane << 46);
+}
 
 template <int W>
 __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__restrict__ packed, ItemSrc src,
@@ -182,9 +190,10 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
                                                           const uint64_t *__restrict__ l1_cap,
                                                           unsigned long long *l1_cursor, uint16_t *__restrict__ l1_sub,
                                                           unsigned long long *prof) {
-    __shared__ uint4 stage[kStage];
+    __shared__ uint64_t stage[kStage];
     __shared__ uint8_t stage_l1[kStage];
     __shared__ uint16_t perm[kStage];         // stage entries in bucket order
+    __shared__ uint64_t sbase[kAWaves][2][64];  // item first base per (wave, batch parity, lane)
     __shared__ uint32_t hist[256];            // entries per bucket in this flush
     __shared__ uint32_t boff[256];            // exclusive scan of hist
     __shared__ uint32_t bcur[256];            // rank cursors
@@ -198,18 +207,20 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
     const int tb = threadIdx.x;  // threads < 256 own bucket tb through every flush
     // each bucket holds its current reservation and, in a register of its owner thread,
     // the next one, requested a flush ahead so the cursor atomic's latency is hidden
-    unsigned long long my_next = 0;
+    // (the atomic's result stays unused until the next flush, so its latency is hidden)
+    unsigned long long my_next = 0, my_base = 0;
     uint32_t prev_need = 0;  // applied to rpos/rleft at the next flush (after its barrier)
     if (tb < 256) {
         rleft[tb] = 0;
         hist[tb] = 0;
         bcur[tb] = 0;
-        rlim[tb] = l1_base[tb] + l1_cap[tb];
-        my_next = l1_base[tb] + atomicAdd(&l1_cursor[tb], (unsigned long long)kMini);
+        my_base = l1_base[tb];
+        rlim[tb] = my_base + l1_cap[tb];
+        my_next = atomicAdd(&l1_cursor[tb], (unsigned long long)kMini);
     }
     if (threadIdx.x == 0) more_flag[0] = more_flag[1] = 0;
     __syncthreads();
-    uint4 *seg = stage + wave * kSeg;
+    uint64_t *seg = stage + wave * kSeg;
     uint8_t *seg_l1 = stage_l1 + wave * kSeg;
     uint32_t nflush = 0;
 
@@ -233,12 +244,12 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
     const uint32_t salt32 = (uint32_t)P.salt;
     const int nmax = P.nmax;
 
-    // per-lane scan state (wave-uniform: active, c, nck, fill)
+    // per-lane scan state (wave-uniform: active, c, nck, fill, par, bsf)
     uint32_t H[3 * kCk];
     uint64_t cw[3], pa = 0, pb = 0;  // the item's first words; the next step's window words
     uint64_t s = 0;
     int np = 0, p_open = 0, c = 0, nck = 0;
-    uint32_t prev_hm = 0, h_open = 0, fill = 0;
+    uint32_t prev_hm = 0, h_open = 0, fill = 0, par = 1, bsf = 0;
     bool active = false;
     auto fetch = [&](uint64_t bt, uint64_t &sb, int &n, uint64_t *w) {
         const uint64_t item = bt * 64 + lane;
@@ -263,7 +274,12 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
         for (;;) {
             if (!active) {
                 if (batch >= n_batches) break;
+                // a segment references at most two batches (the sbase slots)
+                if (bsf >= 2) break;
                 fetch(batch, s, np, cw);
+                par ^= 1u;
+                ++bsf;
+                sbase[wave][par][lane] = s;
                 {
                     const uint64_t q2 = (s + 2 * kCk) >> 5;
                     pa = packed[q2];
@@ -307,8 +323,7 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
                     if (cl) {
                         const uint32_t idx =
                             fill + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0));
-                        const uint64_t B0 = s + (uint64_t)p_open;
-                        seg[idx] = make_uint4((uint32_t)B0, (uint32_t)(B0 >> 32) | ((uint32_t)(i - p_open) << 16), h_open, 0u);
+                        seg[idx] = pre_entry(h_open, (uint32_t)(i - p_open), (uint32_t)p_open, par, (uint32_t)lane);
                         p_open = i;
                         h_open = hm[t];
                     }
@@ -324,39 +339,12 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
             }
         }
         tick(0);
-        // fill in the bases of this wave's entries and count them per L1 bucket; the minimum
-        // hash is biased towards 0, so buckets come from a re-hash of it (a bijection).
-        // kFB entries per lane per round keep 3*kFB loads in flight.
-        for (uint32_t e0 = 0; e0 < fill; e0 += 64 * kFB) {
-            uint4 q[kFB];
-            uint64_t x[kFB][3];
-#pragma unroll
-            for (int k = 0; k < kFB; ++k) {
-                const uint32_t e = e0 + 64 * k + lane;
-                q[k] = e < fill ? seg[e] : make_uint4(0, 0, 0, 0);
-                const uint64_t B0 = (uint64_t)q[k].x | ((uint64_t)(q[k].y & 0xffffu) << 32);
-#pragma unroll
-                for (int j = 0; j < 3; ++j) x[k][j] = packed[(B0 >> 5) + j];
-            }
-#pragma unroll
-            for (int k = 0; k < kFB; ++k) {
-                const uint32_t e = e0 + 64 * k + lane;
-                if (e >= fill) continue;
-                const uint64_t B0 = (uint64_t)q[k].x | ((uint64_t)(q[k].y & 0xffffu) << 32);
-                const uint32_t n = q[k].y >> 16;
-                const int sh = 2 * (int)(B0 & 31);
-                // bases past the last edge are zeroed, so every copy of a super-k-mer is the
-                // same 128-bit descriptor whatever follows it in its read
-                const int L = (int)n + P.E - 1;
-                const uint64_t w0 = (sh ? (x[k][0] >> sh) | (x[k][1] << (64 - sh)) : x[k][0]) & mask_bits(2 * L);
-                uint64_t w1 = (sh ? (x[k][1] >> sh) | (x[k][2] << (64 - sh)) : x[k][1]) & mask_bits(L > 32 ? 2 * (L - 32) : 0);
-                const uint64_t h = mix64((uint64_t)q[k].z ^ 0x7061727469746eULL);
-                const uint32_t l1 = (uint32_t)(h >> 56);
-                w1 |= ((uint64_t)n << kNShift) | (((h >> (56 - kHBits)) & ((1u << kHBits) - 1)) << kHShift);
-                seg[e] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
-                seg_l1[e] = (uint8_t)l1;
-                atomicAdd(&hist[l1], 1u);
-            }
+        // bucket of each entry: the minimum hash is biased towards 0, so buckets come from
+        // a re-hash of it (a bijection)
+        for (uint32_t e = lane; e < fill; e += 64) {
+            const uint32_t l1 = (uint32_t)(mix64((uint64_t)(uint32_t)seg[e] ^ 0x7061727469746eULL) >> 56);
+            seg_l1[e] = (uint8_t)l1;
+            atomicAdd(&hist[l1], 1u);
         }
         tick(1);
         if (lane == 0) wtot[wave] = fill;
@@ -374,12 +362,12 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
             if (need > rleft[tb]) {
                 for (uint32_t z = 0; z < rleft[tb]; ++z) put(tb, rpos[tb] + z, make_uint4(0, 0, 0, 0));
                 if (need <= kMini) {
-                    rpos[tb] = my_next;
+                    rpos[tb] = my_base + my_next;
                     rleft[tb] = kMini;
-                    my_next = l1_base[tb] + atomicAdd(&l1_cursor[tb], (unsigned long long)kMini);
+                    my_next = atomicAdd(&l1_cursor[tb], (unsigned long long)kMini);
                 } else {  // more than a reservation in one flush: grab synchronously
                     const uint32_t grab = ((need + kMini - 1) / kMini) * kMini;
-                    rpos[tb] = l1_base[tb] + atomicAdd(&l1_cursor[tb], (unsigned long long)grab);
+                    rpos[tb] = my_base + atomicAdd(&l1_cursor[tb], (unsigned long long)grab);
                     rleft[tb] = grab;
                 }
             }
@@ -405,17 +393,50 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
             perm[boff[b] + atomicAdd(&bcur[b], 1u)] = (uint16_t)(wave * kSeg + e);
         }
         lds_barrier();  // C: perm ready
-        // consecutive threads write consecutive slots of a bucket's run
+        // consecutive threads write consecutive slots of a bucket's run; each entry's bases
+        // are fetched here (kWB entries per thread per round, their loads in flight together)
         uint32_t total = 0;
 #pragma unroll
         for (int w = 0; w < kAWaves; ++w) total += wtot[w];
-        for (uint32_t j = threadIdx.x; j < total; j += kAThreads) {
-            const uint32_t i = perm[j];
-            const int b = stage_l1[i];
-            put(b, rpos[b] + (j - boff[b]), stage[i]);
+        for (uint32_t j0 = threadIdx.x; j0 < total; j0 += kWB * kAThreads) {
+            uint64_t q[kWB], B0[kWB], x[kWB][3];
+#pragma unroll
+            for (int k = 0; k < kWB; ++k) {
+                const uint32_t j = j0 + k * kAThreads;
+                q[k] = 0;
+                B0[k] = 0;
+                if (j < total) {
+                    const uint32_t i = perm[j];
+                    q[k] = stage[i];
+                    const uint32_t ln = (uint32_t)(q[k] >> 46) & 63, pr = (uint32_t)(q[k] >> 45) & 1;
+                    B0[k] = sbase[i / kSeg][pr][ln] + ((q[k] >> 38) & 127);
+                }
+#pragma unroll
+                for (int z = 0; z < 3; ++z) x[k][z] = packed[(B0[k] >> 5) + z];
+            }
+#pragma unroll
+            for (int k = 0; k < kWB; ++k) {
+                const uint32_t j = j0 + k * kAThreads;
+                if (j >= total) continue;
+                const uint32_t i = perm[j];
+                const int b = stage_l1[i];
+                const uint32_t n = (uint32_t)(q[k] >> 32) & 63;
+                const int sh = 2 * (int)(B0[k] & 31);
+                // bases past the last edge are zeroed, so every copy of a super-k-mer is the
+                // same 128-bit descriptor whatever follows it in its read
+                const int L = (int)n + P.E - 1;
+                const uint64_t w0 = (sh ? (x[k][0] >> sh) | (x[k][1] << (64 - sh)) : x[k][0]) & mask_bits(2 * L);
+                uint64_t w1 = (sh ? (x[k][1] >> sh) | (x[k][2] << (64 - sh)) : x[k][1]) &
+                              mask_bits(L > 32 ? 2 * (L - 32) : 0);
+                const uint64_t h = mix64((uint64_t)(uint32_t)q[k] ^ 0x7061727469746eULL);
+                w1 |= ((uint64_t)n << kNShift) | (((h >> (56 - kHBits)) & ((1u << kHBits) - 1)) << kHShift);
+                put(b, rpos[b] + (j - boff[b]),
+                    make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)));
+            }
         }
         if (tb < 256) bcur[tb] = 0;
         fill = 0;
+        bsf = active ? 1u : 0u;  // the batch in progress keeps its sbase slot
         lds_barrier();  // D: stage free again
         tick(4);
         if (!more) break;
@@ -432,7 +453,7 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
             for (uint32_t z = threadIdx.x; z < rleft[b]; z += kAThreads) put(b, rpos[b] + z, make_uint4(0, 0, 0, 0));
         __syncthreads();
         if (tb < 256) {
-            rpos[tb] = my_next;
+            rpos[tb] = my_base + my_next;
             rleft[tb] = kMini;
         }
         __syncthreads();
@@ -1084,7 +1105,7 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
         unsigned long long hp[8];
         HIP_OK(hipMemcpy(hp, dprof.p, 64, hipMemcpyDeviceToHost));
         const double waves = (double)ctx->n_cu * kAWaves;
-        fprintf(stderr, "[mcaat] pass A per-wave ms (100 MHz clock): scan %.1f fill %.1f wait %.1f reserve %.1f scatter %.1f\n",
+        fprintf(stderr, "[mcaat] pass A per-wave ms (100 MHz clock): scan %.1f bucket %.1f wait %.1f reserve %.1f write %.1f\n",
                 hp[0] / waves / 1e5, hp[1] / waves / 1e5, hp[2] / waves / 1e5, hp[3] / waves / 1e5, hp[4] / waves / 1e5);
     }
     verbose_mark(ctx, "node_counter.A");
