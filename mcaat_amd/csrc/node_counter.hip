@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <ctime>
+#include <type_traits>
 
 #include "internal.h"
 
@@ -131,39 +132,47 @@ __device__ __forceinline__ uint64_t win32(uint64_t a, uint64_t b, uint64_t B) {
     return sh ? (a >> sh) | (b << (64 - sh)) : a;
 }
 
-// hashes of the kCk canonical m-mers starting at the bases 0..kCk-1 of win (m <= 16)
+// hashes of the kCk canonical m-mers starting at the bases 0..kCk-1 of win (m <= 16);
+// FULL: m == 16, so the m-mers need no mask
+template <bool FULL>
 __device__ __forceinline__ void hash_step(uint64_t win, int m, uint32_t mmask, uint32_t salt, uint32_t *h) {
     const uint64_t R = (rev2_dev(win) ^ ~0ULL) >> (2 * (25 - m));  // rc, aligned for t = 7
     const uint32_t wl = (uint32_t)win, wh = (uint32_t)(win >> 32);
     const uint32_t rl = (uint32_t)R, rh = (uint32_t)(R >> 32);
 #pragma unroll
     for (int t = 0; t < kCk; ++t) {
-        const uint32_t f = __builtin_amdgcn_alignbit(wh, wl, 2 * t) & mmask;
-        const uint32_t r = __builtin_amdgcn_alignbit(rh, rl, 2 * (kCk - 1 - t)) & mmask;
+        uint32_t f = __builtin_amdgcn_alignbit(wh, wl, 2 * t);
+        uint32_t r = __builtin_amdgcn_alignbit(rh, rl, 2 * (kCk - 1 - t));
+        if (!FULL) {
+            f &= mmask;
+            r &= mmask;
+        }
         h[t] = mix32(min(f, r) ^ salt);
     }
 }
 
-// minimum over H[t .. t+W-1] for t < kCk (H holds 2*kCk + kCk = 24 hashes; W <= 16)
-template <int W>
+// minimum over the hashes u .. u+W-1 (u < kCk) of the 3*kCk-entry ring H whose logical
+// entry 0 is physical entry G*kCk (W <= 16)
+template <int W, int G>
 __device__ __forceinline__ void window_min(const uint32_t *H, uint32_t *hm) {
+    auto at = [&](int u) { return H[(G * kCk + u) % (3 * kCk)]; };
     if constexpr (W > kCk) {
         // suffix minima of H[t..kCk-1] and prefix minima of H[kCk..kCk+u]
         uint32_t S[kCk], Pm[W - 1];
-        S[kCk - 1] = H[kCk - 1];
+        S[kCk - 1] = at(kCk - 1);
 #pragma unroll
-        for (int t = kCk - 2; t >= 0; --t) S[t] = min(H[t], S[t + 1]);
-        Pm[0] = H[kCk];
+        for (int t = kCk - 2; t >= 0; --t) S[t] = min(at(t), S[t + 1]);
+        Pm[0] = at(kCk);
 #pragma unroll
-        for (int u = 1; u < W - 1; ++u) Pm[u] = min(Pm[u - 1], H[kCk + u]);
+        for (int u = 1; u < W - 1; ++u) Pm[u] = min(Pm[u - 1], at(kCk + u));
 #pragma unroll
         for (int t = 0; t < kCk; ++t) hm[t] = min(S[t], Pm[t + W - 1 - kCk]);
     } else {
 #pragma unroll
         for (int t = 0; t < kCk; ++t) {
-            uint32_t v = H[t];
+            uint32_t v = at(t);
 #pragma unroll
-            for (int q = 1; q < W; ++q) v = min(v, H[t + q]);
+            for (int q = 1; q < W; ++q) v = min(v, at(t + q));
             hm[t] = v;
         }
     }
@@ -175,13 +184,14 @@ constexpr uint16_t kDeadSub = 0xffff;  // sub-partition mark of an inert (n = 0)
 
 constexpr int kWB = 4;  // write batch (entries per thread per round: 12 loads in flight)
 
-// 8-byte pre-entry of a closed super-k-mer: minimizer hash (32 bits), n edges (6), first
-// position in its item (7), batch parity (1), lane (6). The item's first base comes from
-// the wave's table of the current and previous batch (sbase), so the pre-entry is half a
-// descriptor and the stage holds 1600 per wave; bases are fetched when the entry is written.
-__device__ __forceinline__ uint64_t pre_entry(uint32_t h, uint32_t n, uint32_t p, uint32_t par, uint32_t lane) {
-    return (uint64_t)h | ((uint64_t)n << 32) | ((uint64_t)p << 38) | ((uint64_t)par << 45) | ((uint64_t)lane << 46);
-}
+// 8-byte pre-entry of a closed super-k-mer: minimizer hash (low 32 bits); above it the
+// close position (7 bits), the first position (7), batch parity (1) and lane (6), all in
+// its item. The item's first base comes from the wave's table of the current and previous
+// batch (sbase), so the pre-entry is half a descriptor and the stage holds 1600 per wave;
+// bases are fetched when the entry is written. The scan keeps the first position
+// pre-shifted (p7 = p << 7) and the parity and lane pre-placed (ihc), so the high word is
+// one add.
+constexpr int kPeP = 7, kPePar = 14, kPeLane = 15;
 
 template <int W>
 __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__restrict__ packed, ItemSrc src,
@@ -240,16 +250,18 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
     const uint64_t n_batches = (n_items + 63) / 64;
     const uint64_t bstride = (uint64_t)gridDim.x * kAWaves;
     uint64_t batch = (uint64_t)blockIdx.x * kAWaves + wave;
+    constexpr bool kFull = W >= 10;  // the host picks m = 16 whenever W >= 10
     const uint32_t mmask = (uint32_t)mask_bits(2 * P.m);
     const uint32_t salt32 = (uint32_t)P.salt;
     const int nmax = P.nmax;
 
-    // per-lane scan state (wave-uniform: active, c, nck, fill, par, bsf)
-    uint32_t H[3 * kCk];
+    // per-lane scan state (wave-uniform: active, c, ph, nck, fill, par, bsf)
+    uint32_t H[3 * kCk];  // ring of three 8-hash groups; step c reads groups c, c+1, c+2 (mod 3)
     uint64_t cw[3], pa = 0, pb = 0;  // the item's first words; the next step's window words
     uint64_t s = 0;
-    int np = 0, p_open = 0, c = 0, nck = 0;
-    uint32_t prev_hm = 0, h_open = 0, fill = 0, par = 1, bsf = 0;
+    int np = 0, c = 0, ph = 0, nck = 0;
+    uint32_t prev_hm = 0, h_open = 0, p7 = 0, ihc = 0, fill = 0, par = 1, bsf = 0;
+    uint32_t *seg32 = (uint32_t *)seg;
     bool active = false;
     auto fetch = [&](uint64_t bt, uint64_t &sb, int &n, uint64_t *w) {
         const uint64_t item = bt * 64 + lane;
@@ -260,83 +272,128 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
         for (int k = 0; k < 3; ++k) w[k] = packed[(sb >> 5) + k];
     };
 
+    // one step: positions 8c .. 8c+7 of the lane's item; the window's bases start at 8c+16.
+    // G = c mod 3 names the ring group holding positions 8c.. (compile time, so the ring
+    // never moves). Positions are wave-uniform, so the close test is four compares.
+    auto step = [&](auto Gc) {
+        constexpr int G = decltype(Gc)::value;
+        c = __builtin_amdgcn_readfirstlane(c);
+        const int rb = kCk * c + 2 * kCk;
+        const uint64_t win = win32(pa, pb, s + rb);
+        {
+            const uint64_t qn = (s + rb + kCk) >> 5;  // next step's window words
+            pa = packed[qn];
+            pb = packed[qn + 1];
+        }
+        hash_step<kFull>(win, P.m, mmask, salt32, H + ((G + 2) % 3) * kCk);
+        uint32_t hm[kCk];
+        window_min<W, G>(H, hm);
+        if (c == 0) {
+            prev_hm = hm[0];
+            h_open = hm[0];
+            p7 = 0;
+        }
+#pragma unroll
+        for (int t = 0; t < kCk; ++t) {
+            const int i = kCk * c + t;
+            const uint32_t prv = t ? hm[t - 1] : prev_hm;
+            const bool cl = ((uint32_t)(i - 1) < (uint32_t)np) &
+                            ((i == np) | (hm[t] != prv) | ((int)p7 <= (i - nmax) * 128));
+            const unsigned long long bm = __builtin_amdgcn_ballot_w64(cl);
+            if (bm) {
+                if (cl) {
+                    const uint32_t idx =
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, fill));
+                    seg32[2 * idx] = h_open;
+                    seg32[2 * idx + 1] = p7 + ihc + (uint32_t)i;
+                    p7 = (uint32_t)i << kPeP;
+                    h_open = hm[t];
+                }
+                fill += (uint32_t)__popcll(bm);
+            }
+        }
+        prev_hm = hm[kCk - 1];
+    };
+
     // MCAAT_PROF_A=1: 100-MHz real-time ticks per phase, summed over waves
     unsigned long long tp[5] = {0, 0, 0, 0, 0}, t0 = prof ? __builtin_amdgcn_s_memrealtime() : 0;
-    auto tick = [&](int ph) {
+    auto tick = [&](int phase) {
         if (prof) {
             const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-            tp[ph] += t1 - t0;
+            tp[phase] += t1 - t0;
             t0 = t1;
         }
     };
 
+    // a new item hashes its first two groups into the ring groups G, G+1
+    auto start_item = [&](auto Gc) {
+        constexpr int G = decltype(Gc)::value;
+        fetch(batch, s, np, cw);
+        par ^= 1u;
+        ++bsf;
+        sbase[wave][par][lane] = s;
+        ihc = (par << kPePar) | ((uint32_t)lane << kPeLane);
+        {
+            const uint64_t q2 = (s + 2 * kCk) >> 5;
+            pa = packed[q2];
+            pb = packed[q2 + 1];
+        }
+        int mx = np;
+#pragma unroll
+        for (int o = 32; o; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+        nck = mx / kCk + 1;  // steps covering positions 0..max np (the last close)
+        const int o8 = (int)(s & 31) + kCk;
+        hash_step<kFull>(win32(cw[0], cw[1], s), P.m, mmask, salt32, H + G * kCk);
+        hash_step<kFull>(o8 >= 32 ? win32(cw[1], cw[2], s + kCk) : win32(cw[0], cw[1], s + kCk), P.m, mmask,
+                         salt32, H + ((G + 1) % 3) * kCk);
+        c = 0;
+        active = true;
+    };
+    // false: the wave goes to the flush with its ring at phase G
+    auto run = [&](auto Gc) -> bool {
+        constexpr int G = decltype(Gc)::value;
+        if (!active) {
+            // no more items, or the segment already references two batches (the sbase slots)
+            if (batch >= n_batches || bsf >= 2) {
+                ph = G;
+                return false;
+            }
+            start_item(Gc);
+        }
+        // a wave short of room for a worst-case step goes to the flush
+        if (fill + 64 * kCk > (uint32_t)kSeg) {
+            ph = G;
+            return false;
+        }
+        step(Gc);
+        if (++c == nck) {
+            active = false;
+            batch += bstride;
+        }
+        return true;
+    };
+
     for (;;) {
+        // the scan is unrolled over the three ring phases; a flush may interrupt it at any
+        // phase, so the ring is rotated back to phase 0 first (once per flush)
+        ph = __builtin_amdgcn_readfirstlane(ph);
+        if (ph != 0) {
+            uint32_t T[3 * kCk];
+#pragma unroll
+            for (int u = 0; u < 3 * kCk; ++u) T[u] = H[u];
+            if (ph == 1) {
+#pragma unroll
+                for (int u = 0; u < 3 * kCk; ++u) H[u] = T[(u + kCk) % (3 * kCk)];
+            } else {
+#pragma unroll
+                for (int u = 0; u < 3 * kCk; ++u) H[u] = T[(u + 2 * kCk) % (3 * kCk)];
+            }
+            ph = 0;
+        }
         for (;;) {
-            if (!active) {
-                if (batch >= n_batches) break;
-                // a segment references at most two batches (the sbase slots)
-                if (bsf >= 2) break;
-                fetch(batch, s, np, cw);
-                par ^= 1u;
-                ++bsf;
-                sbase[wave][par][lane] = s;
-                {
-                    const uint64_t q2 = (s + 2 * kCk) >> 5;
-                    pa = packed[q2];
-                    pb = packed[q2 + 1];
-                }
-                int mx = np;
-#pragma unroll
-                for (int o = 32; o; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
-                nck = mx / kCk + 1;  // steps covering positions 0..max np (the last close)
-                const int o8 = (int)(s & 31) + kCk;
-                hash_step(win32(cw[0], cw[1], s), P.m, mmask, salt32, H);
-                hash_step(o8 >= 32 ? win32(cw[1], cw[2], s + kCk) : win32(cw[0], cw[1], s + kCk), P.m, mmask,
-                          salt32, H + kCk);
-                c = 0;
-                active = true;
-            }
-            // a wave short of room for a worst-case step goes to the flush
-            if (fill + 64 * kCk > (uint32_t)kSeg) break;
-            // ---- one step: positions 8c .. 8c+7; window bases from 8c+16 ----
-            const int rb = 8 * c + 2 * kCk;
-            const uint64_t win = win32(pa, pb, s + rb);
-            {
-                const uint64_t qn = (s + rb + kCk) >> 5;  // next step's window words
-                pa = packed[qn];
-                pb = packed[qn + 1];
-            }
-            hash_step(win, P.m, mmask, salt32, H + 2 * kCk);
-            uint32_t hm[kCk];
-            window_min<W>(H, hm);
-            if (c == 0) {
-                prev_hm = hm[0];
-                h_open = hm[0];
-                p_open = 0;
-            }
-#pragma unroll
-            for (int t = 0; t < kCk; ++t) {
-                const int i = kCk * c + t;
-                const bool cl = i > 0 && i <= np && (i == np || hm[t] != prev_hm || i - p_open >= nmax);
-                const unsigned long long bm = __ballot(cl);
-                if (bm) {
-                    if (cl) {
-                        const uint32_t idx =
-                            fill + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0));
-                        seg[idx] = pre_entry(h_open, (uint32_t)(i - p_open), (uint32_t)p_open, par, (uint32_t)lane);
-                        p_open = i;
-                        h_open = hm[t];
-                    }
-                    fill += (uint32_t)__popcll(bm);
-                }
-                prev_hm = hm[t];
-            }
-#pragma unroll
-            for (int t = 0; t < 2 * kCk; ++t) H[t] = H[t + kCk];
-            if (++c == nck) {
-                active = false;
-                batch += bstride;
-            }
+            if (!run(std::integral_constant<int, 0>())) break;
+            if (!run(std::integral_constant<int, 1>())) break;
+            if (!run(std::integral_constant<int, 2>())) break;
         }
         tick(0);
         // bucket of each entry: the minimum hash is biased towards 0, so buckets come from
@@ -408,8 +465,9 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
                 if (j < total) {
                     const uint32_t i = perm[j];
                     q[k] = stage[i];
-                    const uint32_t ln = (uint32_t)(q[k] >> 46) & 63, pr = (uint32_t)(q[k] >> 45) & 1;
-                    B0[k] = sbase[i / kSeg][pr][ln] + ((q[k] >> 38) & 127);
+                    const uint32_t hi = (uint32_t)(q[k] >> 32);
+                    const uint32_t ln = (hi >> kPeLane) & 63, pr = (hi >> kPePar) & 1;
+                    B0[k] = sbase[i / kSeg][pr][ln] + ((hi >> kPeP) & 127);
                 }
 #pragma unroll
                 for (int z = 0; z < 3; ++z) x[k][z] = packed[(B0[k] >> 5) + z];
@@ -420,7 +478,8 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
                 if (j >= total) continue;
                 const uint32_t i = perm[j];
                 const int b = stage_l1[i];
-                const uint32_t n = (uint32_t)(q[k] >> 32) & 63;
+                const uint32_t hi = (uint32_t)(q[k] >> 32);
+                const uint32_t n = (hi & 127) - ((hi >> kPeP) & 127);
                 const int sh = 2 * (int)(B0[k] & 31);
                 // bases past the last edge are zeroed, so every copy of a super-k-mer is the
                 // same 128-bit descriptor whatever follows it in its read
@@ -652,10 +711,10 @@ __global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict
     // MCAAT_PROF_C=1: 100-MHz ticks per phase (clear, collapse, expand, emit) and counts of
     // partitions expanded raw
     unsigned long long tp[5] = {0, 0, 0, 0, 0}, t0 = prof ? __builtin_amdgcn_s_memrealtime() : 0;
-    auto tick = [&](int ph) {
+    auto tick = [&](int phase) {
         if (prof) {
             const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
-            tp[ph] += t1 - t0;
+            tp[phase] += t1 - t0;
             t0 = t1;
         }
     };
@@ -1000,6 +1059,7 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     P.m = std::max(3, std::min(16, E - 8));  // <= 16: the m-mer machinery is 32-bit
     if (P.m > E) P.m = E;
     P.w = E - P.m + 1;
+    if (P.w >= 10 && P.m != 16) throw Error(MCAAT_E_INVALID, "node_counter: W >= 10 needs m = 16");
     P.nmax = kDescBases - E + 1;
     P.salt = 0x6d696e696d697aULL;
 

@@ -14,7 +14,7 @@ import sys
 
 src, dst = sys.argv[1], sys.argv[2]
 NAMES = {"k_sk_scatter": "sk_scatter", "k_lds_count": "lds_count", "k_l2_scatter": "l2_partition",
-         "k_l2_hist": "l2_partition"}
+         "k_l2_hist": "l2_hist"}
 fetch = collections.defaultdict(float)
 write = collections.defaultdict(float)
 launches = collections.defaultdict(set)
