@@ -37,6 +37,7 @@ typedef struct mcaat_reads mcaat_reads;
 typedef struct mcaat_graph mcaat_graph;
 typedef struct mcaat_cycles mcaat_cycles;
 typedef struct mcaat_counts mcaat_counts;
+typedef struct mcaat_mapped mcaat_mapped;
 
 /* ---- context ------------------------------------------------------------- */
 /* Replaces: nothing in the reference (single process, OpenMP). Binds one GPU. */
@@ -55,6 +56,11 @@ int mcaat_reads_from_host(mcaat_ctx *ctx, const uint64_t *packed, uint64_t n_wor
 /* Non-ACGT symbols split a read (k-mers spanning them are dropped). gz via zlib. */
 int mcaat_reads_from_fastx(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_reads **out);
 int mcaat_reads_info(const mcaat_reads *r, uint64_t *n_reads, uint64_t *n_bases);
+/* Mapping view used by mcaat_map_reads: one entry per input record (first file as is,
+ * second file reversed and complemented as reads.cpp:20-31 does; any symbol other than
+ * A/C/G maps like T, reads.cpp:44-52). *separate = 0 when it is the counting view itself
+ * (one input file, ACGT only, or reads not loaded from files). */
+int mcaat_reads_records_info(const mcaat_reads *r, uint64_t *n_records, int *separate);
 int mcaat_reads_download(const mcaat_reads *r, uint64_t *packed, uint64_t *offsets);
 void mcaat_reads_free(mcaat_reads *r);
 
@@ -107,7 +113,23 @@ int mcaat_graph_set_valid(mcaat_graph *g, const uint64_t *ids, size_t n, int val
  * counts[i] for each id; order DESCENDING for outgoing, ASCENDING for incoming. */
 int mcaat_graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, int incoming,
                           uint64_t *out, int32_t *counts);
+/* valid &= {ids}: keep_crispr_regions_extended_by_k (spacer_ordering.cpp:129-137) invalidates
+ * every valid edge outside the extended cycle set; here one bitmap AND on the device. */
+int mcaat_graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n);
 void mcaat_graph_free(mcaat_graph *g);
+
+/* ---- relevant-read mapping -------------------------------
+ * Replaces: get_reads (reads.cpp:88-130) with get_read_from_sequence (reads.cpp:57-86)
+ * and k_mer_to_node_id (reads.cpp:33-55): every record of the mapping view whose length
+ * exceeds 2k and whose first or last k-mer's IndexBinarySearch id is one of cycle_nodes
+ * is returned, in input order, as the ids of all its len-k+1 k-mers (~0 = absent label,
+ * the reference's -1). max_batch_ids bounds the device output buffer (0: 2^28 ids).
+ * Results stay valid until mcaat_mapped_free; records[i] is the mapping-view index. */
+int mcaat_map_reads(const mcaat_graph *g, const mcaat_reads *r, const uint64_t *cycle_nodes, size_t n_nodes,
+                    uint64_t max_batch_ids, mcaat_mapped **out);
+int mcaat_mapped_get(const mcaat_mapped *m, uint64_t *n_reads, const uint64_t **ids, const uint64_t **offsets,
+                     const uint64_t **records);
+void mcaat_mapped_free(mcaat_mapped *m);
 
 /* ---- multi-GPU build (one process per GPU) ---------------------
  * Replaces: the single-process Read2SdbgS2::Run of sdbg_build.cpp:171-187 when the reads

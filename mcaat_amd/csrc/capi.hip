@@ -84,8 +84,12 @@ void upload_reads(mcaat_ctx *ctx, const uint64_t *packed, uint64_t n_words, cons
     HIP_OK(hipStreamSynchronize(ctx->stream));
 }
 
-// FASTQ/FASTA(.gz) -> packed reads. Records are split at non-ACGT symbols.
-struct Packer {
+// FASTQ/FASTA(.gz) -> packed reads. Counting view: records are split at non-ACGT symbols.
+// Mapping view (reads.cpp:88-130): one entry per record; records of the second file are
+// reversed and complemented (reverse_pair_ends_sequence, reads.cpp:20-31: only A/C/G/T
+// are complemented), then coded as k_mer_to_node_id does (reads.cpp:44-52: 'A','C','G' ->
+// 0,1,2 and every other character -> 3).
+struct Stream {
     std::vector<uint64_t> words;
     std::vector<uint64_t> offsets{0};
     uint64_t n = 0;
@@ -94,9 +98,17 @@ struct Packer {
         words[n >> 5] |= (uint64_t)b << (2 * (n & 31));
         ++n;
     }
+};
+
+struct Packer {
+    Stream reads;    // counting view
+    Stream records;  // mapping view
+    bool records_differ = false;
+    int file = 0;    // 0: first input file, >0: second (paired) file
     void end_read() {
-        if (n != offsets.back()) offsets.push_back(n);
+        if (reads.n != reads.offsets.back()) reads.offsets.push_back(reads.n);
     }
+    static int map_code(char ch) { return ch == 'A' ? 0 : ch == 'C' ? 1 : ch == 'G' ? 2 : 3; }
     void add_sequence(const std::string &s) {
         for (char ch : s) {
             int b;
@@ -108,11 +120,36 @@ struct Packer {
                 default: b = -1;
             }
             if (b < 0) end_read();
-            else put(b);
+            else reads.put(b);
+            if (ch != 'A' && ch != 'C' && ch != 'G' && ch != 'T') records_differ = true;
         }
         end_read();
+        if (file == 0) {
+            for (char ch : s) records.put(map_code(ch));
+        } else {
+            records_differ = true;
+            for (size_t i = s.size(); i-- > 0;) {
+                const char ch = s[i];
+                records.put(map_code(ch == 'A' ? 'T' : ch == 'T' ? 'A' : ch == 'C' ? 'G' : ch == 'G' ? 'C' : ch));
+            }
+        }
+        records.offsets.push_back(records.n);
     }
 };
+
+void upload_records(mcaat_ctx *ctx, const Stream &rec, mcaat_reads *r) {
+    r->n_records = rec.offsets.size() - 1;
+    r->has_records = true;
+    r->rec_packed.alloc(rec.words.size() + 16);
+    r->rec_offsets.alloc(rec.offsets.size());
+    HIP_OK(hipMemsetAsync(r->rec_packed.p, 0, r->rec_packed.bytes(), ctx->stream));
+    if (!rec.words.empty())
+        HIP_OK(hipMemcpyAsync(r->rec_packed.p, rec.words.data(), 8 * rec.words.size(), hipMemcpyHostToDevice,
+                              ctx->stream));
+    HIP_OK(hipMemcpyAsync(r->rec_offsets.p, rec.offsets.data(), 8 * rec.offsets.size(), hipMemcpyHostToDevice,
+                          ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+}
 
 void read_fastx(const char *path, Packer &pk) {
     gzFile f = gzopen(path, "rb");
@@ -293,10 +330,15 @@ int mcaat_reads_from_fastx(mcaat_ctx *ctx, const char *const *files, int n_files
         require(ctx && out && files && n_files > 0, "null argument");
         HIP_OK(hipSetDevice(ctx->device));
         Packer pk;
-        for (int i = 0; i < n_files; ++i) read_fastx(files[i], pk);
+        for (int i = 0; i < n_files; ++i) {
+            pk.file = i;
+            read_fastx(files[i], pk);
+        }
         auto *r = new mcaat_reads;
         try {
-            upload_reads(ctx, pk.words.data(), pk.words.size(), pk.offsets.data(), pk.offsets.size() - 1, r);
+            upload_reads(ctx, pk.reads.words.data(), pk.reads.words.size(), pk.reads.offsets.data(),
+                         pk.reads.offsets.size() - 1, r);
+            if (pk.records_differ) upload_records(ctx, pk.records, r);
         } catch (...) {
             delete r;
             throw;
@@ -548,7 +590,53 @@ int mcaat_graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, i
     });
 }
 
+int mcaat_graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n) {
+    return guarded([&] {
+        require(g && (ids || n == 0), "null argument");
+        HIP_OK(hipSetDevice(g->ctx->device));
+        graph_keep_only(g, ids, n);
+    });
+}
+
 void mcaat_graph_free(mcaat_graph *g) { delete g; }
+
+int mcaat_reads_records_info(const mcaat_reads *r, uint64_t *n_records, int *separate) {
+    return guarded([&] {
+        require(r != nullptr, "null argument");
+        if (n_records) *n_records = r->has_records ? r->n_records : r->n_reads;
+        if (separate) *separate = r->has_records ? 1 : 0;
+    });
+}
+
+int mcaat_map_reads(const mcaat_graph *g, const mcaat_reads *r, const uint64_t *cycle_nodes, size_t n_nodes,
+                    uint64_t max_batch_ids, mcaat_mapped **out) {
+    return guarded([&] {
+        require(g && r && out && (cycle_nodes || n_nodes == 0), "null argument");
+        require(g->ctx == r->ctx, "graph and reads belong to different contexts");
+        HIP_OK(hipSetDevice(g->ctx->device));
+        auto *m = new mcaat_mapped;
+        try {
+            map_reads(g, r, cycle_nodes, n_nodes, max_batch_ids ? max_batch_ids : (uint64_t)1 << 28, m);
+        } catch (...) {
+            delete m;
+            throw;
+        }
+        *out = m;
+    });
+}
+
+int mcaat_mapped_get(const mcaat_mapped *m, uint64_t *n_reads, const uint64_t **ids, const uint64_t **offsets,
+                     const uint64_t **records) {
+    return guarded([&] {
+        require(m != nullptr, "null argument");
+        if (n_reads) *n_reads = m->offsets.size() - 1;
+        if (ids) *ids = m->ids.data();
+        if (offsets) *offsets = m->offsets.data();
+        if (records) *records = m->records.data();
+    });
+}
+
+void mcaat_mapped_free(mcaat_mapped *m) { delete m; }
 
 void mcaat_cf_default_params(mcaat_cf_params *p) {
     if (!p) return;

@@ -127,6 +127,19 @@ struct mcaat_reads {
     mcaat::DevBuf<uint64_t> offsets;
     uint64_t n_reads = 0, n_bases = 0, n_words = 0;
     uint64_t fixed_len = 0;  // >0 when every read has this length (offsets[i] = i*len)
+    // Mapping view (reads.cpp:88-130): one entry per input record, second-file records
+    // reversed and complemented, A/C/G -> 0/1/2 and any other symbol -> 3. Empty when it
+    // equals the counting view above (one file, ACGT only).
+    mcaat::DevBuf<uint64_t> rec_packed;
+    mcaat::DevBuf<uint64_t> rec_offsets;
+    uint64_t n_records = 0;
+    bool has_records = false;
+};
+
+struct mcaat_mapped {  // relevant reads: node-id chains in reference order
+    std::vector<uint64_t> ids;
+    std::vector<uint64_t> offsets{0};
+    std::vector<uint64_t> records;  // index of each relevant read in the mapping view
 };
 
 struct mcaat_graph {
@@ -138,6 +151,9 @@ struct mcaat_graph {
     mcaat::DevBuf<uint64_t> out_info;
     mcaat::DevBuf<uint64_t> in_info;
     mcaat::DevBuf<uint64_t> valid;
+    // radix directory over the top bits of the BOSS key (label lookups after the build)
+    mcaat::DevBuf<uint64_t> dir;
+    int dir_shift = 0;
     mcaat::GraphView view() const {
         return mcaat::GraphView{k, D, key.p, mult.p, out_info.p, in_info.p, valid.p};
     }
@@ -247,6 +263,9 @@ void graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, int in
                      int32_t *counts);
 void graph_set_valid(mcaat_graph *g, const uint64_t *ids, size_t n, int valid);
 void graph_download_valid(const mcaat_graph *g, uint8_t *valid);
+void graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n);
+void map_reads(const mcaat_graph *g, const mcaat_reads *r, const uint64_t *nodes, size_t n_nodes,
+               uint64_t max_batch_ids, mcaat_mapped *out);
 
 }  // namespace mcaat
 

@@ -1,0 +1,235 @@
+// read_mapping.hip — relevant-read mapping after the cycle finder.
+//
+// Reference: get_reads (reads.cpp:88-130) keeps every read whose FIRST or LAST k-mer maps
+// (IndexBinarySearch, reads.cpp:33-55) to a node of some cycle, and returns for it the node
+// id of every k-mer (get_read_from_sequence, reads.cpp:57-86; reads with length <= 2k are
+// skipped). Host-side that is one binary search per k-mer of every read of the input. Here:
+//
+//  1. k_label_set   — the labels L such that IndexBinarySearch(L) is a cycle node: the
+//                     label of a cycle node e that is the LAST edge of its label group
+//                     (IndexBinarySearch returns the group's last edge).
+//                     Open-addressing table in HBM (L2/MALL resident: 2 slots per node).
+//  2. k_map_ends    — one lane per record: the two end labels are funnel shifts of the
+//                     packed record stream, each probed once in the table (no graph access
+//                     for the ~99.8 % of reads that miss). Writes the record's id count.
+//  3. select + scan — hit records in input order and their output offsets (hipcub).
+//  4. k_map_ids     — one wave per hit record, lanes over its k-mer positions: each label
+//                     is resolved against the BOSS keys through the radix directory kept
+//                     with the graph (upper bound of label<<2|3, then a label check), in
+//                     batches that fit a bounded device buffer.
+//
+// Bytes per record (roofline, HBM): 0.25 B/base read once + 4 B count written; the hit
+// records (a small fraction) add (L-k+1) directory + key probes and 8 B per id.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+
+#include "internal.h"
+
+namespace mcaat {
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ bool set_has(const uint64_t *slot, uint64_t mask, uint64_t x) {
+    for (uint64_t h = mix64(x) & mask;; h = (h + 1) & mask) {
+        const uint64_t v = slot[h];
+        if (v == x) return true;
+        if (v == kEmpty) return false;
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_label_set(const uint64_t *key, uint64_t D, const uint64_t *nodes,
+                                                      uint64_t n, unsigned long long *slot, uint64_t mask) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t e = nodes[i];
+        if (e >= D) continue;
+        const uint64_t R = key[e] >> 2;
+        if (e + 1 < D && (key[e + 1] >> 2) == R) continue;  // not the group's last edge
+        for (uint64_t h = mix64(R) & mask;; h = (h + 1) & mask) {
+            const unsigned long long prev = atomicCAS(&slot[h], (unsigned long long)kEmpty, (unsigned long long)R);
+            if (prev == kEmpty || prev == R) break;
+        }
+    }
+}
+
+// record i -> number of ids it contributes (0 unless it is relevant)
+__global__ void __launch_bounds__(kBlock) k_map_ends(const uint64_t *packed, const uint64_t *off, uint64_t n_rec,
+                                                     int K, const uint64_t *slot, uint64_t mask, uint64_t *n_ids,
+                                                     uint8_t *hit) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_rec; i += stride) {
+        const uint64_t a = off[i], len = off[i + 1] - a;
+        bool h = false;
+        if (len > 2 * (uint64_t)K) {
+            h = set_has(slot, mask, window_at(packed, a, K)) || set_has(slot, mask, window_at(packed, a + len - K, K));
+        }
+        n_ids[i] = h ? len - K + 1 : 0;
+        hit[i] = h;
+    }
+}
+
+// IndexBinarySearch: last edge whose label is R, kEmpty when the label is absent
+__device__ __forceinline__ uint64_t dev_index_search(const uint64_t *key, uint64_t D, const uint64_t *dir, int shift,
+                                                     uint64_t nprefix, uint64_t R) {
+    const uint64_t q = (R + 1) << 2;  // first key past the label group (<= 2^(2E))
+    const uint64_t p = q >> shift;
+    if (p >= nprefix) return (D > 0 && (key[D - 1] >> 2) == R) ? D - 1 : kEmpty;
+    uint64_t lo = dir[p], hi = dir[p + 1];
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (key[mid] < q) lo = mid + 1; else hi = mid;
+    }
+    return (lo > 0 && (key[lo - 1] >> 2) == R) ? lo - 1 : kEmpty;
+}
+
+__global__ void __launch_bounds__(kBlock) k_map_ids(const uint64_t *packed, const uint64_t *off, int K,
+                                                    const uint64_t *key, uint64_t D, const uint64_t *dir, int shift,
+                                                    uint64_t nprefix, const uint64_t *hit_rec, const uint64_t *hit_pos, uint64_t h0,
+                                                    uint64_t h1, uint64_t *ids) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t base = hit_pos[h0];
+    for (uint64_t h = h0 + (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); h < h1; h += waves) {
+        const uint64_t r = hit_rec[h];
+        const uint64_t a = off[r], n = off[r + 1] - a - K + 1;
+        uint64_t *o = ids + (hit_pos[h] - base);
+        for (uint64_t j = lane; j < n; j += 64) o[j] = dev_index_search(key, D, dir, shift, nprefix, window_at(packed, a + j, K));
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_keep_bits(uint64_t *keep, const uint64_t *ids, uint64_t n, uint64_t D) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t e = ids[i];
+        if (e < D) atomicOr((unsigned long long *)&keep[e >> 6], 1ULL << (e & 63));
+    }
+}
+
+__global__ void __launch_bounds__(kBlock) k_and_bits(uint64_t *valid, const uint64_t *keep, uint64_t nw) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) valid[w] &= keep[w];
+}
+
+template <class F>
+void cub_call(hipStream_t st, F &&f) {
+    size_t tmp = 0;
+    HIP_OK(f(nullptr, tmp));
+    DevBuf<uint8_t> t(tmp ? tmp : 1);
+    HIP_OK(f(t.p, tmp));
+}
+
+}  // namespace
+
+void map_reads(const mcaat_graph *g, const mcaat_reads *r, const uint64_t *nodes, size_t n_nodes,
+               uint64_t max_batch_ids, mcaat_mapped *out) {
+    mcaat_ctx *ctx = g->ctx;
+    hipStream_t st = ctx->stream;
+    const int K = g->k;
+    const uint64_t *packed = r->has_records ? r->rec_packed.p : r->packed.p;
+    const uint64_t *off = r->has_records ? r->rec_offsets.p : r->offsets.p;
+    const uint64_t n_rec = r->has_records ? r->n_records : r->n_reads;
+    out->ids.clear();
+    out->offsets.assign(1, 0);
+    out->records.clear();
+    if (n_rec == 0 || n_nodes == 0 || g->D == 0) return;
+    if (!g->dir.p) throw Error(MCAAT_E_INVALID, "graph has no label directory");
+    StageTimer timer(ctx);
+
+    // 1. label set of the cycle nodes
+    const uint64_t cap = next_pow2(std::max<uint64_t>(64, 2 * (uint64_t)n_nodes));
+    DevBuf<uint64_t> slot(cap), dn(n_nodes);
+    HIP_OK(hipMemsetAsync(slot.p, 0xFF, 8 * cap, st));
+    HIP_OK(hipMemcpyAsync(dn.p, nodes, 8 * n_nodes, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_label_set, dim3(grid_for(n_nodes, kBlock)), dim3(kBlock), 0, st, g->key.p, g->D, dn.p,
+                       (uint64_t)n_nodes, (unsigned long long *)slot.p, cap - 1);
+    LAUNCH_OK();
+
+    // 2. end probes
+    DevBuf<uint64_t> nid(n_rec);
+    DevBuf<uint8_t> hit(n_rec);
+    hipLaunchKernelGGL(k_map_ends, dim3(grid_for(n_rec, kBlock, 8 * ctx->n_cu * 8)), dim3(kBlock), 0, st, packed, off,
+                       n_rec, K, slot.p, cap - 1, nid.p, hit.p);
+    LAUNCH_OK();
+    timer.mark("map_ends");
+
+    // 3. hit records in order, their id offsets
+    DevBuf<uint64_t> hrec(n_rec), dcount(1);
+    hipcub::CountingInputIterator<uint64_t> it(0);
+    cub_call(st, [&](void *t, size_t &b) {
+        return hipcub::DeviceSelect::Flagged(t, b, it, hit.p, hrec.p, dcount.p, (size_t)n_rec, st);
+    });
+    uint64_t n_hit = 0;
+    HIP_OK(hipMemcpyAsync(&n_hit, dcount.p, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (n_hit == 0) {
+        timer.mark("map_ids");
+        HIP_OK(hipStreamSynchronize(st));
+        timer.finish();
+        return;
+    }
+    DevBuf<uint64_t> hlen(n_hit), hpos(n_hit + 1);
+    {
+        // gather the hit lengths (select again on the counts, same flags => same order)
+        cub_call(st, [&](void *t, size_t &b) {
+            return hipcub::DeviceSelect::Flagged(t, b, nid.p, hit.p, hlen.p, dcount.p, (size_t)n_rec, st);
+        });
+        cub_call(st, [&](void *t, size_t &b) {
+            return hipcub::DeviceScan::InclusiveSum(t, b, hlen.p, hpos.p + 1, (size_t)n_hit, st);
+        });
+        HIP_OK(hipMemsetAsync(hpos.p, 0, 8, st));
+    }
+    std::vector<uint64_t> pos(n_hit + 1);
+    out->records.resize(n_hit);
+    HIP_OK(hipMemcpyAsync(pos.data(), hpos.p, 8 * (n_hit + 1), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(out->records.data(), hrec.p, 8 * n_hit, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    out->offsets = pos;
+    out->ids.resize(pos[n_hit]);
+
+    // 4. ids, in batches of hit records whose ids fit the device buffer
+    uint64_t max_rec = 1;  // the buffer holds at least the longest record
+    for (uint64_t h = 0; h < n_hit; ++h) max_rec = std::max(max_rec, pos[h + 1] - pos[h]);
+    DevBuf<uint64_t> ids(std::max(std::min(max_batch_ids, pos[n_hit]), max_rec));
+    const uint64_t bufn = ids.n;
+    const uint64_t nprefix = 1ULL << (2 * (K + 1) - g->dir_shift);
+    for (uint64_t h0 = 0; h0 < n_hit;) {
+        uint64_t h1 = h0 + 1;  // at least one record per batch
+        while (h1 < n_hit && pos[h1 + 1] - pos[h0] <= bufn) ++h1;
+        const uint64_t waves = h1 - h0;
+        hipLaunchKernelGGL(k_map_ids, dim3(grid_for(waves, kBlock / 64, 16 * ctx->n_cu * 4)), dim3(kBlock), 0, st,
+                           packed, off, K, g->key.p, g->D, g->dir.p, g->dir_shift, nprefix, hrec.p, hpos.p, h0, h1,
+                           ids.p);
+        LAUNCH_OK();
+        HIP_OK(hipMemcpyAsync(out->ids.data() + pos[h0], ids.p, 8 * (pos[h1] - pos[h0]), hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        h0 = h1;
+    }
+    timer.mark("map_ids");
+    HIP_OK(hipStreamSynchronize(st));
+    timer.finish();
+}
+
+// valid &= {ids}: keep_crispr_regions_extended_by_k's invalidation of every edge outside
+// the extended cycle set (spacer_ordering.cpp:129-137) as one bitmap AND
+void graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n) {
+    hipStream_t st = g->ctx->stream;
+    const uint64_t nw = g->n_words();
+    if (!nw) return;
+    DevBuf<uint64_t> keep(nw);
+    HIP_OK(hipMemsetAsync(keep.p, 0, 8 * nw, st));
+    if (n) {
+        DevBuf<uint64_t> di(n);
+        HIP_OK(hipMemcpyAsync(di.p, ids, 8 * n, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_keep_bits, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, keep.p, di.p, (uint64_t)n,
+                           g->D);
+        LAUNCH_OK();
+        HIP_OK(hipStreamSynchronize(st));
+    }
+    hipLaunchKernelGGL(k_and_bits, dim3(grid_for(nw, kBlock)), dim3(kBlock), 0, st, g->valid.p, keep.p, nw);
+    LAUNCH_OK();
+    HIP_OK(hipStreamSynchronize(st));
+}
+
+}  // namespace mcaat

@@ -599,7 +599,9 @@ void sdbg_finish(mcaat_ctx *ctx, mcaat_graph *g) {
     if (B > 30) B = 30;
     const int shift = 2 * E - B;
     const uint64_t nprefix = 1ULL << B;
-    DevBuf<uint64_t> dir(nprefix + 1);
+    DevBuf<uint64_t> &dir = g->dir;
+    dir.alloc(nprefix + 1);
+    g->dir_shift = shift;
     hipLaunchKernelGGL(k_dir, dim3(grid_for(nprefix + 1, kBlock)), dim3(kBlock), 0, st, g->key.p, D, shift, nprefix,
                        dir.p);
     LAUNCH_OK();

@@ -101,6 +101,11 @@ SIGNATURES = {
                                      _u64p]),
     "mcaat_graph_from_sorted": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64,
                                           C.POINTER(C.c_void_p)]),
+    "mcaat_reads_records_info": (C.c_int, [C.c_void_p, _u64p, C.POINTER(C.c_int)]),
+    "mcaat_graph_keep_only": (C.c_int, [C.c_void_p, _u64p, C.c_size_t]),
+    "mcaat_map_reads": (C.c_int, [C.c_void_p, C.c_void_p, _u64p, C.c_size_t, C.c_uint64, C.POINTER(C.c_void_p)]),
+    "mcaat_mapped_get": (C.c_int, [C.c_void_p, _u64p, C.POINTER(_u64p), C.POINTER(_u64p), C.POINTER(_u64p)]),
+    "mcaat_mapped_free": (None, [C.c_void_p]),
 }
 
 _lib: Optional[C.CDLL] = None
@@ -265,6 +270,12 @@ class Reads:
         _check(self.ctx._lib.mcaat_reads_info(self.h, C.byref(n), C.byref(b)))
         return n.value, b.value
 
+    def records_info(self) -> Tuple[int, bool]:
+        n = C.c_uint64(0)
+        sep = C.c_int(0)
+        _check(self.ctx._lib.mcaat_reads_records_info(self.h, C.byref(n), C.byref(sep)))
+        return n.value, bool(sep.value)
+
     def download(self) -> Tuple[np.ndarray, np.ndarray]:
         n, b = self.info()
         packed = np.zeros((b + 31) // 32, dtype=np.uint64)
@@ -378,6 +389,21 @@ class CycleResult:
     buckets: List[int] = field(default_factory=list)
 
 
+@dataclass
+class MappedReads:
+    """Relevant reads (reads.cpp:88-130): read i = ids[offsets[i]:offsets[i+1]]."""
+
+    ids: np.ndarray
+    offsets: np.ndarray
+    records: np.ndarray
+
+    def __len__(self) -> int:
+        return len(self.offsets) - 1
+
+    def read(self, i: int) -> List[int]:
+        return self.ids[self.offsets[i]:self.offsets[i + 1]].tolist()
+
+
 class Graph:
     """Device-resident SDBG (mcaat_graph)."""
 
@@ -423,6 +449,28 @@ class Graph:
         _check(self.ctx._lib.mcaat_graph_neighbors(self.h, _ptr(ids, _u64p), ids.size, int(incoming),
                                                    _ptr(out, _u64p), _ptr(cnt, _i32p)))
         return out[: 4 * ids.size].reshape(-1, 4), cnt[: ids.size]
+
+    def keep_only(self, ids: np.ndarray) -> None:
+        """valid &= {ids} (keep_crispr_regions_extended_by_k, spacer_ordering.cpp:129-137)."""
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        _check(self.ctx._lib.mcaat_graph_keep_only(self.h, _ptr(ids, _u64p), ids.size))
+
+    def map_reads(self, reads: "Reads", cycle_nodes: np.ndarray, max_batch_ids: int = 0) -> "MappedReads":
+        """get_reads (reads.cpp:88-130) on the GPU: relevant reads as node-id chains."""
+        nodes = np.ascontiguousarray(cycle_nodes, dtype=np.uint64)
+        h = C.c_void_p()
+        lib = self.ctx._lib
+        _check(lib.mcaat_map_reads(self.h, reads.h, _ptr(nodes, _u64p), nodes.size, max_batch_ids, C.byref(h)))
+        try:
+            n = C.c_uint64(0)
+            ip, op, rp = _u64p(), _u64p(), _u64p()
+            _check(lib.mcaat_mapped_get(h, C.byref(n), C.byref(ip), C.byref(op), C.byref(rp)))
+            offs = np.ctypeslib.as_array(op, shape=(n.value + 1,)).copy()
+            ids = np.ctypeslib.as_array(ip, shape=(int(offs[-1]),)).copy() if offs[-1] else np.zeros(0, np.uint64)
+            recs = np.ctypeslib.as_array(rp, shape=(n.value,)).copy() if n.value else np.zeros(0, np.uint64)
+            return MappedReads(ids=ids, offsets=offs, records=recs)
+        finally:
+            lib.mcaat_mapped_free(h)
 
     def set_valid(self, ids: np.ndarray, valid: bool) -> None:
         ids = np.ascontiguousarray(ids, dtype=np.uint64)

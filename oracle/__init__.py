@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 import subprocess
-from typing import List, Tuple
+from typing import List, Sequence, Tuple
 
 import numpy as np
 
@@ -41,6 +41,9 @@ _SIG = {
     "oracle_incoming": (C.c_int, [C.c_void_p, C.c_uint64, _u64p]),
     "oracle_get_label": (C.c_int, [C.c_void_p, C.c_uint64, _u8p]),
     "oracle_index_binary_search": (C.c_int64, [C.c_void_p, _u8p]),
+    "oracle_reverse_pair_ends": (None, [C.c_char_p]),
+    "oracle_get_reads": (C.c_uint64, [C.c_void_p, C.POINTER(C.c_char_p), C.c_uint64, C.c_uint64, _u64p, C.c_uint64,
+                                      C.POINTER(_u64p), C.POINTER(_u64p)]),
     "oracle_cycle_finder": (C.c_void_p, [C.c_void_p, C.POINTER(_Params)]),
     "oracle_collect_tips": (C.c_uint64, [C.c_void_p, _u8p]),
     "oracle_invalidate_mult_one": (C.c_uint64, [C.c_void_p]),
@@ -94,6 +97,13 @@ def count_canonical(packed: np.ndarray, offsets: np.ndarray, k: int, threads: in
     lib().oracle_free(C.cast(kp, C.c_void_p))
     lib().oracle_free(C.cast(cp, C.c_void_p))
     return keys, counts
+
+
+def reverse_pair_ends(s: str) -> str:
+    """reads.cpp:20-31 (test oracle)."""
+    b = C.create_string_buffer(s.encode())
+    lib().oracle_reverse_pair_ends(b)
+    return b.value.decode()
 
 
 class OGraph:
@@ -159,6 +169,19 @@ class OGraph:
     def index_binary_search(self, seq) -> int:
         s = np.ascontiguousarray(seq, dtype=np.uint8)
         return lib().oracle_index_binary_search(self.h, _p(s, _u8p))
+
+    def get_reads(self, seqs: Sequence[str], n_file1: int, cycle_nodes) -> List[List[int]]:
+        """reads.cpp:88-130 (test oracle): relevant reads as node-id chains."""
+        arr = (C.c_char_p * max(len(seqs), 1))(*[x.encode() for x in seqs])
+        nodes = np.ascontiguousarray(np.asarray(list(cycle_nodes), dtype=np.uint64))
+        fp, op = _u64p(), _u64p()
+        n = lib().oracle_get_reads(self.h, arr, len(seqs), n_file1, _p(nodes, _u64p), nodes.size, C.byref(fp),
+                                   C.byref(op))
+        offs = np.ctypeslib.as_array(op, shape=(n + 1,)).copy()
+        flat = np.ctypeslib.as_array(fp, shape=(max(int(offs[-1]), 1),))[: int(offs[-1])].copy()
+        lib().oracle_free(C.cast(fp, C.c_void_p))
+        lib().oracle_free(C.cast(op, C.c_void_p))
+        return [flat[offs[i]:offs[i + 1]].tolist() for i in range(n)]
 
     def collect_tips(self) -> np.ndarray:
         t = np.zeros(max(self.size, 1), dtype=np.uint8)

@@ -24,6 +24,7 @@
 #include <cstring>
 #include <functional>
 #include <map>
+#include <string>
 #include <unordered_map>
 #include <unordered_set>
 #include <utility>
@@ -409,6 +410,41 @@ struct CycleFinderO {
 
 }  // namespace
 
+/* ---------------- relevant reads (reads.cpp) ---------------- */
+// reads.cpp:20-31
+void reverse_pair_ends_sequence(std::string &sequence) {
+    std::reverse(sequence.begin(), sequence.end());
+    for (char &base : sequence) {
+        if (base == 'A') base = 'T';
+        else if (base == 'T') base = 'A';
+        else if (base == 'C') base = 'G';
+        else if (base == 'G') base = 'C';
+    }
+}
+// reads.cpp:33-55
+uint64_t k_mer_to_node_id(const Graph &sdbg, const std::string &k_mer) {
+    if ((int)k_mer.size() != sdbg.k) return 0;
+    std::vector<uint8_t> seq(sdbg.k);
+    for (int i = 0; i < sdbg.k; ++i) {
+        const char c = k_mer[i];
+        seq[i] = c == 'A' ? 1 : c == 'C' ? 2 : c == 'G' ? 3 : 4;
+    }
+    return (uint64_t)sdbg.IndexBinarySearch(seq.data());
+}
+// reads.cpp:57-86
+std::vector<uint64_t> get_read_from_sequence(const Graph &sdbg, const std::unordered_set<uint64_t> &nodes_of_cycles,
+                                             const std::string &sequence) {
+    const uint32_t K = sdbg.k;
+    if (sequence.size() <= 2 * K) return {};
+    const uint64_t start_node_id = k_mer_to_node_id(sdbg, sequence.substr(0, K));
+    const uint64_t end_node_id = k_mer_to_node_id(sdbg, sequence.substr(sequence.size() - K, K));
+    if (!nodes_of_cycles.count(start_node_id) && !nodes_of_cycles.count(end_node_id)) return {};
+    std::vector<uint64_t> read = {start_node_id};
+    for (size_t i = 1; i < sequence.size() - K; ++i) read.push_back(k_mer_to_node_id(sdbg, sequence.substr(i, K)));
+    read.push_back(end_node_id);
+    return read;
+}
+
 struct oracle_graph { Graph g; };
 struct oracle_cf_result {
     vector<uint64_t> starts, cyc_begin, node_begin, nodes, map_order, cand_ids;
@@ -565,5 +601,31 @@ void oracle_cf_candidates(const oracle_cf_result *r, uint64_t *ids, int32_t *buc
 }
 void oracle_cf_free(oracle_cf_result *r) { delete r; }
 void oracle_free(void *p) { free(p); }
+
+void oracle_reverse_pair_ends(char *s) {
+    std::string t(s);
+    reverse_pair_ends_sequence(t);
+    memcpy(s, t.data(), t.size());
+}
+
+// reads.cpp:88-130: seqs[0..n_file1) from the first file, the rest from the second
+uint64_t oracle_get_reads(const oracle_graph *g, const char *const *seqs, uint64_t n_seqs, uint64_t n_file1,
+                          const uint64_t *cycle_nodes, uint64_t n_nodes, uint64_t **flat, uint64_t **offsets) {
+    std::unordered_set<uint64_t> nodes_of_cycles(cycle_nodes, cycle_nodes + n_nodes);
+    std::vector<uint64_t> f, o{0};
+    for (uint64_t i = 0; i < n_seqs; ++i) {
+        std::string seq(seqs[i]);
+        if (i >= n_file1) reverse_pair_ends_sequence(seq);
+        auto read = get_read_from_sequence(g->g, nodes_of_cycles, seq);
+        if (read.empty()) continue;
+        f.insert(f.end(), read.begin(), read.end());
+        o.push_back(f.size());
+    }
+    *flat = (uint64_t *)malloc(8 * (f.size() + 1));
+    *offsets = (uint64_t *)malloc(8 * o.size());
+    memcpy(*flat, f.data(), 8 * f.size());
+    memcpy(*offsets, o.data(), 8 * o.size());
+    return o.size() - 1;
+}
 
 }  // extern "C"

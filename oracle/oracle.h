@@ -92,6 +92,14 @@ void oracle_cf_free(oracle_cf_result *r);
 
 void oracle_free(void *p);
 
+/* Relevant reads (reads.cpp:20-130). reverse_pair_ends_sequence in place (reads.cpp:20-31);
+ * get_reads over sequences seqs[0..n_file1) of the first file and the rest of the second
+ * (reversed and complemented): returns the number of reads, node ids in *flat with
+ * n+1 *offsets (malloc'ed; free with oracle_free). */
+void oracle_reverse_pair_ends(char *s);
+uint64_t oracle_get_reads(const oracle_graph *g, const char *const *seqs, uint64_t n_seqs, uint64_t n_file1,
+                          const uint64_t *cycle_nodes, uint64_t n_nodes, uint64_t **flat, uint64_t **offsets);
+
 #ifdef __cplusplus
 }
 #endif

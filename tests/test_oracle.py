@@ -249,3 +249,28 @@ def test_golden_regression(name):
     assert res["buckets"] == gold["buckets"]
     assert [[s, c] for s, c in res["entries"]] == gold["entries"]
     assert res["map_order"] == gold["map_order"]
+
+
+# reference tests/test_reads.cpp:10-62 (ReadsTest.*): reverse_pair_ends_sequence vectors
+@pytest.mark.parametrize("inp,expected", [
+    ("ACGT", "ACGT"), ("ACGTT", "AACGT"), ("AAGCT", "AGCTT"), ("AXGT", "ACXT"),
+    ("XXXQUIOCPOPYM", "MYPOPGOIUQXXX"),
+])
+def test_reverse_pair_ends_reference_vectors(inp, expected):
+    assert O.reverse_pair_ends(inp) == expected
+
+
+def test_get_reads_restatement_small():
+    """reads.cpp:57-130 on a hand-checked case: ids of every k-mer for reads whose first or
+    last k-mer maps to a cycle node; reads of length <= 2k skipped; N maps like T."""
+    k = 4
+    seqs = ["ACGTACGGTCAG", "TTTTGGGGCCCCAAAA"]
+    packed, offs = pack_reads(seqs)
+    g = O.OGraph.build(packed, offs, k)
+    enc = {"A": 1, "C": 2, "G": 3, "T": 4}
+    ibs = lambda s: g.index_binary_search([enc.get(c, 4) for c in s]) % (1 << 64)
+    first = ibs(seqs[0][:k])
+    got = g.get_reads(seqs + ["ACGTNCGGTCAG", "ACGTACGG"], 4, [first])
+    want0 = [ibs(seqs[0][i:i + k]) for i in range(len(seqs[0]) - k + 1)]
+    want2 = [ibs("ACGTNCGGTCAG"[i:i + k]) for i in range(12 - k + 1)]
+    assert got == [want0, want2]
