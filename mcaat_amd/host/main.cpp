@@ -1,12 +1,13 @@
 // main.cpp — the mcaat CLI over the MI355X hot path. Mirrors the release main of the
-// reference (src/main.cpp:496-591) up to CycleFinder; steps 6-8 (read remapping, spacer
-// ordering, CRISPRAnalyzer -> CRISPR_Arrays.txt) are outside this build's scope
-// (DESIGN.md §Scope), so the cycles themselves are written to <cycles_folder>/cycles.txt.
+// reference (src/main.cpp:496-591): settings check, SDBG build, CycleFinder, relevant reads
+// (step 6), spacer ordering (step 7), results / benchmark (step 8) and CRISPRAnalyzer, which
+// writes settings.output_file (CRISPR_Arrays.txt). The cycles themselves are also written to
+// <cycles_folder>/cycles.txt (not in the reference's release build).
 #include <filesystem>
 #include <fstream>
 #include <iostream>
 
-#include "mcaat_host.h"
+#include "downstream.h"
 
 namespace fs = std::filesystem;
 
@@ -30,6 +31,12 @@ static std::string cycle_sequence(const SDBG &sdbg, const std::vector<uint64_t> 
         else s += "ACGT"[lab[sdbg.k() - 1] - 1];
     }
     return s;
+}
+
+static void banner(const char *title) {
+    std::cout << "\n══════════════════════════════════════════════" << std::endl;
+    std::cout << title << std::endl;
+    std::cout << "══════════════════════════════════════════════" << std::endl;
 }
 
 int main(int argc, char **argv) {
@@ -58,18 +65,44 @@ int main(int argc, char **argv) {
         auto cycles_map = cycle_finder.results;
         std::cout << "Number of nodes in results: " << cycles_map.size() << std::endl;
         auto cycles = cycles_map_to_cycles(cycles_map);        // main.cpp:542
-        const std::string out = settings.cycles_folder + "/cycles.txt";
-        std::ofstream f(out);
-        if (!f) throw std::runtime_error("Error: cannot write " + out);
-        size_t idx = 0;
-        for (const auto &[start, inner] : cycles_map)
-            for (const auto &c : inner) {
-                f << ">cycle_" << idx++ << " start=" << start << " length=" << c.size() << "\n";
-                f << cycle_sequence(sdbg, c) << "\n";
-            }
-        std::cout << "Cycles written to " << out << " (" << cycles.size() << " cycles)" << std::endl;
-        std::cout << "Note: read remapping, spacer ordering and CRISPR_Arrays.txt reporting are not part of "
-                     "this build." << std::endl;
+        {
+            const std::string out = settings.cycles_folder + "/cycles.txt";
+            std::ofstream f(out);
+            size_t idx = 0;
+            for (const auto &[start, inner] : cycles_map)
+                for (const auto &c : inner) {
+                    f << ">cycle_" << idx++ << " start=" << start << " length=" << c.size() << "\n";
+                    f << cycle_sequence(sdbg, c) << "\n";
+                }
+        }
+
+        banner("🔸STEP 6: Finding relevant reads");             // main.cpp:544-551
+        const auto reads = run_and_debug_finding_of_relevant_reads(cycles, sdbg_build.reads(), sdbg);
+
+        banner("🔸STEP 7: Order the spacers");                  // main.cpp:553-556
+        const auto found_systems = run_and_debug_spacer_ordering(reads, sdbg, cycles);
+
+        if (settings.benchmark_file != "") {                   // main.cpp:559-569
+            banner("🔸STEP 8: Compare to ground of truth using benchmark file");
+            run_and_debug_benchmark_results(settings, found_systems);
+        } else {
+            banner("🔸STEP 8: Results");
+            run_and_debug_results(found_systems);
+        }
+        std::cout << "══════════════════════════════════════════════" << std::endl;
+
+        std::cout << "POST PROCESSING START:" << std::endl;    // main.cpp:573-581
+        std::unordered_map<std::string, std::vector<std::string>> all_systems;
+        for (const auto &[_sequence, repeat, spacers, _conf_a, _conf_b] : found_systems) all_systems[repeat] = spacers;
+        CRISPRAnalyzer analyzer(all_systems, settings.output_file);
+        analyzer.run_analysis();
+        std::cout << "Saved in: " << settings.output_file << std::endl;
+
+        try {                                                  // main.cpp:525,584-589: "<graph>/graph"
+            fs::remove_all(settings.graph_folder + "/graph");
+        } catch (const std::filesystem::filesystem_error &e) {
+            std::cerr << "Warning: Could not remove graph folder: " << e.what() << std::endl;
+        }
         return 0;
     } catch (const std::exception &e) {
         std::cerr << e.what() << std::endl;

@@ -79,8 +79,6 @@ void SDBGBuild::BuildLib() {
 void SDBGBuild::BuildSDBG() {
     mcaat_ctx *ctx = mcaat_host_ctx(settings.gpu);
     mcaat_check(mcaat_build_graph(ctx, reads_, settings.kmer_k, &graph_), "building the SDBG");
-    mcaat_reads_free(reads_);
-    reads_ = nullptr;
     std::cout << "\n-----------------------------------------\n" << std::endl;
 }
 
@@ -100,18 +98,38 @@ void SDBG::LoadFromDevice(mcaat_graph *g) {
     mcaat_check(mcaat_graph_download(g_, key_.data(), mult_.data(), valid_.data()), "mcaat_graph_download");
 }
 
+void SDBG::LoadFromArrays(int k, std::vector<uint64_t> keys, std::vector<uint16_t> mult,
+                          std::vector<uint8_t> valid) {
+    if (keys.size() != mult.size() || keys.size() != valid.size())
+        throw std::runtime_error("SDBG::LoadFromArrays: array sizes differ");
+    if (g_) mcaat_graph_free(g_);
+    g_ = nullptr;
+    k_ = k;
+    key_ = std::move(keys);
+    mult_ = std::move(mult);
+    valid_ = std::move(valid);
+}
+
 void SDBG::SyncFromDevice() {
-    mcaat_check(mcaat_graph_download(g_, nullptr, nullptr, valid_.data()), "mcaat_graph_download");
+    if (g_) mcaat_check(mcaat_graph_download(g_, nullptr, nullptr, valid_.data()), "mcaat_graph_download");
+}
+
+void SDBG::KeepOnly(const std::vector<uint64_t> &ids) {
+    std::vector<uint8_t> keep(valid_.size(), 0);
+    for (uint64_t e : ids)
+        if (e < keep.size()) keep[e] = 1;
+    for (size_t e = 0; e < valid_.size(); ++e) valid_[e] &= keep[e];
+    if (g_) mcaat_check(mcaat_graph_keep_only(g_, ids.data(), ids.size()), "mcaat_graph_keep_only");
 }
 
 void SDBG::SetInvalidEdge(uint64_t e) {
     valid_[e] = 0;
-    mcaat_check(mcaat_graph_set_valid(g_, &e, 1, 0), "mcaat_graph_set_valid");
+    if (g_) mcaat_check(mcaat_graph_set_valid(g_, &e, 1, 0), "mcaat_graph_set_valid");
 }
 
 void SDBG::SetValidEdge(uint64_t e) {
     valid_[e] = 1;
-    mcaat_check(mcaat_graph_set_valid(g_, &e, 1, 1), "mcaat_graph_set_valid");
+    if (g_) mcaat_check(mcaat_graph_set_valid(g_, &e, 1, 1), "mcaat_graph_set_valid");
 }
 
 uint64_t SDBG::lower(uint64_t q) const { return std::lower_bound(key_.begin(), key_.end(), q) - key_.begin(); }
@@ -135,6 +153,20 @@ int SDBG::IncomingEdges(uint64_t e, uint64_t *in) const {
     for (uint64_t i = lower(G << 4); i < size() && (key_[i] >> 4) == G; ++i)
         if ((key_[i] & 3) == c && valid_[i]) in[n++] = i;
     return n;
+}
+
+void SDBG::NeighborsBatch(const std::vector<uint64_t> &ids, bool incoming, std::vector<uint64_t> &out,
+                          std::vector<int32_t> &counts) const {
+    out.assign(4 * ids.size(), 0);
+    counts.assign(ids.size(), 0);
+    if (ids.empty()) return;
+    if (g_) {
+        mcaat_check(mcaat_graph_neighbors(g_, ids.data(), ids.size(), incoming ? 1 : 0, out.data(), counts.data()),
+                    "mcaat_graph_neighbors");
+        return;
+    }
+    for (size_t i = 0; i < ids.size(); ++i)
+        counts[i] = incoming ? IncomingEdges(ids[i], &out[4 * i]) : OutgoingEdges(ids[i], &out[4 * i]);
 }
 
 uint32_t SDBG::GetLabel(uint64_t e, uint8_t *seq) const {

@@ -27,6 +27,8 @@ class SDBGBuild {
     explicit SDBGBuild(Settings settings);
     ~SDBGBuild();
     mcaat_graph *graph() const { return graph_; }
+    // the reads stay in HBM for the relevant-read mapping (the reference re-reads the files)
+    const mcaat_reads *reads() const { return reads_; }
     mcaat_graph *release_graph() {
         mcaat_graph *g = graph_;
         graph_ = nullptr;
@@ -52,8 +54,12 @@ class SDBG {
     SDBG &operator=(const SDBG &) = delete;
     // adopt a device graph (replaces SDBG::LoadFromFile of the on-disk MEGAHIT graph)
     void LoadFromDevice(mcaat_graph *g);
+    // host-only graph (no device copy) from sorted BOSS keys, multiplicities and valid bytes
+    void LoadFromArrays(int k, std::vector<uint64_t> keys, std::vector<uint16_t> mult, std::vector<uint8_t> valid);
     // refresh the host mirror after device-side mutation (CycleFinder)
     void SyncFromDevice();
+    // valid &= {ids} on the host mirror and the device graph (one bitmap AND on the GPU)
+    void KeepOnly(const std::vector<uint64_t> &ids);
     mcaat_graph *device() const { return g_; }
 
     uint64_t size() const { return key_.size(); }
@@ -73,6 +79,10 @@ class SDBG {
         return IncomingEdges(e, t);
     }
     bool EdgeOutdegreeZero(uint64_t e) const { return EdgeOutdegree(e) == 0; }
+    // valid neighbours of many edges in one call (on the device when the graph is there):
+    // out[4i .. 4i+counts[i]) in OutgoingEdges / IncomingEdges order
+    void NeighborsBatch(const std::vector<uint64_t> &ids, bool incoming, std::vector<uint64_t> &out,
+                        std::vector<int32_t> &counts) const;
     uint32_t GetLabel(uint64_t e, uint8_t *seq) const;      // symbols 1..4 = ACGT
     int64_t IndexBinarySearch(const uint8_t *seq) const;    // -1 if absent
     static constexpr uint64_t kNullID = ~0ULL;

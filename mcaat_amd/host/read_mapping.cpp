@@ -1,0 +1,65 @@
+// reads.cpp — relevant reads (reference src/reads.cpp). The per-sequence helpers are kept
+// for host callers; get_reads itself runs on the GPU over the reads already in HBM.
+#include <algorithm>
+
+#include "downstream.h"
+
+void reverse_pair_ends_sequence(std::string &sequence) {  // reads.cpp:20-31
+    std::reverse(sequence.begin(), sequence.end());
+    for (char &base : sequence) {
+        switch (base) {
+            case 'A': base = 'T'; break;
+            case 'T': base = 'A'; break;
+            case 'C': base = 'G'; break;
+            case 'G': base = 'C'; break;
+        }
+    }
+}
+
+uint64_t k_mer_to_node_id(const SDBG &sdbg, const std::string k_mer) {  // reads.cpp:33-55
+    if ((int)k_mer.size() != sdbg.k()) return 0;
+    std::vector<uint8_t> seq(sdbg.k());
+    for (int i = 0; i < sdbg.k(); ++i) {
+        const char c = k_mer[i];
+        seq[i] = c == 'A' ? 1 : c == 'C' ? 2 : c == 'G' ? 3 : 4;
+    }
+    return (uint64_t)sdbg.IndexBinarySearch(seq.data());
+}
+
+std::vector<uint64_t> get_read_from_sequence(const SDBG &sdbg, const std::unordered_set<uint64_t> &nodes_of_cycles,
+                                             const std::string &sequence) {  // reads.cpp:57-86
+    const uint32_t K = sdbg.k();
+    if (sequence.size() <= 2 * K) return {};
+    const uint64_t start_node_id = k_mer_to_node_id(sdbg, sequence.substr(0, K));
+    const uint64_t end_node_id = k_mer_to_node_id(sdbg, sequence.substr(sequence.size() - K, K));
+    if (nodes_of_cycles.find(start_node_id) == nodes_of_cycles.end() &&
+        nodes_of_cycles.find(end_node_id) == nodes_of_cycles.end())
+        return {};
+    std::vector<uint64_t> read = {start_node_id};
+    for (size_t i = 1; i < sequence.size() - K; ++i) read.push_back(k_mer_to_node_id(sdbg, sequence.substr(i, K)));
+    read.push_back(end_node_id);
+    return read;
+}
+
+// reads.cpp:88-130. The reference re-reads the FASTQ files (file 2 reverse-complemented) and
+// binary-searches every k-mer of every read; here the reads are still in HBM (mapping view
+// built while parsing, mcaat_reads_records_info) and mcaat_map_reads probes only read ends
+// against the cycle labels before resolving the relevant reads' k-mers.
+std::vector<std::vector<uint64_t>> get_reads(const SDBG &sdbg, const mcaat_reads *reads,
+                                             const std::vector<std::vector<uint64_t>> cycles) {
+    std::unordered_set<uint64_t> nodes_of_cycles;
+    for (const auto &cycle : cycles)
+        for (const auto &node : cycle) nodes_of_cycles.insert(node);
+    std::vector<uint64_t> nodes(nodes_of_cycles.begin(), nodes_of_cycles.end());
+    std::sort(nodes.begin(), nodes.end());
+    if (!sdbg.device()) throw std::runtime_error("get_reads: the SDBG has no device graph");
+    mcaat_mapped *m = nullptr;
+    mcaat_check(mcaat_map_reads(sdbg.device(), reads, nodes.data(), nodes.size(), 0, &m), "mapping the reads");
+    uint64_t n = 0;
+    const uint64_t *ids = nullptr, *off = nullptr;
+    mcaat_check(mcaat_mapped_get(m, &n, &ids, &off, nullptr), "mcaat_mapped_get");
+    std::vector<std::vector<uint64_t>> out(n);
+    for (uint64_t i = 0; i < n; ++i) out[i].assign(ids + off[i], ids + off[i + 1]);
+    mcaat_mapped_free(m);
+    return out;
+}

@@ -110,3 +110,19 @@ def test_bench_two_ranks_gloo_dry_run(mode, port):
     else:  # one dataset split over the ranks
         assert d["scaling"] == "strong" and total == 2 * d["config"]["kmers_per_gpu"]
         assert d["config"]["reads_total"] == 10_000
+
+
+def test_host_library_exports_every_declared_symbol():
+    """libmcaat_host.so (include/mcaat_host.h): the downstream steps' C ABI."""
+    from mcaat_amd import downstream as DS
+
+    txt = open(os.path.join(ROOT, "include", "mcaat_host.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    names = sorted(set(re.findall(r"\b(mcaat_host_[a-z_]+)\s*\(", txt)))
+    assert len(names) >= 6
+    out = subprocess.run(["nm", "-D", "--defined-only", DS.HOST_LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    assert not [n for n in names if n not in exported]
+    assert sorted(DS.HOST_SIGNATURES) == names
+    DS.load_host_library()
