@@ -681,7 +681,9 @@ constexpr int kCapMax = kCap * 85 / 100 - kCWaves * 64;    // distinct edges bef
 constexpr int kDCap = 2048;                                // descriptor slots
 constexpr int kDMax = kDCap * 3 / 4;                       // distinct descriptors before going raw
 constexpr int kDProbe = 128;                               // probe bound of the descriptor table
-constexpr int kCB = 8;                                     // descriptor loads in flight per thread
+constexpr int kCB = 4;                                     // descriptor loads in flight per thread
+constexpr int kDefer = 64;                                 // descriptors with w0 == kEmpty before going raw
+constexpr int kCPerCu = 2;                                 // resident workgroups per CU (LDS, VGPR <= 64)
 
 __device__ __forceinline__ uint32_t edge_slot(uint64_t c) {
     return (((uint32_t)c ^ (uint32_t)(c >> 32)) * 0x9E3779B1u) >> (32 - 12);
@@ -693,16 +695,27 @@ __device__ __forceinline__ uint32_t desc_slot(uint64_t w0, uint64_t w1) {
 }
 static_assert(kDCap == 2048, "desc_slot yields 11 bits");
 
-__global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict__ data, uint64_t gbase,
+template <bool PROF>
+__global__ void __launch_bounds__(kCThreads, kCPerCu * kCThreads / 256) k_lds_count(const uint4 *__restrict__ data, uint64_t gbase,
                                                          const uint64_t *__restrict__ fine_base, uint64_t p0,
                                                          uint64_t F, int E,
                                                          uint64_t *out_keys, uint32_t *out_cnt, uint64_t out_cap,
                                                          unsigned long long *out_cursor, uint32_t *ovf_list,
                                                          unsigned long long *ovf_n, unsigned long long *prof) {
-    __shared__ unsigned long long keys[kCap];
-    __shared__ uint32_t cnt[kCap];
-    __shared__ unsigned long long dk0[kDCap], dk1[kDCap];
-    __shared__ uint32_t dcnt[kDCap];  // > 0: the slot holds a descriptor
+    // The descriptor table (phase 1) and the edge table (phases 2-3) share one LDS region:
+    // between the phases each thread keeps its two descriptor slots in registers. 48 KB per
+    // workgroup, so two 1024-thread workgroups share a CU and one's loads overlap the other's
+    // LDS work.
+    constexpr int kEdgeBytes = kCap * 12, kDescBytes = kDCap * 20;
+    __shared__ __attribute__((aligned(16))) unsigned char region[kEdgeBytes > kDescBytes ? kEdgeBytes : kDescBytes];
+    unsigned long long *const keys = (unsigned long long *)region;
+    uint32_t *const cnt = (uint32_t *)(keys + kCap);
+    unsigned long long *const dk0 = (unsigned long long *)region, *const dk1 = dk0 + kDCap;
+    uint32_t *const dcnt = (uint32_t *)(dk1 + kDCap);  // > 0: the slot holds a descriptor
+    // descriptors whose first word equals the empty marker (a run of >= 32 T) cannot be
+    // keyed in the descriptor table; they wait here and are expanded with weight 1
+    __shared__ uint4 deferred[kDefer];
+    __shared__ uint32_t n_deferred;
     __shared__ uint32_t n_distinct, n_ddistinct;
     __shared__ int ovf, dovf;
     __shared__ uint32_t wsum[kCWaves];
@@ -710,9 +723,9 @@ __global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     // MCAAT_PROF_C=1: 100-MHz ticks per phase (clear, collapse, expand, emit) and counts of
     // partitions expanded raw
-    unsigned long long tp[5] = {0, 0, 0, 0, 0}, t0 = prof ? __builtin_amdgcn_s_memrealtime() : 0;
+    unsigned long long tp[5] = {0, 0, 0, 0, 0}, t0 = PROF ? __builtin_amdgcn_s_memrealtime() : 0;
     auto tick = [&](int phase) {
-        if (prof) {
+        if (PROF) {
             const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
             tp[phase] += t1 - t0;
             t0 = t1;
@@ -746,16 +759,12 @@ __global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict
     };
 
     for (uint64_t p = p0 + blockIdx.x; p < F; p += gridDim.x) {
-        for (int i = threadIdx.x; i < kCap; i += kCThreads) {
-            keys[i] = kEmpty;
-            cnt[i] = 0;
-        }
         for (int i = threadIdx.x; i < kDCap; i += kCThreads) {
             dk0[i] = dk1[i] = kEmpty;
             dcnt[i] = 0;
         }
         if (threadIdx.x == 0) {
-            n_distinct = n_ddistinct = 0;
+            n_distinct = n_ddistinct = n_deferred = 0;
             ovf = dovf = 0;
         }
         __syncthreads();
@@ -765,12 +774,15 @@ __global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict
         // ---- 1: collapse identical descriptors ----
         // wait-free: the two key words are claimed separately, each by a CAS from empty; a
         // lane moves on as soon as either word holds another value, so no lane ever waits on
-        // another (a descriptor whose first word is the empty marker is expanded directly)
+        // another (a descriptor whose first word is the empty marker is deferred)
         auto collapse = [&](uint64_t w0, uint64_t w1) {
             if (((w1 >> kNShift) & 63) == 0) return;  // padding
             if (w0 == kEmpty) {
-                const int n = (int)((w1 >> kNShift) & 63);
-                for (int i = 0; i < n; ++i) insert(canon_edge(desc_window(w0, w1, i, E), E), 1u);
+                const uint32_t j = atomicAdd(&n_deferred, 1u);
+                if (j < (uint32_t)kDefer)
+                    deferred[j] = make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32));
+                else
+                    dovf = 1;
                 return;
             }
             uint32_t h = desc_slot(w0, w1);
@@ -794,7 +806,7 @@ __global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict
                 return;
             }
             dovf = 1;
-            if (prof) atomicAdd(&prof[5], 1ull);
+            if (PROF) atomicAdd(&prof[5], 1ull);
         };
         // kCB descriptors per thread per round: their loads are all in flight together
         for (uint64_t d0 = beg + threadIdx.x; d0 < end; d0 += (uint64_t)kCThreads * kCB) {
@@ -812,7 +824,7 @@ __global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict
         }
         __syncthreads();
         tick(1);
-        if (prof && threadIdx.x == 0) {
+        if (PROF && threadIdx.x == 0) {
             if (dovf) tp[4]++;
             atomicAdd(&prof[6], (unsigned long long)n_ddistinct);
             atomicAdd(&prof[7], (unsigned long long)(end - beg));
@@ -848,12 +860,38 @@ __global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict
                 insert(canon_edge(desc_window(a0, a1, i, E), E), wt);
             }
         };
-        if (!dovf) {
-            for (int i0 = wave * 64; i0 < kDCap; i0 += kCThreads) {
-                const int i = i0 + lane;
-                const bool live = dcnt[i] != 0;
-                const uint64_t w1 = live ? dk1[i] : 0;
-                spread(live ? dk0[i] : 0, w1, (int)((w1 >> kNShift) & 63), live ? dcnt[i] : 0);
+        // the distinct descriptors move to registers (slots threadIdx.x + j * kCThreads), then
+        // the region becomes the edge table
+        static_assert(kDCap == 2 * kCThreads, "two descriptor slots per thread");
+        const bool raw = dovf;
+        uint64_t r0[2] = {0, 0}, r1[2] = {0, 0};
+        uint32_t rc[2] = {0, 0};
+        if (!raw) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int i = threadIdx.x + j * kCThreads;
+                rc[j] = dcnt[i];
+                if (rc[j]) {
+                    r0[j] = dk0[i];
+                    r1[j] = dk1[i];
+                }
+            }
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < kCap; i += kCThreads) {
+            keys[i] = kEmpty;
+            cnt[i] = 0;
+        }
+        __syncthreads();
+        if (!raw) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) spread(r0[j], r1[j], (int)((r1[j] >> kNShift) & 63), rc[j]);
+            if (wave == 0) {
+                // n_deferred <= kDefer here (more sends the partition raw)
+                const bool live = (uint32_t)lane < n_deferred;
+                const uint4 q = live ? deferred[lane] : make_uint4(0, 0, 0, 0);
+                const uint64_t w0 = (uint64_t)q.x | ((uint64_t)q.y << 32), w1 = (uint64_t)q.z | ((uint64_t)q.w << 32);
+                spread(w0, w1, (int)((w1 >> kNShift) & 63), 1u);
             }
         } else {
             for (uint64_t d0 = beg + (uint64_t)wave * 64; d0 < end; d0 += kCThreads) {
@@ -911,7 +949,7 @@ __global__ void __launch_bounds__(kCThreads) k_lds_count(const uint4 *__restrict
         __syncthreads();
         tick(3);
     }
-    if (prof && (threadIdx.x & 63) == 0)
+    if (PROF && (threadIdx.x & 63) == 0)
         for (int i = 0; i < 5; ++i) atomicAdd(&prof[i], tp[i]);
 }
 
@@ -1241,7 +1279,7 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
             HIP_OK(hipMemsetAsync(dcnt.p + 1, 0, 8, st));
             {
                 KernelTimer kt(ctx, "lds_count", 16.0 * (double)gn);
-                hipLaunchKernelGGL(k_lds_count, dim3((unsigned)std::min<uint64_t>(p1 - p0, (uint64_t)ctx->n_cu)),
+                hipLaunchKernelGGL(prof_c ? k_lds_count<true> : k_lds_count<false>, dim3((unsigned)std::min<uint64_t>(p1 - p0, (uint64_t)kCPerCu * ctx->n_cu)),
                                    dim3(kCThreads), 0, st, fine.p, gbase, dfine.p, p0, p1, E, out.keys.p, out.counts.p,
                                    out_cap, dcnt.p, ovf_list.p, dcnt.p + 1, prof_c ? dprof.p : nullptr);
                 LAUNCH_OK();

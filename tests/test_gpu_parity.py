@@ -176,6 +176,24 @@ def test_lds_overflow_fallback_low_coverage(gpu_ctx):
     assert gpu_ctx.kernel_timing("lds_count_overflow_partitions")[1] > 0
 
 
+@pytest.mark.parametrize("n_reads", [12, 400])
+def test_poly_t_runs(gpu_ctx, n_reads):
+    """Super-k-mers starting inside a run of >= 32 T have an all-ones first word, the LDS
+    descriptor table's empty marker: up to 64 per partition are deferred and expanded with
+    weight 1, more send the partition down the raw path. Counts must equal the oracle."""
+    rng = np.random.default_rng(n_reads)
+    seqs = []
+    for i in range(n_reads):
+        flank = "".join(rng.choice(list("ACGT"), size=70))
+        seqs.append(flank[:30] + "T" * (60 + (i * 7) % 90) + flank[30:])
+    packed, offs = pack_reads(seqs)
+    reads = M.Reads.from_host(gpu_ctx, packed, offs)
+    for k in (23, 27):
+        gk, gc = M.count_edges(gpu_ctx, reads, k)
+        ok, oc = O.count_canonical(packed, offs, k)
+        assert np.array_equal(gk, ok) and np.array_equal(gc, oc), k
+
+
 def test_mixed_read_lengths(gpu_ctx):
     """Variable-length reads, longer than one 128-position work item (items split reads)."""
     rng = np.random.default_rng(4)
