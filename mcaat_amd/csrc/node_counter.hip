@@ -90,12 +90,21 @@ __device__ __forceinline__ uint64_t canon_edge(uint64_t lsb, int E) {
 // ballot compaction as {first base, n edges, minimizer hash}; when a segment runs low on
 // room the wave fills in the bases of its entries and the workgroup scatters all segments
 // to the 256 L1 buckets.
-constexpr int kAWaves = 8;
+#ifndef MCAAT_AWAVES
+#define MCAAT_AWAVES 4
+#define MCAAT_ASEG 1500
+#define MCAAT_APERCU 2
+#endif
+#ifndef MCAAT_HASH
+#define MCAAT_HASH 1
+#endif
+constexpr int kAWaves = MCAAT_AWAVES;
 constexpr int kAThreads = kAWaves * 64;
+constexpr int kAPerCu = MCAAT_APERCU;   // resident workgroups per CU (LDS <= 160 KB / kAPerCu)
 constexpr int kItem = 127;              // edge positions per work item (the close at np fits 16 steps)
 constexpr int kCk = 8;                  // positions per step
-constexpr int kSeg = 1600;              // per-wave stage segment (entries); a step appends <= 64*kCk
-constexpr int kStage = kSeg * kAWaves;  // 8-B pre-entries: 100 KB of LDS
+constexpr int kSeg = MCAAT_ASEG;        // per-wave stage segment (entries); a step appends <= 64*kCk
+constexpr int kStage = kSeg * kAWaves;  // 8-B pre-entries
 
 struct ItemSrc {
     const uint64_t *offsets;
@@ -119,6 +128,11 @@ __device__ __forceinline__ void get_item(const ItemSrc &s, int E, uint64_t it, u
         np = (int)s.item_np[it];
     }
 }
+
+// two consecutive words of the packed stream, 8-B aligned: one global_load_dwordx4
+struct __attribute__((aligned(8))) u64x2 {
+    uint64_t a, b;
+};
 
 // 2-bit-group reversal by the hardware bit reverse
 __device__ __forceinline__ uint64_t rev2_dev(uint64_t x) {
@@ -147,7 +161,14 @@ __device__ __forceinline__ void hash_step(uint64_t win, int m, uint32_t mmask, u
             f &= mmask;
             r &= mmask;
         }
+#if MCAAT_HASH == 1
+        // multiply-xorshift: a bijection, and only the minimizer order depends on it (the
+        // buckets and sub-partitions come from a re-hash), so a short one suffices
+        uint32_t x = (min(f, r) ^ salt) * 0x9E3779B1u;
+        h[t] = x ^ (x >> 15);
+#else
         h[t] = mix32(min(f, r) ^ salt);
+#endif
     }
 }
 
@@ -281,9 +302,9 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
         const int rb = kCk * c + 2 * kCk;
         const uint64_t win = win32(pa, pb, s + rb);
         {
-            const uint64_t qn = (s + rb + kCk) >> 5;  // next step's window words
-            pa = packed[qn];
-            pb = packed[qn + 1];
+            const u64x2 nx = *(const u64x2 *)(packed + ((s + rb + kCk) >> 5));  // next step's window words
+            pa = nx.a;
+            pb = nx.b;
         }
         hash_step<kFull>(win, P.m, mmask, salt32, H + ((G + 2) % 3) * kCk);
         uint32_t hm[kCk];
@@ -334,9 +355,9 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
         sbase[wave][par][lane] = s;
         ihc = (par << kPePar) | ((uint32_t)lane << kPeLane);
         {
-            const uint64_t q2 = (s + 2 * kCk) >> 5;
-            pa = packed[q2];
-            pb = packed[q2 + 1];
+            const u64x2 nx = *(const u64x2 *)(packed + ((s + 2 * kCk) >> 5));
+            pa = nx.a;
+            pb = nx.b;
         }
         int mx = np;
 #pragma unroll
@@ -469,8 +490,13 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
                     const uint32_t ln = (hi >> kPeLane) & 63, pr = (hi >> kPePar) & 1;
                     B0[k] = sbase[i / kSeg][pr][ln] + ((hi >> kPeP) & 127);
                 }
-#pragma unroll
-                for (int z = 0; z < 3; ++z) x[k][z] = packed[(B0[k] >> 5) + z];
+                // the first two words in one 16-B load; the third only when the bases reach
+                // it (these loads are uncoalesced, so the vector L1 pays per lane and line)
+                const int L = (int)(((uint32_t)(q[k] >> 32) & 127) - (((uint32_t)(q[k] >> 32) >> kPeP) & 127)) + P.E - 1;
+                const u64x2 x01 = *(const u64x2 *)(packed + (B0[k] >> 5));
+                x[k][0] = x01.a;
+                x[k][1] = x01.b;
+                x[k][2] = j < total && 2 * (int)(B0[k] & 31) + 2 * L > 128 ? packed[(B0[k] >> 5) + 2] : 0;
             }
 #pragma unroll
             for (int k = 0; k < kWB; ++k) {
@@ -595,6 +621,10 @@ __global__ void __launch_bounds__(kBThreads) k_l2_hist(const uint16_t *__restric
 // old line has been written.
 constexpr int kLG = 4;          // descriptors per line
 constexpr int kMaxSub = 2048;   // l2_bits <= 11: 128 KB of line buffers
+#ifndef MCAAT_BPF
+#define MCAAT_BPF 2
+#endif
+constexpr int kBPF = MCAAT_BPF;  // rounds of descriptor loads in flight
 
 __global__ void __launch_bounds__(kBThreads) k_l2_scatter(const uint4 *__restrict__ data,
                                                           const uint16_t *__restrict__ sub,
@@ -622,15 +652,25 @@ __global__ void __launch_bounds__(kBThreads) k_l2_scatter(const uint4 *__restric
         bl[i] = 0;
     }
     __syncthreads();
-    // one descriptor per thread per round, the next round's already in flight
-    uint32_t v = threadIdx.x < n ? sub[s0 + threadIdx.x] : kDeadSub;
-    uint4 d = threadIdx.x < n ? data[s0 + threadIdx.x] : make_uint4(0, 0, 0, 0);
-    for (uint32_t i0 = 0; i0 < n; i0 += kBThreads) {
-        const uint32_t cv = v;
-        const uint4 cd = d;
-        const uint32_t ni = i0 + kBThreads + threadIdx.x;
-        v = ni < n ? sub[s0 + ni] : kDeadSub;
-        if (ni < n) d = data[s0 + ni];
+    // one descriptor per thread per round, the next kBPF rounds' already in flight
+    uint32_t v[kBPF];
+    uint4 d[kBPF];
+#pragma unroll
+    for (int j = 0; j < kBPF; ++j) {
+        const uint32_t i = j * kBThreads + threadIdx.x;
+        v[j] = i < n ? sub[s0 + i] : kDeadSub;
+        d[j] = i < n ? data[s0 + i] : make_uint4(0, 0, 0, 0);
+    }
+    for (uint32_t i00 = 0; i00 < n; i00 += kBPF * kBThreads)
+#pragma unroll
+    for (int j = 0; j < kBPF; ++j) {
+        const uint32_t i0 = i00 + j * kBThreads;
+        if (i0 >= n) break;  // uniform: every thread reaches the same barriers
+        const uint32_t cv = v[j];
+        const uint4 cd = d[j];
+        const uint32_t ni = i0 + kBPF * kBThreads + threadIdx.x;
+        v[j] = ni < n ? sub[s0 + ni] : kDeadSub;
+        if (ni < n) d[j] = data[s0 + ni];
         const bool live = cv != kDeadSub;
         uint32_t r = 0, line = 0;
         bool buffered = false;
@@ -1164,7 +1204,8 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     uint64_t est = (uint64_t)(1.08 * (dens * (double)n_occ + (double)n_items)) + 4096;
     std::vector<uint64_t> cap(256), base(257);
     // + one partially used reservation per (workgroup, bucket)
-    for (int b = 0; b < 256; ++b) cap[b] = (est / 256 + 512ull * kMini + 7) & ~7ull;  // 16-B aligned sub rows
+    const uint64_t a_grid = (uint64_t)kAPerCu * ctx->n_cu;
+    for (int b = 0; b < 256; ++b) cap[b] = (est / 256 + 2 * a_grid * kMini + 7) & ~7ull;  // 16-B aligned sub rows
     DevBuf<uint64_t> dcap(256), dbase(257);
     DevBuf<unsigned long long> dcur(256);
     DevBuf<uint4> l1;
@@ -1183,7 +1224,7 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
         HIP_OK(hipMemsetAsync(dcur.p, 0, dcur.bytes(), st));
         {
             KernelTimer kt(ctx, "sk_scatter", 0.25 * (double)r->n_bases + 16.0 * (double)est / 1.25);
-            hipLaunchKernelGGL(sk_kernel(P.w), dim3(ctx->n_cu), dim3(kAThreads), 0, st, r->packed.p, src, P, l1.p,
+            hipLaunchKernelGGL(sk_kernel(P.w), dim3((unsigned)a_grid), dim3(kAThreads), 0, st, r->packed.p, src, P, l1.p,
                                dbase.p, dcap.p, dcur.p, l1s.p, prof_a ? dprof.p : nullptr);
             LAUNCH_OK();
             kt.stop();
@@ -1202,7 +1243,7 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     if (prof_a) {
         unsigned long long hp[8];
         HIP_OK(hipMemcpy(hp, dprof.p, 64, hipMemcpyDeviceToHost));
-        const double waves = (double)ctx->n_cu * kAWaves;
+        const double waves = (double)a_grid * kAWaves;
         fprintf(stderr, "[mcaat] pass A per-wave ms (100 MHz clock): scan %.1f bucket %.1f wait %.1f reserve %.1f write %.1f\n",
                 hp[0] / waves / 1e5, hp[1] / waves / 1e5, hp[2] / waves / 1e5, hp[3] / waves / 1e5, hp[4] / waves / 1e5);
     }

@@ -608,9 +608,14 @@ void sdbg_finish(mcaat_ctx *ctx, mcaat_graph *g) {
     g->out_info.alloc(D);
     g->in_info.alloc(D);
     if (D) {
+        KernelTimer kt(ctx, "adjacency", 24.0 * (double)D);  // key read, two words written
+        // one edge per lane: neighbouring lanes search neighbouring key ranges, so the
+        // searches' loads share lines across the wave (a thread-per-run merge walk that
+        // loses this was 5x slower)
         hipLaunchKernelGGL(k_adjacency, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, g->key.p, D, k, dir.p, shift,
                            g->out_info.p, g->in_info.p);
         LAUNCH_OK();
+        kt.stop();
     }
     g->valid.alloc((D + 63) / 64);
     hipLaunchKernelGGL(k_valid_init, dim3(grid_for((D + 63) / 64, kBlock)), dim3(kBlock), 0, st, g->valid.p, D);
