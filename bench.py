@@ -108,6 +108,66 @@ class _DryReads:
         pass
 
 
+
+def fastq_records(spec, n_reads: int) -> np.ndarray:
+    """n_reads of the synthetic spec as 4-line FASTQ records, one uint8 row per record."""
+    import dataclasses
+
+    sub = dataclasses.replace(spec, n_reads=n_reads)
+    packed, offs = M.synth_host(sub)
+    L = sub.read_len
+    nb = n_reads * L
+    idx = np.arange(nb, dtype=np.uint64)
+    codes = ((packed[(idx >> np.uint64(5)).astype(np.int64)] >> (np.uint64(2) * (idx & np.uint64(31)))) & np.uint64(3))
+    letters = np.frombuffer(b"ACGT", dtype=np.uint8)[codes.astype(np.int64)].reshape(n_reads, L)
+    rec = np.empty((n_reads, 2 * L + 7), dtype=np.uint8)
+    rec[:, 0:2] = np.frombuffer(b"@r", dtype=np.uint8)
+    rec[:, 2] = 10
+    rec[:, 3:3 + L] = letters
+    rec[:, 3 + L:6 + L] = np.frombuffer(b"\n+\n", dtype=np.uint8)
+    rec[:, 6 + L:6 + 2 * L] = ord("I")
+    rec[:, 6 + 2 * L] = 10
+    return rec, packed
+
+
+def measure_ingest(ctx, spec, n_reads: int) -> dict:
+    """Untimed: FASTQ text -> 2-bit library in HBM through mcaat_reads_from_fastx (the GPU
+    parser, csrc/fastq_ingest.hip). The file (n_reads of the same synthetic spec, 150-bp
+    4-line records) is written to local /tmp first, so it is read from the page cache."""
+    import tempfile
+
+    rec, want = fastq_records(spec, n_reads)
+    nb = n_reads * spec.read_len
+    fd, path = tempfile.mkstemp(suffix=".fq", dir="/tmp")
+    try:
+        with os.fdopen(fd, "wb") as f:
+            f.write(rec.tobytes())
+        size = os.path.getsize(path)
+        del rec
+        ctx.reset_timing()
+        t0 = time.perf_counter()
+        r = M.Reads.from_fastx(ctx, [path])
+        wall = time.perf_counter() - t0
+        n_got, b_got = r.info()
+        got, _ = r.download()
+        nw = (nb + 31) // 32
+        ok = bool(n_got == n_reads and b_got == nb and np.array_equal(got[:nw], want[:nw]))
+        gpu_ms = 0.0
+        kern = {}
+        for n in ("fq_parse", "fq_records", "fq_emit"):
+            a, l, by = ctx.kernel_timing(n)
+            gpu_ms += a * l
+            kern[n] = {"ms": round(a * l, 3), "GBps": round(by / (a * 1e-3) / 1e9, 1) if a > 0 else None}
+        r.free()
+    finally:
+        os.unlink(path)
+    return {
+        "reads": n_reads, "file_bytes": size, "wall_s": round(wall, 3),
+        "text_GBps": round(size / wall / 1e9, 2), "reads_per_s": n_reads / wall,
+        "gpu_parse_ms": round(gpu_ms, 3), "kernels": kern, "library_matches": ok,
+        "note": "page-cached plain FASTQ; wall includes host read, PCIe upload and GPU parse",
+    }
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -119,6 +179,8 @@ def main() -> int:
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-post", action="store_true", help="skip the untimed relevant-read mapping measurement")
+    ap.add_argument("--ingest-reads", type=int, default=2_000_000,
+                    help="untimed FASTQ ingest measurement on a file of this many reads (0: skip)")
     ap.add_argument("--mode", default="shard", choices=["shard", "replicas"],
                     help="N>1: one dataset hash-range sharded over the ranks, or one dataset per rank")
     ap.add_argument("--dry-run", action="store_true",
@@ -217,6 +279,7 @@ def main() -> int:
         return a * l / max(1, args.steps)
     kern = max(HOT_KERNELS, key=per_step_ms)
     avg_ms, launches, bytes_per_launch = ctx.kernel_timing(kern)
+    kernels_ms = {n: round(per_step_ms(n), 3) for n in HOT_KERNELS}
 
     # after the timed region (not part of `value`): the next step of the reference's main,
     # relevant-read mapping (reads.cpp:88-130) on the GPU over the reads still in HBM
@@ -242,6 +305,9 @@ def main() -> int:
             "reads_per_s": spec.n_reads / (wall * 1e-3),
         }
         g.free()
+    ingest = None
+    if rank == 0 and not args.dry_run and args.ingest_reads > 0:
+        ingest = measure_ingest(ctx, spec, args.ingest_reads)
     kmers_rank = count * max(0, spec.read_len - k)
     kmers_total = n_occ(spec, k) if sharded else kmers_rank * world
     value = kmers_total / dt
@@ -281,7 +347,7 @@ def main() -> int:
             },
             "roofline": {
                 "kernel": kern,
-                "kernels_ms_per_step": {n: round(per_step_ms(n), 3) for n in HOT_KERNELS},
+                "kernels_ms_per_step": kernels_ms,
                 "lds_overflow_partitions": ctx.kernel_timing("lds_count_overflow_partitions")[1],
                 "bound": "hbm",
                 "achieved": achieved,
@@ -295,6 +361,7 @@ def main() -> int:
             },
             "stages_ms": {kk: round(vv, 3) for kk, vv in stages.items()},
             "post_path": post,
+            "fastq_ingest": ingest,
             "cpu_baseline": None,
         }
         if world == 1 and not args.no_cpu_baseline and not args.dry_run:

@@ -53,7 +53,10 @@ int mcaat_device_count(int *n);
  * offsets[n_reads+1] are base offsets of each read in the stream. */
 int mcaat_reads_from_host(mcaat_ctx *ctx, const uint64_t *packed, uint64_t n_words,
                           const uint64_t *offsets, uint64_t n_reads, mcaat_reads **out);
-/* Non-ACGT symbols split a read (k-mers spanning them are dropped). gz via zlib. */
+/* Non-ACGT symbols split a read (k-mers spanning them are dropped). gz via zlib.
+ * FASTQ inputs (4-line records) are parsed on the GPU in chunks (csrc/fastq_ingest.hip;
+ * chunk size MCAAT_FASTQ_CHUNK bytes, default 256 MiB); FASTA (multi-line) on the host.
+ * Blank lines are accepted only before the first and after the last record. */
 int mcaat_reads_from_fastx(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_reads **out);
 int mcaat_reads_info(const mcaat_reads *r, uint64_t *n_reads, uint64_t *n_bases);
 /* Mapping view used by mcaat_map_reads: one entry per input record (first file as is,
@@ -62,6 +65,9 @@ int mcaat_reads_info(const mcaat_reads *r, uint64_t *n_reads, uint64_t *n_bases)
  * (one input file, ACGT only, or reads not loaded from files). */
 int mcaat_reads_records_info(const mcaat_reads *r, uint64_t *n_records, int *separate);
 int mcaat_reads_download(const mcaat_reads *r, uint64_t *packed, uint64_t *offsets);
+/* the mapping view (records) as packed stream + offsets[n_records+1]; the counting view
+ * when records_info says it is not separate. Replaces the FASTQ re-parse of reads.cpp:88-130. */
+int mcaat_reads_records_download(const mcaat_reads *r, uint64_t *packed, uint64_t *offsets);
 void mcaat_reads_free(mcaat_reads *r);
 
 /* Synthetic metagenome: iid genomes with CRISPR arrays inserted,

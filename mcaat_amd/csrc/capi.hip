@@ -151,7 +151,19 @@ void upload_records(mcaat_ctx *ctx, const Stream &rec, mcaat_reads *r) {
     HIP_OK(hipStreamSynchronize(ctx->stream));
 }
 
-void read_fastx(const char *path, Packer &pk) {
+// first non-blank byte of a (possibly gzipped) file: '@' FASTQ, '>' FASTA
+int sniff_format(const char *path) {
+    gzFile f = gzopen(path, "rb");
+    if (!f) throw Error(MCAAT_E_IO, std::string("cannot open ") + path);
+    int c;
+    while ((c = gzgetc(f)) != -1 && (c == '\n' || c == '\r' || c == ' ' || c == '\t')) {
+    }
+    gzclose(f);
+    return c;
+}
+
+// FASTA (multi-line records) on the host; FASTQ goes through the GPU parser (fastq_ingest.hip)
+void read_fasta(const char *path, Packer &pk) {
     gzFile f = gzopen(path, "rb");
     if (!f) throw Error(MCAAT_E_IO, std::string("cannot open ") + path);
     std::string line, seq;
@@ -168,33 +180,16 @@ void read_fastx(const char *path, Packer &pk) {
             }
         }
     };
-    bool fastq = false, first = true;
-    std::string pending_header;
-    while (true) {
-        if (!getline(line)) break;
+    while (getline(line)) {
         if (line.empty()) continue;
-        if (first) {
-            first = false;
-            if (line[0] == '@') fastq = true;
-            else if (line[0] != '>') { gzclose(f); throw Error(MCAAT_E_IO, std::string("not FASTA/FASTQ: ") + path); }
-        }
-        if (fastq) {
-            if (line[0] != '@') { gzclose(f); throw Error(MCAAT_E_IO, std::string("malformed FASTQ: ") + path); }
-            std::string s, plus, q;
-            getline(s);
-            getline(plus);
-            getline(q);
-            pk.add_sequence(s);
+        if (line[0] == '>') {
+            if (!seq.empty()) pk.add_sequence(seq);
+            seq.clear();
         } else {
-            if (line[0] == '>') {
-                if (!seq.empty()) pk.add_sequence(seq);
-                seq.clear();
-            } else {
-                seq += line;
-            }
+            seq += line;
         }
     }
-    if (!fastq && !seq.empty()) pk.add_sequence(seq);
+    if (!seq.empty()) pk.add_sequence(seq);
     gzclose(f);
 }
 
@@ -329,21 +324,46 @@ int mcaat_reads_from_fastx(mcaat_ctx *ctx, const char *const *files, int n_files
     return guarded([&] {
         require(ctx && out && files && n_files > 0, "null argument");
         HIP_OK(hipSetDevice(ctx->device));
-        Packer pk;
+        int n_fastq = 0;
         for (int i = 0; i < n_files; ++i) {
-            pk.file = i;
-            read_fastx(files[i], pk);
+            const int c = sniff_format(files[i]);
+            if (c == '@') ++n_fastq;
+            else if (c != '>' && c != -1) throw Error(MCAAT_E_IO, std::string("not FASTA/FASTQ: ") + files[i]);
         }
         auto *r = new mcaat_reads;
         try {
-            upload_reads(ctx, pk.reads.words.data(), pk.reads.words.size(), pk.reads.offsets.data(),
-                         pk.reads.offsets.size() - 1, r);
-            if (pk.records_differ) upload_records(ctx, pk.records, r);
+            if (n_fastq == n_files) {
+                ingest_fastq(ctx, files, n_files, r);
+            } else {
+                require(n_fastq == 0, "mixed FASTA and FASTQ inputs");
+                Packer pk;
+                for (int i = 0; i < n_files; ++i) {
+                    pk.file = i;
+                    read_fasta(files[i], pk);
+                }
+                upload_reads(ctx, pk.reads.words.data(), pk.reads.words.size(), pk.reads.offsets.data(),
+                             pk.reads.offsets.size() - 1, r);
+                if (pk.records_differ) upload_records(ctx, pk.records, r);
+            }
         } catch (...) {
             delete r;
             throw;
         }
         *out = r;
+    });
+}
+
+/* mapping view (the counting view itself when not separate) */
+int mcaat_reads_records_download(const mcaat_reads *r, uint64_t *packed, uint64_t *offsets) {
+    return guarded([&] {
+        require(r != nullptr, "null argument");
+        const uint64_t n = r->has_records ? r->n_records : r->n_reads;
+        const auto &pk = r->has_records ? r->rec_packed : r->packed;
+        const auto &of = r->has_records ? r->rec_offsets : r->offsets;
+        uint64_t nb = 0;
+        HIP_OK(hipMemcpy(&nb, of.p + n, 8, hipMemcpyDeviceToHost));
+        if (packed && nb) HIP_OK(hipMemcpy(packed, pk.p, 8 * ((nb + 31) / 32), hipMemcpyDeviceToHost));
+        if (offsets) HIP_OK(hipMemcpy(offsets, of.p, 8 * (n + 1), hipMemcpyDeviceToHost));
     });
 }
 

@@ -1,0 +1,432 @@
+// fastq_ingest.hip — FASTQ(.gz) -> 2-bit read library in HBM.
+//
+// Replaces SDBGBuild::BuildLib / SequenceLibCollection::Build (sdbg_build.cpp:82-115, the
+// MEGAHIT buildlib step) for FASTQ inputs, and builds in the same pass the mapping view that
+// get_reads re-parses the FASTQ for (reads.cpp:20-52, 88-130). The host only moves bytes: a
+// reader thread fills pinned chunks (zlib inflates .gz; plain files are read straight into
+// the chunk), and each chunk is parsed on the GPU:
+//
+//  1. k_fq_nlcount   one lane per 64-byte segment (4 x 16-B loads): number of '\n' bytes
+//                    (SWAR zero-byte count); exclusive scan -> line index per segment.
+//  2. k_fq_nlpos     the same segments again: position of every '\n' (line starts).
+//                    Records are 4 lines (header '@', sequence, '+', quality); the bytes
+//                    after the last complete record carry over to the next chunk.
+//  3. k_fq_records   one lane per record: header check, sequence bounds ('\r' stripped),
+//                    ACGT base count and maximal-run count (counting view: non-ACGT symbols
+//                    split a read), sequence length (mapping view); three exclusive scans.
+//  4. k_fq_emit      one lane per record: packs the counting view (runs -> reads, global
+//                    read offsets) and the mapping view (second file reversed and
+//                    complemented; A/C/G -> 0/1/2, anything else -> 3, reads.cpp:44-52) into
+//                    the growing device streams; words shared with a neighbouring record are
+//                    merged with atomicOr, whole words are stored.
+//
+// Bytes per chunk byte (roofline, HBM): ~2.5 B read (two newline passes + the record
+// passes) + 0.25 B per sequence byte written per view. The ingest is PCIe/host-read bound
+// (text crosses PCIe once); the parse runs at HBM speed. FASTA (multi-line records) stays
+// on the host parser in capi.hip.
+#include <hipcub/hipcub.hpp>
+#include <zlib.h>
+
+#include <algorithm>
+#include <cstring>
+#include <future>
+#include <string>
+#include <sys/stat.h>
+
+#include "internal.h"
+
+namespace mcaat {
+namespace {
+
+constexpr int kBlock = 256;
+constexpr uint32_t kSeg = 64;  // bytes per lane in the newline passes
+
+// zero-byte mask of a 32-bit word: bit 7 of each byte that is zero (exact, no carries)
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t v) {
+    const uint32_t y = (v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+    return ~(y | v | 0x7F7F7F7Fu);
+}
+__device__ __forceinline__ uint32_t nl_mask(uint32_t v) { return zero_bytes(v ^ 0x0A0A0A0Au); }
+
+__global__ void k_fq_nlcount(const uint8_t *buf, uint32_t nseg, uint32_t *cnt) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += stride) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(buf + (size_t)s * kSeg);
+        uint32_t c = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 v = p[q];
+            c += __popc(nl_mask(v.x)) + __popc(nl_mask(v.y)) + __popc(nl_mask(v.z)) + __popc(nl_mask(v.w));
+        }
+        cnt[s] = c;
+    }
+}
+
+__global__ void k_fq_nlpos(const uint8_t *buf, uint32_t nseg, const uint32_t *first, uint32_t *nl) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < nseg; s += stride) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(buf + (size_t)s * kSeg);
+        uint32_t o = first[s];
+        const uint32_t base = s * kSeg;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 v = p[q];
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t m = nl_mask(w[j]);
+                while (m) {
+                    const int b = __builtin_ctz(m) >> 3;
+                    nl[o++] = base + 16 * q + 4 * j + b;
+                    m &= m - 1;
+                }
+            }
+        }
+    }
+}
+
+// counting-view code: A/C/G/T in either case, -1 splits the read (capi.hip Packer)
+__device__ __forceinline__ int count_code(uint8_t c) {
+    switch (c) {
+        case 'A': case 'a': return 0;
+        case 'C': case 'c': return 1;
+        case 'G': case 'g': return 2;
+        case 'T': case 't': return 3;
+        default: return -1;
+    }
+}
+// mapping-view code (k_mer_to_node_id, reads.cpp:44-52)
+__device__ __forceinline__ uint32_t map_code(uint8_t c) { return c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : 3; }
+// complement then code (reverse_pair_ends_sequence, reads.cpp:20-31: only A/C/G/T change)
+__device__ __forceinline__ uint32_t map_code_rc(uint8_t c) { return c == 'T' ? 0 : c == 'G' ? 1 : c == 'C' ? 2 : 3; }
+
+enum : uint32_t { kBadHeader = 1, kDiffer = 2 };
+
+// per record: sequence start, length, counting-view bases and runs
+__global__ void k_fq_records(const uint8_t *buf, const uint32_t *nl, uint32_t n_rec, uint32_t *sbeg, uint32_t *slen,
+                             uint32_t *nbase, uint32_t *nrun, uint32_t *flags) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    uint32_t fl = 0;
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n_rec; r += stride) {
+        const uint32_t h = r ? nl[4 * r - 1] + 1 : 0;
+        if (buf[h] != '@') fl |= kBadHeader;
+        const uint32_t s = nl[4 * r] + 1;
+        uint32_t e = nl[4 * r + 1];
+        if (e > s && buf[e - 1] == '\r') --e;
+        uint32_t bases = 0, runs = 0;
+        bool in = false, differ = false;
+        for (uint32_t i = s; i < e; ++i) {
+            const uint8_t c = buf[i];
+            if (count_code(c) >= 0) {
+                ++bases;
+                runs += !in;
+                in = true;
+            } else {
+                in = false;
+            }
+            differ |= c != 'A' && c != 'C' && c != 'G' && c != 'T';
+        }
+        // the mapping view equals the counting view only if this record is one ACGT run
+        if (differ || runs != 1) fl |= kDiffer;
+        sbeg[r] = s;
+        slen[r] = e - s;
+        nbase[r] = bases;
+        nrun[r] = runs;
+    }
+    if (fl) atomicOr(flags, fl);
+}
+
+// appends 2-bit symbols at consecutive stream positions; a word this lane does not fill
+// completely may be shared with another record and is merged with atomicOr
+struct PackWriter {
+    uint64_t *out;
+    uint64_t pos;
+    uint64_t acc = 0;
+    bool partial;
+    __device__ PackWriter(uint64_t *o, uint64_t p) : out(o), pos(p), partial((p & 31) != 0) {}
+    __device__ __forceinline__ void put(uint32_t b) {
+        acc |= (uint64_t)b << (2 * (pos & 31));
+        if ((++pos & 31) == 0) {
+            uint64_t *w = out + ((pos - 1) >> 5);
+            if (partial) {
+                if (acc) atomicOr((unsigned long long *)w, (unsigned long long)acc);
+            } else {
+                *w = acc;
+            }
+            acc = 0;
+            partial = false;
+        }
+    }
+    __device__ __forceinline__ void finish() {
+        if ((pos & 31) && acc) atomicOr((unsigned long long *)(out + (pos >> 5)), (unsigned long long)acc);
+    }
+};
+
+__global__ void k_fq_emit(const uint8_t *buf, uint32_t n_rec, const uint32_t *sbeg, const uint32_t *slen,
+                          const uint32_t *boff, const uint32_t *roff, const uint32_t *qoff, uint64_t g_base,
+                          uint64_t g_read, uint64_t g_qbase, uint64_t g_rec, int reverse, uint64_t *packed,
+                          uint64_t *offsets, uint64_t *qpacked, uint64_t *qoffsets) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n_rec; r += stride) {
+        const uint8_t *s = buf + sbeg[r];
+        const uint32_t L = slen[r];
+        // counting view: maximal ACGT runs are reads
+        PackWriter pw(packed, g_base + boff[r]);
+        uint64_t ri = g_read + roff[r];
+        bool in = false;
+        for (uint32_t i = 0; i < L; ++i) {
+            const int b = count_code(s[i]);
+            if (b >= 0) {
+                pw.put((uint32_t)b);
+                in = true;
+            } else if (in) {
+                offsets[1 + ri++] = pw.pos;
+                in = false;
+            }
+        }
+        if (in) offsets[1 + ri] = pw.pos;
+        pw.finish();
+        // mapping view: one entry per record
+        if (qpacked) {
+            PackWriter qw(qpacked, g_qbase + qoff[r]);
+            if (!reverse) {
+                for (uint32_t i = 0; i < L; ++i) qw.put(map_code(s[i]));
+            } else {
+                for (uint32_t i = L; i-- > 0;) qw.put(map_code_rc(s[i]));
+            }
+            qw.finish();
+            qoffsets[1 + g_rec + r] = qw.pos;
+        }
+    }
+}
+
+__global__ void k_fq_fixed_len(const uint64_t *off, uint64_t n, uint64_t L, uint32_t *bad) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    bool b = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += stride) b |= off[i] != i * L;
+    if (b) atomicOr(bad, 1u);
+}
+
+void scan_u32(mcaat_ctx *ctx, const uint32_t *in, uint32_t *out, uint64_t n, DevBuf<uint8_t> &tmp) {
+    size_t need = 0;
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, need, in, out, (size_t)n, ctx->stream));
+    if (need > tmp.bytes()) tmp.alloc(need);
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(tmp.p, need, in, out, (size_t)n, ctx->stream));
+}
+
+// grows a zero-filled device stream, keeping its first `used` elements
+void grow(mcaat_ctx *ctx, DevBuf<uint64_t> &b, uint64_t used, uint64_t need) {
+    if (need <= b.n) return;
+    DevBuf<uint64_t> nb(std::max<uint64_t>(need, b.n + b.n / 2));
+    HIP_OK(hipMemsetAsync(nb.p, 0, nb.bytes(), ctx->stream));
+    if (used) HIP_OK(hipMemcpyAsync(nb.p, b.p, 8 * used, hipMemcpyDeviceToDevice, ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    b = std::move(nb);
+}
+
+struct Pinned {
+    uint8_t *p = nullptr;
+    explicit Pinned(size_t n) { HIP_OK(hipHostMalloc((void **)&p, n, hipHostMallocDefault)); }
+    ~Pinned() {
+        if (p) (void)hipHostFree(p);
+    }
+    Pinned(const Pinned &) = delete;
+    Pinned &operator=(const Pinned &) = delete;
+};
+
+size_t read_full(gzFile f, uint8_t *dst, size_t n, const char *path) {
+    size_t got = 0;
+    while (got < n) {
+        const unsigned want = (unsigned)std::min<size_t>(n - got, 1u << 30);
+        const int r = gzread(f, dst + got, want);
+        if (r < 0) {
+            int errnum = 0;
+            throw Error(MCAAT_E_IO, std::string("read error in ") + path + ": " + gzerror(f, &errnum));
+        }
+        if (r == 0) break;
+        got += (size_t)r;
+    }
+    return got;
+}
+
+bool is_space(uint8_t c) { return c == '\n' || c == '\r' || c == ' ' || c == '\t'; }
+
+}  // namespace
+
+size_t fastq_chunk_bytes() {
+    if (const char *e = getenv("MCAAT_FASTQ_CHUNK")) {
+        const long long v = atoll(e);
+        if (v >= 256) return (size_t)v;
+    }
+    return size_t(256) << 20;
+}
+
+// All inputs are FASTQ (checked by the caller). Files are concatenated; records of files
+// after the first are reversed and complemented in the mapping view (paired-end R2).
+void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_reads *r) {
+    const size_t CH = fastq_chunk_bytes();
+    const size_t R = std::max<size_t>(CH / 4, 4096);  // carry reserve: the longest record that fits
+    const size_t cap = R + CH + 2 * kSeg;
+
+    uint64_t est = 0;  // stream capacity estimate from the input sizes (grown on demand)
+    for (int i = 0; i < n_files; ++i) {
+        struct stat st;
+        const std::string path(files[i]);
+        const bool gz = path.size() > 3 && path.compare(path.size() - 3, 3, ".gz") == 0;
+        if (stat(files[i], &st) == 0) est += (uint64_t)st.st_size * (gz ? 4 : 1);
+    }
+    DevBuf<uint64_t> packed(est / 64 + 1024), offsets(est / 256 + 1024);
+    DevBuf<uint64_t> qpacked(est / 64 + 1024), qoffsets(est / 256 + 1024);
+    for (auto *b : {&packed, &offsets, &qpacked, &qoffsets}) HIP_OK(hipMemsetAsync(b->p, 0, b->bytes(), ctx->stream));
+    uint64_t n_bases = 0, n_reads = 0, q_bases = 0, n_rec = 0;
+    uint32_t flags_all = 0;
+
+    Pinned h0(cap), h1(cap);
+    uint8_t *hb[2] = {h0.p, h1.p};
+    DevBuf<uint8_t> dbuf(cap);
+    const uint64_t max_seg = cap / kSeg + 1;
+    DevBuf<uint32_t> cnt(max_seg + 1), first(max_seg + 1), nl(cap + 16);  // every byte may be a newline
+    DevBuf<uint32_t> sbeg, slen, nbase, nrun, boff, roff, qoff;
+    DevBuf<uint32_t> meta(8);
+    DevBuf<uint8_t> tmp(1 << 20);
+    uint32_t *hmeta = nullptr;
+    HIP_OK(hipHostMalloc((void **)&hmeta, 64, hipHostMallocDefault));
+    struct MetaFree {
+        uint32_t *p;
+        ~MetaFree() { (void)hipHostFree(p); }
+    } meta_free{hmeta};
+
+    for (int fi = 0; fi < n_files; ++fi) {
+        gzFile f = gzopen(files[fi], "rb");
+        if (!f) throw Error(MCAAT_E_IO, std::string("cannot open ") + files[fi]);
+        struct Closer {
+            gzFile f;
+            ~Closer() { gzclose(f); }
+        } closer{f};
+        gzbuffer(f, 1u << 20);
+        int cur = 0;
+        size_t carry = 0;
+        size_t n = read_full(f, hb[cur] + R, CH, files[fi]);
+        bool eof = n < CH;
+        bool first_chunk = true;
+        for (;;) {
+            uint8_t *start = hb[cur] + R - carry;
+            size_t total = carry + n;
+            if (first_chunk) {  // leading blank lines
+                while (total && is_space(*start)) ++start, --total;
+                first_chunk = false;
+            }
+            if (eof) {  // trailing blank lines; the last line gets its newline
+                while (total && is_space(start[total - 1])) --total;
+                if (total) start[total++] = '\n';
+            }
+            std::future<size_t> next;
+            if (!eof) {
+                uint8_t *dst = hb[cur ^ 1] + R;
+                const char *path = files[fi];
+                next = std::async(std::launch::async, [f, dst, CH, path] { return read_full(f, dst, CH, path); });
+            }
+            // ---- newline passes
+            const uint32_t nseg = (uint32_t)((total + kSeg - 1) / kSeg);
+            if (total) {
+                KernelTimer kt(ctx, "fq_parse", 3.0 * (double)total);
+                HIP_OK(hipMemcpyAsync(dbuf.p, start, total, hipMemcpyHostToDevice, ctx->stream));
+                HIP_OK(hipMemsetAsync(dbuf.p + total, 0, (size_t)nseg * kSeg + kSeg - total, ctx->stream));
+                HIP_OK(hipMemsetAsync(cnt.p + nseg, 0, 4, ctx->stream));
+                hipLaunchKernelGGL(k_fq_nlcount, dim3(grid_for(nseg, kBlock)), dim3(kBlock), 0, ctx->stream, dbuf.p,
+                                   nseg, cnt.p);
+                scan_u32(ctx, cnt.p, first.p, (uint64_t)nseg + 1, tmp);
+                hipLaunchKernelGGL(k_fq_nlpos, dim3(grid_for(nseg, kBlock)), dim3(kBlock), 0, ctx->stream, dbuf.p,
+                                   nseg, first.p, nl.p);
+                HIP_OK(hipMemcpyAsync(hmeta, first.p + nseg, 4, hipMemcpyDeviceToHost, ctx->stream));
+                HIP_OK(hipStreamSynchronize(ctx->stream));
+                kt.stop();
+            }
+            const uint32_t NL = total ? hmeta[0] : 0;
+            const uint32_t nrec = NL / 4;
+            if (eof && NL % 4)
+                throw Error(MCAAT_E_IO, std::string("malformed FASTQ (truncated record or blank line): ") + files[fi]);
+            size_t consumed = 0;
+            if (nrec) {
+                HIP_OK(hipMemcpyAsync(hmeta, nl.p + 4 * (uint64_t)nrec - 1, 4, hipMemcpyDeviceToHost, ctx->stream));
+                HIP_OK(hipStreamSynchronize(ctx->stream));
+                consumed = (size_t)hmeta[0] + 1;
+            }
+            if (!eof && total - consumed > R)
+                throw Error(MCAAT_E_IO, std::string("FASTQ record longer than the chunk reserve (") +
+                                            std::to_string(R) + " bytes): " + files[fi]);
+            // ---- records
+            if (nrec) {
+                KernelTimer kt(ctx, "fq_records", (double)consumed + 16.0 * nrec);
+                if (sbeg.n < (uint64_t)nrec + 1) {
+                    const uint64_t m = std::max<uint64_t>((uint64_t)nrec + 1, cap / 64);
+                    for (auto *b : {&sbeg, &slen, &nbase, &nrun, &boff, &roff, &qoff}) b->alloc(m);
+                }
+                HIP_OK(hipMemsetAsync(meta.p, 0, 4, ctx->stream));
+                for (auto *b : {&nbase, &nrun, &slen}) HIP_OK(hipMemsetAsync(b->p + nrec, 0, 4, ctx->stream));
+                hipLaunchKernelGGL(k_fq_records, dim3(grid_for(nrec, kBlock)), dim3(kBlock), 0, ctx->stream, dbuf.p,
+                                   nl.p, nrec, sbeg.p, slen.p, nbase.p, nrun.p, meta.p);
+                scan_u32(ctx, nbase.p, boff.p, (uint64_t)nrec + 1, tmp);
+                scan_u32(ctx, nrun.p, roff.p, (uint64_t)nrec + 1, tmp);
+                scan_u32(ctx, slen.p, qoff.p, (uint64_t)nrec + 1, tmp);
+                HIP_OK(hipMemcpyAsync(hmeta + 0, boff.p + nrec, 4, hipMemcpyDeviceToHost, ctx->stream));
+                HIP_OK(hipMemcpyAsync(hmeta + 1, roff.p + nrec, 4, hipMemcpyDeviceToHost, ctx->stream));
+                HIP_OK(hipMemcpyAsync(hmeta + 2, qoff.p + nrec, 4, hipMemcpyDeviceToHost, ctx->stream));
+                HIP_OK(hipMemcpyAsync(hmeta + 3, meta.p, 4, hipMemcpyDeviceToHost, ctx->stream));
+                HIP_OK(hipStreamSynchronize(ctx->stream));
+                kt.stop();
+                const uint32_t cb = hmeta[0], cr = hmeta[1], cq = hmeta[2], fl = hmeta[3];
+                if (fl & kBadHeader) throw Error(MCAAT_E_IO, std::string("malformed FASTQ: ") + files[fi]);
+                flags_all |= fl;
+                if (fi > 0) flags_all |= kDiffer;  // second file: reverse-complemented records
+                grow(ctx, packed, (n_bases + 31) / 32 + 1, (n_bases + cb + 31) / 32 + 17);
+                grow(ctx, offsets, n_reads + 1, n_reads + cr + 2);
+                grow(ctx, qpacked, (q_bases + 31) / 32 + 1, (q_bases + cq + 31) / 32 + 17);
+                grow(ctx, qoffsets, n_rec + 1, n_rec + nrec + 2);
+                KernelTimer ke(ctx, "fq_emit", (double)consumed + 0.5 * (double)(cb + cq) + 8.0 * (cr + nrec));
+                hipLaunchKernelGGL(k_fq_emit, dim3(grid_for(nrec, kBlock)), dim3(kBlock), 0, ctx->stream, dbuf.p, nrec,
+                                   sbeg.p, slen.p, boff.p, roff.p, qoff.p, n_bases, n_reads, q_bases, n_rec, fi > 0 ? 1 : 0,
+                                   packed.p, offsets.p, qpacked.p, qoffsets.p);
+                HIP_OK(hipGetLastError());
+                ke.stop();
+                n_bases += cb;
+                n_reads += cr;
+                q_bases += cq;
+                n_rec += nrec;
+            }
+            if (eof) break;
+            n = next.get();
+            eof = n < CH;
+            carry = total - consumed;
+            memcpy(hb[cur ^ 1] + R - carry, start + consumed, carry);
+            cur ^= 1;
+        }
+    }
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+
+    r->ctx = ctx;
+    r->n_reads = n_reads;
+    r->n_bases = n_bases;
+    r->n_words = (n_bases + 31) / 32;
+    r->fixed_len = 0;
+    if (n_reads > 0) {
+        uint64_t L = 0;
+        HIP_OK(hipMemcpy(&L, offsets.p + 1, 8, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemsetAsync(meta.p, 0, 4, ctx->stream));
+        hipLaunchKernelGGL(k_fq_fixed_len, dim3(grid_for(n_reads + 1, kBlock)), dim3(kBlock), 0, ctx->stream,
+                           offsets.p, n_reads, L, meta.p);
+        HIP_OK(hipMemcpyAsync(hmeta, meta.p, 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_OK(hipStreamSynchronize(ctx->stream));
+        if (!hmeta[0] && L > 0) r->fixed_len = L;
+    }
+    r->packed = std::move(packed);
+    r->offsets = std::move(offsets);
+    r->n_records = n_rec;
+    r->has_records = (flags_all & kDiffer) != 0;
+    if (r->has_records) {
+        r->rec_packed = std::move(qpacked);
+        r->rec_offsets = std::move(qoffsets);
+    }
+}
+
+}  // namespace mcaat

@@ -65,6 +65,7 @@ SIGNATURES = {
     "mcaat_reads_from_fastx": (C.c_int, [C.c_void_p, C.POINTER(C.c_char_p), C.c_int, C.POINTER(C.c_void_p)]),
     "mcaat_reads_info": (C.c_int, [C.c_void_p, _u64p, _u64p]),
     "mcaat_reads_download": (C.c_int, [C.c_void_p, _u64p, _u64p]),
+    "mcaat_reads_records_download": (C.c_int, [C.c_void_p, _u64p, _u64p]),
     "mcaat_reads_free": (None, [C.c_void_p]),
     "mcaat_reads_synth": (C.c_int, [C.c_void_p, C.POINTER(_SynthSpec), C.POINTER(C.c_void_p)]),
     "mcaat_synth_host": (C.c_int, [C.POINTER(_SynthSpec), _u64p, _u64p]),
@@ -281,6 +282,15 @@ class Reads:
         packed = np.zeros((b + 31) // 32, dtype=np.uint64)
         offsets = np.zeros(n + 1, dtype=np.uint64)
         _check(self.ctx._lib.mcaat_reads_download(self.h, _ptr(packed, _u64p), _ptr(offsets, _u64p)))
+        return packed, offsets
+
+    def download_records(self) -> Tuple[np.ndarray, np.ndarray]:
+        """Mapping view (one entry per input record; reads.cpp:20-52 coding)."""
+        n, _ = self.records_info()
+        offsets = np.zeros(n + 1, dtype=np.uint64)
+        _check(self.ctx._lib.mcaat_reads_records_download(self.h, None, _ptr(offsets, _u64p)))
+        packed = np.zeros((int(offsets[-1]) + 31) // 32 + 1, dtype=np.uint64)
+        _check(self.ctx._lib.mcaat_reads_records_download(self.h, _ptr(packed, _u64p), _ptr(offsets, _u64p)))
         return packed, offsets
 
     def free(self) -> None:

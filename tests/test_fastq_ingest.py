@@ -1,0 +1,164 @@
+"""GPU FASTQ ingest (csrc/fastq_ingest.hip) against the Python restatement
+of the read library (oracle/fastx.py): counting view (reads split at non-ACGT symbols) and
+mapping view (one entry per record, second file reverse-complemented, reads.cpp:20-52).
+
+Bar: bit-exact packed streams and offsets. The chunk size is forced down (MCAAT_FASTQ_CHUNK) so
+records straddle chunk boundaries and the carry path runs many times. Edge cases: N and IUPAC
+symbols, lowercase, CRLF, empty sequences, no final newline, blank lines around the records,
+gzip input, paired-end, records longer than the carry reserve and malformed input (loud errors).
+"""
+import gzip
+import os
+
+import numpy as np
+import pytest
+
+from oracle import fastx as FX
+
+ALPHA = "ACGT" * 6 + "acgtNRY"
+
+
+def _rand_records(rng, n, max_len=300):
+    seqs = []
+    for i in range(n):
+        L = int(rng.integers(0, max_len)) if i % 17 else 0
+        if i % 5 == 0:
+            s = "".join(rng.choice(list(ALPHA), size=L))
+        else:
+            s = "".join(rng.choice(list("ACGT"), size=L))
+        seqs.append(s)
+    return seqs
+
+
+def _fastq_text(seqs, crlf=False, final_newline=True, lead="", trail=""):
+    nl = "\r\n" if crlf else "\n"
+    body = nl.join(f"@r{i} x{nl}{s}{nl}+{nl}{'I' * len(s)}" for i, s in enumerate(seqs))
+    return lead + body + (nl if final_newline else "") + trail
+
+
+def _write(path, text, gz=False):
+    data = text.encode()
+    if gz:
+        with gzip.open(path, "wb") as f:
+            f.write(data)
+    else:
+        with open(path, "wb") as f:
+            f.write(data)
+    return str(path)
+
+
+# ---- restatement (CPU) ------------------------------------------------------------------
+
+def test_restatement_known_answers():
+    text = "\n\n@a\nACGTNacgt\n+\nIIIIIIIII\n@b\r\n\r\n+\r\n\r\n@c\nGGRTT\n+\nIIIII"
+    seqs = FX.fastq_sequences(text)
+    assert seqs == ["ACGTNacgt", "", "GGRTT"]
+    assert FX.counting_view(seqs) == ["ACGT", "ACGT", "GG", "TT"]
+    assert FX.mapping_view([seqs[:2], seqs[2:]]) == [[0, 1, 2, 3, 3, 3, 3, 3, 3], [], [0, 0, 3, 1, 1]]
+    words, offs = FX.pack_bases(["ACGT", "T"])
+    assert list(offs) == [0, 4, 5] and int(words[0]) == 0b11_11100100
+    with pytest.raises(FX.FastqError):
+        FX.fastq_sequences("@a\nACGT\n+\n")  # 3 lines
+    with pytest.raises(FX.FastqError):
+        FX.fastq_sequences("@a\nACGT\n+\nIIII\nb\nA\n+\nI\n")
+
+
+# ---- GPU ------------------------------------------------------------------------------------
+
+def _check(ctx, files, texts, monkeypatch, chunk):
+    import mcaat_amd as M
+
+    if chunk:
+        monkeypatch.setenv("MCAAT_FASTQ_CHUNK", str(chunk))
+    else:
+        monkeypatch.delenv("MCAAT_FASTQ_CHUNK", raising=False)
+    per_file = [FX.fastq_sequences(t) for t in texts]
+    want_p, want_o = FX.pack_bases(FX.counting_view([s for f in per_file for s in f]))
+    want_qp, want_qo = FX.pack_codes(FX.mapping_view(per_file))
+    reads = M.Reads.from_fastx(ctx, files)
+    p, o = reads.download()
+    assert np.array_equal(o, want_o)
+    nw = (int(want_o[-1]) + 31) // 32
+    assert np.array_equal(p[:nw], want_p[:nw])
+    qp, qo = reads.download_records()
+    assert np.array_equal(qo, want_qo)
+    nq = (int(want_qo[-1]) + 31) // 32
+    assert np.array_equal(qp[:nq], want_qp[:nq])
+    n_rec, separate = reads.records_info()
+    assert n_rec == sum(len(f) for f in per_file)
+    one_run = all(len(s) > 0 and set(s) <= set("ACGT") for f in per_file for s in f)
+    assert separate == (len(files) > 1 and len(per_file[1]) > 0 or not one_run)
+    return reads
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", [256, 1000, 4099, 0])
+def test_single_end_chunked(gpu_ctx, tmp_path, monkeypatch, chunk):
+    rng = np.random.default_rng(11 + chunk)
+    seqs = _rand_records(rng, 400)
+    text = _fastq_text(seqs, lead="\n", trail="\n\n")
+    _check(gpu_ctx, [_write(tmp_path / "a.fq", text)], [text], monkeypatch, chunk)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gz", [False, True])
+def test_paired_end_crlf_gzip(gpu_ctx, tmp_path, monkeypatch, gz):
+    rng = np.random.default_rng(5)
+    t1 = _fastq_text(_rand_records(rng, 300), crlf=True)
+    t2 = _fastq_text(_rand_records(rng, 300), final_newline=False)
+    sfx = ".fq.gz" if gz else ".fq"
+    files = [_write(tmp_path / ("r1" + sfx), t1, gz), _write(tmp_path / ("r2" + sfx), t2, gz)]
+    _check(gpu_ctx, files, [t1, t2], monkeypatch, 777)
+
+
+@pytest.mark.gpu
+def test_acgt_only_is_the_counting_view(gpu_ctx, tmp_path, monkeypatch):
+    rng = np.random.default_rng(7)
+    seqs = ["".join(rng.choice(list("ACGT"), size=150)) for _ in range(500)]
+    text = _fastq_text(seqs)
+    reads = _check(gpu_ctx, [_write(tmp_path / "a.fq", text)], [text], monkeypatch, 2048)
+    assert reads.records_info() == (500, False)
+    # fixed-length detection as for host-built libraries
+    n, b = reads.info()
+    assert (n, b) == (500, 75000)
+
+
+@pytest.mark.gpu
+def test_empty_and_blank_files(gpu_ctx, tmp_path, monkeypatch):
+    import mcaat_amd as M
+
+    f = _write(tmp_path / "e.fq", "\n\n")
+    reads = M.Reads.from_fastx(gpu_ctx, [f])
+    assert reads.info() == (0, 0)
+
+
+@pytest.mark.gpu
+def test_malformed_inputs_fail_loudly(gpu_ctx, tmp_path, monkeypatch):
+    import mcaat_amd as M
+
+    monkeypatch.setenv("MCAAT_FASTQ_CHUNK", "256")
+    bad = {
+        "trunc.fq": "@a\nACGT\n+\nIIII\n@b\nACGT\n+\n",
+        "header.fq": "@a\nACGT\n+\nIIII\nb\nACGT\n+\nIIII\n",
+        "blank.fq": "@a\nACGT\n+\nIIII\n\n@b\nACGT\n+\nIIII\n",
+        "long.fq": "@a\n" + "A" * 6000 + "\n+\n" + "I" * 6000 + "\n",
+        "junk.fq": "hello\n",
+    }
+    for name, text in bad.items():
+        with pytest.raises(RuntimeError):
+            M.Reads.from_fastx(gpu_ctx, [_write(tmp_path / name, text)])
+    fa = _write(tmp_path / "x.fa", ">a\nACGT\nAC\n")
+    fq = _write(tmp_path / "y.fq", "@a\nACGT\n+\nIIII\n")
+    with pytest.raises(RuntimeError):
+        M.Reads.from_fastx(gpu_ctx, [fa, fq])
+
+
+@pytest.mark.gpu
+def test_fasta_still_parsed(gpu_ctx, tmp_path):
+    import mcaat_amd as M
+
+    f = _write(tmp_path / "x.fa", ">a\nACGTN\nACG\n>b\nTTTT\n")
+    reads = M.Reads.from_fastx(gpu_ctx, [f])
+    p, o = reads.download()
+    wp, wo = FX.pack_bases(["ACGT", "ACG", "TTTT"])
+    assert np.array_equal(o, wo) and np.array_equal(p[:1], wp[:1])
