@@ -214,7 +214,7 @@ constexpr int kWB = 4;  // write batch (entries per thread per round: 12 loads i
 // one add.
 constexpr int kPeP = 7, kPePar = 14, kPeLane = 15;
 
-template <int W>
+template <int W, bool FULL>
 __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__restrict__ packed, ItemSrc src,
                                                           SkParams P, uint4 *__restrict__ l1_data,
                                                           const uint64_t *__restrict__ l1_base,
@@ -271,7 +271,7 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
     const uint64_t n_batches = (n_items + 63) / 64;
     const uint64_t bstride = (uint64_t)gridDim.x * kAWaves;
     uint64_t batch = (uint64_t)blockIdx.x * kAWaves + wave;
-    constexpr bool kFull = W >= 10;  // the host picks m = 16 whenever W >= 10
+    constexpr bool kFull = FULL;  // m == 16: the m-mers need no mask
     const uint32_t mmask = (uint32_t)mask_bits(2 * P.m);
     const uint32_t salt32 = (uint32_t)P.salt;
     const int nmax = P.nmax;
@@ -549,14 +549,24 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
 
 typedef void (*SkKernel)(const uint64_t *, ItemSrc, SkParams, uint4 *, const uint64_t *, const uint64_t *,
                          unsigned long long *, uint16_t *, unsigned long long *);
-SkKernel sk_kernel(int w) {
-    switch (w) {
+SkKernel sk_kernel(int w, bool full) {
+    if (full) {
+        switch (w) {
 #define MCAAT_SK(W) \
     case W:         \
-        return k_sk_scatter<W>;
-        MCAAT_SK(1) MCAAT_SK(2) MCAAT_SK(3) MCAAT_SK(4) MCAAT_SK(5) MCAAT_SK(6) MCAAT_SK(7) MCAAT_SK(8)
-        MCAAT_SK(9) MCAAT_SK(10) MCAAT_SK(11) MCAAT_SK(12) MCAAT_SK(13) MCAAT_SK(14) MCAAT_SK(15) MCAAT_SK(16)
+        return k_sk_scatter<W, true>;
+            MCAAT_SK(9) MCAAT_SK(10) MCAAT_SK(11) MCAAT_SK(12) MCAAT_SK(13) MCAAT_SK(14) MCAAT_SK(15) MCAAT_SK(16)
 #undef MCAAT_SK
+        }
+    } else {
+        switch (w) {
+#define MCAAT_SK(W) \
+    case W:         \
+        return k_sk_scatter<W, false>;
+            MCAAT_SK(1) MCAAT_SK(2) MCAAT_SK(3) MCAAT_SK(4) MCAAT_SK(5) MCAAT_SK(6) MCAAT_SK(7) MCAAT_SK(8)
+            MCAAT_SK(9) MCAAT_SK(10) MCAAT_SK(11) MCAAT_SK(12) MCAAT_SK(13) MCAAT_SK(14) MCAAT_SK(15) MCAAT_SK(16)
+#undef MCAAT_SK
+        }
     }
     throw Error(MCAAT_E_INVALID, "node_counter: minimizer window out of range");
 }
@@ -724,6 +734,20 @@ constexpr int kDProbe = 128;                               // probe bound of the
 constexpr int kCB = 4;                                     // descriptor loads in flight per thread
 constexpr int kDefer = 64;                                 // descriptors with w0 == kEmpty before going raw
 constexpr int kCPerCu = 2;                                 // resident workgroups per CU (LDS, VGPR <= 64)
+#ifndef MCAAT_CSPLIT
+#define MCAAT_CSPLIT 2
+#endif
+constexpr uint32_t kSplitLg = MCAAT_CSPLIT;                // log2 classes of an overflowing partition (<= 3 spare hash bits)
+static_assert(kSplitLg <= 3, "the sub-partition takes the top 11 of the 14 stored hash bits");
+// the deferred list only overflows on pathological T runs: those partitions go raw at once
+__device__ __forceinline__ bool n_deferred_over(uint32_t n) { return n > (uint32_t)kDefer; }
+
+// overflow-list entry: partition (24 bits), class (4), log2 class count (4)
+__device__ __forceinline__ uint32_t ovf_part(uint32_t e) { return e & 0xFFFFFFu; }
+__device__ __forceinline__ bool ovf_in_class(uint32_t e, uint32_t dw) {  // dw: descriptor word 3
+    const uint32_t lgn = e >> 28, cls = (e >> 24) & 15;
+    return ((dw >> (kHShift - 32)) & ((1u << lgn) - 1)) == cls;
+}
 
 __device__ __forceinline__ uint32_t edge_slot(uint64_t c) {
     return (((uint32_t)c ^ (uint32_t)(c >> 32)) * 0x9E3779B1u) >> (32 - 12);
@@ -799,6 +823,12 @@ __global__ void __launch_bounds__(kCThreads, kCPerCu * kCThreads / 256) k_lds_co
     };
 
     for (uint64_t p = p0 + blockIdx.x; p < F; p += gridDim.x) {
+      // a partition whose distinct descriptors overflow the table is counted again as
+      // 2^kSplitLg edge-disjoint classes (spare minimizer-hash bits: every occurrence of a
+      // canonical edge carries the same minimizer), each collapsed, expanded and emitted alone
+      uint32_t lgn = 0;
+      for (uint32_t cls = 0; cls < (1u << lgn); ++cls) {
+        const uint32_t cmask = (1u << lgn) - 1;
         for (int i = threadIdx.x; i < kDCap; i += kCThreads) {
             dk0[i] = dk1[i] = kEmpty;
             dcnt[i] = 0;
@@ -817,6 +847,7 @@ __global__ void __launch_bounds__(kCThreads, kCPerCu * kCThreads / 256) k_lds_co
         // another (a descriptor whose first word is the empty marker is deferred)
         auto collapse = [&](uint64_t w0, uint64_t w1) {
             if (((w1 >> kNShift) & 63) == 0) return;  // padding
+            if (((uint32_t)(w1 >> kHShift) & cmask) != cls) return;  // another class
             if (w0 == kEmpty) {
                 const uint32_t j = atomicAdd(&n_deferred, 1u);
                 if (j < (uint32_t)kDefer)
@@ -864,6 +895,12 @@ __global__ void __launch_bounds__(kCThreads, kCPerCu * kCThreads / 256) k_lds_co
         }
         __syncthreads();
         tick(1);
+        if (dovf && lgn == 0 && !n_deferred_over(n_deferred)) {
+            lgn = kSplitLg;
+            cls = ~0u;  // -> class 0 of 2^kSplitLg
+            __syncthreads();  // every thread has read dovf before the next clear resets it
+            continue;
+        }
         if (PROF && threadIdx.x == 0) {
             if (dovf) tp[4]++;
             atomicAdd(&prof[6], (unsigned long long)n_ddistinct);
@@ -942,6 +979,7 @@ __global__ void __launch_bounds__(kCThreads, kCPerCu * kCThreads / 256) k_lds_co
                     const uint4 q = data[d];
                     w0 = (uint64_t)q.x | ((uint64_t)q.y << 32);
                     w1 = (uint64_t)q.z | ((uint64_t)q.w << 32);
+                    if (((uint32_t)(w1 >> kHShift) & cmask) != cls) w0 = w1 = 0;
                 }
                 spread(w0, w1, (int)((w1 >> kNShift) & 63), 1u);
             }
@@ -949,7 +987,7 @@ __global__ void __launch_bounds__(kCThreads, kCPerCu * kCThreads / 256) k_lds_co
         __syncthreads();
         tick(2);
         if (ovf) {
-            if (threadIdx.x == 0) ovf_list[atomicAdd(ovf_n, 1ull)] = (uint32_t)p;
+            if (threadIdx.x == 0) ovf_list[atomicAdd(ovf_n, 1ull)] = (uint32_t)p | (cls << 24) | (lgn << 28);
             __syncthreads();
             continue;
         }
@@ -988,6 +1026,7 @@ __global__ void __launch_bounds__(kCThreads, kCPerCu * kCThreads / 256) k_lds_co
         }
         __syncthreads();
         tick(3);
+      }
     }
     if (PROF && (threadIdx.x & 63) == 0)
         for (int i = 0; i < 5; ++i) atomicAdd(&prof[i], tp[i]);
@@ -1028,10 +1067,13 @@ __device__ __forceinline__ void table_insert(uint64_t key, Slot *tab, uint64_t m
 __global__ void __launch_bounds__(kBlock) k_part_occ(const uint4 *data, uint64_t gbase, const uint64_t *fine_base,
                                                      const uint32_t *parts, uint64_t np, uint64_t *occ) {
     for (uint64_t q = blockIdx.x; q < np; q += gridDim.x) {
-        const uint64_t p = parts[q];
+        const uint32_t e = parts[q];
+        const uint64_t p = ovf_part(e);
         unsigned long long acc = 0;
-        for (uint64_t d = fine_base[p] - gbase + threadIdx.x; d < fine_base[p + 1] - gbase; d += blockDim.x)
-            acc += (data[d].w >> (kNShift - 32)) & 63;
+        for (uint64_t d = fine_base[p] - gbase + threadIdx.x; d < fine_base[p + 1] - gbase; d += blockDim.x) {
+            const uint32_t dw = data[d].w;
+            if (ovf_in_class(e, dw)) acc += (dw >> (kNShift - 32)) & 63;
+        }
         __shared__ unsigned long long s;
         if (threadIdx.x == 0) s = 0;
         __syncthreads();
@@ -1046,9 +1088,11 @@ __global__ void __launch_bounds__(kBlock) k_fallback(const uint4 *data, uint64_t
                                                      const uint32_t *parts, uint64_t np, int E, Slot *tab,
                                                      uint64_t mask, unsigned long long *n_new, int *overflow) {
     for (uint64_t q = blockIdx.x; q < np; q += gridDim.x) {
-        const uint64_t p = parts[q];
+        const uint32_t e = parts[q];
+        const uint64_t p = ovf_part(e);
         for (uint64_t d = fine_base[p] - gbase + threadIdx.x; d < fine_base[p + 1] - gbase; d += blockDim.x) {
             const uint4 x = data[d];
+            if (!ovf_in_class(e, x.w)) continue;
             const uint64_t w0 = (uint64_t)x.x | ((uint64_t)x.y << 32);
             const uint64_t w1 = (uint64_t)x.z | ((uint64_t)x.w << 32);
             const int n = (int)((w1 >> kNShift) & 63);
@@ -1135,9 +1179,18 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     // long minimizers (near-unique per genome locus) keep the per-partition load uniform;
     // short ones (m=11) concentrate thousands of distinct edges on small-hash m-mers
     P.m = std::max(3, std::min(16, E - 8));  // <= 16: the m-mer machinery is 32-bit
+    // longer windows mean longer super-k-mers (fewer descriptors to write, partition and
+    // collapse); m >= 14 keeps minimizers near-unique per locus. k=27: W 13 -> 15 (m 14)
+    // took node_counter 201 -> 194 ms at C3 (pass C splits the partitions that then overflow
+    // the descriptor table into edge-disjoint classes)
+    if (E >= 22) P.m = std::max(14, std::min(16, E - 14));
+    if (const char *e = getenv("MCAAT_MINI_W")) {  // A/B knob: minimizer window (m-mers per edge)
+        const int wt = atoi(e);
+        if (wt >= 1 && wt <= 16) P.m = std::max(3, std::min(16, E - wt + 1));
+    }
     if (P.m > E) P.m = E;
     P.w = E - P.m + 1;
-    if (P.w >= 10 && P.m != 16) throw Error(MCAAT_E_INVALID, "node_counter: W >= 10 needs m = 16");
+    if (P.w > 16) throw Error(MCAAT_E_INVALID, "node_counter: minimizer window above 16");
     P.nmax = kDescBases - E + 1;
     P.salt = 0x6d696e696d697aULL;
 
@@ -1223,8 +1276,8 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
         HIP_OK(hipMemcpyAsync(dbase.p, base.data(), 8 * 257, hipMemcpyHostToDevice, st));
         HIP_OK(hipMemsetAsync(dcur.p, 0, dcur.bytes(), st));
         {
-            KernelTimer kt(ctx, "sk_scatter", 0.25 * (double)r->n_bases + 16.0 * (double)est / 1.25);
-            hipLaunchKernelGGL(sk_kernel(P.w), dim3((unsigned)a_grid), dim3(kAThreads), 0, st, r->packed.p, src, P, l1.p,
+            KernelTimer kt(ctx, "sk_scatter", 0.0);  // bytes added below, once the descriptor count is known
+            hipLaunchKernelGGL(sk_kernel(P.w, P.m == 16), dim3((unsigned)a_grid), dim3(kAThreads), 0, st, r->packed.p, src, P, l1.p,
                                dbase.p, dcap.p, dcur.p, l1s.p, prof_a ? dprof.p : nullptr);
             LAUNCH_OK();
             kt.stop();
@@ -1240,6 +1293,9 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     }
     uint64_t n_desc = 0;
     for (int b = 0; b < 256; ++b) n_desc += tot[b];
+    // algorithmic bytes of the launch: the 2-bit stream read once, a 16-B descriptor and its
+    // 2-B sub row written per reserved slot (the tail slots of a reservation are written inert)
+    ctx->kstats["sk_scatter"].total_bytes += 0.25 * (double)r->n_bases + 18.0 * (double)n_desc;
     if (prof_a) {
         unsigned long long hp[8];
         HIP_OK(hipMemcpy(hp, dprof.p, 64, hipMemcpyDeviceToHost));
@@ -1294,7 +1350,7 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     out.counts.alloc(out_cap);
     DevBuf<unsigned long long> dcnt(4);
     HIP_OK(hipMemsetAsync(dcnt.p, 0, dcnt.bytes(), st));
-    DevBuf<uint32_t> ovf_list(F);
+    DevBuf<uint32_t> ovf_list(F << kSplitLg);  // one entry per (partition, class)
     static const bool prof_c = getenv("MCAAT_PROF_C") && getenv("MCAAT_PROF_C")[0] == '1';
     if (prof_c) HIP_OK(hipMemsetAsync(dprof.p, 0, dprof.bytes(), st));
     const uint64_t group_budget = std::max<uint64_t>(n_live / 4 + 1, 1ULL << 28);  // descriptors per group

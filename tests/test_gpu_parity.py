@@ -176,6 +176,25 @@ def test_lds_overflow_fallback_low_coverage(gpu_ctx):
     assert gpu_ctx.kernel_timing("lds_count_overflow_partitions")[1] > 0
 
 
+@pytest.mark.parametrize("mini_w", ["", "14", "16"])
+def test_descriptor_overflow_classes(gpu_ctx, monkeypatch, mini_w):
+    """~2x coverage with 1% errors: fine partitions hold more distinct super-k-mers than the
+    LDS descriptor table, so pass C counts them as edge-disjoint minimizer-hash classes (and
+    sends classes whose edges overflow to the class-filtered global fallback). Also covers the
+    minimizer-window knob. Counts must equal the oracle."""
+    if mini_w:
+        monkeypatch.setenv("MCAAT_MINI_W", mini_w)
+    else:
+        monkeypatch.delenv("MCAAT_MINI_W", raising=False)
+    spec = M.SynthSpec(seed=41, n_genomes=10, genome_len=1_000_000, arrays_per_genome=0, n_reads=150_000,
+                       error_rate=0.01)
+    packed, offs = M.synth_host(spec)
+    reads = M.Reads.synth(gpu_ctx, spec)
+    gk, gc = M.count_edges(gpu_ctx, reads, 27)
+    ok, oc = O.count_canonical(packed, offs, 27, threads=4)
+    assert np.array_equal(gk, ok) and np.array_equal(gc, oc)
+
+
 @pytest.mark.parametrize("n_reads", [12, 400])
 def test_poly_t_runs(gpu_ctx, n_reads):
     """Super-k-mers starting inside a run of >= 32 T have an all-ones first word, the LDS
