@@ -82,28 +82,37 @@ __device__ __forceinline__ uint64_t lower_bound_dir(const uint64_t *key, const u
     return lo;
 }
 
+// out_info[e]: the target node's first edge and its W mask, by a directory-bounded search
+// (consecutive edges' targets form 4 monotone streams, one per W). in_info is written from
+// the predecessor side: the in-edges of node N are the edges with W == c in the (k-1)-suffix
+// group of any of them, so the first such edge of the group (a local scan around e) writes
+// in_info for every edge of N = target(e) — no search from the random in-group of each edge.
+// Edges of nodes without predecessors keep in_info = 0 (an empty mask).
 __global__ void __launch_bounds__(kBlock) k_adjacency(const uint64_t *key, uint64_t D, int k, const uint64_t *dir,
                                                       int shift, uint64_t *out_info, uint64_t *in_info) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t gmask = mask_bits(2 * (k - 1));
     for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < D; e += stride) {
         const uint64_t K = key[e];
         const uint64_t W = K & 3, R = K >> 2;
         // out: edges of node target(e) = label s[1..k-1]W
         const uint64_t Rt = (W << (2 * (k - 1))) | (R >> 2);
-        uint64_t lo = lower_bound_dir(key, dir, shift, Rt << 2);
+        const uint64_t lo = lower_bound_dir(key, dir, shift, Rt << 2);
         unsigned m = 0;
         for (uint64_t i = lo; i < D && (key[i] >> 2) == Rt; ++i) m |= 1u << (key[i] & 3);
         out_info[e] = lo | ((uint64_t)m << kIdxBits);
-        // in: group of labels x s[0..k-2], edges with W == s[k-1]
-        const uint64_t c = (K >> (2 * k)) & 3;
-        const uint64_t G = R & gmask;
-        lo = lower_bound_dir(key, dir, shift, G << 4);
+        if (!m) continue;  // target has no out-edges: no edge has it as source
+        // e's group: edges whose labels share s[1..k-1] (key >> 4); positions with W == W_e
+        const uint64_t gk = K >> 4;
+        uint64_t gs = e;
+        while (gs > 0 && (key[gs - 1] >> 4) == gk) --gs;
         unsigned pm = 0;
         int j = 0;
-        for (uint64_t i = lo; i < D && (key[i] >> 4) == G && j < 16; ++i, ++j)
-            if ((key[i] & 3) == c) pm |= 1u << j;
-        in_info[e] = lo | ((uint64_t)pm << kIdxBits);
+        for (uint64_t i = gs; i < D && (key[i] >> 4) == gk && j < 16; ++i, ++j)
+            if ((key[i] & 3) == W) pm |= 1u << j;
+        if ((uint64_t)(__ffs(pm) - 1) != e - gs) continue;  // another in-edge of N writes
+        const uint64_t v = gs | ((uint64_t)pm << kIdxBits);
+        const int deg = __popc(m);
+        for (int r = 0; r < deg; ++r) in_info[lo + r] = v;
     }
 }
 
@@ -608,10 +617,11 @@ void sdbg_finish(mcaat_ctx *ctx, mcaat_graph *g) {
     g->out_info.alloc(D);
     g->in_info.alloc(D);
     if (D) {
-        KernelTimer kt(ctx, "adjacency", 24.0 * (double)D);  // key read, two words written
+        KernelTimer kt(ctx, "adjacency", 32.0 * (double)D);  // key read, in_info cleared, two words written
         // one edge per lane: neighbouring lanes search neighbouring key ranges, so the
         // searches' loads share lines across the wave (a thread-per-run merge walk that
         // loses this was 5x slower)
+        HIP_OK(hipMemsetAsync(g->in_info.p, 0, 8 * D, st));
         hipLaunchKernelGGL(k_adjacency, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, g->key.p, D, k, dir.p, shift,
                            g->out_info.p, g->in_info.p);
         LAUNCH_OK();
