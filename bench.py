@@ -306,7 +306,7 @@ def main() -> int:
         }
         g.free()
     ingest = None
-    if rank == 0 and not args.dry_run and args.ingest_reads > 0:
+    if rank == 0 and world == 1 and not args.dry_run and args.ingest_reads > 0:
         ingest = measure_ingest(ctx, spec, args.ingest_reads)
     kmers_rank = count * max(0, spec.read_len - k)
     kmers_total = n_occ(spec, k) if sharded else kmers_rank * world

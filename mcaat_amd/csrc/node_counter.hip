@@ -90,10 +90,13 @@ __device__ __forceinline__ uint64_t canon_edge(uint64_t lsb, int E) {
 // ballot compaction as {first base, n edges, minimizer hash}; when a segment runs low on
 // room the wave fills in the bases of its entries and the workgroup scatters all segments
 // to the 256 L1 buckets.
+// 4 waves x 900-entry segments: ~52 KB of LDS, so three workgroups (12 waves, the VGPR
+// limit at 145 registers) share a CU and one's flush overlaps two others' scans (C3:
+// 87.6 -> 77.8 ms against 2 x 1500)
 #ifndef MCAAT_AWAVES
 #define MCAAT_AWAVES 4
-#define MCAAT_ASEG 1500
-#define MCAAT_APERCU 2
+#define MCAAT_ASEG 900
+#define MCAAT_APERCU 3
 #endif
 #ifndef MCAAT_HASH
 #define MCAAT_HASH 1
@@ -105,6 +108,9 @@ constexpr int kItem = 127;              // edge positions per work item (the clo
 constexpr int kCk = 8;                  // positions per step
 constexpr int kSeg = MCAAT_ASEG;        // per-wave stage segment (entries); a step appends <= 64*kCk
 constexpr int kStage = kSeg * kAWaves;  // 8-B pre-entries
+static_assert(kAThreads >= 256, "threads < 256 own one L1 bucket each");
+static_assert(kSeg > 64 * kCk, "a segment must hold a worst-case step");
+static_assert(kStage <= 65536, "perm holds 16-bit stage indices");
 
 struct ItemSrc {
     const uint64_t *offsets;
@@ -731,7 +737,10 @@ constexpr int kCapMax = kCap * 85 / 100 - kCWaves * 64;    // distinct edges bef
 constexpr int kDCap = 2048;                                // descriptor slots
 constexpr int kDMax = kDCap * 3 / 4;                       // distinct descriptors before going raw
 constexpr int kDProbe = 128;                               // probe bound of the descriptor table
-constexpr int kCB = 4;                                     // descriptor loads in flight per thread
+#ifndef MCAAT_CB
+#define MCAAT_CB 4
+#endif
+constexpr int kCB = MCAAT_CB;                              // descriptor loads in flight per thread
 constexpr int kDefer = 64;                                 // descriptors with w0 == kEmpty before going raw
 constexpr int kCPerCu = 2;                                 // resident workgroups per CU (LDS, VGPR <= 64)
 #ifndef MCAAT_CSPLIT
