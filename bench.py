@@ -241,7 +241,7 @@ def main() -> int:
             g = M.Graph.build(ctx, reads, k)
             st_build = ctx.stage_times()
         d = g.size
-        res = g.cycle_finder(prm)
+        res = g.cycle_finder(prm, as_arrays=True)  # results copied to host arrays
         st_cf = ctx.stage_times()
         g.free()
         return d, res, {**st_build, **st_cf}

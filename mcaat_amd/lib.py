@@ -486,7 +486,9 @@ class Graph:
         ids = np.ascontiguousarray(ids, dtype=np.uint64)
         _check(self.ctx._lib.mcaat_graph_set_valid(self.h, _ptr(ids, _u64p), ids.size, int(valid)))
 
-    def cycle_finder(self, params: Optional[CfParams] = None) -> CycleResult:
+    def cycle_finder(self, params: Optional[CfParams] = None, as_arrays: bool = False) -> CycleResult:
+        """CycleFinder results in the reference's commit order. as_arrays: each entry is
+        (start, (flat node ids, cycle offsets)) as numpy copies instead of Python lists."""
         p = (params or CfParams()).to_c()
         h = C.c_void_p()
         lib = self.ctx._lib
@@ -501,6 +503,13 @@ class Graph:
                 of = _u64p()
                 nc = C.c_size_t(0)
                 _check(lib.mcaat_cycles_get(h, i, C.byref(s), C.byref(fl), C.byref(of), C.byref(nc)))
+                if as_arrays:
+                    offs_a = np.ctypeslib.as_array(of, shape=(nc.value + 1,)).copy()
+                    n_ids = int(offs_a[-1])
+                    flat_a = (np.ctypeslib.as_array(fl, shape=(n_ids,)).copy() if n_ids
+                              else np.zeros(0, dtype=np.uint64))
+                    res.entries.append((s.value, (flat_a, offs_a)))
+                    continue
                 offs = np.ctypeslib.as_array(of, shape=(nc.value + 1,)).tolist()
                 flat = np.ctypeslib.as_array(fl, shape=(max(offs[-1], 1),))[: offs[-1]].tolist() if offs[-1] else []
                 cycles = [flat[offs[j]:offs[j + 1]] for j in range(nc.value)]
@@ -512,8 +521,12 @@ class Graph:
             ip = _u64p()
             bp = _i32p()
             _check(lib.mcaat_cycles_candidates(h, C.byref(nca), C.byref(ip), C.byref(bp)))
-            res.candidates = [ip[j] for j in range(nca.value)]
-            res.buckets = [bp[j] for j in range(nca.value)]
+            if as_arrays:
+                res.candidates = np.ctypeslib.as_array(ip, shape=(nca.value,)).copy() if nca.value else np.zeros(0, np.uint64)
+                res.buckets = np.ctypeslib.as_array(bp, shape=(nca.value,)).copy() if nca.value else np.zeros(0, np.int32)
+            else:
+                res.candidates = [ip[j] for j in range(nca.value)]
+                res.buckets = [bp[j] for j in range(nca.value)]
             return res
         finally:
             lib.mcaat_cycles_free(h)

@@ -252,3 +252,15 @@ def test_long_peel_chains(gpu_ctx, glen):
     _, _, valid = g.download()
     assert np.array_equal(valid, og.valid())
     assert ores["stats"][2] < og.size // 2  # most of the genome was peeled
+
+
+def test_cycle_results_as_arrays(gpu_ctx):
+    """The bench's array form of the results holds exactly the list form's cycles."""
+    reads = M.Reads.synth(gpu_ctx, M.SynthSpec())
+    a = M.Graph.build(gpu_ctx, reads, 23).cycle_finder(M.CfParams())
+    b = M.Graph.build(gpu_ctx, reads, 23).cycle_finder(M.CfParams(), as_arrays=True)
+    assert len(a.entries) == len(b.entries) and a.stats == b.stats
+    for (s1, cyc), (s2, (flat, offs)) in zip(a.entries, b.entries):
+        assert s1 == s2
+        assert cyc == [flat[offs[j]:offs[j + 1]].tolist() for j in range(len(offs) - 1)]
+    assert list(b.candidates) == a.candidates and list(b.buckets) == a.buckets
