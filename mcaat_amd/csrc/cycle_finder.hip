@@ -201,13 +201,20 @@ __global__ void __launch_bounds__(kBlock) k_peel_walk(PeelArrays pa, const uint6
     }
 }
 
-__global__ void __launch_bounds__(kBlock) k_peel_jump(PeelArrays pa, const uint64_t *list, uint64_t nr) {
+// one pointer-jumping round; *changed is raised when some ruler still pointed at a unary
+// node (a round that changes nothing proves every jump final)
+__global__ void __launch_bounds__(kBlock) k_peel_jump(PeelArrays pa, const uint64_t *list, uint64_t nr, int *changed) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    bool ch = false;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nr; i += stride) {
         const uint64_t r = list[i];
         const uint64_t j = pa.jump[r];
-        if (j != kNone && kind_od(pa.kind[j]) == 1) pa.jump[r] = pa.jump[j];
+        if (j != kNone && kind_od(pa.kind[j]) == 1) {
+            pa.jump[r] = pa.jump[j];
+            ch = true;
+        }
     }
+    if (__ballot(ch) && (threadIdx.x & 63) == 0) *changed = 1;
 }
 
 __device__ __forceinline__ uint8_t peel_res(const PeelArrays &pa, uint64_t y) {
@@ -810,9 +817,19 @@ static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm) {
         int rounds = 2;
         while ((1ULL << rounds) < nr + 1) ++rounds;
         rounds += 1;
+        // log2(nr)+1 rounds bound the chain depth; most inputs converge far earlier, which
+        // a round without changes proves (checked from the fourth round on)
+        DevBuf<int> chg(1);
+        int hchg = 1;
         for (int r = 0; r < rounds; ++r) {
-            hipLaunchKernelGGL(k_peel_jump, dim3(grid_for(nr, kBlock)), dim3(kBlock), 0, st, pa, list.p, nr);
+            if (r >= 4) HIP_OK(hipMemsetAsync(chg.p, 0, 4, st));
+            hipLaunchKernelGGL(k_peel_jump, dim3(grid_for(nr, kBlock)), dim3(kBlock), 0, st, pa, list.p, nr, chg.p);
             LAUNCH_OK();
+            if (r >= 4) {
+                HIP_OK(hipMemcpyAsync(&hchg, chg.p, 4, hipMemcpyDeviceToHost, st));
+                HIP_OK(hipStreamSynchronize(st));
+                if (!hchg) break;
+            }
         }
     }
     DevBuf<uint64_t> blist(D);
@@ -1023,6 +1040,8 @@ struct FcRunner {
                 if (sel_of[j] >= 0) {
                     const uint64_t q = (uint64_t)sel_of[j];
                     for (uint64_t a = noff[q]; a < noff[q + 1]; ++a) {
+                        // random bits of a D-bit map: keep a few misses in flight
+                        if (a + 16 < nodes.size()) __builtin_prefetch(hvis.w + (nodes[a + 16] >> 6), 1);
                         const uint64_t x = nodes[a];
                         if (!hvis.get(x)) {
                             hvis.set(x);
