@@ -185,6 +185,12 @@ int mcaat_cycles_count(const mcaat_cycles *c, size_t *n_entries);
  * n_cycles+1 offsets into it; pointers stay valid until mcaat_cycles_free */
 int mcaat_cycles_get(const mcaat_cycles *c, size_t i, uint64_t *start, const uint64_t **flat,
                      const uint64_t **offsets, size_t *n_cycles);
+/* All entries at once, flattened (bulk consumers): sizes[3] = {entries, cycles, node ids}.
+ * Call with the four arrays NULL to size them; then entry i starts at starts[i], owns cycles
+ * [entry_offsets[i], entry_offsets[i+1]) and cycle q is nodes[cycle_offsets[q] ..
+ * cycle_offsets[q+1]). Same commit order as mcaat_cycles_get. */
+int mcaat_cycles_export(const mcaat_cycles *c, uint64_t *sizes, uint64_t *starts, uint64_t *entry_offsets,
+                        uint64_t *cycle_offsets, uint64_t *nodes);
 /* stats: [0] tips before pruning, [1] invalidated mult<=1, [2] valid after pruning,
  * [3] tips after pruning, [4] start candidates passing DLS, [5] total cycles,
  * [6] FindCycle speculation rounds, [7] FindCycle re-runs after conflicts */

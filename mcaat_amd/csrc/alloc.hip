@@ -8,6 +8,8 @@
 // coalesces neighbouring free segments of a chunk on free, so after the first step the whole
 // pipeline runs inside memory it already owns. On an allocation failure, wholly free chunks
 // are released and the request retried.
+#include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <set>
@@ -112,10 +114,13 @@ void *dev_alloc(size_t bytes) {
     if (void *p = a.take(bytes)) return p;
     size_t chunk = bytes < kMinChunk ? kMinChunk : bytes;
     void *raw = nullptr;
+    static const bool verbose = getenv("MCAAT_VERBOSE") && getenv("MCAAT_VERBOSE")[0] == '1';
+    if (verbose) fprintf(stderr, "[mcaat] arena: new chunk of %zu MiB for a %zu MiB request\n", chunk >> 20, bytes >> 20);
     hipError_t e = hipMalloc(&raw, chunk);
     if (e != hipSuccess) {
         (void)hipGetLastError();
         (void)hipDeviceSynchronize();
+        if (verbose) fprintf(stderr, "[mcaat] arena: hipMalloc failed, trimming free chunks\n");
         a.trim();
         chunk = bytes;
         e = hipMalloc(&raw, chunk);

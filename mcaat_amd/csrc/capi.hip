@@ -5,6 +5,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 
 #include "internal.h"
@@ -702,6 +703,34 @@ int mcaat_cycles_get(const mcaat_cycles *c, size_t i, uint64_t *start, const uin
         if (flat) *flat = c->flat[i].data();
         if (offsets) *offsets = c->offsets[i].data();
         if (n_cycles) *n_cycles = c->offsets[i].size() - 1;
+    });
+}
+
+int mcaat_cycles_export(const mcaat_cycles *c, uint64_t *sizes, uint64_t *starts, uint64_t *entry_offsets,
+                        uint64_t *cycle_offsets, uint64_t *nodes) {
+    return guarded([&] {
+        require(c && sizes, "null argument");
+        const size_t n = c->starts.size();
+        uint64_t ncyc = 0, nnodes = 0;
+        for (size_t i = 0; i < n; ++i) {
+            ncyc += c->offsets[i].size() - 1;
+            nnodes += c->flat[i].size();
+        }
+        sizes[0] = n;
+        sizes[1] = ncyc;
+        sizes[2] = nnodes;
+        if (!starts || !entry_offsets || !cycle_offsets || !nodes) return;  // sizing call
+        uint64_t e = 0, q = 0;
+        entry_offsets[0] = 0;
+        cycle_offsets[0] = 0;
+        for (size_t i = 0; i < n; ++i) {
+            starts[i] = c->starts[i];
+            const auto &of = c->offsets[i];
+            for (size_t j = 1; j < of.size(); ++j) cycle_offsets[++e] = q + of[j];
+            entry_offsets[i + 1] = e;
+            if (!c->flat[i].empty()) memcpy(nodes + q, c->flat[i].data(), 8 * c->flat[i].size());
+            q += c->flat[i].size();
+        }
     });
 }
 

@@ -86,6 +86,7 @@ SIGNATURES = {
         [C.c_void_p, C.c_size_t, _u64p, C.POINTER(_u64p), C.POINTER(_u64p), C.POINTER(C.c_size_t)],
     ),
     "mcaat_cycles_stats": (C.c_int, [C.c_void_p, _u64p]),
+    "mcaat_cycles_export": (C.c_int, [C.c_void_p, _u64p, _u64p, _u64p, _u64p, _u64p]),
     "mcaat_cycles_candidates": (C.c_int, [C.c_void_p, C.POINTER(C.c_size_t), C.POINTER(_u64p), C.POINTER(_i32p)]),
     "mcaat_cycles_free": (None, [C.c_void_p]),
     "mcaat_stage_times": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_char_p), C.POINTER(C.c_double), C.POINTER(C.c_int)]),
@@ -497,19 +498,27 @@ class Graph:
             res = CycleResult()
             n = C.c_size_t(0)
             _check(lib.mcaat_cycles_count(h, C.byref(n)))
-            for i in range(n.value):
+            if as_arrays:  # one bulk copy (mcaat_cycles_export), then per-entry views
+                sz = np.zeros(3, dtype=np.uint64)
+                _check(lib.mcaat_cycles_export(h, _ptr(sz, _u64p), None, None, None, None))
+                ne, nc_all, nn = (int(x) for x in sz)
+                starts = np.zeros(max(ne, 1), dtype=np.uint64)
+                eoff = np.zeros(ne + 1, dtype=np.uint64)
+                coff = np.zeros(nc_all + 1, dtype=np.uint64)
+                nodes = np.zeros(max(nn, 1), dtype=np.uint64)
+                _check(lib.mcaat_cycles_export(h, _ptr(sz, _u64p), _ptr(starts, _u64p), _ptr(eoff, _u64p),
+                                               _ptr(coff, _u64p), _ptr(nodes, _u64p)))
+                for i in range(ne):
+                    c0, c1 = int(eoff[i]), int(eoff[i + 1])
+                    offs_a = coff[c0:c1 + 1] - coff[c0]
+                    flat_a = nodes[int(coff[c0]):int(coff[c1])]
+                    res.entries.append((int(starts[i]), (flat_a, offs_a)))
+            for i in range(0 if as_arrays else n.value):
                 s = C.c_uint64(0)
                 fl = _u64p()
                 of = _u64p()
                 nc = C.c_size_t(0)
                 _check(lib.mcaat_cycles_get(h, i, C.byref(s), C.byref(fl), C.byref(of), C.byref(nc)))
-                if as_arrays:
-                    offs_a = np.ctypeslib.as_array(of, shape=(nc.value + 1,)).copy()
-                    n_ids = int(offs_a[-1])
-                    flat_a = (np.ctypeslib.as_array(fl, shape=(n_ids,)).copy() if n_ids
-                              else np.zeros(0, dtype=np.uint64))
-                    res.entries.append((s.value, (flat_a, offs_a)))
-                    continue
                 offs = np.ctypeslib.as_array(of, shape=(nc.value + 1,)).tolist()
                 flat = np.ctypeslib.as_array(fl, shape=(max(offs[-1], 1),))[: offs[-1]].tolist() if offs[-1] else []
                 cycles = [flat[offs[j]:offs[j + 1]] for j in range(nc.value)]
