@@ -172,7 +172,7 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--reads", type=int, default=0, help="override n_reads")
     ap.add_argument("--cpu-sample-reads", type=int, default=2_000_000)

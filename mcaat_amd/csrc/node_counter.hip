@@ -996,7 +996,15 @@ __global__ void __launch_bounds__(kCThreads, kCPerCu * kCThreads / 256) k_lds_co
         __syncthreads();
         tick(2);
         if (ovf) {
-            if (threadIdx.x == 0) ovf_list[atomicAdd(ovf_n, 1ull)] = (uint32_t)p | (cls << 24) | (lgn << 28);
+            // too many distinct edges for the LDS table: count the partition again as
+            // edge-disjoint classes (shallow or error-rich data); a class that still overflows
+            // goes to the global-table fallback
+            if (lgn == 0) {
+                lgn = kSplitLg;
+                cls = ~0u;
+            } else if (threadIdx.x == 0) {
+                ovf_list[atomicAdd(ovf_n, 1ull)] = (uint32_t)p | (cls << 24) | (lgn << 28);
+            }
             __syncthreads();
             continue;
         }
