@@ -138,6 +138,7 @@ constexpr uint64_t kPad = ~0ULL;
 constexpr uint32_t kCh1 = 32768;      // canonical entries per level-1 chunk (<= 2 items each)
 constexpr uint32_t kCh2 = 65536;      // items per level-2 chunk
 constexpr int kWaveSort = 512;        // largest level-3 bucket sorted by one wave
+constexpr int kMidSort = 2048;        // largest sorted by a 256-thread workgroup (16 KB)
 constexpr int kBlockSort = 16384;     // largest sorted by a 1024-thread workgroup (128 KB)
 
 __device__ __forceinline__ uint32_t round8(uint32_t x) { return (x + kIL - 1) & ~(uint32_t)(kIL - 1); }
@@ -427,24 +428,31 @@ __global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in,
     }
 }
 
-__global__ void __launch_bounds__(1024) k_msd3_block(const uint64_t *in, const uint64_t *off2, const uint64_t *real2,
-                                                     const uint64_t *base3, int k, const uint32_t *big, uint64_t nbig,
-                                                     uint64_t *key, uint16_t *mult, int *too_big) {
-    __shared__ uint64_t s[kBlockSort];
+// one workgroup per listed level-3 bucket of <= CAP items; larger ones are forwarded to the
+// next list (or flagged when there is none: the caller falls back to the radix sort)
+template <int THREADS, int CAP>
+__global__ void __launch_bounds__(THREADS) k_msd3_block(const uint64_t *in, const uint64_t *off2, const uint64_t *real2,
+                                                        const uint64_t *base3, int k, const uint32_t *big, uint64_t nbig,
+                                                        uint64_t *key, uint16_t *mult, uint32_t *fwd,
+                                                        unsigned long long *nfwd, int *too_big) {
+    __shared__ uint64_t s[CAP];
     const int E = k + 1;
     for (uint64_t q = blockIdx.x; q < nbig; q += gridDim.x) {
         const uint64_t b = big[q], lo = off2[b], n = off2[b + 1] - lo;
-        if (n > (uint64_t)kBlockSort) {
-            if (threadIdx.x == 0) *too_big = 1;
+        if (n > (uint64_t)CAP) {
+            if (threadIdx.x == 0) {
+                if (fwd) fwd[atomicAdd(nfwd, 1ull)] = (uint32_t)b;
+                else *too_big = 1;
+            }
             continue;
         }
         uint32_t P = 8;
         while (P < n) P <<= 1;
-        for (uint32_t i = threadIdx.x; i < P; i += 1024) s[i] = i < n ? in[lo + i] : kPad;
+        for (uint32_t i = threadIdx.x; i < P; i += THREADS) s[i] = i < n ? in[lo + i] : kPad;
         __syncthreads();
-        lds_bitonic(s, P, threadIdx.x, 1024, false);
+        lds_bitonic(s, P, threadIdx.x, THREADS, false);
         const uint64_t hi = (b >> kMB) << (2 * E - kMB);
-        msd_emit(s, (uint32_t)real2[b], threadIdx.x, 1024, hi, key, mult, base3[b]);
+        msd_emit(s, (uint32_t)real2[b], threadIdx.x, THREADS, hi, key, mult, base3[b]);
         __syncthreads();
     }
 }
@@ -526,10 +534,25 @@ bool msd_sort(mcaat_ctx *ctx, const uint64_t *ckeys, const uint32_t *ccnt, uint6
     HIP_OK(hipMemcpyAsync(&hb, nbig.p, 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     if (hb) {
-        hipLaunchKernelGGL(k_msd3_block, dim3((unsigned)std::min<uint64_t>(hb, (uint64_t)ctx->n_cu)), dim3(1024), 0, st,
-                           l2.p, off2.p, (const uint64_t *)real2.p, (const uint64_t *)base3.p, k, big.p, (uint64_t)hb,
-                           key, mult, too.p);
+        // mid-size buckets (deep graphs: D / 2^22 above the wave limit) by 256-thread
+        // workgroups, many per CU; the rare larger ones by one 1024-thread workgroup each
+        DevBuf<uint32_t> big2(hb);
+        DevBuf<unsigned long long> nbig2(1);
+        HIP_OK(hipMemsetAsync(nbig2.p, 0, 8, st));
+        hipLaunchKernelGGL((k_msd3_block<256, kMidSort>), dim3((unsigned)std::min<uint64_t>(hb, (uint64_t)ctx->n_cu * 8)),
+                           dim3(256), 0, st, l2.p, off2.p, (const uint64_t *)real2.p, (const uint64_t *)base3.p, k, big.p,
+                           (uint64_t)hb, key, mult, big2.p, nbig2.p, too.p);
         LAUNCH_OK();
+        unsigned long long hb2 = 0;
+        HIP_OK(hipMemcpyAsync(&hb2, nbig2.p, 8, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        if (hb2) {
+            hipLaunchKernelGGL((k_msd3_block<1024, kBlockSort>), dim3((unsigned)std::min<uint64_t>(hb2, (uint64_t)ctx->n_cu)),
+                               dim3(1024), 0, st, l2.p, off2.p, (const uint64_t *)real2.p, (const uint64_t *)base3.p, k,
+                               big2.p, (uint64_t)hb2, key, mult, (uint32_t *)nullptr,
+                               (unsigned long long *)nullptr, too.p);
+            LAUNCH_OK();
+        }
         int h = 0;
         HIP_OK(hipMemcpyAsync(&h, too.p, 4, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
