@@ -738,7 +738,7 @@ constexpr int kDCap = 2048;                                // descriptor slots
 constexpr int kDMax = kDCap * 3 / 4;                       // distinct descriptors before going raw
 constexpr int kDProbe = 128;                               // probe bound of the descriptor table
 #ifndef MCAAT_CB
-#define MCAAT_CB 4
+#define MCAAT_CB 2
 #endif
 constexpr int kCB = MCAAT_CB;                              // descriptor loads in flight per thread
 constexpr int kDefer = 64;                                 // descriptors with w0 == kEmpty before going raw
