@@ -551,7 +551,12 @@ struct FcThread {
 
 // lpw searches per wave: each search is a divergent pointer-chasing state machine, so lanes
 // of one wave serialise each other's branches; few lanes per wave keep searches independent
-__global__ void __launch_bounds__(64) k_findcycle(GraphView g, const uint64_t *visited, const uint64_t *starts,
+// A/B knob: minimum waves per SIMD (6 or 8 force 80 / 64 VGPRs with spills; measured no
+// faster at C3: the kernel's time is its longest search, not its occupancy)
+#ifndef MCAAT_FC_MINW
+#define MCAAT_FC_MINW 1
+#endif
+__global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, const uint64_t *visited, const uint64_t *starts,
                                                   uint64_t n, FcCaps caps, FcParams prm, uint64_t *sbase,
                                                   FcStatus *stat, int lpw) {
     if ((int)threadIdx.x >= lpw) return;
