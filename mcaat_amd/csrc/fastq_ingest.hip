@@ -256,7 +256,8 @@ bool is_space(uint8_t c) { return c == '\n' || c == '\r' || c == ' ' || c == '\t
 size_t fastq_chunk_bytes() {
     if (const char *e = getenv("MCAAT_FASTQ_CHUNK")) {
         const long long v = atoll(e);
-        if (v >= 256) return (size_t)v;
+        // chunk positions are 32-bit: keep chunk + carry reserve well below 4 GiB
+        if (v >= 256) return (size_t)std::min<long long>(v, 1LL << 30);
     }
     return size_t(256) << 20;
 }
