@@ -3,8 +3,8 @@
 // Replaces SDBGBuild::BuildLib / SequenceLibCollection::Build (sdbg_build.cpp:82-115, the
 // MEGAHIT buildlib step) for FASTQ inputs, and builds in the same pass the mapping view that
 // get_reads re-parses the FASTQ for (reads.cpp:20-52, 88-130). The host only moves bytes: a
-// reader thread fills pinned chunks (zlib inflates .gz; plain files are read straight into
-// the chunk), and each chunk is parsed on the GPU:
+// reader task fills pinned chunks (zlib inflates .gz; plain files are copied straight into
+// the chunk by four pread() threads) while the GPU parses the previous chunk:
 //
 //  1. k_fq_nlcount   one lane per 64-byte segment (4 x 16-B loads): number of '\n' bytes
 //                    (SWAR zero-byte count); exclusive scan -> line index per segment.
@@ -31,7 +31,11 @@
 #include <cstring>
 #include <future>
 #include <string>
+#include <fcntl.h>
 #include <sys/stat.h>
+#include <unistd.h>
+
+#include <thread>
 
 #include "internal.h"
 
@@ -249,6 +253,67 @@ size_t read_full(gzFile f, uint8_t *dst, size_t n, const char *path) {
     return got;
 }
 
+// Source of input bytes: zlib for .gz (one inflate stream), parallel pread() for plain
+// files (one thread copies page-cache data at ~13 GB/s; four keep up with PCIe).
+struct Source {
+    gzFile gz = nullptr;
+    int fd = -1;
+    uint64_t off = 0;
+    const char *path;
+    explicit Source(const char *p) : path(p) {
+        unsigned char magic[2] = {0, 0};
+        fd = open(p, O_RDONLY);
+        if (fd < 0) throw Error(MCAAT_E_IO, std::string("cannot open ") + p);
+        const bool is_gz = pread(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b;
+        if (is_gz) {
+            close(fd);
+            fd = -1;
+            gz = gzopen(p, "rb");
+            if (!gz) throw Error(MCAAT_E_IO, std::string("cannot open ") + p);
+            gzbuffer(gz, 1u << 20);
+        } else {
+            posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
+        }
+    }
+    ~Source() {
+        if (gz) gzclose(gz);
+        if (fd >= 0) close(fd);
+    }
+    Source(const Source &) = delete;
+    Source &operator=(const Source &) = delete;
+    size_t read(uint8_t *dst, size_t n) {
+        if (gz) return read_full(gz, dst, n, path);
+        constexpr int kThreads = 4;
+        const size_t piece = (n + kThreads - 1) / kThreads;
+        size_t got[kThreads] = {0, 0, 0, 0};
+        bool err[kThreads] = {false, false, false, false};
+        auto job = [&](int t) {
+            const size_t a = std::min(n, t * piece), b = std::min(n, a + piece);
+            size_t g = 0;
+            while (a + g < b) {
+                const ssize_t r = pread(fd, dst + a + g, b - a - g, (off_t)(off + a + g));
+                if (r < 0) { err[t] = true; break; }
+                if (r == 0) break;
+                g += (size_t)r;
+            }
+            got[t] = g;
+        };
+        std::thread th[kThreads - 1];
+        for (int t = 1; t < kThreads; ++t) th[t - 1] = std::thread(job, t);
+        job(0);
+        for (auto &x : th) x.join();
+        size_t total = 0;
+        for (int t = 0; t < kThreads; ++t) {
+            if (err[t]) throw Error(MCAAT_E_IO, std::string("read error in ") + path);
+            const size_t a = std::min(n, t * piece), b = std::min(n, a + piece);
+            total += got[t];
+            if (got[t] < b - a) break;  // end of file inside piece t: later pieces read nothing
+        }
+        off += total;
+        return total;
+    }
+};
+
 bool is_space(uint8_t c) { return c == '\n' || c == '\r' || c == ' ' || c == '\t'; }
 
 }  // namespace
@@ -298,16 +363,10 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
     } meta_free{hmeta};
 
     for (int fi = 0; fi < n_files; ++fi) {
-        gzFile f = gzopen(files[fi], "rb");
-        if (!f) throw Error(MCAAT_E_IO, std::string("cannot open ") + files[fi]);
-        struct Closer {
-            gzFile f;
-            ~Closer() { gzclose(f); }
-        } closer{f};
-        gzbuffer(f, 1u << 20);
+        Source src(files[fi]);
         int cur = 0;
         size_t carry = 0;
-        size_t n = read_full(f, hb[cur] + R, CH, files[fi]);
+        size_t n = src.read(hb[cur] + R, CH);
         bool eof = n < CH;
         bool first_chunk = true;
         for (;;) {
@@ -324,8 +383,7 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
             std::future<size_t> next;
             if (!eof) {
                 uint8_t *dst = hb[cur ^ 1] + R;
-                const char *path = files[fi];
-                next = std::async(std::launch::async, [f, dst, CH, path] { return read_full(f, dst, CH, path); });
+                next = std::async(std::launch::async, [&src, dst, CH] { return src.read(dst, CH); });
             }
             // ---- newline passes
             const uint32_t nseg = (uint32_t)((total + kSeg - 1) / kSeg);
