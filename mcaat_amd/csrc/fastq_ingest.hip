@@ -349,7 +349,24 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
 
     Pinned h0(cap), h1(cap);
     uint8_t *hb[2] = {h0.p, h1.p};
-    DevBuf<uint8_t> dbuf(cap);
+    DevBuf<uint8_t> dbufs[2];
+    dbufs[0].alloc(cap);
+    dbufs[1].alloc(cap);
+    struct CopyStream {  // uploads overlap the parse of the previous chunk
+        hipStream_t s = nullptr;
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        CopyStream() {
+            HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+            for (auto &e : ev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
+        ~CopyStream() {
+            if (s) (void)hipStreamSynchronize(s);
+            for (auto &e : ev)
+                if (e) (void)hipEventDestroy(e);
+            if (s) (void)hipStreamDestroy(s);
+        }
+    } cs;
+    hipEvent_t *up_ev = cs.ev;
     const uint64_t max_seg = cap / kSeg + 1;
     DevBuf<uint32_t> cnt(max_seg + 1), first(max_seg + 1), nl(cap + 16);  // every byte may be a newline
     DevBuf<uint32_t> sbeg, slen, nbase, nrun, boff, roff, qoff;
@@ -362,41 +379,50 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
         ~MetaFree() { (void)hipHostFree(p); }
     } meta_free{hmeta};
 
+    // chunk x: host bytes [start, start+total) of hb[x] (carry + new data, blank lines trimmed
+    // at the file's ends) uploaded on the copy stream into dbufs[x]; up_ev[x] marks completion
+    auto prepare = [&](int x, size_t carry_x, size_t n_x, bool eof_x, bool first_x, uint8_t *&start_x,
+                       size_t &total_x) {
+        start_x = hb[x] + R - carry_x;
+        total_x = carry_x + n_x;
+        if (first_x)  // leading blank lines
+            while (total_x && is_space(*start_x)) ++start_x, --total_x;
+        if (eof_x) {  // trailing blank lines; the last line gets its newline
+            while (total_x && is_space(start_x[total_x - 1])) --total_x;
+            if (total_x) start_x[total_x++] = '\n';
+        }
+        if (total_x) {
+            const size_t padded = (total_x + kSeg - 1) / kSeg * kSeg + kSeg;
+            HIP_OK(hipMemcpyAsync(dbufs[x].p, start_x, total_x, hipMemcpyHostToDevice, cs.s));
+            HIP_OK(hipMemsetAsync(dbufs[x].p + total_x, 0, padded - total_x, cs.s));
+            HIP_OK(hipEventRecord(up_ev[x], cs.s));
+        }
+    };
     for (int fi = 0; fi < n_files; ++fi) {
         Source src(files[fi]);
         int cur = 0;
-        size_t carry = 0;
         size_t n = src.read(hb[cur] + R, CH);
         bool eof = n < CH;
-        bool first_chunk = true;
+        uint8_t *start = nullptr;
+        size_t total = 0;
+        prepare(cur, 0, n, eof, true, start, total);
+        std::future<size_t> next;
+        if (!eof) {
+            uint8_t *dst = hb[cur ^ 1] + R;
+            next = std::async(std::launch::async, [&src, dst, CH] { return src.read(dst, CH); });
+        }
         for (;;) {
-            uint8_t *start = hb[cur] + R - carry;
-            size_t total = carry + n;
-            if (first_chunk) {  // leading blank lines
-                while (total && is_space(*start)) ++start, --total;
-                first_chunk = false;
-            }
-            if (eof) {  // trailing blank lines; the last line gets its newline
-                while (total && is_space(start[total - 1])) --total;
-                if (total) start[total++] = '\n';
-            }
-            std::future<size_t> next;
-            if (!eof) {
-                uint8_t *dst = hb[cur ^ 1] + R;
-                next = std::async(std::launch::async, [&src, dst, CH] { return src.read(dst, CH); });
-            }
-            // ---- newline passes
+            // ---- newline passes (after this chunk's upload)
             const uint32_t nseg = (uint32_t)((total + kSeg - 1) / kSeg);
             if (total) {
-                KernelTimer kt(ctx, "fq_parse", 3.0 * (double)total);
-                HIP_OK(hipMemcpyAsync(dbuf.p, start, total, hipMemcpyHostToDevice, ctx->stream));
-                HIP_OK(hipMemsetAsync(dbuf.p + total, 0, (size_t)nseg * kSeg + kSeg - total, ctx->stream));
+                HIP_OK(hipStreamWaitEvent(ctx->stream, up_ev[cur], 0));
+                KernelTimer kt(ctx, "fq_parse", 2.0 * (double)total);
                 HIP_OK(hipMemsetAsync(cnt.p + nseg, 0, 4, ctx->stream));
-                hipLaunchKernelGGL(k_fq_nlcount, dim3(grid_for(nseg, kBlock)), dim3(kBlock), 0, ctx->stream, dbuf.p,
-                                   nseg, cnt.p);
+                hipLaunchKernelGGL(k_fq_nlcount, dim3(grid_for(nseg, kBlock)), dim3(kBlock), 0, ctx->stream,
+                                   dbufs[cur].p, nseg, cnt.p);
                 scan_u32(ctx, cnt.p, first.p, (uint64_t)nseg + 1, tmp);
-                hipLaunchKernelGGL(k_fq_nlpos, dim3(grid_for(nseg, kBlock)), dim3(kBlock), 0, ctx->stream, dbuf.p,
-                                   nseg, first.p, nl.p);
+                hipLaunchKernelGGL(k_fq_nlpos, dim3(grid_for(nseg, kBlock)), dim3(kBlock), 0, ctx->stream,
+                                   dbufs[cur].p, nseg, first.p, nl.p);
                 HIP_OK(hipMemcpyAsync(hmeta, first.p + nseg, 4, hipMemcpyDeviceToHost, ctx->stream));
                 HIP_OK(hipStreamSynchronize(ctx->stream));
                 kt.stop();
@@ -414,6 +440,23 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
             if (!eof && total - consumed > R)
                 throw Error(MCAAT_E_IO, std::string("FASTQ record longer than the chunk reserve (") +
                                             std::to_string(R) + " bytes): " + files[fi]);
+            // ---- the next chunk: its carry is known now, so it uploads while this chunk's
+            // records are parsed; this chunk's host buffer is free again for the reader
+            const bool have_next = !eof;
+            uint8_t *nstart = nullptr;
+            size_t ntotal = 0;
+            bool neof = true;
+            if (have_next) {
+                const size_t nn = next.get();
+                neof = nn < CH;
+                const size_t ncarry = total - consumed;
+                memcpy(hb[cur ^ 1] + R - ncarry, start + consumed, ncarry);
+                prepare(cur ^ 1, ncarry, nn, neof, false, nstart, ntotal);
+                if (!neof) {
+                    uint8_t *dst = hb[cur] + R;
+                    next = std::async(std::launch::async, [&src, dst, CH] { return src.read(dst, CH); });
+                }
+            }
             // ---- records
             if (nrec) {
                 KernelTimer kt(ctx, "fq_records", (double)consumed + 16.0 * nrec);
@@ -423,7 +466,7 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
                 }
                 HIP_OK(hipMemsetAsync(meta.p, 0, 4, ctx->stream));
                 for (auto *b : {&nbase, &nrun, &slen}) HIP_OK(hipMemsetAsync(b->p + nrec, 0, 4, ctx->stream));
-                hipLaunchKernelGGL(k_fq_records, dim3(grid_for(nrec, kBlock)), dim3(kBlock), 0, ctx->stream, dbuf.p,
+                hipLaunchKernelGGL(k_fq_records, dim3(grid_for(nrec, kBlock)), dim3(kBlock), 0, ctx->stream, dbufs[cur].p,
                                    nl.p, nrec, sbeg.p, slen.p, nbase.p, nrun.p, meta.p);
                 scan_u32(ctx, nbase.p, boff.p, (uint64_t)nrec + 1, tmp);
                 scan_u32(ctx, nrun.p, roff.p, (uint64_t)nrec + 1, tmp);
@@ -443,7 +486,7 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
                 grow(ctx, qpacked, (q_bases + 31) / 32 + 1, (q_bases + cq + 31) / 32 + 17);
                 grow(ctx, qoffsets, n_rec + 1, n_rec + nrec + 2);
                 KernelTimer ke(ctx, "fq_emit", (double)consumed + 0.5 * (double)(cb + cq) + 8.0 * (cr + nrec));
-                hipLaunchKernelGGL(k_fq_emit, dim3(grid_for(nrec, kBlock)), dim3(kBlock), 0, ctx->stream, dbuf.p, nrec,
+                hipLaunchKernelGGL(k_fq_emit, dim3(grid_for(nrec, kBlock)), dim3(kBlock), 0, ctx->stream, dbufs[cur].p, nrec,
                                    sbeg.p, slen.p, boff.p, roff.p, qoff.p, n_bases, n_reads, q_bases, n_rec, fi > 0 ? 1 : 0,
                                    packed.p, offsets.p, qpacked.p, qoffsets.p);
                 HIP_OK(hipGetLastError());
@@ -453,12 +496,11 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
                 q_bases += cq;
                 n_rec += nrec;
             }
-            if (eof) break;
-            n = next.get();
-            eof = n < CH;
-            carry = total - consumed;
-            memcpy(hb[cur ^ 1] + R - carry, start + consumed, carry);
+            if (!have_next) break;
             cur ^= 1;
+            start = nstart;
+            total = ntotal;
+            eof = neof;
         }
     }
     HIP_OK(hipStreamSynchronize(ctx->stream));
