@@ -104,6 +104,47 @@ __device__ __forceinline__ uint32_t map_code(uint8_t c) { return c == 'A' ? 0 : 
 // complement then code (reverse_pair_ends_sequence, reads.cpp:20-31: only A/C/G/T change)
 __device__ __forceinline__ uint32_t map_code_rc(uint8_t c) { return c == 'T' ? 0 : c == 'G' ? 1 : c == 'C' ? 2 : 3; }
 
+// a lane's sequential byte readers over the chunk (4-byte aligned loads instead of one load
+// per byte; the chunk buffer is 256-B aligned and padded, so reading up to 3 bytes past the
+// end is in bounds)
+struct Fwd {
+    const uint32_t *w;
+    uint32_t cur;
+    int avail;
+    __device__ Fwd(const uint8_t *buf, uint32_t pos) {
+        w = reinterpret_cast<const uint32_t *>(buf + (pos & ~3u));
+        cur = *w++ >> (8 * (pos & 3));
+        avail = 4 - (int)(pos & 3);
+    }
+    __device__ __forceinline__ uint8_t next() {
+        if (!avail) {
+            cur = *w++;
+            avail = 4;
+        }
+        const uint8_t c = (uint8_t)cur;
+        cur >>= 8;
+        --avail;
+        return c;
+    }
+};
+struct Bwd {  // from pos downwards
+    const uint32_t *w;
+    uint32_t cur;
+    int idx;
+    __device__ Bwd(const uint8_t *buf, uint32_t pos) {
+        w = reinterpret_cast<const uint32_t *>(buf + (pos & ~3u));
+        cur = *w;
+        idx = (int)(pos & 3);
+    }
+    __device__ __forceinline__ uint8_t next() {
+        if (idx < 0) {
+            cur = *--w;
+            idx = 3;
+        }
+        return (uint8_t)(cur >> (8 * idx--));
+    }
+};
+
 enum : uint32_t { kBadHeader = 1, kDiffer = 2 };
 
 // per record: sequence start, length, counting-view bases and runs
@@ -119,8 +160,9 @@ __global__ void k_fq_records(const uint8_t *buf, const uint32_t *nl, uint32_t n_
         if (e > s && buf[e - 1] == '\r') --e;
         uint32_t bases = 0, runs = 0;
         bool in = false, differ = false;
+        Fwd rd(buf, s);
         for (uint32_t i = s; i < e; ++i) {
-            const uint8_t c = buf[i];
+            const uint8_t c = rd.next();
             if (count_code(c) >= 0) {
                 ++bases;
                 runs += !in;
@@ -172,14 +214,15 @@ __global__ void k_fq_emit(const uint8_t *buf, uint32_t n_rec, const uint32_t *sb
                           uint64_t *offsets, uint64_t *qpacked, uint64_t *qoffsets) {
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < n_rec; r += stride) {
-        const uint8_t *s = buf + sbeg[r];
+        const uint32_t sb = sbeg[r];
         const uint32_t L = slen[r];
         // counting view: maximal ACGT runs are reads
         PackWriter pw(packed, g_base + boff[r]);
         uint64_t ri = g_read + roff[r];
         bool in = false;
+        Fwd rd(buf, sb);
         for (uint32_t i = 0; i < L; ++i) {
-            const int b = count_code(s[i]);
+            const int b = count_code(rd.next());
             if (b >= 0) {
                 pw.put((uint32_t)b);
                 in = true;
@@ -194,9 +237,11 @@ __global__ void k_fq_emit(const uint8_t *buf, uint32_t n_rec, const uint32_t *sb
         if (qpacked) {
             PackWriter qw(qpacked, g_qbase + qoff[r]);
             if (!reverse) {
-                for (uint32_t i = 0; i < L; ++i) qw.put(map_code(s[i]));
-            } else {
-                for (uint32_t i = L; i-- > 0;) qw.put(map_code_rc(s[i]));
+                Fwd rq(buf, sb);
+                for (uint32_t i = 0; i < L; ++i) qw.put(map_code(rq.next()));
+            } else if (L) {
+                Bwd rq(buf, sb + L - 1);
+                for (uint32_t i = 0; i < L; ++i) qw.put(map_code_rc(rq.next()));
             }
             qw.finish();
             qoffsets[1 + g_rec + r] = qw.pos;
@@ -254,7 +299,7 @@ size_t read_full(gzFile f, uint8_t *dst, size_t n, const char *path) {
 }
 
 // Source of input bytes: zlib for .gz (one inflate stream), parallel pread() for plain
-// files (one thread copies page-cache data at ~13 GB/s; four keep up with PCIe).
+// files (one thread copies page-cache data at ~13 GB/s; four reach 20-30 GB/s end to end).
 struct Source {
     gzFile gz = nullptr;
     int fd = -1;
@@ -283,10 +328,10 @@ struct Source {
     Source &operator=(const Source &) = delete;
     size_t read(uint8_t *dst, size_t n) {
         if (gz) return read_full(gz, dst, n, path);
-        constexpr int kThreads = 4;
+        constexpr int kThreads = 4;  // 8 measured slower (18.9 vs 23-25 GB/s)
         const size_t piece = (n + kThreads - 1) / kThreads;
-        size_t got[kThreads] = {0, 0, 0, 0};
-        bool err[kThreads] = {false, false, false, false};
+        size_t got[kThreads] = {};
+        bool err[kThreads] = {};
         auto job = [&](int t) {
             const size_t a = std::min(n, t * piece), b = std::min(n, a + piece);
             size_t g = 0;
