@@ -144,6 +144,11 @@ def measure_ingest(ctx, spec, n_reads: int) -> dict:
             f.write(rec.tobytes())
         size = os.path.getsize(path)
         del rec
+        # the first call also allocates the reader's pinned chunks and device buffers (kept on
+        # the context); the second is the steady-state rate
+        t0 = time.perf_counter()
+        M.Reads.from_fastx(ctx, [path]).free()
+        first = time.perf_counter() - t0
         ctx.reset_timing()
         t0 = time.perf_counter()
         r = M.Reads.from_fastx(ctx, [path])
@@ -162,10 +167,10 @@ def measure_ingest(ctx, spec, n_reads: int) -> dict:
     finally:
         os.unlink(path)
     return {
-        "reads": n_reads, "file_bytes": size, "wall_s": round(wall, 3),
+        "reads": n_reads, "file_bytes": size, "wall_s": round(wall, 3), "first_call_s": round(first, 3),
         "text_GBps": round(size / wall / 1e9, 2), "reads_per_s": n_reads / wall,
         "gpu_parse_ms": round(gpu_ms, 3), "kernels": kern, "library_matches": ok,
-        "note": "page-cached plain FASTQ; wall includes host read, PCIe upload and GPU parse",
+        "note": "page-cached plain FASTQ, second call on the context; wall includes host read, PCIe upload and GPU parse",
     }
 
 def main() -> int:

@@ -301,6 +301,8 @@ void mcaat_finalize(mcaat_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     mcaat::dev_trim();
+    for (auto *&p : ctx->pinned)
+        if (p) (void)hipHostFree(p);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

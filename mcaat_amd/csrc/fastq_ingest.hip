@@ -273,16 +273,6 @@ void grow(mcaat_ctx *ctx, DevBuf<uint64_t> &b, uint64_t used, uint64_t need) {
     b = std::move(nb);
 }
 
-struct Pinned {
-    uint8_t *p = nullptr;
-    explicit Pinned(size_t n) { HIP_OK(hipHostMalloc((void **)&p, n, hipHostMallocDefault)); }
-    ~Pinned() {
-        if (p) (void)hipHostFree(p);
-    }
-    Pinned(const Pinned &) = delete;
-    Pinned &operator=(const Pinned &) = delete;
-};
-
 size_t read_full(gzFile f, uint8_t *dst, size_t n, const char *path) {
     size_t got = 0;
     while (got < n) {
@@ -392,8 +382,16 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
     uint64_t n_bases = 0, n_reads = 0, q_bases = 0, n_rec = 0;
     uint32_t flags_all = 0;
 
-    Pinned h0(cap), h1(cap);
-    uint8_t *hb[2] = {h0.p, h1.p};
+    if (ctx->pinned_bytes < cap) {
+        for (auto *&p : ctx->pinned) {
+            if (p) (void)hipHostFree(p);
+            p = nullptr;
+        }
+        ctx->pinned_bytes = 0;
+        for (auto *&p : ctx->pinned) HIP_OK(hipHostMalloc((void **)&p, cap, hipHostMallocDefault));
+        ctx->pinned_bytes = cap;
+    }
+    uint8_t *hb[2] = {ctx->pinned[0], ctx->pinned[1]};
     DevBuf<uint8_t> dbufs[2];
     dbufs[0].alloc(cap);
     dbufs[1].alloc(cap);

@@ -119,6 +119,10 @@ struct mcaat_ctx {
     // pages (random bit probes over ~D/8 bytes), faulted in once; each call zeroes only the
     // words it touched
     mcaat::HostPool host_bits;
+    // pinned staging chunks of the FASTQ reader, kept between calls (hipHostMalloc of a few
+    // hundred MB costs more than parsing a small file); freed by mcaat_finalize
+    uint8_t *pinned[2] = {nullptr, nullptr};
+    size_t pinned_bytes = 0;
 };
 
 struct mcaat_reads {
