@@ -112,6 +112,9 @@ int mcaat_graph_info(const mcaat_graph *g, int *k, uint64_t *n_edges);
 /* Host view for the SDBG mirror (MEGAHIT SDBG API subset):
  * BOSS keys, multiplicities and one valid byte per edge (any pointer may be NULL). */
 int mcaat_graph_download(const mcaat_graph *g, uint64_t *keys, uint16_t *mult, uint8_t *valid);
+/* the same for edges [first, first+count) (paged host views of graphs larger than host RAM) */
+int mcaat_graph_download_range(const mcaat_graph *g, uint64_t first, uint64_t count, uint64_t *keys, uint16_t *mult,
+                               uint8_t *valid);
 /* Keeps device valid bits coherent with host SetInvalidEdge/SetValidEdge
  * (spacer_ordering.cpp:96-138 mutates them downstream). */
 int mcaat_graph_set_valid(mcaat_graph *g, const uint64_t *ids, size_t n, int valid);
@@ -208,6 +211,26 @@ int mcaat_stage_times(const mcaat_ctx *ctx, int max, const char **names, double 
 int mcaat_kernel_timing(const mcaat_ctx *ctx, const char *kernel, double *avg_ms, uint64_t *launches,
                         double *bytes_per_launch);
 void mcaat_reset_timing(mcaat_ctx *ctx);
+
+/* ---- tuning / test knobs ----------------------------------------------------------
+ * Replaces: nothing in the reference. Size limits that decide which code path a stage takes
+ * (results never depend on them), so small parity inputs can reach the branches that
+ * otherwise only run at C2/C3 scale. value < 0 restores the default. Known names:
+ *   nc.group_budget    descriptors per pass-B/C group of L1 buckets (multi-group counting)
+ *   nc.fallback_budget occurrences per global-table fallback batch
+ *   nc.out_cap         initial capacity of the count output (regrowth + recount)
+ *   nc.l1_slots        first-attempt capacity of each L1 bucket (pass A resize + re-run)
+ *   nc.fine_bits       log2 fine partitions (8..19)
+ *   nc.edge_cap        distinct edges per LDS partition before the class split / fallback
+ *   nc.desc_cap        distinct super-k-mers per LDS partition before the class split / raw path
+ *   sort.msd           0: radix sort only, 1: MSD sort whenever k <= 28 (default: D >= 2^16)
+ *   sort.wave_limit / sort.mid_limit / sort.block_limit   level-3 bucket size limits of the
+ *                      one-wave, 256-thread and 1024-thread LDS sorts (above the last: radix)
+ *   cf.dls_stack / cf.dls_visited   initial DepthLevelSearch scratch (grows x8 on overflow)
+ *   cf.fc_lock / cf.fc_relax / cf.fc_out   initial FindCycle scratch (grows on overflow)
+ *   cf.fc_window       initial FindCycle speculation window
+ *   cf.walk_budget     steps of a counter-driven peel walk before the list-ranking peel */
+int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value);
 
 #ifdef __cplusplus
 }

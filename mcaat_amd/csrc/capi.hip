@@ -595,6 +595,27 @@ int mcaat_graph_download(const mcaat_graph *g, uint64_t *keys, uint16_t *mult, u
     });
 }
 
+int mcaat_graph_download_range(const mcaat_graph *g, uint64_t first, uint64_t count, uint64_t *keys, uint16_t *mult,
+                               uint8_t *valid) {
+    return guarded([&] {
+        require(g != nullptr, "null argument");
+        require(first <= g->D && count <= g->D - first, "edge range out of bounds");
+        if (!count) return;
+        HIP_OK(hipSetDevice(g->ctx->device));
+        if (keys) HIP_OK(hipMemcpy(keys, g->key.p + first, 8 * count, hipMemcpyDeviceToHost));
+        if (mult) HIP_OK(hipMemcpy(mult, g->mult.p + first, 2 * count, hipMemcpyDeviceToHost));
+        if (valid) {
+            const uint64_t w0 = first / 64, w1 = (first + count + 63) / 64;
+            std::vector<uint64_t> bits(w1 - w0);
+            HIP_OK(hipMemcpy(bits.data(), g->valid.p + w0, 8 * (w1 - w0), hipMemcpyDeviceToHost));
+            for (uint64_t i = 0; i < count; ++i) {
+                const uint64_t e = first + i;
+                valid[i] = (uint8_t)((bits[e / 64 - w0] >> (e & 63)) & 1);
+            }
+        }
+    });
+}
+
 int mcaat_graph_set_valid(mcaat_graph *g, const uint64_t *ids, size_t n, int valid) {
     return guarded([&] {
         require(g && (ids || n == 0), "null argument");
@@ -783,6 +804,22 @@ int mcaat_kernel_timing(const mcaat_ctx *ctx, const char *kernel, double *avg_ms
 
 void mcaat_reset_timing(mcaat_ctx *ctx) {
     if (ctx) ctx->kstats.clear();
+}
+
+int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value) {
+    static const char *const known[] = {
+        "nc.group_budget", "nc.fallback_budget", "nc.out_cap", "nc.l1_slots", "nc.fine_bits",
+        "nc.edge_cap",     "nc.desc_cap",        "sort.msd",   "sort.wave_limit", "sort.mid_limit",
+        "sort.block_limit", "cf.dls_stack",      "cf.dls_visited", "cf.fc_lock", "cf.fc_relax",
+        "cf.fc_out",       "cf.fc_window",       "cf.walk_budget"};
+    return guarded([&] {
+        require(ctx && name, "null argument");
+        bool ok = false;
+        for (const char *k : known) ok = ok || strcmp(k, name) == 0;
+        if (!ok) throw Error(MCAAT_E_INVALID, std::string("unknown knob: ") + name);
+        if (value < 0) ctx->knobs.erase(name);
+        else ctx->knobs[name] = value;
+    });
 }
 
 }  // extern "C"

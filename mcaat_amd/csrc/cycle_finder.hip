@@ -870,8 +870,8 @@ static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm) {
 // frontier seeds the parallel ruler/list-ranking peel, whose fixpoint from this state is
 // the same (every pending node is valid, has no valid successor and must be removed).
 static void run_peel(mcaat_graph *g, const uint64_t *seed_bm) {
-    constexpr uint32_t kBudget = 512;
     mcaat_ctx *ctx = g->ctx;
+    const uint32_t kBudget = (uint32_t)std::max<int64_t>(1, knob(ctx, "cf.walk_budget", 512));
     hipStream_t st = ctx->stream;
     const uint64_t D = g->D, nw = g->n_words();
     if (!D) return;
@@ -913,7 +913,8 @@ static std::vector<uint64_t> run_dls(mcaat_graph *g, const std::vector<uint64_t>
     std::vector<int8_t> res(cand.size(), -1);
     std::vector<uint64_t> todo(cand.size());
     for (size_t i = 0; i < cand.size(); ++i) todo[i] = i;
-    uint32_t cs = 1024, cv = 2048;
+    uint32_t cs = (uint32_t)std::max<int64_t>(1, knob(ctx, "cf.dls_stack", 1024));
+    uint32_t cv = (uint32_t)next_pow2((uint64_t)std::max<int64_t>(2, knob(ctx, "cf.dls_visited", 2048)));
     while (!todo.empty()) {
         const uint64_t batch_cap = std::max<uint64_t>(64, (512ULL << 20) / (8ULL * (cs + cv)));
         std::vector<uint64_t> next;
@@ -965,10 +966,12 @@ struct FcRunner {
         prm.cluster = p.cluster_bound;
         prm.step_cap = p.step_cap;
         caps.P = (uint32_t)std::max(4, p.cycle_max_length + 2);
-        caps.CL = 4096;
-        caps.CR = 2048;
+        const mcaat_ctx *ctx = gr->ctx;
+        caps.CL = (uint32_t)next_pow2((uint64_t)std::max<int64_t>(4, knob(ctx, "cf.fc_lock", 4096)));
+        caps.CR = (uint32_t)std::max<int64_t>(1, knob(ctx, "cf.fc_relax", 2048));
         caps.CC = (uint32_t)std::max(1, p.cluster_bound);
         caps.CO = (uint32_t)std::max<uint64_t>(caps.P, (uint64_t)caps.CC * (caps.P - 1));
+        if (const int64_t co = knob(ctx, "cf.fc_out", 0)) caps.CO = (uint32_t)co;
         dvis.alloc(gr->n_words());
         HIP_OK(hipMemsetAsync(dvis.p, 0, dvis.bytes(), gr->ctx->stream));
     }
@@ -981,7 +984,7 @@ struct FcRunner {
     void run_bucket(const std::vector<uint64_t> &bucket) {
         hipStream_t st = g->ctx->stream;
         std::vector<uint64_t> pending(bucket);
-        uint64_t window = 8192;
+        uint64_t window = (uint64_t)std::max<int64_t>(1, knob(g->ctx, "cf.fc_window", 8192));
         while (!pending.empty()) {
             // starts already visited are skipped by the reference (:476) -> no entry
             std::vector<uint64_t> keep;

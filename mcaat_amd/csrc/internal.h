@@ -123,6 +123,9 @@ struct mcaat_ctx {
     // hundred MB costs more than parsing a small file); freed by mcaat_finalize
     uint8_t *pinned[2] = {nullptr, nullptr};
     size_t pinned_bytes = 0;
+    // tuning/test knobs (mcaat_set_knob): size limits that decide which code path a stage
+    // takes, so small parity inputs can drive the branches that only large inputs reach
+    std::map<std::string, int64_t> knobs;
 };
 
 struct mcaat_reads {
@@ -228,6 +231,12 @@ struct KernelTimer {
         if (b) (void)hipEventDestroy(b);
     }
 };
+
+// value of a knob set with mcaat_set_knob, or the default
+inline int64_t knob(const mcaat_ctx *ctx, const char *name, int64_t dflt) {
+    auto it = ctx->knobs.find(name);
+    return it == ctx->knobs.end() ? dflt : it->second;
+}
 
 inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 65535u * 16) {
     uint64_t g = (n + block - 1) / block;

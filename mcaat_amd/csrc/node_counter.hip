@@ -774,7 +774,8 @@ __global__ void __launch_bounds__(kCThreads, kCPerCu * kCThreads / 256) k_lds_co
                                                          uint64_t F, int E,
                                                          uint64_t *out_keys, uint32_t *out_cnt, uint64_t out_cap,
                                                          unsigned long long *out_cursor, uint32_t *ovf_list,
-                                                         unsigned long long *ovf_n, unsigned long long *prof) {
+                                                         unsigned long long *ovf_n, uint32_t cap_max, uint32_t dmax,
+                                                         unsigned long long *prof) {
     // The descriptor table (phase 1) and the edge table (phases 2-3) share one LDS region:
     // between the phases each thread keeps its two descriptor slots in registers. 48 KB per
     // workgroup, so two 1024-thread workgroups share a CU and one's loads overlap the other's
@@ -818,7 +819,7 @@ __global__ void __launch_bounds__(kCThreads, kCPerCu * kCThreads / 256) k_lds_co
                 const unsigned long long prev = atomicCAS(&keys[h], kEmpty, (unsigned long long)c);
                 if (prev == kEmpty) {
                     atomicAdd(&cnt[h], weight);
-                    if (atomicAdd(&n_distinct, 1u) + 1 > (uint32_t)kCapMax) ovf = 1;
+                    if (atomicAdd(&n_distinct, 1u) + 1 > cap_max) ovf = 1;
                     return;
                 }
                 if (prev == c) {
@@ -872,7 +873,7 @@ __global__ void __launch_bounds__(kCThreads, kCPerCu * kCThreads / 256) k_lds_co
                     k1 = atomicCAS(&dk1[h], kEmpty, (unsigned long long)w1);
                     if (k1 == kEmpty) {
                         k1 = w1;
-                        if (atomicAdd(&n_ddistinct, 1u) + 1 > (uint32_t)kDMax) dovf = 1;
+                        if (atomicAdd(&n_ddistinct, 1u) + 1 > dmax) dovf = 1;
                     }
                 }
                 if (k1 != w1) continue;
@@ -1263,6 +1264,7 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     // ~1K distinct descriptors after the collapse)
     int fine_bits = 0;
     while ((1ULL << (fine_bits + 1)) * 8192ULL <= n_occ) ++fine_bits;
+    fine_bits = (int)knob(ctx, "nc.fine_bits", fine_bits);
     fine_bits = std::max(8, std::min(19, fine_bits));  // l2_bits <= 11: k_l2_scatter's line buffers
     P.l2_bits = fine_bits - 8;
     const uint32_t S = 1u << P.l2_bits;
@@ -1276,6 +1278,8 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     // + one partially used reservation per (workgroup, bucket)
     const uint64_t a_grid = (uint64_t)kAPerCu * ctx->n_cu;
     for (int b = 0; b < 256; ++b) cap[b] = (est / 256 + 2 * a_grid * kMini + 7) & ~7ull;  // 16-B aligned sub rows
+    if (const int64_t fixed = knob(ctx, "nc.l1_slots", 0))  // test knob: undersize -> resize and re-run
+        for (int b = 0; b < 256; ++b) cap[b] = ((uint64_t)fixed + 7) & ~7ull;
     DevBuf<uint64_t> dcap(256), dbase(257);
     DevBuf<unsigned long long> dcur(256);
     DevBuf<uint4> l1;
@@ -1362,7 +1366,8 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     const uint64_t n_live = hfine[F];
     verbose_mark(ctx, "node_counter.B_hist");
 
-    uint64_t out_cap = std::max<uint64_t>(n_occ / 32, 1u << 20);
+    uint64_t out_cap = (uint64_t)knob(ctx, "nc.out_cap", (int64_t)std::max<uint64_t>(n_occ / 32, 1u << 20));
+    if (out_cap < 1) out_cap = 1;
     out.keys.alloc(out_cap);
     out.counts.alloc(out_cap);
     DevBuf<unsigned long long> dcnt(4);
@@ -1370,7 +1375,10 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     DevBuf<uint32_t> ovf_list(F << kSplitLg);  // one entry per (partition, class)
     static const bool prof_c = getenv("MCAAT_PROF_C") && getenv("MCAAT_PROF_C")[0] == '1';
     if (prof_c) HIP_OK(hipMemsetAsync(dprof.p, 0, dprof.bytes(), st));
-    const uint64_t group_budget = std::max<uint64_t>(n_live / 4 + 1, 1ULL << 28);  // descriptors per group
+    const uint64_t group_budget =
+        (uint64_t)knob(ctx, "nc.group_budget", (int64_t)std::max<uint64_t>(n_live / 4 + 1, 1ULL << 28));  // descriptors per group
+    const uint32_t cap_max = (uint32_t)std::min<int64_t>(kCapMax, std::max<int64_t>(1, knob(ctx, "nc.edge_cap", kCapMax)));
+    const uint32_t dmax = (uint32_t)std::min<int64_t>(kDMax, std::max<int64_t>(1, knob(ctx, "nc.desc_cap", kDMax)));
     uint64_t n_out = 0;
     for (int b0 = 0; b0 < 256;) {
         int b1 = b0 + 1;
@@ -1395,7 +1403,7 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
                 KernelTimer kt(ctx, "lds_count", 16.0 * (double)gn);
                 hipLaunchKernelGGL(prof_c ? k_lds_count<true> : k_lds_count<false>, dim3((unsigned)std::min<uint64_t>(p1 - p0, (uint64_t)kCPerCu * ctx->n_cu)),
                                    dim3(kCThreads), 0, st, fine.p, gbase, dfine.p, p0, p1, E, out.keys.p, out.counts.p,
-                                   out_cap, dcnt.p, ovf_list.p, dcnt.p + 1, prof_c ? dprof.p : nullptr);
+                                   out_cap, dcnt.p, ovf_list.p, dcnt.p + 1, cap_max, dmax, prof_c ? dprof.p : nullptr);
                 LAUNCH_OK();
                 kt.stop();
             }
@@ -1416,7 +1424,8 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
                 HIP_OK(hipMemcpyAsync(occ_h.data(), occ.p, 8 * n_ovf, hipMemcpyDeviceToHost, st));
                 HIP_OK(hipMemcpyAsync(parts_h.data(), ovf_list.p, 4 * n_ovf, hipMemcpyDeviceToHost, st));
                 HIP_OK(hipStreamSynchronize(st));
-                const uint64_t budget = 1ULL << 30;  // occurrences per batch (table <= 32 GB)
+                const uint64_t budget =
+                    (uint64_t)std::max<int64_t>(1, knob(ctx, "nc.fallback_budget", 1LL << 30));  // occurrences per batch (table <= 32 GB)
                 DevBuf<unsigned long long> nn(1);
                 DevBuf<int> dover(1);
                 DevBuf<uint32_t> dparts(n_ovf);

@@ -365,7 +365,7 @@ constexpr int kL3Waves = 4;
 __global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in, const uint64_t *off2,
                                                              const uint64_t *real2, const uint64_t *base3, int k,
                                                              uint64_t *key, uint16_t *mult, uint32_t *big,
-                                                             unsigned long long *nbig) {
+                                                             unsigned long long *nbig, uint32_t limit) {
     __shared__ uint64_t sm[kL3Waves][kWaveSort];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     uint64_t *s = sm[wave];
@@ -392,7 +392,7 @@ __global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in,
             m_base = base3[bn];
         }
         if (n == 0) continue;
-        if (nr64 > (uint64_t)kWaveSort || n > (uint64_t)NL * 64) {
+        if (nr64 > (uint64_t)limit || n > (uint64_t)NL * 64) {
             if (lane == 0) big[atomicAdd(nbig, 1ull)] = (uint32_t)b;
             continue;
         }
@@ -434,12 +434,12 @@ template <int THREADS, int CAP>
 __global__ void __launch_bounds__(THREADS) k_msd3_block(const uint64_t *in, const uint64_t *off2, const uint64_t *real2,
                                                         const uint64_t *base3, int k, const uint32_t *big, uint64_t nbig,
                                                         uint64_t *key, uint16_t *mult, uint32_t *fwd,
-                                                        unsigned long long *nfwd, int *too_big) {
+                                                        unsigned long long *nfwd, int *too_big, uint32_t limit) {
     __shared__ uint64_t s[CAP];
     const int E = k + 1;
     for (uint64_t q = blockIdx.x; q < nbig; q += gridDim.x) {
         const uint64_t b = big[q], lo = off2[b], n = off2[b + 1] - lo;
-        if (n > (uint64_t)CAP) {
+        if (n > (uint64_t)CAP || n > (uint64_t)limit) {
             if (threadIdx.x == 0) {
                 if (fwd) fwd[atomicAdd(nfwd, 1ull)] = (uint32_t)b;
                 else *too_big = 1;
@@ -528,7 +528,8 @@ bool msd_sort(mcaat_ctx *ctx, const uint64_t *ckeys, const uint32_t *ccnt, uint6
     HIP_OK(hipMemsetAsync(nbig.p, 0, 8, st));
     HIP_OK(hipMemsetAsync(too.p, 0, 4, st));
     hipLaunchKernelGGL(k_msd3_wave, dim3((unsigned)ctx->n_cu * 16), dim3(kL3Waves * 64), 0, st, l2.p, off2.p,
-                       (const uint64_t *)real2.p, (const uint64_t *)base3.p, k, key, mult, big.p, nbig.p);
+                       (const uint64_t *)real2.p, (const uint64_t *)base3.p, k, key, mult, big.p, nbig.p,
+                       (uint32_t)std::min<int64_t>(kWaveSort, knob(ctx, "sort.wave_limit", kWaveSort)));
     LAUNCH_OK();
     unsigned long long hb = 0;
     HIP_OK(hipMemcpyAsync(&hb, nbig.p, 8, hipMemcpyDeviceToHost, st));
@@ -541,7 +542,8 @@ bool msd_sort(mcaat_ctx *ctx, const uint64_t *ckeys, const uint32_t *ccnt, uint6
         HIP_OK(hipMemsetAsync(nbig2.p, 0, 8, st));
         hipLaunchKernelGGL((k_msd3_block<256, kMidSort>), dim3((unsigned)std::min<uint64_t>(hb, (uint64_t)ctx->n_cu * 8)),
                            dim3(256), 0, st, l2.p, off2.p, (const uint64_t *)real2.p, (const uint64_t *)base3.p, k, big.p,
-                           (uint64_t)hb, key, mult, big2.p, nbig2.p, too.p);
+                           (uint64_t)hb, key, mult, big2.p, nbig2.p, too.p,
+                           (uint32_t)std::min<int64_t>(kMidSort, knob(ctx, "sort.mid_limit", kMidSort)));
         LAUNCH_OK();
         unsigned long long hb2 = 0;
         HIP_OK(hipMemcpyAsync(&hb2, nbig2.p, 8, hipMemcpyDeviceToHost, st));
@@ -550,7 +552,8 @@ bool msd_sort(mcaat_ctx *ctx, const uint64_t *ckeys, const uint32_t *ccnt, uint6
             hipLaunchKernelGGL((k_msd3_block<1024, kBlockSort>), dim3((unsigned)std::min<uint64_t>(hb2, (uint64_t)ctx->n_cu)),
                                dim3(1024), 0, st, l2.p, off2.p, (const uint64_t *)real2.p, (const uint64_t *)base3.p, k,
                                big2.p, (uint64_t)hb2, key, mult, (uint32_t *)nullptr,
-                               (unsigned long long *)nullptr, too.p);
+                               (unsigned long long *)nullptr, too.p,
+                               (uint32_t)std::min<int64_t>(kBlockSort, knob(ctx, "sort.block_limit", kBlockSort)));
             LAUNCH_OK();
         }
         int h = 0;
@@ -586,7 +589,8 @@ void sdbg_build(mcaat_ctx *ctx, CountResult &c, int k, mcaat_graph *g) {
     // MSD sort with LDS bucket sorts (k <= 28: key remainder and mult share one word);
     // the radix sort otherwise, or when a bucket is too skewed for LDS
     bool done = false;
-    if (k <= 28 && D >= (1u << 16)) {
+    const int64_t msd = knob(ctx, "sort.msd", -1);  // test knob: 0 never, 1 whenever k <= 28
+    if (k <= 28 && msd != 0 && (D >= (1u << 16) || (msd == 1 && D > 0))) {
         KernelTimer kt(ctx, "edge_sort", 64.0 * (double)D);
         done = msd_sort(ctx, c.keys.p, c.counts.p, c.n, k, D, g->key.p, g->mult.p);
         kt.stop();

@@ -108,6 +108,8 @@ SIGNATURES = {
     "mcaat_map_reads": (C.c_int, [C.c_void_p, C.c_void_p, _u64p, C.c_size_t, C.c_uint64, C.POINTER(C.c_void_p)]),
     "mcaat_mapped_get": (C.c_int, [C.c_void_p, _u64p, C.POINTER(_u64p), C.POINTER(_u64p), C.POINTER(_u64p)]),
     "mcaat_mapped_free": (None, [C.c_void_p]),
+    "mcaat_set_knob": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
+    "mcaat_graph_download_range": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, _u64p, _u16p, _u8p]),
 }
 
 _lib: Optional[C.CDLL] = None
@@ -226,6 +228,29 @@ class Context:
 
     def reset_timing(self) -> None:
         self._lib.mcaat_reset_timing(self.h)
+
+    def set_knob(self, name: str, value: int) -> None:
+        """Size limit that picks a code path (include/mcaat_gpu.h, mcaat_set_knob); value < 0
+        restores the default."""
+        _check(self._lib.mcaat_set_knob(self.h, name.encode(), int(value)))
+
+    def knobs(self, **values):
+        """Context manager: knobs set for the block (keyword names use '__' for '.'),
+        restored to their defaults afterwards."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def _cm():
+            names = [k.replace("__", ".") for k in values]
+            try:
+                for n, v in zip(names, values.values()):
+                    self.set_knob(n, v)
+                yield self
+            finally:
+                for n in names:
+                    self.set_knob(n, -1)
+
+        return _cm()
 
 
 class Reads:
@@ -452,6 +477,16 @@ class Graph:
         valid = np.zeros(max(d, 1), dtype=np.uint8)
         _check(self.ctx._lib.mcaat_graph_download(self.h, _ptr(keys, _u64p), _ptr(mult, _u16p), _ptr(valid, _u8p)))
         return keys[:d], mult[:d], valid[:d]
+
+    def download_range(self, first: int, count: int, keys=True, mult=True, valid=False):
+        """(keys, mult, valid) of edges [first, first+count); None for the parts not asked for."""
+        kk = np.zeros(max(count, 1), dtype=np.uint64) if keys else None
+        mm = np.zeros(max(count, 1), dtype=np.uint16) if mult else None
+        vv = np.zeros(max(count, 1), dtype=np.uint8) if valid else None
+        _check(self.ctx._lib.mcaat_graph_download_range(
+            self.h, first, count, _ptr(kk, _u64p) if keys else None, _ptr(mm, _u16p) if mult else None,
+            _ptr(vv, _u8p) if valid else None))
+        return (kk[:count] if keys else None, mm[:count] if mult else None, vv[:count] if valid else None)
 
     def neighbors(self, ids: np.ndarray, incoming: bool = False) -> Tuple[np.ndarray, np.ndarray]:
         ids = np.ascontiguousarray(ids, dtype=np.uint64)

@@ -1,0 +1,246 @@
+"""Parity of the code paths that only large inputs reach, and properties of full-size graphs.
+
+1. Knob-forced branches (include/mcaat_gpu.h, mcaat_set_knob): the size limits that pick a
+   code path are shrunk so the small parity fixtures run every branch that C2/C3 take —
+   multi-group B/C counting, output regrowth + recount, the pass-A resize re-run, the class
+   split / raw path / class-filtered global fallback in small batches, the 256- and
+   1024-thread level-3 LDS sorts and the radix fallback, DepthLevelSearch and FindCycle
+   scratch regrowth, a one-start speculation window, and the list-ranking peel. Results must
+   equal the oracle bit for bit (keys, multiplicities, valid bits, candidates, buckets,
+   entries, stats).
+2. Coverage-matched samples of C3 (150x, 2M reads, k=27, thr=20) and C2 (paired-end, 0.5 %
+   errors): the same graph regime as the bench configs (D/N_occ), against the oracle.
+3. Full C2 / C3 (D > 2^31 at C2): size-independent properties — strictly ascending BOSS
+   keys, sum of multiplicities = 2 N_occ, neighbour symmetry and label consistency on a
+   sample, every cycle a closed walk of valid edges of length in (min, max].
+Oracle parity status: "parity unpinned" (DESIGN.md §5).
+"""
+import numpy as np
+import pytest
+
+import mcaat_amd as M
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+CASES = {
+    "c1_k27": (M.SynthSpec(), 27, M.CfParams()),
+    "pe_err": (M.SynthSpec(seed=7, n_genomes=4, genome_len=20_000, arrays_per_genome=2, spacers_per_array=8,
+                           repeat_len_min=32, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
+                           n_reads=24_000, error_rate=0.002, paired=True), 23, M.CfParams(threshold_multiplicity=5)),
+    "low_thr": (M.SynthSpec(seed=11, n_genomes=3, genome_len=15_000, arrays_per_genome=2, spacers_per_array=10,
+                            repeat_len_min=30, repeat_len_max=34, spacer_len_min=30, spacer_len_max=34,
+                            n_reads=12_000, error_rate=0.004), 23,
+                M.CfParams(threshold_multiplicity=2, low_abundance=True)),
+}
+
+KNOBS = {
+    # one L1 bucket per pass-B/C group, the count output regrown (and the group recounted)
+    "multi_group": {"nc.group_budget": 1, "nc.out_cap": 1},
+    # L1 buckets undersized on the first pass-A attempt: resize and re-run
+    "l1_resize": {"nc.l1_slots": 64, "nc.fine_bits": 12},
+    # every partition overflows the LDS edge table: class split, then the class-filtered global
+    # fallback, one (partition, class) per batch
+    "fallback": {"nc.edge_cap": 8, "nc.fallback_budget": 1},
+    # every partition overflows the descriptor table: class split, then the raw path
+    "desc_raw": {"nc.desc_cap": 2, "nc.fine_bits": 9},
+    # level-3 buckets through the 256-thread LDS sort, the 1024-thread one, and the radix fallback
+    "sort_mid": {"sort.msd": 1, "sort.wave_limit": 0},
+    "sort_block": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_limit": 0},
+    "sort_radix": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_limit": 0, "sort.block_limit": 0},
+    "sort_radix_only": {"sort.msd": 0},
+    # scratch regrowth in DepthLevelSearch and FindCycle, one speculative start per round
+    "cf_scratch": {"cf.dls_stack": 1, "cf.dls_visited": 2, "cf.fc_lock": 4, "cf.fc_relax": 1, "cf.fc_out": 1,
+                   "cf.fc_window": 1},
+    # every peel walk hands over after one step: the list-ranking peel does the rest
+    "peel_rulers": {"cf.walk_budget": 1},
+}
+
+_oracle_cache = {}
+
+
+def _oracle(name):
+    if name not in _oracle_cache:
+        spec, k, prm = CASES[name]
+        packed, offs = M.synth_host(spec)
+        og = O.OGraph.build(packed, offs, k, threads=4)
+        okeys, omult = og.arrays()
+        ores = og.cycle_finder(threshold_multiplicity=prm.threshold_multiplicity, low_abundance=prm.low_abundance,
+                               cycle_max_length=prm.cycle_max_length, cycle_min_length=prm.cycle_min_length,
+                               threads=1)
+        ok, oc = O.count_canonical(packed, offs, k, threads=4)
+        _oracle_cache[name] = dict(keys=okeys, mult=omult, res=ores, valid=og.valid(), ck=ok, cc=oc)
+    return _oracle_cache[name]
+
+
+def _check_graph_and_cycles(g, res, ref, tag):
+    keys, mult, valid = g.download()
+    assert np.array_equal(keys, ref["keys"]), tag
+    assert np.array_equal(mult, ref["mult"]), tag
+    ores = ref["res"]
+    assert res.stats[:6] == ores["stats"], tag
+    assert res.candidates == ores["candidates"], tag
+    assert res.buckets == ores["buckets"], tag
+    assert [(s, c) for s, c in res.entries] == [tuple(e) for e in ores["entries"]], tag
+    assert np.array_equal(valid, ref["valid"]), tag
+
+
+@pytest.mark.parametrize("knobset", sorted(KNOBS))
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_forced_branches_match_oracle(gpu_ctx, name, knobset):
+    spec, k, prm = CASES[name]
+    ref = _oracle(name)
+    reads = M.Reads.synth(gpu_ctx, spec)
+    with gpu_ctx.knobs(**{n.replace(".", "__"): v for n, v in KNOBS[knobset].items()}):
+        if knobset.startswith(("multi", "l1", "fallback", "desc")):
+            gk, gc = M.count_edges(gpu_ctx, reads, k)
+            assert np.array_equal(gk, ref["ck"]) and np.array_equal(gc, ref["cc"]), (name, knobset)
+        g = M.Graph.build(gpu_ctx, reads, k)
+        res = g.cycle_finder(prm)
+        _check_graph_and_cycles(g, res, ref, (name, knobset))
+        g.free()
+    reads.free()
+
+
+def test_forced_branches_really_taken(gpu_ctx):
+    """The knobs reach their branches: the fallback path counted partitions, and FindCycle
+    started from a one-start speculation window."""
+    spec, k, prm = CASES["pe_err"]
+    reads = M.Reads.synth(gpu_ctx, spec)
+    gpu_ctx.reset_timing()
+    with gpu_ctx.knobs(nc__edge_cap=8):
+        M.count_edges(gpu_ctx, reads, k)
+    assert gpu_ctx.kernel_timing("lds_count_overflow_partitions")[1] > 0
+    base = M.Graph.build(gpu_ctx, reads, k).cycle_finder(prm)
+    with gpu_ctx.knobs(cf__fc_window=1):
+        g = M.Graph.build(gpu_ctx, reads, k)
+        res = g.cycle_finder(prm)
+    # the window starts at one start and doubles: more speculation rounds than the default
+    assert res.stats[6] > base.stats[6] and res.stats[4] == base.stats[4] > 0
+    with pytest.raises(M.McaatError):
+        gpu_ctx.set_knob("no.such_knob", 1)
+
+
+# ---- coverage-matched samples of the bench configs ----------------------------------
+SAMPLES = {
+    # C3 regime: 150x coverage (2M x 150 bp over 2 Mbp), e = 2e-4, k = 27, thr = 20
+    "c3_sample": (M.SynthSpec(seed=3, n_genomes=20, genome_len=100_000, arrays_per_genome=2, spacers_per_array=12,
+                              repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
+                              read_len=150, n_reads=2_000_000, error_rate=2.0e-4), 27, 20),
+    # C2 regime: paired-end, 0.5 % errors, ~19x coverage (1M x 150 bp over 8 Mbp)
+    "c2_sample": (M.SynthSpec(seed=2, n_genomes=40, genome_len=200_000, arrays_per_genome=2, spacers_per_array=12,
+                              repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
+                              read_len=150, n_reads=1_000_000, error_rate=5.0e-3, paired=True), 27, 20),
+}
+
+
+@pytest.mark.parametrize("name", sorted(SAMPLES))
+def test_bench_regime_sample_matches_oracle(gpu_ctx, name):
+    spec, k, thr = SAMPLES[name]
+    packed, offs = M.synth_host(spec)
+    og = O.OGraph.build(packed, offs, k, threads=16)
+    okeys, omult = og.arrays()
+    reads = M.Reads.synth(gpu_ctx, spec)
+    g = M.Graph.build(gpu_ctx, reads, k)
+    keys, mult, _ = g.download()
+    assert g.size == og.size
+    assert np.array_equal(keys, okeys) and np.array_equal(mult, omult)
+    del keys, mult, okeys, omult
+    res = g.cycle_finder(M.CfParams(threshold_multiplicity=thr))
+    ores = og.cycle_finder(threshold_multiplicity=thr, threads=1)
+    assert res.stats[:6] == ores["stats"]
+    assert res.candidates == ores["candidates"] and res.buckets == ores["buckets"]
+    assert [(s, c) for s, c in res.entries] == [tuple(e) for e in ores["entries"]]
+    _, _, valid = g.download()
+    assert np.array_equal(valid, og.valid())
+    assert ores["stats"][5] > 0  # the sample holds arrays that yield cycles
+    g.free()
+    reads.free()
+
+
+# ---- full-size properties (bench configs) ---------------------------------------------
+FULL = {
+    # bench.py "c2": 50M PE reads, 0.5 % errors -> D ~ 2.4e9 > 2^31
+    "c2_full": (M.SynthSpec(seed=2, n_genomes=200, genome_len=2_000_000, arrays_per_genome=2, spacers_per_array=12,
+                            repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
+                            read_len=150, n_reads=50_000_000, error_rate=5.0e-3, paired=True), 27, 20),
+    # bench.py "c3": 300M reads, D ~ 1.0e9
+    "c3_full": (M.SynthSpec(seed=3, n_genomes=200, genome_len=1_500_000, arrays_per_genome=2, spacers_per_array=12,
+                            repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
+                            read_len=150, n_reads=300_000_000, error_rate=2.0e-4), 27, 20),
+}
+
+
+def _lsb_of_boss(K, k):
+    return (K >> 2) | ((K & 3) << (2 * k))
+
+
+@pytest.mark.parametrize("name", sorted(FULL))
+def test_full_size_graph_properties(gpu_ctx, name):
+    spec, k, thr = FULL[name]
+    E = k + 1
+    reads = M.Reads.synth(gpu_ctx, spec)
+    g = M.Graph.build(gpu_ctx, reads, k)
+    reads.free()
+    D = g.size
+    n_occ = spec.n_reads * (spec.read_len - k)
+    if name == "c2_full":
+        assert D > 2 ** 31  # ids above int32 (reference UB region)
+    # 1. keys strictly ascending and inside 2E bits; sum of multiplicities = 2 N_occ
+    chunk = 1 << 27
+    prev = -1
+    msum = 0
+    mmax = 0
+    for a in range(0, D, chunk):
+        kk, mm, _ = g.download_range(a, min(chunk, D - a))
+        assert int(kk[0]) > prev
+        assert bool(np.all(kk[1:] > kk[:-1]))
+        assert int(kk[-1]) < (1 << (2 * E))
+        assert int(mm.min()) >= 1
+        prev = int(kk[-1])
+        msum += int(mm.sum(dtype=np.uint64))
+        mmax = max(mmax, int(mm.max()))
+    if mmax < 65535:
+        assert msum == 2 * n_occ
+    else:
+        assert msum <= 2 * n_occ
+    # 2. neighbour symmetry and label consistency on a sample of edges
+    rng = np.random.default_rng(5)
+    ids = np.unique(rng.integers(0, D, size=20_000, dtype=np.uint64))
+    out, oc = g.neighbors(ids, incoming=False)
+    inn, ic = g.neighbors(ids, incoming=True)
+    mask = (1 << (2 * k)) - 1
+    for i, e in enumerate(ids.tolist()):
+        (ke,), _, _ = g.download_range(e, 1, mult=False)
+        le = _lsb_of_boss(int(ke), k)
+        for o in out[i, : oc[i]].tolist():
+            (ko,), _, _ = g.download_range(o, 1, mult=False)
+            # target label of e == source label of o
+            assert (le >> 2) == (_lsb_of_boss(int(ko), k) & mask)
+            back, bc = g.neighbors(np.array([o], dtype=np.uint64), incoming=True)
+            assert e in back[0, : bc[0]].tolist()
+        for p in inn[i, : ic[i]].tolist():
+            fwd, fc = g.neighbors(np.array([p], dtype=np.uint64), incoming=False)
+            assert e in fwd[0, : fc[0]].tolist()
+        if i >= 400:
+            break
+    # 3. CycleFinder: every cycle a closed walk of valid edges, length in (min, max]
+    prm = M.CfParams(threshold_multiplicity=thr)
+    res = g.cycle_finder(prm, as_arrays=True)
+    assert res.stats[5] > 0
+    n_checked = 0
+    for s, (flat, offs) in res.entries:
+        for j in range(len(offs) - 1):
+            cyc = flat[offs[j]:offs[j + 1]].astype(np.uint64)
+            assert int(cyc[0]) == s
+            assert prm.cycle_min_length < cyc.size <= prm.cycle_max_length
+            nb, nc = g.neighbors(cyc, incoming=False)
+            nxt = np.roll(cyc, -1)
+            for q in range(cyc.size):
+                assert int(nxt[q]) in nb[q, : nc[q]].tolist()
+            n_checked += 1
+            if n_checked >= 300:
+                break
+        if n_checked >= 300:
+            break
+    g.free()
