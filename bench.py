@@ -43,13 +43,21 @@ CONFIGS = {
     "c3": dict(spec=M.SynthSpec(seed=3, n_genomes=200, genome_len=1_500_000, arrays_per_genome=2,
                                 spacers_per_array=12, repeat_len_min=30, repeat_len_max=36, spacer_len_min=30,
                                 spacer_len_max=36, read_len=150, n_reads=300_000_000, error_rate=2.0e-4),
-               k=27, thr=20, name="C3 1B-node synthetic metagenome (300M x 150bp SE, k=27, thr=20)"),
+               k=27, thr=20, name="C3 1B-node synthetic metagenome (300M x 150bp SE, k=27, thr=20)",
+               # CPU-baseline sample in the same regime: 150x coverage, D/N_occ ~ 0.027 as at C3
+               sample=M.SynthSpec(seed=3, n_genomes=20, genome_len=100_000, arrays_per_genome=2, spacers_per_array=12,
+                                  repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
+                                  read_len=150, n_reads=2_000_000, error_rate=2.0e-4)),
     # C2-shaped, smaller: 50M PE reads over a 400 Mbp community
     "c2": dict(spec=M.SynthSpec(seed=2, n_genomes=200, genome_len=2_000_000, arrays_per_genome=2,
                                 spacers_per_array=12, repeat_len_min=30, repeat_len_max=36, spacer_len_min=30,
                                 spacer_len_max=36, read_len=150, n_reads=50_000_000, error_rate=5.0e-3, paired=True),
-               k=27, thr=20, name="C2 50M PE synthetic metagenome (k=27)"),
-    "tiny": dict(spec=M.SynthSpec(), k=27, thr=20, name="C1 tiny (10k x 150bp, 50 kbp genome, k=27)"),
+               k=27, thr=20, name="C2 50M PE synthetic metagenome (k=27)",
+               sample=M.SynthSpec(seed=2, n_genomes=40, genome_len=200_000, arrays_per_genome=2, spacers_per_array=12,
+                                  repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
+                                  read_len=150, n_reads=1_000_000, error_rate=5.0e-3, paired=True)),
+    "tiny": dict(spec=M.SynthSpec(), k=27, thr=20, name="C1 tiny (10k x 150bp, 50 kbp genome, k=27)",
+                 sample=M.SynthSpec()),
 }
 
 
@@ -57,25 +65,119 @@ def n_occ(spec: M.SynthSpec, k: int) -> int:
     return spec.n_reads * max(0, spec.read_len - k)
 
 
-def cpu_baseline(cfg: dict, sample_reads: int, threads: int) -> dict:
-    """The oracle (CPU restatement, OpenMP) on a bounded sample of the same workload."""
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def host_threads() -> int:
+    """Host cores this job may use: OMP_NUM_THREADS (16 on the GPU box), else the affinity set."""
+    try:
+        return max(1, int(os.environ["OMP_NUM_THREADS"]))
+    except (KeyError, ValueError):
+        return max(1, len(os.sched_getaffinity(0)))
+
+
+def _oracle_path(path: str, k: int, thr: int, threads: int) -> tuple:
+    """The CPU restatement over the reference's span: FASTQ parse -> count -> SDBG -> CycleFinder."""
     import oracle as O
 
-    spec = M.SynthSpec(**{**cfg["spec"].__dict__, "n_reads": sample_reads})
-    packed, offs = M.synth_host(spec)
     t0 = time.perf_counter()
-    g = O.OGraph.build(packed, offs, cfg["k"], threads=threads)
-    g.cycle_finder(threshold_multiplicity=cfg["thr"], threads=threads)
-    dt = time.perf_counter() - t0
-    kmers = n_occ(spec, cfg["k"])
-    return {
-        "value": kmers / dt,
-        "unit": "k-mers/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": f"{sample_reads} reads of the same synthetic spec ({kmers} k-mers, D={g.size}), "
-                  f"oracle count+SDBG+CycleFinder, {dt:.2f} s",
-    }
+    packed, offs = O.read_fastq(path)
+    t1 = time.perf_counter()
+    g = O.OGraph.build(packed, offs, k, threads=threads)
+    res = g.cycle_finder(threshold_multiplicity=thr, threads=threads)
+    t2 = time.perf_counter()
+    n_occ_s = int(np.maximum(np.diff(offs.astype(np.int64)) - k, 0).sum())
+    return t2 - t0, t1 - t0, n_occ_s, g.size, res["stats"][5]
+
+
+def cpu_baseline(ctx, cfg: dict, threads: int) -> dict:
+    """The oracle (CPU restatement, OpenMP) timed from FASTQ to CycleFinder results, as the
+    reference's span (main.cpp:517-536), on a coverage-matched sample of the workload (same
+    D/N_occ regime), plus C1 tiny at threads=1 (the reference's deterministic mode)."""
+    import tempfile
+
+    out = {"unit": "k-mers/s", "cores": threads, "kind": "port", "cpu": cpu_model()}
+    for key, spec, thr_n in (("sample", cfg["sample"], threads), ("c1_threads1", CONFIGS["tiny"]["spec"], 1)):
+        r = M.Reads.synth(ctx, spec)
+        fd, path = tempfile.mkstemp(suffix=".fq", dir="/tmp")
+        os.close(fd)
+        try:
+            r.write_fastq(path, threads=threads)
+            r.free()
+            size = os.path.getsize(path)
+            dt, parse, kmers, D, cyc = _oracle_path(path, cfg["k"], cfg["thr"], thr_n)
+        finally:
+            os.unlink(path)
+        leg = {"value": kmers / dt, "seconds": round(dt, 3), "fastq_parse_s": round(parse, 3), "kmers": kmers,
+               "D": D, "cycles": cyc, "threads": thr_n,
+               "sample": f"{spec.n_reads} x {spec.read_len} bp over {spec.n_genomes} x {spec.genome_len} bp "
+                         f"(coverage {spec.n_reads * spec.read_len / (spec.n_genomes * spec.genome_len):.0f}x), "
+                         f"e={spec.error_rate}, {size / 1e6:.0f} MB FASTQ in /tmp, FASTQ parse -> count -> SDBG -> "
+                         f"CycleFinder, D/N_occ={D / max(1, kmers):.4f}"}
+        if key == "sample":
+            out.update(value=leg["value"], sample=leg["sample"], seconds=leg["seconds"], D=D, kmers=kmers)
+            out["fastq_parse_s"] = leg["fastq_parse_s"]
+        else:
+            out[key] = leg
+    return out
+
+
+def measure_e2e(cfg: dict, spec, fastq: str, threads: int, n_kmers: int) -> dict:
+    """The reference's headline T: the mcaat CLI (C++ host over the C ABI) in a fresh process on
+    the FASTQ, timed by the CLI itself from SDBGBuild start to CycleFinder end (main.cpp:517-536:
+    GPU FASTQ ingest + node_counter + sdbg_build + host SDBG load + CycleFinder)."""
+    import re
+    import shutil
+    import subprocess
+    import tempfile
+
+    exe = os.path.join(ROOT, "mcaat_amd", "mcaat")
+    work = tempfile.mkdtemp(dir="/tmp")
+    try:
+        st = os.path.join(work, "settings.txt")
+        with open(st, "w") as f:
+            f.write(f"kmer_k={cfg['k']}\nthreshold_multiplicity={cfg['thr']}\nthreads={threads}\n")
+        t0 = time.perf_counter()
+        p = subprocess.run([exe, "--settings", st, "--input-files", fastq, "--output-folder",
+                            os.path.join(work, "out")], capture_output=True, text=True, timeout=900)
+        wall = time.perf_counter() - t0
+        m = re.search(r"TIMING span_s=([0-9.]+) sdbg_build_s=([0-9.]+) build_lib_s=([0-9.]+) cycle_finder_s=([0-9.]+)",
+                      p.stdout)
+        if p.returncode != 0 or not m:
+            return {"error": f"CLI rc={p.returncode}: {(p.stderr or p.stdout)[-400:]}"}
+        span, build, lib, cf = (float(x) for x in m.groups())
+        arrays = os.path.join(work, "out", "CRISPR_Arrays.txt")
+        n_arr = sum(1 for line in open(arrays) if line.startswith(">")) if os.path.exists(arrays) else None
+        return {
+            "value": n_kmers / span, "unit": "k-mers/s", "T_s": round(span, 3),
+            "build_lib_s": round(lib, 3), "sdbg_build_s": round(build, 3), "cycle_finder_s": round(cf, 3),
+            "fastq_bytes": os.path.getsize(fastq), "fastq_GBps": round(os.path.getsize(fastq) / lib / 1e9, 2),
+            "cli_wall_s": round(wall, 3), "crispr_arrays_records": n_arr,
+            "note": "fresh CLI process, FASTQ in tmpfs (/dev/shm); span excludes process start, HIP runtime "
+                    "init (input check) and the downstream steps 6-8",
+        }
+    finally:
+        shutil.rmtree(work, ignore_errors=True)
+
+
+def step_traffic_from_profiles() -> float | None:
+    """HBM bytes of one profiled step: every kernel's per-launch PMC bytes times its launches
+    (profiles/traffic.json), the synthetic-read generator excluded."""
+    path = os.path.join(ROOT, "profiles", "traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        return float(sum(v["hbm_bytes_per_launch"] * v["launches"] for kk, v in d.items() if kk != "k_synth"))
+    except Exception:
+        return None
 
 
 def traffic_from_profiles(kernel: str) -> float | None:
@@ -157,6 +259,10 @@ def measure_ingest(ctx, spec, n_reads: int) -> dict:
         got, _ = r.download()
         nw = (nb + 31) // 32
         ok = bool(n_got == n_reads and b_got == nb and np.array_equal(got[:nw], want[:nw]))
+        # the mapping view (one entry per record; the counting view itself for ACGT-only SE input)
+        n_rec, _sep = r.records_info()
+        rp, ro = r.download_records()
+        ok = ok and bool(n_rec == n_reads and np.array_equal(rp[:nw], want[:nw]) and int(ro[-1]) == nb)
         gpu_ms = 0.0
         kern = {}
         for n in ("fq_parse", "fq_records", "fq_emit"):
@@ -168,9 +274,11 @@ def measure_ingest(ctx, spec, n_reads: int) -> dict:
         os.unlink(path)
     return {
         "reads": n_reads, "file_bytes": size, "wall_s": round(wall, 3), "first_call_s": round(first, 3),
-        "text_GBps": round(size / wall / 1e9, 2), "reads_per_s": n_reads / wall,
-        "gpu_parse_ms": round(gpu_ms, 3), "kernels": kern, "library_matches": ok,
-        "note": "page-cached plain FASTQ, second call on the context; wall includes host read, PCIe upload and GPU parse",
+        "text_GBps": round(size / first / 1e9, 2), "text_GBps_warm_context": round(size / wall / 1e9, 2),
+        "reads_per_s": n_reads / first, "gpu_parse_ms": round(gpu_ms, 3), "kernels": kern, "library_matches": ok,
+        "note": "page-cached plain FASTQ; text_GBps = first call on the context (includes allocating the "
+                "reader's pinned chunks), warm = second call reusing them; wall includes host read, PCIe upload "
+                "and GPU parse",
     }
 
 def main() -> int:
@@ -180,9 +288,10 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--reads", type=int, default=0, help="override n_reads")
-    ap.add_argument("--cpu-sample-reads", type=int, default=2_000_000)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: OMP_NUM_THREADS or the affinity set")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the FASTQ-inclusive span (the workload as FASTQ in /dev/shm through the mcaat CLI)")
     ap.add_argument("--no-post", action="store_true", help="skip the untimed relevant-read mapping measurement")
     ap.add_argument("--ingest-reads", type=int, default=2_000_000,
                     help="untimed FASTQ ingest measurement on a file of this many reads (0: skip)")
@@ -369,14 +478,55 @@ def main() -> int:
             "fastq_ingest": ingest,
             "cpu_baseline": None,
         }
-        if world == 1 and not args.no_cpu_baseline and not args.dry_run:
+        # step-level roofline: B_alg = 0.25 N_bases + 16 N_occ + 8 C + 8 D_c + 41 D with
+        # C = 2 D_c (count table model) and D_c ~ D/2 distinct canonical edges
+        if D:
+            d_c = (D + 1) // 2
+            b_alg = 0.25 * spec.n_reads * spec.read_len * (1 if sharded else world) + 16.0 * kmers_total \
+                + 8.0 * 2 * d_c + 8.0 * d_c + 41.0 * D
+            out["step_roofline"] = {
+                "B_alg": b_alg, "achieved_GBps": b_alg / dt / 1e9 / world,
+                "frac": b_alg / dt / 1e9 / world / PEAK_HBM_GBS,
+                "pmc_bytes_per_step": step_traffic_from_profiles(),
+                "note": "SURVEY.md §8d algorithmic bytes over the step time, per GPU; pmc_bytes_per_step = "
+                        "FETCH+WRITE of every kernel of one profiled step (profiles/traffic.json)",
+            }
+    e2e_file = None
+    want_e2e = rank == 0 and world == 1 and not args.dry_run and not args.no_e2e
+    if want_e2e:
+        import shutil
+
+        need = 2 * spec.n_reads * spec.read_len + 7 * spec.n_reads
+        if shutil.disk_usage("/dev/shm").free > 1.2 * need:
+            e2e_file = f"/dev/shm/mcaat_bench_{os.getpid()}.fq"
             try:
-                out["cpu_baseline"] = cpu_baseline(cfg, min(args.cpu_sample_reads, spec.n_reads), args.cpu_threads)
-            except Exception as e:  # reported, never fatal for the GPU number
-                out["cpu_baseline"] = {"error": str(e)}
-        print(json.dumps(out), flush=True)
+                t0 = time.perf_counter()
+                reads.write_fastq(e2e_file, threads=host_threads())
+                write_s = time.perf_counter() - t0
+            except Exception as e:
+                out["e2e"] = {"error": f"writing the FASTQ failed: {e}"}
+                if os.path.exists(e2e_file):
+                    os.unlink(e2e_file)
+                e2e_file = None
+        else:
+            out["e2e"] = {"error": f"/dev/shm holds less than 1.2 x {need / 1e9:.0f} GB"}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
+        try:
+            out["cpu_baseline"] = cpu_baseline(ctx, cfg, args.cpu_threads or host_threads())
+        except Exception as e:  # reported, never fatal for the GPU number
+            out["cpu_baseline"] = {"error": str(e)}
     reads.free()
-    ctx.close()
+    ctx.close()  # returns the cached device memory: the CLI below is another process on this GPU
+    if e2e_file:
+        try:
+            out["e2e"] = measure_e2e(cfg, spec, e2e_file, host_threads(), kmers_total)
+            out["e2e"]["fastq_write_s"] = round(write_s, 3)
+        except Exception as e:
+            out["e2e"] = {"error": str(e)}
+        finally:
+            os.unlink(e2e_file)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
     if dist is not None:
         dist.destroy_process_group()
     return 0

@@ -68,6 +68,10 @@ int mcaat_reads_download(const mcaat_reads *r, uint64_t *packed, uint64_t *offse
 /* the mapping view (records) as packed stream + offsets[n_records+1]; the counting view
  * when records_info says it is not separate. Replaces the FASTQ re-parse of reads.cpp:88-130. */
 int mcaat_reads_records_download(const mcaat_reads *r, uint64_t *packed, uint64_t *offsets);
+/* The counting view written as 4-line FASTQ (header "@r", quality 'I'), formatted by
+ * `threads` host threads: a FASTQ input for mcaat_reads_from_fastx / the CLI made from
+ * resident reads (synthetic configs). Replaces: nothing in the reference. */
+int mcaat_reads_write_fastq(const mcaat_reads *r, const char *path, int threads);
 void mcaat_reads_free(mcaat_reads *r);
 
 /* Synthetic metagenome: iid genomes with CRISPR arrays inserted,

@@ -387,6 +387,14 @@ int mcaat_reads_download(const mcaat_reads *r, uint64_t *packed, uint64_t *offse
     });
 }
 
+int mcaat_reads_write_fastq(const mcaat_reads *r, const char *path, int threads) {
+    return guarded([&] {
+        require(r && path, "null argument");
+        HIP_OK(hipSetDevice(r->ctx->device));
+        write_fastq(r, path, threads);
+    });
+}
+
 void mcaat_reads_free(mcaat_reads *r) { delete r; }
 
 int mcaat_reads_synth(mcaat_ctx *ctx, const mcaat_synth_spec *spec, mcaat_reads **out) {

@@ -29,6 +29,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <atomic>
 #include <future>
 #include <string>
 #include <fcntl.h>
@@ -571,6 +572,66 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
         r->rec_packed = std::move(qpacked);
         r->rec_offsets = std::move(qoffsets);
     }
+}
+
+}  // namespace mcaat
+
+namespace mcaat {
+
+// The counting view as 4-line FASTQ ("@r", sequence, "+", all-'I' qualities): record i
+// starts at byte 2*offsets[i] + 7*i, so host threads format disjoint read ranges and pwrite
+// them independently. Used to make FASTQ inputs of the synthetic configs (bench, tests).
+void write_fastq(const mcaat_reads *r, const char *path, int threads) {
+    std::vector<uint64_t> packed(r->n_words + 1, 0), offs(r->n_reads + 1);
+    if (r->n_words) HIP_OK(hipMemcpy(packed.data(), r->packed.p, 8 * r->n_words, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(offs.data(), r->offsets.p, 8 * (r->n_reads + 1), hipMemcpyDeviceToHost));
+    const int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd < 0) throw Error(MCAAT_E_IO, std::string("cannot create ") + path);
+    const uint64_t n = r->n_reads;
+    const uint64_t total = 2 * (offs[n] - offs[0]) + 7 * n;
+    if (ftruncate(fd, (off_t)total) != 0) {
+        close(fd);
+        throw Error(MCAAT_E_IO, std::string("cannot size ") + path);
+    }
+    if (threads < 1) threads = 1;
+    std::atomic<bool> failed{false};
+    auto work = [&](uint64_t a, uint64_t b) {
+        std::vector<char> buf;
+        buf.reserve(8u << 20);
+        uint64_t pos = 2 * (offs[a] - offs[0]) + 7 * a;
+        auto flush = [&]() {
+            size_t done = 0;
+            while (done < buf.size()) {
+                const ssize_t w = pwrite(fd, buf.data() + done, buf.size() - done, (off_t)(pos + done));
+                if (w <= 0) { failed = true; return; }
+                done += (size_t)w;
+            }
+            pos += buf.size();
+            buf.clear();
+        };
+        for (uint64_t i = a; i < b && !failed; ++i) {
+            const uint64_t s = offs[i], L = offs[i + 1] - s;
+            const size_t at = buf.size();
+            buf.resize(at + 2 * L + 7);
+            char *o = buf.data() + at;
+            *o++ = '@'; *o++ = 'r'; *o++ = '\n';
+            for (uint64_t j = 0; j < L; ++j) o[j] = "ACGT"[(packed[(s + j) >> 5] >> (2 * ((s + j) & 31))) & 3];
+            o += L;
+            *o++ = '\n'; *o++ = '+'; *o++ = '\n';
+            memset(o, 'I', L);
+            o[L] = '\n';
+            if (buf.size() >= (8u << 20)) flush();
+        }
+        flush();
+    };
+    std::vector<std::thread> pool;
+    for (int t = 0; t < threads; ++t) {
+        const uint64_t a = n * t / threads, b = n * (t + 1) / threads;
+        if (a < b) pool.emplace_back(work, a, b);
+    }
+    for (auto &th : pool) th.join();
+    close(fd);
+    if (failed) throw Error(MCAAT_E_IO, std::string("write failed: ") + path);
 }
 
 }  // namespace mcaat

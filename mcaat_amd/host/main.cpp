@@ -3,6 +3,8 @@
 // (step 6), spacer ordering (step 7), results / benchmark (step 8) and CRISPRAnalyzer, which
 // writes settings.output_file (CRISPR_Arrays.txt). The cycles themselves are also written to
 // <cycles_folder>/cycles.txt (not in the reference's release build).
+#include <chrono>
+#include <cstdio>
 #include <filesystem>
 #include <fstream>
 #include <iostream>
@@ -55,13 +57,34 @@ int main(int argc, char **argv) {
             fs::remove_all(settings.output_folder);
             return 1;
         }
+        {
+            // the GPU named by --gpu must exist (also brings the HIP runtime up before the span)
+            int n_dev = 0;
+            mcaat_check(mcaat_device_count(&n_dev), "mcaat_device_count");
+            if (settings.gpu < 0 || settings.gpu >= n_dev)
+                throw std::runtime_error("Error: --gpu " + std::to_string(settings.gpu) + " but " +
+                                         std::to_string(n_dev) + " GPU(s) visible");
+        }
+        using clk = std::chrono::steady_clock;
+        const auto t_start = clk::now();
         SDBGBuild sdbg_build(settings);                        // main.cpp:517
+        const auto t_built = clk::now();
         SDBG sdbg;                                             // main.cpp:522-530
         sdbg.LoadFromDevice(sdbg_build.release_graph());
         std::cout << "Loaded the graph" << std::endl;
         settings.sdbg = &sdbg;
         std::cout << "FBCE START:" << std::endl;
         CycleFinder cycle_finder(settings);                    // main.cpp:536
+        {
+            // the reference's hot-path span, SDBGBuild start -> CycleFinder end (main.cpp:517-536)
+            const auto t_end = clk::now();
+            auto sec = [](clk::duration d) { return std::chrono::duration<double>(d).count(); };
+            char line[256];
+            snprintf(line, sizeof line,
+                     "TIMING span_s=%.6f sdbg_build_s=%.6f build_lib_s=%.6f cycle_finder_s=%.6f",
+                     sec(t_end - t_start), sec(t_built - t_start), sdbg_build.lib_seconds, sec(t_end - t_built));
+            std::cout << line << std::endl;
+        }
         auto cycles_map = cycle_finder.results;
         std::cout << "Number of nodes in results: " << cycles_map.size() << std::endl;
         auto cycles = cycles_map_to_cycles(cycles_map);        // main.cpp:542

@@ -2,6 +2,7 @@
 #include "mcaat_host.h"
 
 #include <algorithm>
+#include <chrono>
 #include <filesystem>
 #include <fstream>
 #include <iostream>
@@ -29,7 +30,9 @@ mcaat_ctx *mcaat_host_ctx(int device) {
 
 // ---------------------------------------------------------------- SDBGBuild
 SDBGBuild::SDBGBuild(Settings s) : settings(s) {
+    const auto t0 = std::chrono::steady_clock::now();
     BuildLib();
+    lib_seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     BuildSDBG();
 }
 

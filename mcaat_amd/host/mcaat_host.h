@@ -34,6 +34,7 @@ class SDBGBuild {
         graph_ = nullptr;
         return g;
     }
+    double lib_seconds = 0;  // BuildLib wall time (FASTQ -> 2-bit reads in HBM)
 
    private:
     std::string WriteLibFile();

@@ -109,6 +109,7 @@ SIGNATURES = {
     "mcaat_mapped_get": (C.c_int, [C.c_void_p, _u64p, C.POINTER(_u64p), C.POINTER(_u64p), C.POINTER(_u64p)]),
     "mcaat_mapped_free": (None, [C.c_void_p]),
     "mcaat_set_knob": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
+    "mcaat_reads_write_fastq": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),
     "mcaat_graph_download_range": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, _u64p, _u16p, _u8p]),
 }
 
@@ -318,6 +319,10 @@ class Reads:
         packed = np.zeros((int(offsets[-1]) + 31) // 32 + 1, dtype=np.uint64)
         _check(self.ctx._lib.mcaat_reads_records_download(self.h, _ptr(packed, _u64p), _ptr(offsets, _u64p)))
         return packed, offsets
+
+    def write_fastq(self, path: str, threads: int = 8) -> None:
+        """The counting view as 4-line FASTQ (mcaat_reads_write_fastq)."""
+        _check(self.ctx._lib.mcaat_reads_write_fastq(self.h, path.encode(), threads))
 
     def free(self) -> None:
         if self.h:

@@ -60,6 +60,7 @@ _SIG = {
     "oracle_cf_candidates": (None, [C.c_void_p, _u64p, _i32p]),
     "oracle_cf_free": (None, [C.c_void_p]),
     "oracle_free": (None, [C.c_void_p]),
+    "oracle_read_fastq": (C.c_uint64, [C.c_char_p, C.POINTER(_u64p), _u64p, C.POINTER(_u64p)]),
 }
 _lib = None
 
@@ -97,6 +98,20 @@ def count_canonical(packed: np.ndarray, offsets: np.ndarray, k: int, threads: in
     lib().oracle_free(C.cast(kp, C.c_void_p))
     lib().oracle_free(C.cast(cp, C.c_void_p))
     return keys, counts
+
+
+def read_fastq(path: str) -> Tuple[np.ndarray, np.ndarray]:
+    """4-line FASTQ -> (packed, offsets), reads split at non-ACGT (C parser, test/baseline only)."""
+    pp, op = _u64p(), _u64p()
+    nw = C.c_uint64(0)
+    n = lib().oracle_read_fastq(path.encode(), C.byref(pp), C.byref(nw), C.byref(op))
+    if n == (1 << 64) - 1:
+        raise ValueError(f"oracle_read_fastq failed on {path}")
+    packed = np.ctypeslib.as_array(pp, shape=(max(nw.value, 1),))[: nw.value].copy()
+    offs = np.ctypeslib.as_array(op, shape=(n + 1,)).copy()
+    lib().oracle_free(C.cast(pp, C.c_void_p))
+    lib().oracle_free(C.cast(op, C.c_void_p))
+    return packed, offs
 
 
 def reverse_pair_ends(s: str) -> str:

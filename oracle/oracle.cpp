@@ -475,6 +475,57 @@ uint64_t oracle_count_canonical(const uint64_t *packed, const uint64_t *offsets,
     return n;
 }
 
+uint64_t oracle_read_fastq(const char *path, uint64_t **packed, uint64_t *n_words, uint64_t **offsets) {
+    FILE *f = fopen(path, "rb");
+    if (!f) return ~0ULL;
+    vector<uint64_t> words, offs{0};
+    uint64_t nb = 0;
+    auto put = [&](int c) {
+        if ((nb & 31) == 0) words.push_back(0);
+        words.back() |= (uint64_t)c << (2 * (nb & 31));
+        ++nb;
+    };
+    auto close_read = [&]() { if (nb != offs.back()) offs.push_back(nb); };
+    std::vector<char> buf(1 << 24);
+    std::string line;
+    uint64_t lineno = 0;
+    bool bad = false;
+    size_t got;
+    auto on_line = [&](const std::string &l) {
+        const uint64_t r = lineno++ & 3;
+        if (r == 0 && (l.empty() || l[0] != '@')) bad = true;
+        if (r != 1) return;
+        for (char ch : l) {
+            const int c = ch == 'A' || ch == 'a' ? 0 : ch == 'C' || ch == 'c' ? 1 : ch == 'G' || ch == 'g' ? 2
+                          : ch == 'T' || ch == 't' ? 3 : -1;
+            if (c < 0) close_read();
+            else put(c);
+        }
+        close_read();
+    };
+    while ((got = fread(buf.data(), 1, buf.size(), f)) > 0) {
+        size_t a = 0;
+        for (size_t i = 0; i < got; ++i)
+            if (buf[i] == '\n') {
+                line.append(buf.data() + a, i - a);
+                if (!line.empty() && line.back() == '\r') line.pop_back();
+                on_line(line);
+                line.clear();
+                a = i + 1;
+            }
+        line.append(buf.data() + a, got - a);
+    }
+    if (!line.empty()) on_line(line);
+    fclose(f);
+    if (bad || (lineno & 3) != 0) return ~0ULL;
+    *n_words = words.size();
+    *packed = (uint64_t *)malloc(8 * (words.size() ? words.size() : 1));
+    if (!words.empty()) memcpy(*packed, words.data(), 8 * words.size());
+    *offsets = (uint64_t *)malloc(8 * offs.size());
+    memcpy(*offsets, offs.data(), 8 * offs.size());
+    return offs.size() - 1;
+}
+
 oracle_graph *oracle_build(const uint64_t *packed, const uint64_t *offsets, uint64_t n_reads, int k, int threads) {
     uint64_t *ck = nullptr; uint32_t *cc = nullptr;
     uint64_t n = oracle_count_canonical(packed, offsets, n_reads, k, threads, &ck, &cc);

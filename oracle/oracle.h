@@ -92,6 +92,12 @@ void oracle_cf_free(oracle_cf_result *r);
 
 void oracle_free(void *p);
 
+/* 4-line FASTQ -> packed 2-bit reads, split at non-ACGT symbols (the counting view of
+ * DESIGN.md §2; the CPU leg of the reference's BuildLib, sdbg_build.cpp:82-115). Returns the
+ * number of reads; *packed (n_words) and *offsets (n_reads+1) malloc'ed, free with oracle_free;
+ * (uint64_t)-1 on an I/O or format error. */
+uint64_t oracle_read_fastq(const char *path, uint64_t **packed, uint64_t *n_words, uint64_t **offsets);
+
 /* Relevant reads (reads.cpp:20-130). reverse_pair_ends_sequence in place (reads.cpp:20-31);
  * get_reads over sequences seqs[0..n_file1) of the first file and the rest of the second
  * (reversed and complemented): returns the number of reads, node ids in *flat with

@@ -274,3 +274,25 @@ def test_get_reads_restatement_small():
     want0 = [ibs(seqs[0][i:i + k]) for i in range(len(seqs[0]) - k + 1)]
     want2 = [ibs("ACGTNCGGTCAG"[i:i + k]) for i in range(12 - k + 1)]
     assert got == [want0, want2]
+
+
+def test_oracle_c_fastq_reader_matches_fastx_restatement(tmp_path):
+    """The C FASTQ reader of the CPU baseline (oracle_read_fastq) gives the counting view of
+    the Python restatement (oracle/fastx.py): reads split at non-ACGT, lowercase, CRLF."""
+    from oracle import fastx as FX
+
+    rng = np.random.default_rng(9)
+    seqs = ["".join(rng.choice(list("ACGTacgtN"), size=int(rng.integers(0, 200)))) for _ in range(300)]
+    text = "".join(f"@r{i}\n{s}\n+\n{'I' * len(s)}\n" for i, s in enumerate(seqs))
+    for crlf in (False, True):
+        f = tmp_path / f"x{int(crlf)}.fq"
+        f.write_bytes((text.replace("\n", "\r\n") if crlf else text).encode())
+        packed, offs = O.read_fastq(str(f))
+        want_p, want_o = FX.pack_bases(FX.counting_view(FX.fastq_sequences(text)))
+        assert np.array_equal(offs, want_o)
+        nw = (int(want_o[-1]) + 31) // 32
+        assert packed.size == nw and np.array_equal(packed, want_p[:nw])
+    bad = tmp_path / "bad.fq"
+    bad.write_text("@r\nACGT\n+\n")
+    with pytest.raises(ValueError):
+        O.read_fastq(str(bad))
