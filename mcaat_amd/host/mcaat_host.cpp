@@ -93,12 +93,11 @@ SDBG::~SDBG() {
 void SDBG::LoadFromDevice(mcaat_graph *g) {
     if (g_ && g_ != g) mcaat_graph_free(g_);
     g_ = g;
-    uint64_t D = 0;
-    mcaat_check(mcaat_graph_info(g_, &k_, &D), "mcaat_graph_info");
-    key_.resize(D);
-    mult_.resize(D);
-    valid_.resize(D);
-    mcaat_check(mcaat_graph_download(g_, key_.data(), mult_.data(), valid_.data()), "mcaat_graph_download");
+    mcaat_check(mcaat_graph_info(g_, &k_, &D_), "mcaat_graph_info");
+    have_arrays_ = have_valid_ = false;
+    std::vector<uint64_t>().swap(key_);
+    std::vector<uint16_t>().swap(mult_);
+    std::vector<uint8_t>().swap(valid_);
 }
 
 void SDBG::LoadFromArrays(int k, std::vector<uint64_t> keys, std::vector<uint16_t> mult,
@@ -108,36 +107,69 @@ void SDBG::LoadFromArrays(int k, std::vector<uint64_t> keys, std::vector<uint16_
     if (g_) mcaat_graph_free(g_);
     g_ = nullptr;
     k_ = k;
+    D_ = keys.size();
     key_ = std::move(keys);
     mult_ = std::move(mult);
     valid_ = std::move(valid);
+    have_arrays_ = have_valid_ = true;
+}
+
+const std::vector<uint64_t> &SDBG::host_key() const {
+    if (!have_arrays_ && g_) {
+        key_.resize(D_);
+        mult_.resize(D_);
+        mcaat_check(mcaat_graph_download(g_, key_.data(), mult_.data(), nullptr), "mcaat_graph_download");
+        have_arrays_ = true;
+    }
+    return key_;
+}
+
+const std::vector<uint16_t> &SDBG::host_mult() const {
+    host_key();
+    return mult_;
+}
+
+const std::vector<uint8_t> &SDBG::host_valid() const {
+    if (!have_valid_ && g_) {
+        valid_.resize(D_);
+        mcaat_check(mcaat_graph_download(g_, nullptr, nullptr, valid_.data()), "mcaat_graph_download");
+        have_valid_ = true;
+    }
+    return valid_;
 }
 
 void SDBG::SyncFromDevice() {
-    if (g_) mcaat_check(mcaat_graph_download(g_, nullptr, nullptr, valid_.data()), "mcaat_graph_download");
+    if (g_) have_valid_ = false;  // re-read on the next host query
 }
 
 void SDBG::KeepOnly(const std::vector<uint64_t> &ids) {
-    std::vector<uint8_t> keep(valid_.size(), 0);
-    for (uint64_t e : ids)
-        if (e < keep.size()) keep[e] = 1;
-    for (size_t e = 0; e < valid_.size(); ++e) valid_[e] &= keep[e];
+    if (have_valid_ || !g_) {
+        std::vector<uint8_t> keep(valid_.size(), 0);
+        for (uint64_t e : ids)
+            if (e < keep.size()) keep[e] = 1;
+        for (size_t e = 0; e < valid_.size(); ++e) valid_[e] &= keep[e];
+    }
     if (g_) mcaat_check(mcaat_graph_keep_only(g_, ids.data(), ids.size()), "mcaat_graph_keep_only");
 }
 
 void SDBG::SetInvalidEdge(uint64_t e) {
-    valid_[e] = 0;
+    if (have_valid_ || !g_) valid_[e] = 0;
     if (g_) mcaat_check(mcaat_graph_set_valid(g_, &e, 1, 0), "mcaat_graph_set_valid");
 }
 
 void SDBG::SetValidEdge(uint64_t e) {
-    valid_[e] = 1;
+    if (have_valid_ || !g_) valid_[e] = 1;
     if (g_) mcaat_check(mcaat_graph_set_valid(g_, &e, 1, 1), "mcaat_graph_set_valid");
 }
 
-uint64_t SDBG::lower(uint64_t q) const { return std::lower_bound(key_.begin(), key_.end(), q) - key_.begin(); }
+uint64_t SDBG::lower(uint64_t q) const {
+    const auto &key = host_key();
+    return std::lower_bound(key.begin(), key.end(), q) - key.begin();
+}
 
 int SDBG::OutgoingEdges(uint64_t e, uint64_t *out) const {
+    const auto &key_ = host_key();
+    const auto &valid_ = host_valid();
     const uint64_t K = key_[e], W = K & 3, R = K >> 2;
     const uint64_t Rt = (W << (2 * (k_ - 1))) | (R >> 2);
     uint64_t tmp[4];
@@ -149,6 +181,8 @@ int SDBG::OutgoingEdges(uint64_t e, uint64_t *out) const {
 }
 
 int SDBG::IncomingEdges(uint64_t e, uint64_t *in) const {
+    const auto &key_ = host_key();
+    const auto &valid_ = host_valid();
     const uint64_t K = key_[e];
     const uint64_t c = (K >> (2 * k_)) & 3;
     const uint64_t G = (K >> 2) & ((1ULL << (2 * (k_ - 1))) - 1);
@@ -173,7 +207,7 @@ void SDBG::NeighborsBatch(const std::vector<uint64_t> &ids, bool incoming, std::
 }
 
 uint32_t SDBG::GetLabel(uint64_t e, uint8_t *seq) const {
-    const uint64_t R = key_[e] >> 2;
+    const uint64_t R = host_key()[e] >> 2;
     for (int i = 0; i < k_; ++i) seq[i] = (uint8_t)(((R >> (2 * i)) & 3) + 1);
     return (uint32_t)k_;
 }
@@ -181,6 +215,7 @@ uint32_t SDBG::GetLabel(uint64_t e, uint8_t *seq) const {
 int64_t SDBG::IndexBinarySearch(const uint8_t *seq) const {
     uint64_t R = 0;
     for (int i = 0; i < k_; ++i) R |= (uint64_t)((seq[i] - 1) & 3) << (2 * i);
+    const auto &key_ = host_key();
     int64_t last = -1;
     for (uint64_t i = lower(R << 2); i < size() && (key_[i] >> 2) == R; ++i) last = (int64_t)i;
     return last;

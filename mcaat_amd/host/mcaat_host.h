@@ -63,12 +63,12 @@ class SDBG {
     void KeepOnly(const std::vector<uint64_t> &ids);
     mcaat_graph *device() const { return g_; }
 
-    uint64_t size() const { return key_.size(); }
+    uint64_t size() const { return D_; }
     int k() const { return k_; }
-    bool IsValidEdge(uint64_t e) const { return valid_[e] != 0; }
+    bool IsValidEdge(uint64_t e) const { return host_valid()[e] != 0; }
     void SetInvalidEdge(uint64_t e);
     void SetValidEdge(uint64_t e);
-    uint16_t EdgeMultiplicity(uint64_t e) const { return mult_[e]; }
+    uint16_t EdgeMultiplicity(uint64_t e) const { return host_mult()[e]; }
     int OutgoingEdges(uint64_t e, uint64_t *out) const;  // descending ids
     int IncomingEdges(uint64_t e, uint64_t *in) const;   // ascending ids
     int EdgeOutdegree(uint64_t e) const {
@@ -90,11 +90,19 @@ class SDBG {
 
    private:
     uint64_t lower(uint64_t q) const;
+    // The host arrays are materialised from the device graph on the first host-side query
+    // (none of the hot path needs them: CycleFinder runs on the device), and the valid bytes
+    // are re-read after a device-side mutation.
+    const std::vector<uint64_t> &host_key() const;
+    const std::vector<uint16_t> &host_mult() const;
+    const std::vector<uint8_t> &host_valid() const;
     mcaat_graph *g_ = nullptr;
     int k_ = 0;
-    std::vector<uint64_t> key_;
-    std::vector<uint16_t> mult_;
-    std::vector<uint8_t> valid_;
+    uint64_t D_ = 0;
+    mutable bool have_arrays_ = false, have_valid_ = false;
+    mutable std::vector<uint64_t> key_;
+    mutable std::vector<uint16_t> mult_;
+    mutable std::vector<uint8_t> valid_;
 };
 
 // Reference: CycleFinder(Settings&) runs FindApproximateCRISPRArrays in the constructor and
