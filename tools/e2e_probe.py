@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--reads", type=int, default=0)
     ap.add_argument("--variants", default="")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--settle", type=float, default=0.0, help="seconds to wait after writing the FASTQ")
+    ap.add_argument("--preread", action="store_true", help="read the file once (8 threads) before the runs")
     a = ap.parse_args()
     cfg = bench.CONFIGS[a.config]
     spec = M.SynthSpec(**cfg["spec"].__dict__)
@@ -38,6 +40,29 @@ def main():
         r.write_fastq(path, threads=bench.host_threads())
         print(f"wrote {os.path.getsize(path) / 1e9:.1f} GB in {time.perf_counter() - t0:.1f} s", flush=True)
         r.free()
+    if a.settle:
+        time.sleep(a.settle)
+        print(f"settled {a.settle} s", flush=True)
+    if a.preread:
+        import concurrent.futures as cf
+
+        size = os.path.getsize(path)
+        piece = (size + 7) // 8
+
+        def rd(i):
+            with open(path, "rb", buffering=0) as f:
+                f.seek(i * piece)
+                left = min(piece, size - i * piece)
+                while left > 0:
+                    b = f.read(min(left, 64 << 20))
+                    if not b:
+                        break
+                    left -= len(b)
+
+        t0 = time.perf_counter()
+        with cf.ThreadPoolExecutor(8) as ex:
+            list(ex.map(rd, range(8)))
+        print(f"pre-read {size / 1e9:.1f} GB in {time.perf_counter() - t0:.2f} s", flush=True)
     work = tempfile.mkdtemp(dir="/tmp")
     try:
         st = os.path.join(work, "s.txt")
