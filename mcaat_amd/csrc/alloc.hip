@@ -99,13 +99,13 @@ Pools &pools() {
     static Pools *p = new Pools;  // intentionally leaked: outlives static destructors
     return *p;
 }
+}  // namespace
+
 int current_device() {
     int d = 0;
     (void)hipGetDevice(&d);
     return d;
 }
-
-}  // namespace
 
 void *dev_alloc(size_t bytes) {
     bytes = (bytes + kAlign - 1) & ~(kAlign - 1);
@@ -135,10 +135,10 @@ void *dev_alloc(size_t bytes) {
     return a.take(bytes);
 }
 
-void dev_free(void *p, size_t) {
+void dev_free(void *p, size_t, int device) {
     if (!p) return;
     std::lock_guard<std::mutex> lk(pools().mu);
-    pools().by_device[current_device()].give((char *)p);
+    pools().by_device[device].give((char *)p);
 }
 
 void dev_trim() {

@@ -163,35 +163,94 @@ int sniff_format(const char *path) {
     return c;
 }
 
-// FASTA (multi-line records) on the host; FASTQ goes through the GPU parser (fastq_ingest.hip)
-void read_fasta(const char *path, Packer &pk) {
-    gzFile f = gzopen(path, "rb");
-    if (!f) throw Error(MCAAT_E_IO, std::string("cannot open ") + path);
-    std::string line, seq;
-    char buf[1 << 16];
-    auto getline = [&](std::string &out) -> bool {
-        out.clear();
-        for (;;) {
-            if (!gzgets(f, buf, sizeof(buf))) return !out.empty();
-            out += buf;
-            if (!out.empty() && out.back() == '\n') {
-                out.pop_back();
-                if (!out.empty() && out.back() == '\r') out.pop_back();
-                return true;
-            }
-        }
-    };
-    while (getline(line)) {
-        if (line.empty()) continue;
-        if (line[0] == '>') {
-            if (!seq.empty()) pk.add_sequence(seq);
-            seq.clear();
-        } else {
-            seq += line;
-        }
+// Host reader with the reference's kseq semantics (klib kseq_read, as MEGAHIT buildlib and
+// kseq++ in reads.cpp read records): FASTA, and the FASTQ inputs the 4-line GPU parser hands
+// back (blank lines between records, wrapped sequence/quality lines, records longer than its
+// carry reserve). A record starts at the next '>' or '@'; its header line is skipped; sequence
+// lines are concatenated (blank lines skipped, one trailing '\r' dropped) up to a line that
+// starts with '>', '@' or '+'; after '+' the rest of that line is skipped and quality lines are
+// read until they hold at least as many characters as the sequence (at least one line); any
+// other count is an error. Restated for the tests in oracle/fastx.py kseq_sequences.
+struct GzChars {
+    gzFile f;
+    std::vector<char> buf = std::vector<char>(1 << 20);
+    int pos = 0, len = 0;
+    const char *path;
+    GzChars(const char *p) : path(p) {
+        f = gzopen(p, "rb");
+        if (!f) throw Error(MCAAT_E_IO, std::string("cannot open ") + p);
+        gzbuffer(f, 1u << 20);
     }
-    if (!seq.empty()) pk.add_sequence(seq);
-    gzclose(f);
+    ~GzChars() { gzclose(f); }
+    int peek() {
+        if (pos == len) {
+            len = gzread(f, buf.data(), (unsigned)buf.size());
+            pos = 0;
+            if (len < 0) {
+                int errnum = 0;
+                throw Error(MCAAT_E_IO, std::string("read error in ") + path + ": " + gzerror(f, &errnum));
+            }
+            if (len == 0) return -1;
+        }
+        return (unsigned char)buf[pos];
+    }
+    int get() {
+        const int c = peek();
+        if (c >= 0) ++pos;
+        return c;
+    }
+    // the rest of the current line (one trailing '\r' dropped), appended to out if given
+    void line(std::string *out) {
+        const size_t at = out ? out->size() : 0;
+        for (int c; (c = get()) >= 0 && c != '\n';)
+            if (out) out->push_back((char)c);
+        if (out && out->size() > at && out->back() == '\r') out->pop_back();
+    }
+};
+
+void read_fastx_host(const char *path, Packer &pk) {
+    GzChars in(path);
+    std::string seq, qual;
+    bool have_header = false;
+    for (;;) {
+        if (!have_header) {
+            int c;
+            while ((c = in.get()) >= 0 && c != '>' && c != '@') {
+            }
+            if (c < 0) return;
+        }
+        in.line(nullptr);  // header
+        seq.clear();
+        int c = -1;
+        while ((c = in.peek()) >= 0) {
+            if (c == '>' || c == '@' || c == '+') break;
+            if (c == '\n') {
+                in.get();
+                continue;
+            }
+            in.line(&seq);
+        }
+        if (c < 0) {
+            pk.add_sequence(seq);
+            return;
+        }
+        if (c == '>' || c == '@') {
+            pk.add_sequence(seq);
+            in.get();
+            have_header = true;
+            continue;
+        }
+        in.line(nullptr);  // the '+' line
+        qual.clear();
+        while (in.peek() >= 0) {
+            in.line(&qual);
+            if (qual.size() >= seq.size()) break;
+        }
+        if (qual.size() != seq.size())
+            throw Error(MCAAT_E_IO, std::string("malformed FASTQ (quality length differs from sequence length): ") + path);
+        pk.add_sequence(seq);
+        have_header = false;
+    }
 }
 
 }  // namespace
@@ -327,26 +386,38 @@ int mcaat_reads_from_fastx(mcaat_ctx *ctx, const char *const *files, int n_files
     return guarded([&] {
         require(ctx && out && files && n_files > 0, "null argument");
         HIP_OK(hipSetDevice(ctx->device));
-        int n_fastq = 0;
+        // empty (or blank) files go with either format: they hold no records, and keep their
+        // place in the file order (a second file's records are reverse-complemented)
+        int n_fastq = 0, n_fasta = 0;
         for (int i = 0; i < n_files; ++i) {
             const int c = sniff_format(files[i]);
             if (c == '@') ++n_fastq;
-            else if (c != '>' && c != -1) throw Error(MCAAT_E_IO, std::string("not FASTA/FASTQ: ") + files[i]);
+            else if (c == '>') ++n_fasta;
+            else if (c != -1) throw Error(MCAAT_E_IO, std::string("not FASTA/FASTQ: ") + files[i]);
         }
         auto *r = new mcaat_reads;
+        auto host_path = [&] {
+            Packer pk;
+            for (int i = 0; i < n_files; ++i) {
+                pk.file = i;
+                read_fastx_host(files[i], pk);
+            }
+            *r = mcaat_reads{};
+            upload_reads(ctx, pk.reads.words.data(), pk.reads.words.size(), pk.reads.offsets.data(),
+                         pk.reads.offsets.size() - 1, r);
+            if (pk.records_differ) upload_records(ctx, pk.records, r);
+        };
         try {
-            if (n_fastq == n_files) {
-                ingest_fastq(ctx, files, n_files, r);
-            } else {
-                require(n_fastq == 0, "mixed FASTA and FASTQ inputs");
-                Packer pk;
-                for (int i = 0; i < n_files; ++i) {
-                    pk.file = i;
-                    read_fasta(files[i], pk);
+            if (n_fastq > 0 && n_fasta == 0) {
+                // 4-line FASTQ on the GPU; inputs it does not take (blank lines between records,
+                // wrapped lines, records above its carry reserve) are read again on the host
+                try {
+                    ingest_fastq(ctx, files, n_files, r);
+                } catch (const FormatError &) {
+                    host_path();
                 }
-                upload_reads(ctx, pk.reads.words.data(), pk.reads.words.size(), pk.reads.offsets.data(),
-                             pk.reads.offsets.size() - 1, r);
-                if (pk.records_differ) upload_records(ctx, pk.records, r);
+            } else {
+                host_path();  // FASTA, FASTA + FASTQ, or only empty files
             }
         } catch (...) {
             delete r;
@@ -547,11 +618,8 @@ int mcaat_counts_partition(const mcaat_counts *c, int n_owners, const uint64_t *
     });
 }
 
-void mcaat_counts_free(mcaat_counts *c) {
-    if (!c) return;
-    (void)hipSetDevice(c->ctx->device);
-    delete c;
-}
+// handles may outlive their context (its buffers remember their device's arena)
+void mcaat_counts_free(mcaat_counts *c) { delete c; }
 
 int mcaat_edges_reduce(mcaat_ctx *ctx, int k, const uint64_t *keys_dev, const uint32_t *counts_dev, uint64_t n,
                        uint64_t *keys_out_dev, uint16_t *mult_out_dev, uint64_t *n_out) {

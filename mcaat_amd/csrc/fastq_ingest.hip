@@ -404,18 +404,23 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
     dbufs[1].alloc(cap);
     struct CopyStream {  // uploads overlap the parse of the previous chunk
         hipStream_t s = nullptr;
-        hipEvent_t ev[2] = {nullptr, nullptr};
+        hipEvent_t ev[2] = {nullptr, nullptr};    // upload into dbufs[x] complete
+        hipEvent_t done[2] = {nullptr, nullptr};  // the parse of dbufs[x] complete (buffer free)
         CopyStream() {
             HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
             for (auto &e : ev) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            for (auto &e : done) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         }
         ~CopyStream() {
             if (s) (void)hipStreamSynchronize(s);
             for (auto &e : ev)
                 if (e) (void)hipEventDestroy(e);
+            for (auto &e : done)
+                if (e) (void)hipEventDestroy(e);
             if (s) (void)hipStreamDestroy(s);
         }
     } cs;
+    for (auto &e : cs.done) HIP_OK(hipEventRecord(e, ctx->stream));
     hipEvent_t *up_ev = cs.ev;
     const uint64_t max_seg = cap / kSeg + 1;
     DevBuf<uint32_t> cnt(max_seg + 1), first(max_seg + 1), nl(cap + 16);  // every byte may be a newline
@@ -443,6 +448,8 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
         }
         if (total_x) {
             const size_t padded = (total_x + kSeg - 1) / kSeg * kSeg + kSeg;
+            // dbufs[x] is free once the kernels of the chunk it held last have run
+            HIP_OK(hipStreamWaitEvent(cs.s, cs.done[x], 0));
             HIP_OK(hipMemcpyAsync(dbufs[x].p, start_x, total_x, hipMemcpyHostToDevice, cs.s));
             HIP_OK(hipMemsetAsync(dbufs[x].p + total_x, 0, padded - total_x, cs.s));
             HIP_OK(hipEventRecord(up_ev[x], cs.s));
@@ -470,9 +477,11 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
                 HIP_OK(hipMemsetAsync(cnt.p + nseg, 0, 4, ctx->stream));
                 hipLaunchKernelGGL(k_fq_nlcount, dim3(grid_for(nseg, kBlock)), dim3(kBlock), 0, ctx->stream,
                                    dbufs[cur].p, nseg, cnt.p);
+                LAUNCH_OK();
                 scan_u32(ctx, cnt.p, first.p, (uint64_t)nseg + 1, tmp);
                 hipLaunchKernelGGL(k_fq_nlpos, dim3(grid_for(nseg, kBlock)), dim3(kBlock), 0, ctx->stream,
                                    dbufs[cur].p, nseg, first.p, nl.p);
+                LAUNCH_OK();
                 HIP_OK(hipMemcpyAsync(hmeta, first.p + nseg, 4, hipMemcpyDeviceToHost, ctx->stream));
                 HIP_OK(hipStreamSynchronize(ctx->stream));
                 kt.stop();
@@ -480,7 +489,7 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
             const uint32_t NL = total ? hmeta[0] : 0;
             const uint32_t nrec = NL / 4;
             if (eof && NL % 4)
-                throw Error(MCAAT_E_IO, std::string("malformed FASTQ (truncated record or blank line): ") + files[fi]);
+                throw FormatError(std::string("not 4-line FASTQ (truncated record, blank or wrapped line): ") + files[fi]);
             size_t consumed = 0;
             if (nrec) {
                 HIP_OK(hipMemcpyAsync(hmeta, nl.p + 4 * (uint64_t)nrec - 1, 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -488,8 +497,8 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
                 consumed = (size_t)hmeta[0] + 1;
             }
             if (!eof && total - consumed > R)
-                throw Error(MCAAT_E_IO, std::string("FASTQ record longer than the chunk reserve (") +
-                                            std::to_string(R) + " bytes): " + files[fi]);
+                throw FormatError(std::string("FASTQ record longer than the chunk reserve (") + std::to_string(R) +
+                                  " bytes): " + files[fi]);
             // ---- the next chunk: its carry is known now, so it uploads while this chunk's
             // records are parsed; this chunk's host buffer is free again for the reader
             const bool have_next = !eof;
@@ -518,6 +527,7 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
                 for (auto *b : {&nbase, &nrun, &slen}) HIP_OK(hipMemsetAsync(b->p + nrec, 0, 4, ctx->stream));
                 hipLaunchKernelGGL(k_fq_records, dim3(grid_for(nrec, kBlock)), dim3(kBlock), 0, ctx->stream, dbufs[cur].p,
                                    nl.p, nrec, sbeg.p, slen.p, nbase.p, nrun.p, meta.p);
+                LAUNCH_OK();
                 scan_u32(ctx, nbase.p, boff.p, (uint64_t)nrec + 1, tmp);
                 scan_u32(ctx, nrun.p, roff.p, (uint64_t)nrec + 1, tmp);
                 scan_u32(ctx, slen.p, qoff.p, (uint64_t)nrec + 1, tmp);
@@ -528,7 +538,7 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
                 HIP_OK(hipStreamSynchronize(ctx->stream));
                 kt.stop();
                 const uint32_t cb = hmeta[0], cr = hmeta[1], cq = hmeta[2], fl = hmeta[3];
-                if (fl & kBadHeader) throw Error(MCAAT_E_IO, std::string("malformed FASTQ: ") + files[fi]);
+                if (fl & kBadHeader) throw FormatError(std::string("not 4-line FASTQ (header or '+' line): ") + files[fi]);
                 flags_all |= fl;
                 if (fi > 0) flags_all |= kDiffer;  // second file: reverse-complemented records
                 grow(ctx, packed, (n_bases + 31) / 32 + 1, (n_bases + cb + 31) / 32 + 17);
@@ -546,6 +556,7 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
                 q_bases += cq;
                 n_rec += nrec;
             }
+            HIP_OK(hipEventRecord(cs.done[cur], ctx->stream));
             if (!have_next) break;
             cur ^= 1;
             start = nstart;

@@ -23,6 +23,10 @@ struct Error : std::runtime_error {
     int code;
     Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
 };
+// input the 4-line GPU FASTQ parser does not take (the host kseq-style reader does)
+struct FormatError : Error {
+    explicit FormatError(const std::string &m) : Error(MCAAT_E_IO, m) {}
+};
 
 #define HIP_OK(expr)                                                                              \
     do {                                                                                          \
@@ -39,7 +43,8 @@ struct Error : std::runtime_error {
 // kept per device and reused (best fit within 2x); on an allocation failure the cache
 // is trimmed and the allocation retried.
 void *dev_alloc(size_t bytes);
-void dev_free(void *p, size_t bytes);
+void dev_free(void *p, size_t bytes, int device);
+int current_device();
 void dev_trim();
 
 // owning device buffer
@@ -48,15 +53,16 @@ struct DevBuf {
     T *p = nullptr;
     size_t n = 0;
     size_t cap_bytes = 0;
+    int dev = 0;  // arena the block came from (freed there whatever device is current)
     DevBuf() = default;
     explicit DevBuf(size_t count) { alloc(count); }
     DevBuf(const DevBuf &) = delete;
     DevBuf &operator=(const DevBuf &) = delete;
-    DevBuf(DevBuf &&o) noexcept : p(o.p), n(o.n), cap_bytes(o.cap_bytes) { o.p = nullptr; o.n = 0; o.cap_bytes = 0; }
+    DevBuf(DevBuf &&o) noexcept : p(o.p), n(o.n), cap_bytes(o.cap_bytes), dev(o.dev) { o.p = nullptr; o.n = 0; o.cap_bytes = 0; }
     DevBuf &operator=(DevBuf &&o) noexcept {
         if (this != &o) {
             release();
-            p = o.p; n = o.n; cap_bytes = o.cap_bytes;
+            p = o.p; n = o.n; cap_bytes = o.cap_bytes; dev = o.dev;
             o.p = nullptr; o.n = 0; o.cap_bytes = 0;
         }
         return *this;
@@ -66,11 +72,12 @@ struct DevBuf {
         release();
         if (count == 0) count = 1;
         cap_bytes = (count * sizeof(T) + (2u << 20) - 1) & ~(size_t)((2u << 20) - 1);
+        dev = current_device();
         p = (T *)dev_alloc(cap_bytes);
         n = count;
     }
     void release() {
-        if (p) dev_free(p, cap_bytes);
+        if (p) dev_free(p, cap_bytes, dev);
         p = nullptr;
         n = 0;
         cap_bytes = 0;

@@ -58,12 +58,10 @@ int main(int argc, char **argv) {
             return 1;
         }
         {
-            // the GPU named by --gpu must exist (also brings the HIP runtime up before the span)
+            // brings the HIP runtime up before the timed span (errors surface in SDBGBuild, after
+            // it has written data.lib as the reference does)
             int n_dev = 0;
-            mcaat_check(mcaat_device_count(&n_dev), "mcaat_device_count");
-            if (settings.gpu < 0 || settings.gpu >= n_dev)
-                throw std::runtime_error("Error: --gpu " + std::to_string(settings.gpu) + " but " +
-                                         std::to_string(n_dev) + " GPU(s) visible");
+            (void)mcaat_device_count(&n_dev);
         }
         using clk = std::chrono::steady_clock;
         const auto t_start = clk::now();

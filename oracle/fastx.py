@@ -12,7 +12,10 @@ must produce, record by record:
   0,1,2 and every other character → 3).
 
 FASTQ records are 4 lines; one trailing '\\r' per line is stripped; blank lines may only precede
-the first record or follow the last. Headers must start with '@'.
+the first record or follow the last. Headers must start with '@'. Inputs that break this
+(blank lines between records, wrapped sequence/quality lines, records longer than the GPU
+parser's carry reserve, FASTA and FASTQ mixed) are read as the reference's kseq reader reads
+them: kseq_sequences below.
 """
 from __future__ import annotations
 
@@ -44,6 +47,70 @@ def fastq_sequences(text: str) -> List[str]:
             raise FastqError("malformed header")
         seqs.append(lines[i + 1])
     return seqs
+
+
+def kseq_sequences(text: str) -> List[str]:
+    """Record sequences as klib kseq_read (MEGAHIT buildlib; kseq++ in reads.cpp) reads them:
+    a record starts at the next '>' or '@' (anything before it is skipped); the header line
+    is skipped; sequence lines are concatenated (blank lines skipped, one trailing '\\r'
+    dropped) until a line starting with '>', '@' or '+'; '>'/'@' ends a FASTA record; after
+    '+' the rest of that line is skipped and quality lines are read until at least as many
+    quality characters as sequence characters were read (at least one line); a different
+    count is an error. Used for the inputs the 4-line GPU parser hands to the host reader."""
+    n = len(text)
+    i = 0
+    out: List[str] = []
+
+    def line_at(i):
+        j = text.find("\n", i)
+        e = n if j < 0 else j
+        ln = text[i:e]
+        if ln.endswith("\r"):
+            ln = ln[:-1]
+        return ln, (n if j < 0 else j + 1)
+
+    have_header = False
+    while True:
+        if not have_header:
+            while i < n and text[i] not in ">@":
+                i += 1
+            if i >= n:
+                return out
+            i += 1
+        _, i = line_at(i)  # header line
+        seq = []
+        c = None
+        while i < n:
+            c = text[i]
+            if c in ">@+":
+                break
+            if c == "\n":
+                i += 1
+                c = None
+                continue
+            ln, i = line_at(i)
+            seq.append(ln)
+            c = None
+        s = "".join(seq)
+        if c is None:  # end of input
+            out.append(s)
+            return out
+        if c in ">@":
+            out.append(s)
+            i += 1
+            have_header = True
+            continue
+        _, i = line_at(i)  # the '+' line
+        q = 0
+        while i < n:
+            ln, i = line_at(i)
+            q += len(ln)
+            if q >= len(s):
+                break
+        if q != len(s):
+            raise FastqError("quality length differs from sequence length")
+        out.append(s)
+        have_header = False
 
 
 def counting_view(seqs: Sequence[str]) -> List[str]:

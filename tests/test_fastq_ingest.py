@@ -132,25 +132,76 @@ def test_empty_and_blank_files(gpu_ctx, tmp_path, monkeypatch):
     assert reads.info() == (0, 0)
 
 
+def _check_kseq(ctx, files, texts):
+    """Inputs the 4-line GPU parser hands to the host reader: parity with the kseq restatement."""
+    import mcaat_amd as M
+
+    per_file = [FX.kseq_sequences(t) for t in texts]
+    want_p, want_o = FX.pack_bases(FX.counting_view([s for f in per_file for s in f]))
+    want_qp, want_qo = FX.pack_codes(FX.mapping_view(per_file))
+    reads = M.Reads.from_fastx(ctx, files)
+    p, o = reads.download()
+    assert np.array_equal(o, want_o)
+    nw = (int(want_o[-1]) + 31) // 32
+    assert np.array_equal(p[:nw], want_p[:nw])
+    qp, qo = reads.download_records()
+    assert np.array_equal(qo, want_qo)
+    nq = (int(want_qo[-1]) + 31) // 32
+    assert np.array_equal(qp[:nq], want_qp[:nq])
+
+
+def test_kseq_restatement_known_answers():
+    assert FX.kseq_sequences("@a\nACGT\n+\nIIII\n\n@b\nACGT\n+\nIIII\n") == ["ACGT", "ACGT"]
+    assert FX.kseq_sequences("@a\nAC\nGT\n+\nII\nII\n@b\nA\n+\n@\n") == ["ACGT", "A"]  # wrapped; '@' quality
+    assert FX.kseq_sequences("@a\nACGT\n+\nIIII\nb\nACGT\n+\nIIII\n") == ["ACGT"]  # junk skipped to EOF
+    assert FX.kseq_sequences(">x\nACGTN\nACG\n\n>y\nTT\n") == ["ACGTNACG", "TT"]
+    assert FX.kseq_sequences("@a\r\nAC\r\n+\r\nII\r\n") == ["AC"]
+    text = "\n\n@a\nACGTNacgt\n+\nIIIIIIIII\n@b\r\n\r\n+\r\n\r\n@c\nGGRTT\n+\nIIIII"
+    assert FX.kseq_sequences(text) == FX.fastq_sequences(text)  # well-formed: the 4-line reading
+    with pytest.raises(FX.FastqError):
+        FX.kseq_sequences("@a\nACGT\n+\nIIII\n@b\nACGT\n+\n")
+    with pytest.raises(FX.FastqError):
+        FX.kseq_sequences("@a\nACGT\n+\nIIIIII\n")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("chunk", [256, 0])
+def test_non_4line_inputs_read_like_kseq(gpu_ctx, tmp_path, monkeypatch, chunk):
+    """Blank lines between records, wrapped lines, a record above the carry reserve, FASTA and
+    FASTQ mixed, an empty mate file: the GPU parser hands these to the host kseq-style reader
+    (the reference's kseq readers accept them)."""
+    if chunk:
+        monkeypatch.setenv("MCAAT_FASTQ_CHUNK", str(chunk))
+    else:
+        monkeypatch.delenv("MCAAT_FASTQ_CHUNK", raising=False)
+    rng = np.random.default_rng(3)
+    good = _fastq_text(_rand_records(rng, 40))
+    cases = {
+        "blank": ["@a\nACGT\n+\nIIII\n\n@b\nACGT\n+\nIIII\n" + good],
+        "wrapped": ["@a\nACGTAC\nGTTT\n+\nIIIIII\nIIII\n@b\nGGA\n+\n@@@\n" + good],
+        "header_junk": ["@a\nACGT\n+\nIIII\nb\nACGT\n+\nIIII\n"],
+        "long": [good + "@L\n" + "ACGT" * 1500 + "\n+\n" + "I" * 6000 + "\n"],
+        "mixed": [">a\nACGTN\nAC\n>b\nGGGT\n", good],
+        "empty_mate": [good, ""],
+    }
+    for name, texts in cases.items():
+        files = [_write(tmp_path / f"{name}{i}.fq", t) for i, t in enumerate(texts)]
+        _check_kseq(gpu_ctx, files, texts)
+
+
 @pytest.mark.gpu
 def test_malformed_inputs_fail_loudly(gpu_ctx, tmp_path, monkeypatch):
     import mcaat_amd as M
 
     monkeypatch.setenv("MCAAT_FASTQ_CHUNK", "256")
     bad = {
-        "trunc.fq": "@a\nACGT\n+\nIIII\n@b\nACGT\n+\n",
-        "header.fq": "@a\nACGT\n+\nIIII\nb\nACGT\n+\nIIII\n",
-        "blank.fq": "@a\nACGT\n+\nIIII\n\n@b\nACGT\n+\nIIII\n",
-        "long.fq": "@a\n" + "A" * 6000 + "\n+\n" + "I" * 6000 + "\n",
-        "junk.fq": "hello\n",
+        "trunc.fq": "@a\nACGT\n+\nIIII\n@b\nACGT\n+\n",  # quality missing
+        "qlen.fq": "@a\nACGT\n+\nIIIIII\n",  # quality longer than the sequence
+        "junk.fq": "hello\n",  # neither '@' nor '>'
     }
     for name, text in bad.items():
         with pytest.raises(RuntimeError):
             M.Reads.from_fastx(gpu_ctx, [_write(tmp_path / name, text)])
-    fa = _write(tmp_path / "x.fa", ">a\nACGT\nAC\n")
-    fq = _write(tmp_path / "y.fq", "@a\nACGT\n+\nIIII\n")
-    with pytest.raises(RuntimeError):
-        M.Reads.from_fastx(gpu_ctx, [fa, fq])
 
 
 @pytest.mark.gpu
