@@ -159,6 +159,12 @@ __global__ void k_fq_records(const uint8_t *buf, const uint32_t *nl, uint32_t n_
         const uint32_t s = nl[4 * r] + 1;
         uint32_t e = nl[4 * r + 1];
         if (e > s && buf[e - 1] == '\r') --e;
+        // '+' line, and a quality line as long as the sequence: otherwise not 4-line FASTQ
+        // (wrapped lines), which the host kseq-style reader takes
+        const uint32_t qs = nl[4 * r + 2] + 1;
+        uint32_t qe = nl[4 * r + 3];
+        if (qe > qs && buf[qe - 1] == '\r') --qe;
+        if (buf[nl[4 * r + 1] + 1] != '+' || qe - qs != e - s) fl |= kBadHeader;
         uint32_t bases = 0, runs = 0;
         bool in = false, differ = false;
         Fwd rd(buf, s);
