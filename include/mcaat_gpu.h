@@ -129,6 +129,13 @@ int mcaat_graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, i
 /* valid &= {ids}: keep_crispr_regions_extended_by_k (spacer_ordering.cpp:129-137) invalidates
  * every valid edge outside the extended cycle set; here one bitmap AND on the device. */
 int mcaat_graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n);
+/* Checkpoint / resume. Replaces: the on-disk graph between SDBGBuild and CycleFinder
+ * (MEGAHIT graph.sdbg* + SDBG::LoadFromFile, main.cpp:386-393, 522-530). The library's own
+ * format (MEGAHIT's is unpinned offline): sorted BOSS keys, multiplicities and valid bits with
+ * a checksum; adjacency and directory are rebuilt on load, so the loaded graph answers every
+ * query as the saved one (valid bits included, e.g. after CycleFinder). */
+int mcaat_graph_save(const mcaat_graph *g, const char *path);
+int mcaat_graph_load(mcaat_ctx *ctx, const char *path, mcaat_graph **out);
 void mcaat_graph_free(mcaat_graph *g);
 
 /* ---- relevant-read mapping -------------------------------

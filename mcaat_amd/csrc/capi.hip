@@ -718,6 +718,29 @@ int mcaat_graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n) {
     });
 }
 
+int mcaat_graph_save(const mcaat_graph *g, const char *path) {
+    return guarded([&] {
+        require(g && path, "null argument");
+        HIP_OK(hipSetDevice(g->ctx->device));
+        graph_save(g, path);
+    });
+}
+
+int mcaat_graph_load(mcaat_ctx *ctx, const char *path, mcaat_graph **out) {
+    return guarded([&] {
+        require(ctx && path && out, "null argument");
+        HIP_OK(hipSetDevice(ctx->device));
+        auto *g = new mcaat_graph;
+        try {
+            graph_load(ctx, path, g);
+        } catch (...) {
+            delete g;
+            throw;
+        }
+        *out = g;
+    });
+}
+
 void mcaat_graph_free(mcaat_graph *g) { delete g; }
 
 int mcaat_reads_records_info(const mcaat_reads *r, uint64_t *n_records, int *separate) {

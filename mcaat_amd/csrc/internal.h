@@ -287,6 +287,8 @@ void graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n);
 // FASTQ(.gz) inputs parsed on the GPU (fastq_ingest.hip)
 void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_reads *r);
 void write_fastq(const mcaat_reads *r, const char *path, int threads);
+void graph_save(const mcaat_graph *g, const char *path);
+void graph_load(mcaat_ctx *ctx, const char *path, mcaat_graph *g);
 void map_reads(const mcaat_graph *g, const mcaat_reads *r, const uint64_t *nodes, size_t n_nodes,
                uint64_t max_batch_ids, mcaat_mapped *out);
 

@@ -81,7 +81,17 @@ void SDBGBuild::BuildLib() {
 
 void SDBGBuild::BuildSDBG() {
     mcaat_ctx *ctx = mcaat_host_ctx(settings.gpu);
-    mcaat_check(mcaat_build_graph(ctx, reads_, settings.kmer_k, &graph_), "building the SDBG");
+    if (!settings.load_graph.empty()) {
+        mcaat_check(mcaat_graph_load(ctx, settings.load_graph.c_str(), &graph_), "loading the graph");
+        std::cout << "Resumed the graph from " << settings.load_graph << std::endl;
+    } else {
+        mcaat_check(mcaat_build_graph(ctx, reads_, settings.kmer_k, &graph_), "building the SDBG");
+        if (settings.keep_graph) {
+            const std::string out = settings.graph_folder + "/graph.mcaat_sdbg";
+            mcaat_check(mcaat_graph_save(graph_, out.c_str()), "saving the graph");
+            std::cout << "Graph kept in " << out << std::endl;
+        }
+    }
     std::cout << "\n-----------------------------------------\n" << std::endl;
 }
 
@@ -98,6 +108,17 @@ void SDBG::LoadFromDevice(mcaat_graph *g) {
     std::vector<uint64_t>().swap(key_);
     std::vector<uint16_t>().swap(mult_);
     std::vector<uint8_t>().swap(valid_);
+}
+
+void SDBG::LoadFromFile(const char *path) {
+    mcaat_graph *g = nullptr;
+    mcaat_check(mcaat_graph_load(mcaat_host_ctx(0), path, &g), "SDBG::LoadFromFile");
+    LoadFromDevice(g);
+}
+
+void SDBG::SaveToFile(const char *path) const {
+    if (!g_) throw std::runtime_error("SDBG::SaveToFile: no device graph");
+    mcaat_check(mcaat_graph_save(g_, path), "SDBG::SaveToFile");
 }
 
 void SDBG::LoadFromArrays(int k, std::vector<uint64_t> keys, std::vector<uint16_t> mult,

@@ -55,6 +55,9 @@ class SDBG {
     SDBG &operator=(const SDBG &) = delete;
     // adopt a device graph (replaces SDBG::LoadFromFile of the on-disk MEGAHIT graph)
     void LoadFromDevice(mcaat_graph *g);
+    // the library's own graph file (mcaat_graph_save / mcaat_graph_load), on GPU 0's context
+    void LoadFromFile(const char *path);
+    void SaveToFile(const char *path) const;
     // host-only graph (no device copy) from sorted BOSS keys, multiplicities and valid bytes
     void LoadFromArrays(int k, std::vector<uint64_t> keys, std::vector<uint16_t> mult, std::vector<uint8_t> valid);
     // refresh the host mirror after device-side mutation (CycleFinder)

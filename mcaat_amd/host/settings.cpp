@@ -26,6 +26,8 @@ static void print_help() {
               << "  --low-abundance <true|false>    Enable low abundance mode for cycle filtering\n"
               << "  --settings <path>               Path to a key=value settings file (overridden by CLI args)\n"
               << "  --gpu <index>                   GPU to run the hot path on (default 0)\n"
+              << "  --keep-graph                    Keep the graph as <graph folder>/graph.mcaat_sdbg (checkpoint)\n"
+              << "  --load-graph <file>             Resume from a kept graph instead of building it\n"
               << "  --help, -h                      Show this help message\n";
 }
 
@@ -98,6 +100,11 @@ Settings parse_arguments(int argc, char *argv[], bool create_dirs) {
         } else if (arg == "--gpu") {
             if (++i < argc) settings.gpu = std::stoi(argv[i]);
             else throw std::runtime_error("Error: Missing value for --gpu");
+        } else if (arg == "--keep-graph") {
+            settings.keep_graph = true;
+        } else if (arg == "--load-graph") {
+            if (++i < argc) settings.load_graph = argv[i];
+            else throw std::runtime_error("Error: Missing value for --load-graph");
         } else if (arg == "--settings") {
             ++i;  // handled in the pre-scan
         }

@@ -31,6 +31,12 @@ struct Settings {
     std::string benchmark_file;
     int kmer_k = 23;           // reference: "-k 23" (sdbg_build.cpp:217)
     int gpu = 0;
+    // checkpoint / resume of the graph (the reference keeps MEGAHIT's graph.sdbg* on disk
+    // between SDBGBuild and CycleFinder, main.cpp:386-393): keep_graph writes
+    // <graph_folder>/graph.mcaat_sdbg after the build and keeps it; load_graph resumes from
+    // such a file instead of building (the reads are still read for the downstream steps)
+    bool keep_graph = false;
+    std::string load_graph;
 
     struct CycleFinderSettings {           // settings.h:33-38
         uint64_t threshold_multiplicity = 20;
@@ -163,6 +169,10 @@ struct Settings {
             else if (key == "repeat_min_length") dna_sequence_settings.repeat_min_length = std::stoi(val);
             else if (key == "repeat_max_length") dna_sequence_settings.repeat_max_length = std::stoi(val);
             else if (key == "kmer_k") kmer_k = std::stoi(val);
+            else if (key == "keep_graph") {
+                std::transform(val.begin(), val.end(), val.begin(), ::tolower);
+                keep_graph = (val == "true" || val == "1" || val == "yes");
+            } else if (key == "load_graph") load_graph = val;
             // unknown keys are ignored for forward-compatibility (settings.h:216)
         }
         return true;

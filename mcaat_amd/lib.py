@@ -110,6 +110,8 @@ SIGNATURES = {
     "mcaat_mapped_free": (None, [C.c_void_p]),
     "mcaat_set_knob": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int64]),
     "mcaat_reads_write_fastq": (C.c_int, [C.c_void_p, C.c_char_p, C.c_int]),
+    "mcaat_graph_save": (C.c_int, [C.c_void_p, C.c_char_p]),
+    "mcaat_graph_load": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_void_p)]),
     "mcaat_graph_download_range": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, _u64p, _u16p, _u8p]),
 }
 
@@ -464,6 +466,16 @@ class Graph:
         h = C.c_void_p()
         _check(ctx._lib.mcaat_graph_from_sorted(ctx.h, k, C.c_void_p(keys_dev), C.c_void_p(mult_dev), D, C.byref(h)))
         return cls(ctx, h)
+
+    @classmethod
+    def load(cls, ctx: Context, path: str) -> "Graph":
+        """Graph saved by Graph.save (mcaat_graph_load)."""
+        h = C.c_void_p()
+        _check(ctx._lib.mcaat_graph_load(ctx.h, path.encode(), C.byref(h)))
+        return cls(ctx, h)
+
+    def save(self, path: str) -> None:
+        _check(self.ctx._lib.mcaat_graph_save(self.h, path.encode()))
 
     def info(self) -> Tuple[int, int]:
         k = C.c_int(0)

@@ -408,8 +408,6 @@ struct CycleFinderO {
     }
 };
 
-}  // namespace
-
 /* ---------------- relevant reads (reads.cpp) ---------------- */
 // reads.cpp:20-31
 void reverse_pair_ends_sequence(std::string &sequence) {
@@ -444,6 +442,8 @@ std::vector<uint64_t> get_read_from_sequence(const Graph &sdbg, const std::unord
     read.push_back(end_node_id);
     return read;
 }
+
+}  // namespace
 
 struct oracle_graph { Graph g; };
 struct oracle_cf_result {

@@ -1,0 +1,67 @@
+"""CPU sanitizer leg: the oracle and the host downstream code (spacer ordering,
+get_systems, CRISPRAnalyzer, rapidfuzz restatement) built with AddressSanitizer and
+UndefinedBehaviorSanitizer (tests/sanitize/Makefile, UB aborts) and run on C1 and on an
+error-rich multi-array read set. The run must be clean (exit 0, no sanitizer report) and give
+the same CycleFinder stats and CRISPR_Arrays.txt as the normally built libraries."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import mcaat_amd as M
+import mcaat_amd.downstream as DS
+import oracle as O
+from tests.helpers import unpack_read
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SAN = os.path.join(ROOT, "tests", "sanitize")
+DRIVER = os.path.join(SAN, "build", "driver")
+
+CASES = {
+    "c1_k23": (M.SynthSpec(), 23, 20),
+    "arrays_err": (M.SynthSpec(seed=21, n_genomes=3, genome_len=20_000, arrays_per_genome=1, spacers_per_array=9,
+                               repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
+                               n_reads=15_000, error_rate=0.001), 23, 5),
+}
+
+
+@pytest.fixture(scope="module")
+def driver():
+    subprocess.run(["make", "-s", "-j4", "-C", SAN], check=True, timeout=900)
+    return DRIVER
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_sanitized_oracle_and_downstream(driver, tmp_path, name):
+    spec, k, thr = CASES[name]
+    packed, offs = M.synth_host(spec)
+    blob = tmp_path / "reads.bin"
+    with open(blob, "wb") as f:
+        f.write(np.array([packed.size, offs.size - 1], dtype=np.uint64).tobytes())
+        f.write(packed.astype(np.uint64).tobytes())
+        f.write(offs.astype(np.uint64).tobytes())
+    report = tmp_path / "san_CRISPR_Arrays.txt"
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1")
+    p = subprocess.run([driver, str(blob), str(k), str(thr), str(report)], capture_output=True, text=True,
+                       timeout=600, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    assert "AddressSanitizer" not in p.stderr and "runtime error" not in p.stderr, p.stderr[-3000:]
+    line = [ln for ln in p.stdout.splitlines() if ln.startswith("stats ")][0].split()
+    stats = [int(x) for x in line[1:7]]
+    # the same flow through the normally built libraries
+    og = O.OGraph.build(packed, offs, k, threads=1)
+    res = og.cycle_finder(threshold_multiplicity=thr, threads=1)
+    assert stats == res["stats"]
+    ent = res["entries"]
+    cycles = [c for i in res["map_order"] for c in ent[i][1]]
+    nodes = sorted({x for c in cycles for x in c})
+    seqs = [unpack_read(packed, int(offs[i]), int(offs[i + 1])) for i in range(len(offs) - 1)]
+    reads = og.get_reads(seqs, len(seqs), nodes)
+    assert int(line[8]) == len(reads)
+    keys, mult = og.arrays()
+    valid = og.valid().astype(np.uint8).copy()
+    want = tmp_path / "CRISPR_Arrays.txt"
+    n = DS.crispr_arrays(k, keys, mult, valid, cycles, reads, str(want))
+    assert int(line[10]) == n
+    assert report.read_text() == want.read_text()
