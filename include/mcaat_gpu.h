@@ -240,7 +240,8 @@ void mcaat_reset_timing(mcaat_ctx *ctx);
  *   cf.dls_stack / cf.dls_visited   initial DepthLevelSearch scratch (grows x8 on overflow)
  *   cf.fc_lock / cf.fc_relax / cf.fc_out   initial FindCycle scratch (grows on overflow)
  *   cf.fc_window       initial FindCycle speculation window
- *   cf.walk_budget     steps of a counter-driven peel walk before the list-ranking peel */
+ *   cf.walk_budget     > 0: counter-driven peel walks of this many steps before the
+ *                      list-ranking peel (default 0: the list-ranking peel alone) */
 int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value);
 
 #ifdef __cplusplus

@@ -147,6 +147,9 @@ __global__ void __launch_bounds__(kBlock) k_peel_rulers(uint64_t D, PeelArrays p
             }
             m[j] = __ballot(r);
             c += __popcll(m[j]);
+            // only unary non-ruler successors of branch nodes have their owner read (peel_res);
+            // their owner starts empty here instead of a D-wide fill
+            if (e < D && !r && kind_chain(pa.kind[e]) && (pa.kind[e] & kBranchSucc)) pa.owner[e] = kNone;
         }
         if (lane == 0) wcnt[wave] = c;
         __syncthreads();
@@ -802,7 +805,6 @@ static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm) {
     DevBuf<uint8_t> kind(D), upred(D), stt(D);
     DevBuf<uint64_t> nxk(D), owner(D), jump(D);
     HIP_OK(hipMemsetAsync(upred.p, 0, D, st));
-    HIP_OK(hipMemsetAsync(owner.p, 0xFF, owner.bytes(), st));
     PeelArrays pa{kind.p, upred.p, stt.p, nxk.p, owner.p, jump.p, seed_bm};
     hipLaunchKernelGGL(k_peel_init, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, v, pa);
     LAUNCH_OK();
@@ -871,7 +873,16 @@ static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm) {
 // the same (every pending node is valid, has no valid successor and must be removed).
 static void run_peel(mcaat_graph *g, const uint64_t *seed_bm) {
     mcaat_ctx *ctx = g->ctx;
-    const uint32_t kBudget = (uint32_t)std::max<int64_t>(1, knob(ctx, "cf.walk_budget", 512));
+    // C3: the reduction walks chains of tens of thousands of edges back from a few hundred
+    // seeds (budget 512: 164 walks still pending; 32768: 12, at 0.5 s), so by default the
+    // list-ranking peel runs alone from the seeds (the same fixpoint); cf.walk_budget > 0 runs
+    // counter-driven walks with that step budget first
+    const int64_t walk_budget = knob(ctx, "cf.walk_budget", 0);
+    if (walk_budget <= 0) {
+        run_peel_rulers(g, seed_bm);
+        return;
+    }
+    const uint32_t kBudget = (uint32_t)std::min<int64_t>(walk_budget, 0xFFFFFFFFLL);
     hipStream_t st = ctx->stream;
     const uint64_t D = g->D, nw = g->n_words();
     if (!D) return;

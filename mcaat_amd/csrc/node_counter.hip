@@ -71,6 +71,11 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
     return x;
 }
 
+// partition hash of a minimizer hash (a bijection; the minimum is biased towards 0): the L1
+// bucket is its top 8 bits, the next 14 go into the descriptor (sub-partition + class bits).
+// 32-bit mixing (lowbias32) instead of a 64-bit finaliser: two of these per super-k-mer in pass A
+__device__ __forceinline__ uint32_t part_mix(uint32_t h) { return mix32(h ^ 0x70617274u); }
+
 // canonical (smaller of the edge and its reverse complement); 2-bit reversal by the
 // hardware bit reverse plus one swap of adjacent bits
 __device__ __forceinline__ uint64_t canon_edge(uint64_t lsb, int E) {
@@ -426,7 +431,7 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
         // bucket of each entry: the minimum hash is biased towards 0, so buckets come from
         // a re-hash of it (a bijection)
         for (uint32_t e = lane; e < fill; e += 64) {
-            const uint32_t l1 = (uint32_t)(mix64((uint64_t)(uint32_t)seg[e] ^ 0x7061727469746eULL) >> 56);
+            const uint32_t l1 = part_mix((uint32_t)seg[e]) >> 24;
             seg_l1[e] = (uint8_t)l1;
             atomicAdd(&hist[l1], 1u);
         }
@@ -519,8 +524,8 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
                 const uint64_t w0 = (sh ? (x[k][0] >> sh) | (x[k][1] << (64 - sh)) : x[k][0]) & mask_bits(2 * L);
                 uint64_t w1 = (sh ? (x[k][1] >> sh) | (x[k][2] << (64 - sh)) : x[k][1]) &
                               mask_bits(L > 32 ? 2 * (L - 32) : 0);
-                const uint64_t h = mix64((uint64_t)(uint32_t)q[k] ^ 0x7061727469746eULL);
-                w1 |= ((uint64_t)n << kNShift) | (((h >> (56 - kHBits)) & ((1u << kHBits) - 1)) << kHShift);
+                const uint32_t h = part_mix((uint32_t)q[k]);
+                w1 |= ((uint64_t)n << kNShift) | ((uint64_t)((h >> (24 - kHBits)) & ((1u << kHBits) - 1)) << kHShift);
                 put(b, rpos[b] + (j - boff[b]),
                     make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)));
             }
@@ -742,7 +747,10 @@ constexpr int kDProbe = 128;                               // probe bound of the
 #endif
 constexpr int kCB = MCAAT_CB;                              // descriptor loads in flight per thread
 constexpr int kDefer = 64;                                 // descriptors with w0 == kEmpty before going raw
-constexpr int kCPerCu = 2;                                 // resident workgroups per CU (LDS, VGPR <= 64)
+#ifndef MCAAT_CPERCU
+#define MCAAT_CPERCU 2
+#endif
+constexpr int kCPerCu = MCAAT_CPERCU;                      // resident workgroups per CU (LDS, VGPR <= 64)
 #ifndef MCAAT_CSPLIT
 #define MCAAT_CSPLIT 2
 #endif
@@ -1391,7 +1399,7 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
             KernelTimer kt(ctx, "l2_partition", 34.0 * (double)gn);  // sub rows + descriptors read, descriptors written
             if (c1 > c0) {
                 hipLaunchKernelGGL(k_l2_scatter, dim3((unsigned)(c1 - c0)), dim3(kBThreads), 0, st, l1.p, l1s.p,
-                                   dcs.p + c0, dcl.p + c0, dcb.p + c0, P.l2_bits, dcursor.p, fine.p, gbase);
+                                       dcs.p + c0, dcl.p + c0, dcb.p + c0, P.l2_bits, dcursor.p, fine.p, gbase);
                 LAUNCH_OK();
             }
             kt.stop();

@@ -52,8 +52,10 @@ KNOBS = {
     # scratch regrowth in DepthLevelSearch and FindCycle, one speculative start per round
     "cf_scratch": {"cf.dls_stack": 1, "cf.dls_visited": 2, "cf.fc_lock": 4, "cf.fc_relax": 1, "cf.fc_out": 1,
                    "cf.fc_window": 1},
-    # every peel walk hands over after one step: the list-ranking peel does the rest
-    "peel_rulers": {"cf.walk_budget": 1},
+    # counter-driven peel walks first: one step before the list-ranking peel takes over, or
+    # (nearly) unbounded walks that finish every chain themselves
+    "peel_walk1": {"cf.walk_budget": 1},
+    "peel_kahn": {"cf.walk_budget": 1 << 30},
 }
 
 _oracle_cache = {}

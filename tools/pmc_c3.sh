@@ -1,7 +1,7 @@
 # PMC counters for the hot-path kernels, one rocprofv3 pass per counter group
 # (never combined with --sys-trace / runtime traces). Usage: bash tools/pmc_c3.sh [reads] [groups]
 R=$PWD; N=${1:-300000000}; G=${2:-"f w"}; mkdir -p gpurun_out/pmc; export TMPDIR=/tmp; cd /tmp
-B="python $R/bench.py --config c3 --reads $N --steps 1 --warmup 0 --no-cpu-baseline --no-post --ingest-reads 0"
+B="python $R/bench.py --config c3 --reads $N --steps 1 --warmup 0 --no-cpu-baseline --no-post --ingest-reads 0 --no-e2e"
 run() { name=$1; shift; timeout -k 10 400 rocprofv3 --pmc "$@" --output-format csv -d $R/gpurun_out/pmc/$name -o $name -- $B > $R/gpurun_out/pmc/$name.log 2>&1; }
 for g in $G; do
   case $g in
@@ -11,6 +11,7 @@ for g in $G; do
     s2) run s2 SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY ;;
     s3) run s3 SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAIT_INST_LDS ;;
     s4) run s4 SQ_INST_CYCLES_VMEM SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH ;;
+    s5) run s5 SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_WAIT_INST_LDS ;;
   esac || exit $?
 done
 echo exit=0
