@@ -228,7 +228,9 @@ def step_traffic_from_profiles() -> float | None:
     try:
         with open(path) as f:
             d = json.load(f)
-        return float(sum(v["hbm_bytes_per_launch"] * v["launches"] for kk, v in d.items() if kk != "k_synth"))
+        # entries without "launches" are the bench's short-name aliases of a k_* entry
+        return float(sum(v["hbm_bytes_per_launch"] * v["launches"] for kk, v in d.items()
+                         if kk != "k_synth" and "launches" in v))
     except Exception:
         return None
 
