@@ -10,10 +10,16 @@ Workload (N=1): config C3 — ~300M x 150 bp reads, k=27, threshold_multiplicity
 error rate tuned so the SDBG has ~1e9 edges (D).
 N>1, default --mode shard (config C4): the SAME C3 dataset is split over
 the ranks; each counts its slice, the oriented edges are routed to their owner rank by a
-hash(BOSS-key)-range all-to-all over RCCL (torch.distributed "nccl"), owners sort and sum,
-an all-gather in rank order gives every rank the single-GPU graph, and CycleFinder runs on
-it (scaling "strong": total work fixed). --mode replicas: every rank runs its own
-independent C3-sized sample, no collective on the data path (scaling "weak").
+BOSS-key-range all-to-all, owners sort and sum, an exact-size all-gather in rank order gives
+every rank the single-GPU graph, and CycleFinder runs over the ranks (pruning on every rank,
+candidate scan by id range, DLS and FindCycle starts dealt round-robin with one ordered
+commit). All of it is the library's native path (mcaat_build_graph_sharded,
+mcaat_cycle_finder_comm) over an RCCL communicator whose id travels over torch.distributed
+(gloo, control plane only); MCAAT_COMM_BACKEND=gloo uses the shared-memory transport instead
+(ranks sharing one GPU); --shard-impl torch keeps the Python orchestration (mcaat_amd/shard.py,
+torch.distributed collectives) with CycleFinder replicated. Scaling "strong": total work fixed.
+--mode replicas: every rank runs its own independent C3-sized sample, no collective on the
+data path (scaling "weak").
 value = all k-mers processed / max-over-ranks step time.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|tiny] [--mode shard|replicas]
@@ -352,6 +358,8 @@ def main() -> int:
                     help="untimed FASTQ ingest measurement on a file of this many reads (0: skip)")
     ap.add_argument("--mode", default="shard", choices=["shard", "replicas"],
                     help="N>1: one dataset hash-range sharded over the ranks, or one dataset per rank")
+    ap.add_argument("--shard-impl", default="native", choices=["native", "torch"],
+                    help="shard mode: the library's native path (RCCL communicator) or the Python orchestration")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU-only rehearsal of the control flow (ranks, barrier, max-reduce, JSON); no GPU work")
     args = ap.parse_args()
@@ -364,10 +372,11 @@ def main() -> int:
 
     dist = None
     cdev = torch.device("cpu")
+    native = sharded and args.shard_impl == "native"
     if world > 1:
         import torch.distributed as dist
 
-        if sharded and not args.dry_run and os.environ.get("MCAAT_COMM_BACKEND", "nccl") == "nccl":
+        if sharded and not native and not args.dry_run and os.environ.get("MCAAT_COMM_BACKEND", "nccl") == "nccl":
             # data path: RCCL all-to-all / all-gather of device tensors (MCAAT_COMM_BACKEND=gloo
             # stages them through host memory instead: a rehearsal with ranks sharing one GPU)
             torch.cuda.set_device(local)
@@ -395,6 +404,18 @@ def main() -> int:
             torch.cuda.set_device(local)
         ctx = M.Context(local)
         reads = M.Reads.synth_range(ctx, spec, first, count) if sharded else M.Reads.synth(ctx, spec)
+    comm = None
+    if native and not args.dry_run:
+        # the library's communicator: RCCL (its id broadcast over the gloo control plane), or
+        # the shared-memory transport for ranks that share one GPU (MCAAT_COMM_BACKEND=gloo)
+        if os.environ.get("MCAAT_COMM_BACKEND", "nccl") == "nccl":
+            obj = [M.Comm.unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            comm = M.Comm.rccl(ctx, world, rank, obj[0])
+        else:
+            obj = [f"/mcaat_bench_{os.getpid()}_{int(time.time() * 1e6) % 10**9}" if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            comm = M.Comm.shm(ctx, world, rank, obj[0])
     prm = M.CfParams(threshold_multiplicity=thr)
     # The FASTQ-inclusive span runs first, on a GPU that no earlier process of this job has
     # used: VRAM released by a process is scrubbed by the driver, and a CLI started right after
@@ -407,7 +428,10 @@ def main() -> int:
         if args.dry_run:
             time.sleep(0.01 * (1 + rank))
             return 0, None, {}
-        if sharded:
+        if native:
+            g = M.Graph.build_sharded(ctx, comm, reads, k)
+            st_build = ctx.stage_times()
+        elif sharded:
             from mcaat_amd import shard
 
             st_build = {}
@@ -416,7 +440,7 @@ def main() -> int:
             g = M.Graph.build(ctx, reads, k)
             st_build = ctx.stage_times()
         d = g.size
-        res = g.cycle_finder(prm, as_arrays=True)  # results copied to host arrays
+        res = g.cycle_finder(prm, as_arrays=True, comm=comm)  # results copied to host arrays
         st_cf = ctx.stage_times()
         g.free()
         return d, res, {**st_build, **st_cf}
@@ -486,6 +510,12 @@ def main() -> int:
     kmers_rank = count * max(0, spec.read_len - k)
     kmers_total = n_occ(spec, k) if sharded else kmers_rank * world
     value = kmers_total / dt
+    if not native:
+        impl = "torch.distributed collectives, CycleFinder replicated"
+    elif os.environ.get("MCAAT_COMM_BACKEND", "nccl") == "nccl":
+        impl = "native RCCL communicator, CycleFinder over the ranks"
+    else:
+        impl = "native shared-memory communicator, CycleFinder over the ranks"
     if rank == 0:
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
         traffic = traffic_from_profiles(kern)
@@ -513,8 +543,8 @@ def main() -> int:
                 "kmers_per_gpu": kmers_rank,
                 "kmers_total": kmers_total,
                 "sdbg_edges_D": D,
-                "parallelism": (f"shard{world} (BOSS-key-range all-to-all + all-gather over RCCL)" if sharded
-                                else f"replicas{world}"),
+                "parallelism": (f"shard{world} (BOSS-key-range all-to-all + all-gather; {impl})"
+                                if sharded else f"replicas{world}"),
                 "cycle_entries": len(res.entries) if res else 0,
                 "cycles": res.stats[5] if res else 0,
                 "cf_stats": list(res.stats) if res else None,
@@ -558,6 +588,8 @@ def main() -> int:
         except Exception as e:  # reported, never fatal for the GPU number
             out["cpu_baseline"] = {"error": str(e)}
     reads.free()
+    if comm is not None:
+        comm.close()
     ctx.close()
     if rank == 0:
         out["e2e"] = e2e

@@ -38,6 +38,7 @@ typedef struct mcaat_graph mcaat_graph;
 typedef struct mcaat_cycles mcaat_cycles;
 typedef struct mcaat_counts mcaat_counts;
 typedef struct mcaat_mapped mcaat_mapped;
+typedef struct mcaat_comm mcaat_comm;
 
 /* ---- context ------------------------------------------------------------- */
 /* Replaces: nothing in the reference (single process, OpenMP). Binds one GPU. */
@@ -212,6 +213,47 @@ int mcaat_cycles_stats(const mcaat_cycles *c, uint64_t *stats);
 /* start candidates in processing order and their ceil(log2 mult) bucket */
 int mcaat_cycles_candidates(const mcaat_cycles *c, size_t *n, const uint64_t **ids, const int32_t **buckets);
 void mcaat_cycles_free(mcaat_cycles *c);
+
+/* ---- multi-GPU, native (one process per GPU) ----------
+ * Replaces: nothing in the reference (one process, OpenMP); the C++ host drives a multi-GPU
+ * run through these. A communicator joins the `world` processes of one run:
+ *   RCCL: rank 0 makes a 128-byte id (mcaat_comm_unique_id), the caller hands it to every
+ *         rank (pipe, file, torch.distributed), each rank calls mcaat_comm_init_rccl on its
+ *         own GPU; device data moves GPU to GPU over xGMI.
+ *   SHM:  every rank calls mcaat_comm_init_shm with the same "/name" (POSIX shared memory,
+ *         removed once all ranks are attached); device data is staged through host memory
+ *         (ranks sharing one GPU, rehearsals). ctx may be NULL: host collectives only.
+ * Every comm call is collective (all ranks, same order) and synchronous. */
+#define MCAAT_COMM_ID_BYTES 128
+int mcaat_comm_unique_id(uint8_t *id);
+int mcaat_comm_init_rccl(mcaat_ctx *ctx, int world, int rank, const uint8_t *id, mcaat_comm **out);
+/* slot_bytes: staging bytes per rank (0: 256 MiB); larger messages move in rounds */
+int mcaat_comm_init_shm(mcaat_ctx *ctx, int world, int rank, const char *name, uint64_t slot_bytes,
+                        mcaat_comm **out);
+int mcaat_comm_info(const mcaat_comm *c, int *world, int *rank);
+int mcaat_comm_barrier(mcaat_comm *c);
+/* host memory: sizes[world] = every rank's byte count; then the bytes in rank order */
+int mcaat_comm_allgather_sizes(mcaat_comm *c, uint64_t bytes, uint64_t *sizes);
+int mcaat_comm_allgatherv(mcaat_comm *c, const void *send, uint64_t bytes, void *recv, const uint64_t *sizes);
+void mcaat_comm_free(mcaat_comm *c);
+/* Part `part` of n_parts of the FASTQ inputs (replaces BuildLib for one rank): each plain
+ * file is cut at 4-line record starts near part/n_parts of its size, a .gz file goes whole
+ * to part 0 (one inflate stream cannot be split). MCAAT_E_IO for inputs the GPU parser does
+ * not take (FASTA, wrapped or gapped records): read them whole with mcaat_reads_from_fastx
+ * on one rank instead. n_parts == 1 is mcaat_reads_from_fastx. */
+int mcaat_reads_from_fastx_part(mcaat_ctx *ctx, const char *const *files, int n_files, int part, int n_parts,
+                                mcaat_reads **out);
+/* mapping-view records that came from input file `file` (they are in file order) */
+int mcaat_reads_file_records(const mcaat_reads *r, int file, uint64_t *n_records);
+/* The graph of all ranks' reads (each passes its own part), built with one key-range
+ * all-to-all and one all-gather; every rank receives the whole graph, edge ids identical to
+ * mcaat_build_graph over all the reads. Replaces Read2SdbgS2::Run (sdbg_build.cpp:171-187). */
+int mcaat_build_graph_sharded(mcaat_ctx *ctx, mcaat_comm *comm, const mcaat_reads *r, int k, mcaat_graph **out);
+/* CycleFinder over ranks that each hold the same graph: pruning runs on every rank, the
+ * start-candidate scan is split by id range, DepthLevelSearch and FindCycle starts are dealt
+ * round-robin with one ordered commit; every rank gets the results mcaat_cycle_finder gives
+ * (comm NULL: mcaat_cycle_finder). Replaces cycle_finder.cpp:394-419, 468-487. */
+int mcaat_cycle_finder_comm(mcaat_graph *g, mcaat_comm *comm, const mcaat_cf_params *p, mcaat_cycles **out);
 
 /* ---- measurement -------------------------------------------------------------
  * Per-stage device time of the last build/cycle_finder call on this ctx, measured

@@ -7,6 +7,7 @@ is present, the calls raise.
 from .lib import (  # noqa: F401
     LIB_PATH,
     CfParams,
+    Comm,
     Context,
     CycleResult,
     Graph,

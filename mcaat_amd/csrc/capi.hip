@@ -1,6 +1,7 @@
 // capi.hip — extern "C" boundary of libmcaat_gpu.so (include/mcaat_gpu.h).
 // Every entry point converts internal exceptions into a negative status plus a
 // thread-local message (mcaat_last_error), the way the host mirror expects.
+#include <sys/stat.h>
 #include <zlib.h>
 
 #include <cstdio>
@@ -9,6 +10,7 @@
 #include <string>
 
 #include "internal.h"
+#include "comm.h"
 #include "synth.h"
 
 using namespace mcaat;
@@ -398,14 +400,18 @@ int mcaat_reads_from_fastx(mcaat_ctx *ctx, const char *const *files, int n_files
         auto *r = new mcaat_reads;
         auto host_path = [&] {
             Packer pk;
+            std::vector<uint64_t> per_file;
             for (int i = 0; i < n_files; ++i) {
                 pk.file = i;
+                const uint64_t before = pk.records.offsets.size();
                 read_fastx_host(files[i], pk);
+                per_file.push_back(pk.records.offsets.size() - before);
             }
             *r = mcaat_reads{};
             upload_reads(ctx, pk.reads.words.data(), pk.reads.words.size(), pk.reads.offsets.data(),
                          pk.reads.offsets.size() - 1, r);
             if (pk.records_differ) upload_records(ctx, pk.records, r);
+            r->file_records = per_file;
         };
         try {
             if (n_fastq > 0 && n_fasta == 0) {
@@ -792,21 +798,7 @@ void mcaat_cf_default_params(mcaat_cf_params *p) {
 }
 
 int mcaat_cycle_finder(mcaat_graph *g, const mcaat_cf_params *p, mcaat_cycles **out) {
-    return guarded([&] {
-        require(g && p && out, "null argument");
-        require(p->cycle_max_length >= 2 && p->cycle_max_length <= 250, "cycle_max_length must be in [2, 250]");
-        require(p->cluster_bound >= 1 && p->cluster_bound <= 65535, "cluster_bound must be in [1, 65535]");
-        require(p->step_cap >= 1, "step_cap must be positive");
-        HIP_OK(hipSetDevice(g->ctx->device));
-        auto *c = new mcaat_cycles;
-        try {
-            cycle_finder(g, *p, c);
-        } catch (...) {
-            delete c;
-            throw;
-        }
-        *out = c;
-    });
+    return mcaat_cycle_finder_comm(g, nullptr, p, out);
 }
 
 int mcaat_cycles_count(const mcaat_cycles *c, size_t *n) {
@@ -918,6 +910,173 @@ int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value) {
         if (!ok) throw Error(MCAAT_E_INVALID, std::string("unknown knob: ") + name);
         if (value < 0) ctx->knobs.erase(name);
         else ctx->knobs[name] = value;
+    });
+}
+
+/* ---- multi-GPU: communicators and the native sharded path ----------------------- */
+int mcaat_comm_unique_id(uint8_t *id) {
+    return guarded([&] {
+        require(id != nullptr, "null argument");
+        comm_unique_id(id);
+    });
+}
+
+int mcaat_comm_init_rccl(mcaat_ctx *ctx, int world, int rank, const uint8_t *id, mcaat_comm **out) {
+    return guarded([&] {
+        require(ctx && id && out, "null argument");
+        require(world >= 1 && rank >= 0 && rank < world, "rank must be in [0, world)");
+        HIP_OK(hipSetDevice(ctx->device));
+        auto *c = new mcaat_comm;
+        try {
+            c->c = comm_rccl(ctx, world, rank, id);
+        } catch (...) {
+            delete c;
+            throw;
+        }
+        *out = c;
+    });
+}
+
+int mcaat_comm_init_shm(mcaat_ctx *ctx, int world, int rank, const char *name, uint64_t slot_bytes,
+                        mcaat_comm **out) {
+    return guarded([&] {
+        require(name && out, "null argument");
+        require(name[0] == '/' && !strchr(name + 1, '/'), "shared-memory name must be \"/name\"");
+        require(world >= 1 && rank >= 0 && rank < world, "rank must be in [0, world)");
+        if (ctx) HIP_OK(hipSetDevice(ctx->device));
+        auto *c = new mcaat_comm;
+        try {
+            c->c = comm_shm(ctx, world, rank, name, slot_bytes ? slot_bytes : (256ULL << 20));
+        } catch (...) {
+            delete c;
+            throw;
+        }
+        *out = c;
+    });
+}
+
+int mcaat_comm_info(const mcaat_comm *c, int *world, int *rank) {
+    return guarded([&] {
+        require(c != nullptr, "null argument");
+        if (world) *world = c->c->world;
+        if (rank) *rank = c->c->rank;
+    });
+}
+
+int mcaat_comm_barrier(mcaat_comm *c) {
+    return guarded([&] {
+        require(c != nullptr, "null argument");
+        c->c->barrier();
+    });
+}
+
+int mcaat_comm_allgather_sizes(mcaat_comm *c, uint64_t bytes, uint64_t *sizes) {
+    return guarded([&] {
+        require(c && sizes, "null argument");
+        const std::vector<uint64_t> all = c->c->allgather_one(bytes);
+        std::copy(all.begin(), all.end(), sizes);
+    });
+}
+
+int mcaat_comm_allgatherv(mcaat_comm *c, const void *send, uint64_t bytes, void *recv, const uint64_t *sizes) {
+    return guarded([&] {
+        require(c && sizes && (send || !bytes), "null argument");
+        require(sizes[c->c->rank] == bytes, "sizes[rank] differs from bytes");
+        std::vector<uint8_t> all;
+        std::vector<uint64_t> got;
+        c->c->allgatherv_host(send, bytes, all, got);
+        for (int r = 0; r < c->c->world; ++r) require(got[r] == sizes[r], "sizes differ from the ranks' byte counts");
+        require(recv || all.empty(), "null argument");
+        if (!all.empty()) memcpy(recv, all.data(), all.size());
+    });
+}
+
+void mcaat_comm_free(mcaat_comm *c) { delete c; }
+
+int mcaat_reads_from_fastx_part(mcaat_ctx *ctx, const char *const *files, int n_files, int part, int n_parts,
+                                mcaat_reads **out) {
+    if (n_parts == 1 && part == 0) return mcaat_reads_from_fastx(ctx, files, n_files, out);
+    return guarded([&] {
+        require(n_parts >= 1 && part >= 0 && part < n_parts, "part must be in [0, n_parts)");
+        require(ctx && out && files && n_files > 0, "null argument");
+        HIP_OK(hipSetDevice(ctx->device));
+        std::vector<std::pair<uint64_t, uint64_t>> ranges;
+        for (int i = 0; i < n_files; ++i) {
+            const int c = sniff_format(files[i]);
+            if (c == '>') throw Error(MCAAT_E_IO, std::string("FASTA inputs are not split over ranks: ") + files[i]);
+            if (is_gzip_file(files[i])) {
+                // one inflate stream cannot be split: part 0 reads the whole file
+                ranges.push_back(part == 0 ? std::make_pair(0ULL, ~0ULL) : std::make_pair(0ULL, 0ULL));
+                continue;
+            }
+            struct stat st;
+            if (stat(files[i], &st) != 0) throw Error(MCAAT_E_IO, std::string("cannot stat ") + files[i]);
+            const uint64_t S = (uint64_t)st.st_size;
+            const uint64_t b = fastq_record_start(files[i], (uint64_t)((unsigned __int128)S * part / n_parts));
+            const uint64_t e = part + 1 == n_parts
+                                   ? S
+                                   : fastq_record_start(files[i], (uint64_t)((unsigned __int128)S * (part + 1) / n_parts));
+            ranges.push_back({b, std::max(b, e)});
+        }
+        auto *r = new mcaat_reads;
+        try {
+            ingest_fastq(ctx, files, n_files, r, &ranges);
+        } catch (const FormatError &e) {
+            delete r;
+            throw Error(MCAAT_E_IO, std::string("input not split over ranks (read it whole): ") + e.what());
+        } catch (...) {
+            delete r;
+            throw;
+        }
+        *out = r;
+    });
+}
+
+int mcaat_reads_file_records(const mcaat_reads *r, int file, uint64_t *n_records) {
+    return guarded([&] {
+        require(r && n_records, "null argument");
+        require(file >= 0, "file index out of range");
+        if (r->file_records.empty()) {  // reads not loaded from files: one source, file 0
+            *n_records = file == 0 ? (r->has_records ? r->n_records : r->n_reads) : 0;
+            return;
+        }
+        require((size_t)file < r->file_records.size(), "file index out of range");
+        *n_records = r->file_records[file];
+    });
+}
+
+int mcaat_build_graph_sharded(mcaat_ctx *ctx, mcaat_comm *comm, const mcaat_reads *r, int k, mcaat_graph **out) {
+    return guarded([&] {
+        require(ctx && comm && r && out, "null argument");
+        require(k >= 2 && k <= kMaxK, "k must be in [2, 30]");
+        HIP_OK(hipSetDevice(ctx->device));
+        auto *g = new mcaat_graph;
+        g->ctx = ctx;
+        try {
+            build_graph_sharded(ctx, *comm->c, r, k, g);
+        } catch (...) {
+            delete g;
+            throw;
+        }
+        *out = g;
+    });
+}
+
+int mcaat_cycle_finder_comm(mcaat_graph *g, mcaat_comm *comm, const mcaat_cf_params *p, mcaat_cycles **out) {
+    return guarded([&] {
+        require(g && p && out, "null argument");
+        require(p->cycle_max_length >= 2 && p->cycle_max_length <= 250, "cycle_max_length must be in [2, 250]");
+        require(p->cluster_bound >= 1 && p->cluster_bound <= 65535, "cluster_bound must be in [1, 65535]");
+        require(p->step_cap >= 1, "step_cap must be positive");
+        HIP_OK(hipSetDevice(g->ctx->device));
+        auto *c = new mcaat_cycles;
+        try {
+            cycle_finder(g, *p, c, comm ? comm->c.get() : nullptr);
+        } catch (...) {
+            delete c;
+            throw;
+        }
+        *out = c;
     });
 }
 

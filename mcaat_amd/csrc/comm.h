@@ -1,0 +1,61 @@
+// comm.h — collectives between the ranks of a multi-GPU run (comm.hip) and the
+// distributed pieces of the hot path built on them (dist.hip).
+#pragma once
+#include <memory>
+#include <vector>
+
+#include "internal.h"
+
+namespace mcaat {
+
+// One rank of `world`. Every call is collective (all ranks, same order) and returns when
+// this rank's part is complete. Device buffers live on the context's GPU.
+struct Comm {
+    int rank = 0, world = 1;
+    virtual ~Comm() = default;
+    virtual const char *kind() const = 0;
+    virtual void barrier() = 0;
+    // every rank contributes `bytes` host bytes; `out` = all contributions in rank order,
+    // sizes[r] = rank r's byte count
+    virtual void allgatherv_host(const void *send, uint64_t bytes, std::vector<uint8_t> &out,
+                                 std::vector<uint64_t> &sizes) = 0;
+    // rank r sends send_bytes[d] bytes (at the prefix-sum offset) to each rank d and receives
+    // recv_bytes[s] bytes from each rank s into recv (prefix-sum offsets, rank order)
+    virtual void alltoallv_dev(const void *send, const uint64_t *send_bytes, void *recv,
+                               const uint64_t *recv_bytes) = 0;
+    // rank r's sizes[r] bytes at `send`, concatenated in rank order into recv (sizes known to all)
+    virtual void allgatherv_dev(const void *send, void *recv, const uint64_t *sizes) = 0;
+
+    // typed helpers over allgatherv_host
+    template <class T>
+    std::vector<T> allgather_vec(const std::vector<T> &mine, std::vector<uint64_t> *counts = nullptr) {
+        std::vector<uint8_t> raw;
+        std::vector<uint64_t> sizes;
+        allgatherv_host(mine.data(), mine.size() * sizeof(T), raw, sizes);
+        std::vector<T> out(raw.size() / sizeof(T));
+        if (!raw.empty()) memcpy(out.data(), raw.data(), raw.size());
+        if (counts) {
+            counts->resize(sizes.size());
+            for (size_t r = 0; r < sizes.size(); ++r) (*counts)[r] = sizes[r] / sizeof(T);
+        }
+        return out;
+    }
+    template <class T>
+    std::vector<T> allgather_one(T v) {
+        return allgather_vec(std::vector<T>{v});
+    }
+};
+
+std::unique_ptr<Comm> comm_rccl(mcaat_ctx *ctx, int world, int rank, const uint8_t *unique_id);
+std::unique_ptr<Comm> comm_shm(mcaat_ctx *ctx, int world, int rank, const char *name, uint64_t slot_bytes);
+void comm_unique_id(uint8_t *out);  // 128 bytes (ncclGetUniqueId)
+
+// dist.hip: the graph of the reads of all ranks (each passes its own slice), bit-identical
+// to the single-GPU graph of all reads; every rank holds the whole graph afterwards
+void build_graph_sharded(mcaat_ctx *ctx, Comm &comm, const mcaat_reads *r, int k, mcaat_graph *g);
+
+}  // namespace mcaat
+
+struct mcaat_comm {
+    std::unique_ptr<mcaat::Comm> c;
+};

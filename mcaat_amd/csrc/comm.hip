@@ -1,0 +1,393 @@
+// comm.hip — collectives between the ranks of a multi-GPU run (one process per GPU;
+// SURVEY.md §8e). Two transports behind one interface (comm.h):
+//   RCCL  device buffers move GPU to GPU over xGMI (ncclSend/ncclRecv groups for the
+//         all-to-all, grouped ncclBroadcast for the exact-size all-gather). librccl is
+//         opened on first use, so single-GPU runs never load it.
+//   SHM   a POSIX shared-memory segment on the host: device buffers are staged through it
+//         (ranks sharing one GPU, rehearsals, and host-only tests without a GPU).
+// Every operation is collective and synchronous: it returns once this rank's part is done.
+#include <dlfcn.h>
+#include <fcntl.h>
+#include <sched.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "comm.h"
+
+namespace mcaat {
+
+namespace {
+
+// exclusive prefix sums of per-rank byte counts
+std::vector<uint64_t> offsets_of(const uint64_t *bytes, int n) {
+    std::vector<uint64_t> o(n + 1, 0);
+    for (int i = 0; i < n; ++i) o[i + 1] = o[i] + bytes[i];
+    return o;
+}
+
+// ------------------------------------------------------------------ RCCL ----
+struct Rccl {
+    ncclResult_t (*GetUniqueId)(ncclUniqueId *);
+    ncclResult_t (*CommInitRank)(ncclComm_t *, int, ncclUniqueId, int);
+    ncclResult_t (*CommDestroy)(ncclComm_t);
+    ncclResult_t (*AllGather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
+    ncclResult_t (*Broadcast)(const void *, void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+    ncclResult_t (*Send)(const void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+    ncclResult_t (*Recv)(void *, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t);
+    ncclResult_t (*GroupStart)();
+    ncclResult_t (*GroupEnd)();
+    const char *(*GetErrorString)(ncclResult_t);
+};
+
+const Rccl &rccl() {
+    static Rccl r = [] {
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) throw Error(MCAAT_E_HIP, std::string("cannot load librccl: ") + dlerror());
+        Rccl x{};
+        auto sym = [&](const char *name) {
+            void *p = dlsym(h, name);
+            if (!p) throw Error(MCAAT_E_HIP, std::string("librccl lacks ") + name);
+            return p;
+        };
+        x.GetUniqueId = (decltype(x.GetUniqueId))sym("ncclGetUniqueId");
+        x.CommInitRank = (decltype(x.CommInitRank))sym("ncclCommInitRank");
+        x.CommDestroy = (decltype(x.CommDestroy))sym("ncclCommDestroy");
+        x.AllGather = (decltype(x.AllGather))sym("ncclAllGather");
+        x.Broadcast = (decltype(x.Broadcast))sym("ncclBroadcast");
+        x.Send = (decltype(x.Send))sym("ncclSend");
+        x.Recv = (decltype(x.Recv))sym("ncclRecv");
+        x.GroupStart = (decltype(x.GroupStart))sym("ncclGroupStart");
+        x.GroupEnd = (decltype(x.GroupEnd))sym("ncclGroupEnd");
+        x.GetErrorString = (decltype(x.GetErrorString))sym("ncclGetErrorString");
+        return x;
+    }();
+    return r;
+}
+
+#define NCCL_OK(expr)                                                                              \
+    do {                                                                                           \
+        ncclResult_t r__ = (expr);                                                                 \
+        if (r__ != ncclSuccess)                                                                    \
+            throw ::mcaat::Error(MCAAT_E_HIP, std::string(#expr " failed: ") + rccl().GetErrorString(r__)); \
+    } while (0)
+
+// RCCL counts are size_t, but pieces of at most 1 GiB keep every message well inside the
+// ranges all RCCL versions test
+constexpr uint64_t kPiece = 1ULL << 30;
+
+struct RcclComm final : Comm {
+    mcaat_ctx *ctx;
+    ncclComm_t comm = nullptr;
+    RcclComm(mcaat_ctx *c, int world_, int rank_, const uint8_t *id) : ctx(c) {
+        world = world_;
+        rank = rank_;
+        ncclUniqueId u;
+        memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
+        HIP_OK(hipSetDevice(ctx->device));
+        NCCL_OK(rccl().CommInitRank(&comm, world, u, rank));
+    }
+    ~RcclComm() override {
+        if (comm) (void)rccl().CommDestroy(comm);
+    }
+    const char *kind() const override { return "rccl"; }
+
+    void sync() { HIP_OK(hipStreamSynchronize(ctx->stream)); }
+
+    void barrier() override {
+        DevBuf<uint64_t> a(1), b(world);
+        HIP_OK(hipMemsetAsync(a.p, 0, 8, ctx->stream));
+        NCCL_OK(rccl().AllGather(a.p, b.p, 8, ncclUint8, comm, ctx->stream));
+        sync();
+    }
+
+    void allgather_u64(uint64_t v, std::vector<uint64_t> &out) {
+        DevBuf<uint64_t> a(1), b(world);
+        HIP_OK(hipMemcpyAsync(a.p, &v, 8, hipMemcpyHostToDevice, ctx->stream));
+        NCCL_OK(rccl().AllGather(a.p, b.p, 8, ncclUint8, comm, ctx->stream));
+        out.resize(world);
+        HIP_OK(hipMemcpyAsync(out.data(), b.p, 8 * (uint64_t)world, hipMemcpyDeviceToHost, ctx->stream));
+        sync();
+    }
+
+    void allgatherv_host(const void *send, uint64_t bytes, std::vector<uint8_t> &out,
+                         std::vector<uint64_t> &sizes) override {
+        allgather_u64(bytes, sizes);
+        const auto off = offsets_of(sizes.data(), world);
+        out.resize(off[world]);
+        if (!off[world]) return;
+        DevBuf<uint8_t> s(bytes ? bytes : 1), r(off[world]);
+        if (bytes) HIP_OK(hipMemcpyAsync(s.p, send, bytes, hipMemcpyHostToDevice, ctx->stream));
+        allgatherv_dev(s.p, r.p, sizes.data());
+        HIP_OK(hipMemcpyAsync(out.data(), r.p, off[world], hipMemcpyDeviceToHost, ctx->stream));
+        sync();
+    }
+
+    void alltoallv_dev(const void *send, const uint64_t *send_bytes, void *recv,
+                       const uint64_t *recv_bytes) override {
+        const auto so = offsets_of(send_bytes, world), ro = offsets_of(recv_bytes, world);
+        const uint8_t *s = (const uint8_t *)send;
+        uint8_t *d = (uint8_t *)recv;
+        if (send_bytes[rank] != recv_bytes[rank]) throw Error(MCAAT_E_INVALID, "alltoallv: self sizes differ");
+        if (send_bytes[rank])
+            HIP_OK(hipMemcpyAsync(d + ro[rank], s + so[rank], send_bytes[rank], hipMemcpyDeviceToDevice, ctx->stream));
+        uint64_t most = 0;
+        for (int p = 0; p < world; ++p)
+            if (p != rank) most = std::max({most, send_bytes[p], recv_bytes[p]});
+        // piece c of every peer's message in one group (matching send/recv order on all ranks)
+        for (uint64_t c0 = 0; c0 < most; c0 += kPiece) {
+            NCCL_OK(rccl().GroupStart());
+            for (int p = 0; p < world; ++p) {
+                if (p == rank) continue;
+                if (send_bytes[p] > c0)
+                    NCCL_OK(rccl().Send(s + so[p] + c0, std::min(kPiece, send_bytes[p] - c0), ncclUint8, p, comm,
+                                        ctx->stream));
+                if (recv_bytes[p] > c0)
+                    NCCL_OK(rccl().Recv(d + ro[p] + c0, std::min(kPiece, recv_bytes[p] - c0), ncclUint8, p, comm,
+                                        ctx->stream));
+            }
+            NCCL_OK(rccl().GroupEnd());
+        }
+        sync();
+    }
+
+    // exact-size all-gather: one broadcast per root into its place in the output, grouped
+    void allgatherv_dev(const void *send, void *recv, const uint64_t *sizes) override {
+        const auto off = offsets_of(sizes, world);
+        uint8_t *d = (uint8_t *)recv;
+        uint64_t most = 0;
+        for (int r = 0; r < world; ++r) most = std::max(most, sizes[r]);
+        for (uint64_t c0 = 0; c0 < most; c0 += kPiece) {
+            NCCL_OK(rccl().GroupStart());
+            for (int r = 0; r < world; ++r) {
+                if (sizes[r] <= c0) continue;
+                const uint64_t n = std::min(kPiece, sizes[r] - c0);
+                const void *src = r == rank ? (const uint8_t *)send + c0 : d + off[r] + c0;
+                NCCL_OK(rccl().Broadcast(src, d + off[r] + c0, n, ncclUint8, r, comm, ctx->stream));
+            }
+            NCCL_OK(rccl().GroupEnd());
+        }
+        sync();
+    }
+};
+
+// ------------------------------------------------------------------- SHM ----
+constexpr int kMaxRanks = 64;
+
+struct ShmHeader {
+    std::atomic<uint32_t> arrived;
+    std::atomic<uint32_t> generation;
+    std::atomic<uint32_t> attached;
+    uint32_t world;
+    uint64_t slot_bytes;
+    uint64_t pub[kMaxRanks];  // per-rank published value of the current operation
+};
+static_assert(std::atomic<uint32_t>::is_always_lock_free, "process-shared atomics must be lock-free");
+
+struct ShmComm final : Comm {
+    mcaat_ctx *ctx;  // may be null: host collectives only
+    std::string name;
+    ShmHeader *hdr = nullptr;
+    uint8_t *slots = nullptr;
+    size_t map_bytes = 0;
+    uint64_t slot = 0;
+    double timeout_s = 900.0;
+
+    ShmComm(mcaat_ctx *c, int world_, int rank_, const char *nm, uint64_t slot_bytes) : ctx(c), name(nm) {
+        world = world_;
+        rank = rank_;
+        slot = std::max<uint64_t>(4096, (slot_bytes + 4095) & ~4095ULL);
+        if (const char *e = getenv("MCAAT_COMM_TIMEOUT")) timeout_s = std::max(1.0, atof(e));
+        const uint64_t hb = (sizeof(ShmHeader) + 4095) & ~4095ULL;
+        map_bytes = hb + slot * (uint64_t)world;
+        int fd = -1;
+        const auto t0 = std::chrono::steady_clock::now();
+        if (rank == 0) {
+            fd = shm_open(name.c_str(), O_CREAT | O_EXCL | O_RDWR, 0600);
+            if (fd < 0) throw Error(MCAAT_E_IO, "shm_open(" + name + ") failed (name in use?)");
+            if (ftruncate(fd, (off_t)map_bytes) != 0) {
+                close(fd);
+                shm_unlink(name.c_str());
+                throw Error(MCAAT_E_NOMEM, "ftruncate of the shared segment failed");
+            }
+        } else {
+            // rank 0 creates and sizes the segment; the others wait for it
+            for (;;) {
+                fd = shm_open(name.c_str(), O_RDWR, 0600);
+                if (fd >= 0) {
+                    struct stat st;
+                    if (fstat(fd, &st) == 0 && (uint64_t)st.st_size == map_bytes) break;
+                    close(fd);
+                    fd = -1;
+                }
+                check_timeout(t0, "attach");
+                std::this_thread::sleep_for(std::chrono::milliseconds(2));
+            }
+        }
+        void *p = mmap(nullptr, map_bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        close(fd);
+        if (p == MAP_FAILED) throw Error(MCAAT_E_NOMEM, "mmap of the shared segment failed");
+        hdr = (ShmHeader *)p;
+        slots = (uint8_t *)p + hb;
+        if (rank == 0) {
+            hdr->world = (uint32_t)world;
+            hdr->slot_bytes = slot;
+        }
+        hdr->attached.fetch_add(1, std::memory_order_acq_rel);
+        while (hdr->attached.load(std::memory_order_acquire) < (uint32_t)world) {
+            check_timeout(t0, "attach");
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+        }
+        barrier();
+        if (rank == 0) shm_unlink(name.c_str());  // the mappings stay; nothing is left behind
+    }
+    ~ShmComm() override {
+        if (hdr) munmap(hdr, map_bytes);
+    }
+    const char *kind() const override { return "shm"; }
+
+    void check_timeout(std::chrono::steady_clock::time_point t0, const char *what) const {
+        const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (s > timeout_s)
+            throw Error(MCAAT_E_IO, std::string("shared-memory comm: ") + what + " timed out (a rank is missing?)");
+    }
+
+    void barrier() override {
+        const uint32_t g = hdr->generation.load(std::memory_order_acquire);
+        if (hdr->arrived.fetch_add(1, std::memory_order_acq_rel) == (uint32_t)world - 1) {
+            hdr->arrived.store(0, std::memory_order_relaxed);
+            hdr->generation.fetch_add(1, std::memory_order_acq_rel);
+            return;
+        }
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t spin = 0; hdr->generation.load(std::memory_order_acquire) == g; ++spin) {
+            if (spin < 1024) continue;
+            if ((spin & 1023) == 0) check_timeout(t0, "barrier");
+            sched_yield();
+        }
+    }
+
+    // every rank publishes one value; returns all of them (rank order)
+    std::vector<uint64_t> exchange(uint64_t v) {
+        hdr->pub[rank] = v;
+        barrier();
+        std::vector<uint64_t> all(hdr->pub, hdr->pub + world);
+        barrier();  // nobody overwrites pub before everyone has read it
+        return all;
+    }
+
+    uint8_t *slot_of(int r) const { return slots + slot * (uint64_t)r; }
+
+    // copies between host or device memory and a slot (ctx null: host memory only)
+    void put(uint8_t *dst, const void *src, uint64_t n, bool dev) {
+        if (!n) return;
+        if (dev) HIP_OK(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost));
+        else memcpy(dst, src, n);
+    }
+    void get(void *dst, const uint8_t *src, uint64_t n, bool dev) {
+        if (!n) return;
+        if (dev) HIP_OK(hipMemcpy(dst, src, n, hipMemcpyHostToDevice));
+        else memcpy(dst, src, n);
+    }
+
+    // all-gather of sizes[r] bytes per rank (known to all) through the slots, in rounds
+    void gather_through_slots(const void *send, void *recv, const uint64_t *sizes, bool dev) {
+        const auto off = offsets_of(sizes, world);
+        uint64_t most = 0;
+        for (int r = 0; r < world; ++r) most = std::max(most, sizes[r]);
+        for (uint64_t c0 = 0; c0 < most; c0 += slot) {
+            if (sizes[rank] > c0) put(slot_of(rank), (const uint8_t *)send + c0, std::min(slot, sizes[rank] - c0), dev);
+            barrier();
+            for (int r = 0; r < world; ++r) {
+                if (sizes[r] <= c0) continue;
+                const uint64_t n = std::min(slot, sizes[r] - c0);
+                uint8_t *dst = (uint8_t *)recv + off[r] + c0;
+                if (r == rank) {
+                    if (dev) HIP_OK(hipMemcpy(dst, (const uint8_t *)send + c0, n, hipMemcpyDeviceToDevice));
+                    else memcpy(dst, (const uint8_t *)send + c0, n);
+                } else {
+                    get(dst, slot_of(r), n, dev);
+                }
+            }
+            barrier();
+        }
+    }
+
+    void allgatherv_host(const void *send, uint64_t bytes, std::vector<uint8_t> &out,
+                         std::vector<uint64_t> &sizes) override {
+        sizes = exchange(bytes);
+        const auto off = offsets_of(sizes.data(), world);
+        out.resize(off[world]);
+        gather_through_slots(send, out.data(), sizes.data(), false);
+    }
+
+    void need_ctx() const {
+        if (!ctx) throw Error(MCAAT_E_INVALID, "shared-memory comm without a context moves host memory only");
+        HIP_OK(hipSetDevice(ctx->device));
+        HIP_OK(hipStreamSynchronize(ctx->stream));
+    }
+
+    void alltoallv_dev(const void *send, const uint64_t *send_bytes, void *recv,
+                       const uint64_t *recv_bytes) override {
+        need_ctx();
+        const auto so = offsets_of(send_bytes, world), ro = offsets_of(recv_bytes, world);
+        // shift s: this rank sends to rank+s and receives from rank-s
+        for (int s = 0; s < world; ++s) {
+            const int to = (rank + s) % world, from = (rank - s + world) % world;
+            const uint8_t *src = (const uint8_t *)send + so[to];
+            uint8_t *dst = (uint8_t *)recv + ro[from];
+            if (s == 0) {
+                if (send_bytes[rank] != recv_bytes[rank]) throw Error(MCAAT_E_INVALID, "alltoallv: self sizes differ");
+                if (send_bytes[rank]) HIP_OK(hipMemcpy(dst, src, send_bytes[rank], hipMemcpyDeviceToDevice));
+                continue;
+            }
+            const auto out_n = exchange(send_bytes[to]);
+            uint64_t most = 0;
+            for (int r = 0; r < world; ++r) most = std::max(most, out_n[r]);
+            for (uint64_t c0 = 0; c0 < most; c0 += slot) {
+                if (send_bytes[to] > c0) put(slot_of(rank), src + c0, std::min(slot, send_bytes[to] - c0), true);
+                barrier();
+                if (recv_bytes[from] > c0) get(dst + c0, slot_of(from), std::min(slot, recv_bytes[from] - c0), true);
+                barrier();
+            }
+        }
+    }
+
+    void allgatherv_dev(const void *send, void *recv, const uint64_t *sizes) override {
+        need_ctx();
+        gather_through_slots(send, recv, sizes, true);
+    }
+};
+
+}  // namespace
+
+std::unique_ptr<Comm> comm_rccl(mcaat_ctx *ctx, int world, int rank, const uint8_t *id) {
+    return std::make_unique<RcclComm>(ctx, world, rank, id);
+}
+
+std::unique_ptr<Comm> comm_shm(mcaat_ctx *ctx, int world, int rank, const char *name, uint64_t slot_bytes) {
+    if (world > kMaxRanks) throw Error(MCAAT_E_INVALID, "shared-memory comm: at most 64 ranks");
+    return std::make_unique<ShmComm>(ctx, world, rank, name, slot_bytes);
+}
+
+void comm_unique_id(uint8_t *out) {
+    ncclUniqueId u;
+    NCCL_OK(rccl().GetUniqueId(&u));
+    memcpy(out, u.internal, NCCL_UNIQUE_ID_BYTES);
+}
+
+}  // namespace mcaat

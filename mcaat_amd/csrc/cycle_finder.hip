@@ -21,7 +21,7 @@
 #include <map>
 #include <unordered_set>
 
-#include "internal.h"
+#include "comm.h"
 
 namespace mcaat {
 
@@ -363,14 +363,15 @@ __global__ void __launch_bounds__(kBlock) k_ids_to_bits(const uint64_t *ids, uin
 }
 
 // --------------------------- start candidates --------------------------------
-__global__ void __launch_bounds__(kBlock) k_candidates(GraphView g, uint64_t thr, uint64_t *list,
-                                                       unsigned long long *cursor) {
+// ids [lo, hi) (a rank's share of the scan; [0, D) on one GPU)
+__global__ void __launch_bounds__(kBlock) k_candidates(GraphView g, uint64_t thr, uint64_t lo, uint64_t hi,
+                                                       uint64_t *list, unsigned long long *cursor) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const int lane = threadIdx.x & 63;
-    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < g.D; base += stride) {
+    for (uint64_t base = lo + (uint64_t)blockIdx.x * blockDim.x; base < hi; base += stride) {
         const uint64_t e = base + threadIdx.x;
         bool c = false;
-        if (e < g.D && bit_get(g.valid, e) && (uint64_t)g.mult[e] > thr) {
+        if (e < hi && bit_get(g.valid, e) && (uint64_t)g.mult[e] > thr) {
             uint64_t in[4];
             const int n = dev_incoming(g, e, in);
             if (n >= 2) {
@@ -709,16 +710,17 @@ __global__ void k_fc_gather(const uint64_t *sbase, uint64_t per_al, FcCaps caps,
 
 // conflict[q] = 1 if a node first visited by a tentative commit c < jlist[q] is in the
 // footprint (lock table) of speculative start jlist[q]
+// (jslot[q]: the scratch slot of that start on this rank)
 __global__ void k_fc_conflict(const uint64_t *sbase, uint64_t per_al, uint32_t CL, const uint64_t *newly,
-                              const uint32_t *newly_c, uint64_t n_newly, const uint32_t *jlist, uint64_t nj,
-                              int *conflict) {
+                              const uint32_t *newly_c, uint64_t n_newly, const uint32_t *jlist,
+                              const uint32_t *jslot, uint64_t nj, int *conflict) {
     const uint64_t tot = n_newly * nj;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < tot; idx += stride) {
         const uint64_t a = idx / nj, q = idx - a * nj;
         const uint32_t j = jlist[q];
         if (j <= newly_c[a] || conflict[q]) continue;
-        const uint64_t *lk = (const uint64_t *)((const uint8_t *)sbase + (uint64_t)j * per_al);
+        const uint64_t *lk = (const uint64_t *)((const uint8_t *)sbase + (uint64_t)jslot[q] * per_al);
         if (set_contains(lk, CL, newly[a])) conflict[q] = 1;
     }
 }
@@ -964,6 +966,8 @@ static std::vector<uint64_t> run_dls(mcaat_graph *g, const std::vector<uint64_t>
 // ---------------------------- FindCycle driver -----------------------------------
 struct FcRunner {
     mcaat_graph *g;
+    Comm *comm;  // null: one GPU
+    int N = 1, R = 0;
     FcParams prm;
     FcCaps caps;
     DevBuf<uint64_t> dvis;
@@ -971,7 +975,12 @@ struct FcRunner {
     mcaat_cycles *out;
     uint64_t rounds = 0, reruns = 0;
 
-    FcRunner(mcaat_graph *gr, const mcaat_cf_params &p, mcaat_cycles *o) : g(gr), hvis(gr->ctx, gr->D), out(o) {
+    FcRunner(mcaat_graph *gr, const mcaat_cf_params &p, mcaat_cycles *o, Comm *cm)
+        : g(gr), comm(cm), hvis(gr->ctx, gr->D), out(o) {
+        if (comm) {
+            N = comm->world;
+            R = comm->rank;
+        }
         prm.maxl = p.cycle_max_length;
         prm.minl = p.cycle_min_length;
         prm.cluster = p.cluster_bound;
@@ -992,10 +1001,21 @@ struct FcRunner {
         return (per + 255) & ~255ULL;
     }
 
+    // One speculative round's outputs as seen by every rank: the window's starts are dealt
+    // round-robin (start j runs on rank j % N in its slot j / N), each rank runs its share
+    // against the same visited snapshot, and the statuses and found cycles are all-gathered,
+    // so every rank commits the same prefix in the same order (threads=1 semantics).
+    struct RankOut {
+        std::vector<FcStatus> st;
+        std::vector<uint64_t> nodes;
+        std::vector<uint16_t> lens;
+    };
+
     void run_bucket(const std::vector<uint64_t> &bucket) {
         hipStream_t st = g->ctx->stream;
         std::vector<uint64_t> pending(bucket);
         uint64_t window = (uint64_t)std::max<int64_t>(1, knob(g->ctx, "cf.fc_window", 8192));
+        if (N > 1) window *= (uint64_t)N;  // each rank keeps the single-GPU window of searches
         while (!pending.empty()) {
             // starts already visited are skipped by the reference (:476) -> no entry
             std::vector<uint64_t> keep;
@@ -1006,46 +1026,96 @@ struct FcRunner {
             if (pending.empty()) break;
             ++rounds;
             const uint64_t W = std::min<uint64_t>(window, pending.size());
+            const uint64_t Wl = W > (uint64_t)R ? (W - R + N - 1) / N : 0;  // this rank's starts
             const uint64_t pa = per_al();
-            DevBuf<uint64_t> dst(W);
-            DevBuf<uint8_t> scratch(W * pa);
-            DevBuf<FcStatus> dstat(W);
-            HIP_OK(hipMemcpyAsync(dst.p, pending.data(), 8 * W, hipMemcpyHostToDevice, st));
-            static const int lpw = getenv("MCAAT_FC_LPW") ? atoi(getenv("MCAAT_FC_LPW")) : 1;  // measured: 64 lanes 93 ms, 16: 44, 4: 30, 1: 23 (C3)
-            hipLaunchKernelGGL(k_findcycle, dim3(grid_for(W, (unsigned)lpw)), dim3(64), 0, st, g->view(), dvis.p, dst.p,
-                               W, caps, prm, (uint64_t *)scratch.p, dstat.p, lpw);
-            LAUNCH_OK();
-            std::vector<FcStatus> hs(W);
-            HIP_OK(hipMemcpyAsync(hs.data(), dstat.p, W * sizeof(FcStatus), hipMemcpyDeviceToHost, st));
-            HIP_OK(hipStreamSynchronize(st));
+            DevBuf<uint64_t> dst(Wl);
+            DevBuf<uint8_t> scratch(Wl * pa);
+            DevBuf<FcStatus> dstat(Wl);
+            RankOut mine;
+            mine.st.resize(Wl);
+            if (Wl) {
+                std::vector<uint64_t> ls(Wl);
+                for (uint64_t i = 0; i < Wl; ++i) ls[i] = pending[R + N * i];
+                HIP_OK(hipMemcpyAsync(dst.p, ls.data(), 8 * Wl, hipMemcpyHostToDevice, st));
+                static const int lpw = getenv("MCAAT_FC_LPW") ? atoi(getenv("MCAAT_FC_LPW")) : 1;  // measured: 64 lanes 93 ms, 16: 44, 4: 30, 1: 23 (C3)
+                hipLaunchKernelGGL(k_findcycle, dim3(grid_for(Wl, (unsigned)lpw)), dim3(64), 0, st, g->view(), dvis.p,
+                                   dst.p, Wl, caps, prm, (uint64_t *)scratch.p, dstat.p, lpw);
+                LAUNCH_OK();
+                HIP_OK(hipMemcpyAsync(mine.st.data(), dstat.p, Wl * sizeof(FcStatus), hipMemcpyDeviceToHost, st));
+                HIP_OK(hipStreamSynchronize(st));
+            }
             verbose_mark(g->ctx, "fc.round_kernel");
-            // outputs of every thread that finished (status 0) with cycles
-            std::vector<uint64_t> sel, noff{0}, coff{0};
-            std::vector<int64_t> sel_of(W, -1);
-            uint64_t first_bad = W;
-            for (uint64_t j = 0; j < W; ++j) {
-                if (hs[j].status != 0) { first_bad = j; break; }
-                if (hs[j].ncyc > 0) {
-                    sel_of[j] = (int64_t)sel.size();
-                    sel.push_back(j);
-                    noff.push_back(noff.back() + hs[j].nnodes);
-                    coff.push_back(coff.back() + hs[j].ncyc);
+            // this rank's finished searches (status 0) with cycles, in slot order
+            {
+                std::vector<uint64_t> sel, noff{0}, coff{0};
+                for (uint64_t i = 0; i < Wl; ++i) {
+                    if (mine.st[i].status != 0 && N == 1) break;  // one GPU: nothing past the first overflow is used
+                    if (mine.st[i].status == 0 && mine.st[i].ncyc > 0) {
+                        sel.push_back(i);
+                        noff.push_back(noff.back() + mine.st[i].nnodes);
+                        coff.push_back(coff.back() + mine.st[i].ncyc);
+                    }
+                }
+                mine.nodes.resize(noff.back());
+                mine.lens.resize(coff.back());
+                if (!sel.empty()) {
+                    DevBuf<uint64_t> dsel(sel.size()), dno(noff.size()), dco(coff.size()), dn(noff.back());
+                    DevBuf<uint16_t> dl(coff.back());
+                    HIP_OK(hipMemcpyAsync(dsel.p, sel.data(), 8 * sel.size(), hipMemcpyHostToDevice, st));
+                    HIP_OK(hipMemcpyAsync(dno.p, noff.data(), 8 * noff.size(), hipMemcpyHostToDevice, st));
+                    HIP_OK(hipMemcpyAsync(dco.p, coff.data(), 8 * coff.size(), hipMemcpyHostToDevice, st));
+                    hipLaunchKernelGGL(k_fc_gather, dim3((unsigned)sel.size()), dim3(256), 0, st, (uint64_t *)scratch.p,
+                                       pa, caps, dsel.p, dno.p, dco.p, dn.p, dl.p, (uint64_t)sel.size());
+                    LAUNCH_OK();
+                    HIP_OK(hipMemcpyAsync(mine.nodes.data(), dn.p, 8 * mine.nodes.size(), hipMemcpyDeviceToHost, st));
+                    HIP_OK(hipMemcpyAsync(mine.lens.data(), dl.p, 2 * mine.lens.size(), hipMemcpyDeviceToHost, st));
+                    HIP_OK(hipStreamSynchronize(st));
                 }
             }
-            std::vector<uint64_t> nodes(noff.back());
-            std::vector<uint16_t> lens(coff.back());
-            if (!sel.empty()) {
-                DevBuf<uint64_t> dsel(sel.size()), dno(noff.size()), dco(coff.size()), dn(noff.back());
-                DevBuf<uint16_t> dl(coff.back());
-                HIP_OK(hipMemcpyAsync(dsel.p, sel.data(), 8 * sel.size(), hipMemcpyHostToDevice, st));
-                HIP_OK(hipMemcpyAsync(dno.p, noff.data(), 8 * noff.size(), hipMemcpyHostToDevice, st));
-                HIP_OK(hipMemcpyAsync(dco.p, coff.data(), 8 * coff.size(), hipMemcpyHostToDevice, st));
-                hipLaunchKernelGGL(k_fc_gather, dim3((unsigned)sel.size()), dim3(256), 0, st, (uint64_t *)scratch.p,
-                                   pa, caps, dsel.p, dno.p, dco.p, dn.p, dl.p, (uint64_t)sel.size());
-                LAUNCH_OK();
-                HIP_OK(hipMemcpyAsync(nodes.data(), dn.p, 8 * nodes.size(), hipMemcpyDeviceToHost, st));
-                HIP_OK(hipMemcpyAsync(lens.data(), dl.p, 2 * lens.size(), hipMemcpyDeviceToHost, st));
-                HIP_OK(hipStreamSynchronize(st));
+            // every rank's outputs (one GPU: its own)
+            std::vector<RankOut> others;
+            std::vector<const RankOut *> ro(N);
+            if (N == 1) {
+                ro[0] = &mine;
+            } else {
+                others.resize(N);
+                std::vector<uint64_t> cs, cn, cl;
+                auto st_all = comm->allgather_vec(mine.st, &cs);
+                auto nd_all = comm->allgather_vec(mine.nodes, &cn);
+                auto ln_all = comm->allgather_vec(mine.lens, &cl);
+                uint64_t a = 0, b = 0, c = 0;
+                for (int r = 0; r < N; ++r) {
+                    others[r].st.assign(st_all.begin() + a, st_all.begin() + a + cs[r]);
+                    others[r].nodes.assign(nd_all.begin() + b, nd_all.begin() + b + cn[r]);
+                    others[r].lens.assign(ln_all.begin() + c, ln_all.begin() + c + cl[r]);
+                    a += cs[r];
+                    b += cn[r];
+                    c += cl[r];
+                    ro[r] = &others[r];
+                }
+            }
+            // global view: status of start j and, for starts with cycles, their nodes/lengths
+            std::vector<const FcStatus *> hs(W);
+            uint64_t first_bad = W;
+            for (uint64_t j = 0; j < W; ++j) {
+                hs[j] = &ro[j % N]->st[j / N];
+                if (hs[j]->status != 0 && first_bad == W) first_bad = j;
+            }
+            std::vector<const uint64_t *> jn(W, nullptr);
+            std::vector<const uint16_t *> jc(W, nullptr);
+            {
+                // each rank's outputs are in slot order; only starts before the first overflow
+                // are used (one GPU gathers nothing past it)
+                std::vector<uint64_t> nptr(N, 0), cptr(N, 0);
+                for (uint64_t j = 0; j < first_bad; ++j) {
+                    const int o = (int)(j % N);
+                    if (hs[j]->ncyc > 0) {
+                        jn[j] = ro[o]->nodes.data() + nptr[o];
+                        jc[j] = ro[o]->lens.data() + cptr[o];
+                        nptr[o] += hs[j]->nnodes;
+                        cptr[o] += hs[j]->ncyc;
+                    }
+                }
             }
             verbose_mark(g->ctx, "fc.round_gather");
             // tentative sequential commit (threads=1 semantics), applied directly to the
@@ -1056,12 +1126,12 @@ struct FcRunner {
             for (uint64_t j = 0; j < first_bad; ++j) {
                 const uint64_t s = pending[j];
                 if (hvis.get(s)) { skip[j] = 1; continue; }
-                if (sel_of[j] >= 0) {
-                    const uint64_t q = (uint64_t)sel_of[j];
-                    for (uint64_t a = noff[q]; a < noff[q + 1]; ++a) {
+                if (jn[j]) {
+                    const uint64_t nn = hs[j]->nnodes;
+                    for (uint64_t a = 0; a < nn; ++a) {
                         // random bits of a D-bit map: keep a few misses in flight
-                        if (a + 16 < nodes.size()) __builtin_prefetch(hvis.w + (nodes[a + 16] >> 6), 1);
-                        const uint64_t x = nodes[a];
+                        if (a + 16 < nn) __builtin_prefetch(hvis.w + (jn[j][a + 16] >> 6), 1);
+                        const uint64_t x = jn[j][a];
                         if (!hvis.get(x)) {
                             hvis.set(x);
                             newly.push_back(x);
@@ -1081,22 +1151,36 @@ struct FcRunner {
                 seen_commit = true;
             }
             if (!newly.empty() && !jl.empty()) {
-                DevBuf<uint64_t> dnw(newly.size());
-                DevBuf<uint32_t> dnc(newly.size()), djl(jl.size());
-                DevBuf<int> dconf(jl.size());
-                HIP_OK(hipMemsetAsync(dconf.p, 0, 4 * jl.size(), st));
-                HIP_OK(hipMemcpyAsync(dnw.p, newly.data(), 8 * newly.size(), hipMemcpyHostToDevice, st));
-                HIP_OK(hipMemcpyAsync(dnc.p, newly_c.data(), 4 * newly.size(), hipMemcpyHostToDevice, st));
-                HIP_OK(hipMemcpyAsync(djl.p, jl.data(), 4 * jl.size(), hipMemcpyHostToDevice, st));
-                hipLaunchKernelGGL(k_fc_conflict, dim3(grid_for((uint64_t)newly.size() * jl.size(), kBlock)),
-                                   dim3(kBlock), 0, st, (uint64_t *)scratch.p, pa, caps.CL, dnw.p, dnc.p,
-                                   (uint64_t)newly.size(), djl.p, (uint64_t)jl.size(), dconf.p);
-                LAUNCH_OK();
-                std::vector<int> conf(jl.size());
-                HIP_OK(hipMemcpyAsync(conf.data(), dconf.p, 4 * jl.size(), hipMemcpyDeviceToHost, st));
-                HIP_OK(hipStreamSynchronize(st));
-                for (size_t q = 0; q < jl.size(); ++q)
-                    if (conf[q]) { f = jl[q]; break; }
+                // each rank checks the footprints of its own starts
+                std::vector<uint32_t> jm, js;
+                for (uint32_t j : jl)
+                    if ((int)(j % N) == R) {
+                        jm.push_back(j);
+                        js.push_back(j / N);
+                    }
+                uint64_t my_first = W;
+                if (!jm.empty()) {
+                    DevBuf<uint64_t> dnw(newly.size());
+                    DevBuf<uint32_t> dnc(newly.size()), djl(jm.size()), djs(js.size());
+                    DevBuf<int> dconf(jm.size());
+                    HIP_OK(hipMemsetAsync(dconf.p, 0, 4 * jm.size(), st));
+                    HIP_OK(hipMemcpyAsync(dnw.p, newly.data(), 8 * newly.size(), hipMemcpyHostToDevice, st));
+                    HIP_OK(hipMemcpyAsync(dnc.p, newly_c.data(), 4 * newly.size(), hipMemcpyHostToDevice, st));
+                    HIP_OK(hipMemcpyAsync(djl.p, jm.data(), 4 * jm.size(), hipMemcpyHostToDevice, st));
+                    HIP_OK(hipMemcpyAsync(djs.p, js.data(), 4 * js.size(), hipMemcpyHostToDevice, st));
+                    hipLaunchKernelGGL(k_fc_conflict, dim3(grid_for((uint64_t)newly.size() * jm.size(), kBlock)),
+                                       dim3(kBlock), 0, st, (uint64_t *)scratch.p, pa, caps.CL, dnw.p, dnc.p,
+                                       (uint64_t)newly.size(), djl.p, djs.p, (uint64_t)jm.size(), dconf.p);
+                    LAUNCH_OK();
+                    std::vector<int> conf(jm.size());
+                    HIP_OK(hipMemcpyAsync(conf.data(), dconf.p, 4 * jm.size(), hipMemcpyDeviceToHost, st));
+                    HIP_OK(hipStreamSynchronize(st));
+                    for (size_t q = 0; q < jm.size(); ++q)
+                        if (conf[q]) { my_first = jm[q]; break; }
+                }
+                if (N > 1)
+                    for (uint64_t x : comm->allgather_one(my_first)) my_first = std::min(my_first, x);
+                f = std::min(f, my_first);
             }
             verbose_mark(g->ctx, "fc.commit_conflicts");
             // commit the prefix [0, f)
@@ -1105,10 +1189,9 @@ struct FcRunner {
                 if (skip[j]) continue;
                 out->starts.push_back(pending[j]);
                 std::vector<uint64_t> fl, of{0};
-                if (sel_of[j] >= 0) {
-                    const uint64_t q = (uint64_t)sel_of[j];
-                    fl.assign(nodes.begin() + noff[q], nodes.begin() + noff[q + 1]);
-                    for (uint64_t c = coff[q]; c < coff[q + 1]; ++c) of.push_back(of.back() + lens[c]);
+                if (jn[j]) {
+                    fl.assign(jn[j], jn[j] + hs[j]->nnodes);
+                    for (int32_t c = 0; c < hs[j]->ncyc; ++c) of.push_back(of.back() + jc[j][c]);
                 }
                 out->stats[5] += of.size() - 1;
                 out->flat.push_back(std::move(fl));
@@ -1131,7 +1214,7 @@ struct FcRunner {
             if (f < W) ++reruns;
             if (f == first_bad && first_bad < W) {
                 // scratch overflow at position f: grow the exhausted structure and re-run
-                const int code = hs[f].status;
+                const int code = hs[f]->status;
                 if (code == 1) caps.CL *= 4;
                 else if (code == 2) caps.CR *= 4;
                 else caps.CO *= 2;
@@ -1140,25 +1223,38 @@ struct FcRunner {
             }
             pending.erase(pending.begin(), pending.begin() + f);
             // adapt the speculation window to the observed conflict rate
+            const uint64_t wmax = 8192ULL * N;
             if (f < W / 4) window = std::max<uint64_t>(16, window / 2);
-            else if (f == W) window = std::min<uint64_t>(8192, window * 2);
+            else if (f == W) window = std::min<uint64_t>(wmax, window * 2);
         }
     }
 };
 
-void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out) {
+// sorted union of every rank's ascending id list
+static std::vector<uint64_t> gather_sorted(Comm *comm, const std::vector<uint64_t> &mine) {
+    std::vector<uint64_t> all = comm->allgather_vec(mine);
+    std::sort(all.begin(), all.end());
+    return all;
+}
+
+void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, Comm *comm) {
     mcaat_ctx *ctx = g->ctx;
     hipStream_t st = ctx->stream;
     const uint64_t D = g->D;
     const uint64_t nw = g->n_words();
     GraphView v = g->view();
     StageTimer timer(ctx);
+    if (comm && comm->world == 1) comm = nullptr;
+    const int N = comm ? comm->world : 1, R = comm ? comm->rank : 0;
     DevBuf<unsigned long long> cnt(1);
     auto zero = [&]() { HIP_OK(hipMemsetAsync(cnt.p, 0, 8, st)); };
     // grid-stride scans whose per-block totals meet in one counter: a capped grid keeps that
     // counter's atomics to a few thousand
     const unsigned wgrid = grid_for(nw * 64, kBlock, (unsigned)ctx->n_cu * 16);
 
+    // Steps 1-4 change the valid bits every later step reads, so every rank runs them on its
+    // replica of the graph (the peel is a global fixpoint); the scans of step 5 and the
+    // searches of steps 5-6 are split over the ranks.
     // 1. CollectTips (before the multiplicity filter) -> seeds of the reduction
     DevBuf<uint64_t> seeds(nw);
     zero();
@@ -1198,19 +1294,32 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out) {
     }
     std::vector<uint64_t> cand;
     {
-        DevBuf<uint64_t> list(D ? D : 1);
+        // rank R scans ids [R*D/N, (R+1)*D/N)
+        const uint64_t lo = (uint64_t)((unsigned __int128)D * R / N), hi = (uint64_t)((unsigned __int128)D * (R + 1) / N);
+        DevBuf<uint64_t> list(hi > lo ? hi - lo : 1);
         zero();
-        hipLaunchKernelGGL(k_candidates, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, v, p.threshold_multiplicity,
-                           list.p, cnt.p);
-        LAUNCH_OK();
+        if (hi > lo) {
+            hipLaunchKernelGGL(k_candidates, dim3(grid_for(hi - lo, kBlock)), dim3(kBlock), 0, st, v,
+                               p.threshold_multiplicity, lo, hi, list.p, cnt.p);
+            LAUNCH_OK();
+        }
         const uint64_t nc = read_counter(ctx, cnt.p);
         cand.resize(nc);
         if (nc) HIP_OK(hipMemcpy(cand.data(), list.p, 8 * nc, hipMemcpyDeviceToHost));
     }
     std::sort(cand.begin(), cand.end());
+    if (comm) cand = gather_sorted(comm, cand);
     timer.mark("candidates");
     verbose_mark(ctx, "cf.candidates");
-    std::vector<uint64_t> pass = run_dls(g, cand, p.cycle_max_length);
+    std::vector<uint64_t> pass;
+    if (comm) {
+        // candidate i is searched on rank i % N
+        std::vector<uint64_t> mine;
+        for (size_t i = R; i < cand.size(); i += N) mine.push_back(cand[i]);
+        pass = gather_sorted(comm, run_dls(g, mine, p.cycle_max_length));
+    } else {
+        pass = run_dls(g, cand, p.cycle_max_length);
+    }
     timer.mark("dls");
     verbose_mark(ctx, "cf.dls");
     std::map<int, std::vector<uint64_t>, std::greater<int>> chunks;
@@ -1234,7 +1343,7 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out) {
     out->stats[4] = out->cand_ids.size();
     // 6. bucket loop
     verbose_mark(ctx, "cf.chunks");
-    FcRunner fr(g, p, out);
+    FcRunner fr(g, p, out, comm);
     verbose_mark(ctx, "cf.fc_setup");
     // with threads=1 the reference's bucket loop is one ordered sequence of starts, so the
     // speculative windows run across bucket boundaries
@@ -1246,7 +1355,6 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out) {
     HIP_OK(hipStreamSynchronize(st));
     timer.finish();
 }
-
 void graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, int incoming, uint64_t *out,
                      int32_t *counts) {
     if (!n) return;

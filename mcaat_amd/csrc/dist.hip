@@ -1,0 +1,117 @@
+// dist.hip — the hash-range sharded graph build of a multi-GPU run, natively over a Comm
+// (RCCL or shared memory; comm.hip). The C++ counterpart of mcaat_amd/shard.py with the same
+// steps and the same result:
+//   1. every rank counts its own reads (node_counter; the LDS collapse pre-aggregates);
+//   2. the ranks sum a histogram of the top BOSS-key bits and cut it into `world` owner
+//      ranges of equal weight, contiguous in BOSS order;
+//   3. each rank writes its oriented (BOSS key, partial count) pairs owner-major and the ranks
+//      exchange them in one all-to-all (keys and counts);
+//   4. each owner sorts its pairs and sums equal keys (saturating at 65535 after the sum);
+//   5. an exact-size all-gather in rank order concatenates the owners' ranges into the
+//      single-GPU edge array (edge ids bit-identical), and every rank builds the adjacency.
+// Replaces: Read2SdbgS2::Run driven from sdbg_build.cpp:171-187, for reads split over ranks.
+#include <algorithm>
+#include <vector>
+
+#include "comm.h"
+
+namespace mcaat {
+
+namespace {
+
+constexpr int kHistBits = 12;
+
+// world-1 ascending split points at histogram-bin edges with equal weight (owner o takes
+// keys in [splits[o-1], splits[o])); the same rule as shard.choose_splits
+std::vector<uint64_t> choose_splits(const std::vector<uint64_t> &hist, int world, int key_bits) {
+    const int nb = (int)hist.size();
+    int bits = 0;
+    while ((1 << bits) < nb) ++bits;
+    const int shift = key_bits - bits;
+    std::vector<double> cum(nb);
+    double acc = 0;
+    for (int i = 0; i < nb; ++i) cum[i] = acc += (double)hist[i];
+    const double total = nb ? cum[nb - 1] : 0.0;
+    std::vector<uint64_t> out;
+    int prev = 0;
+    for (int o = 1; o < world; ++o) {
+        int b = nb;
+        if (total > 0) b = (int)(std::lower_bound(cum.begin(), cum.end(), total * o / world) - cum.begin()) + 1;
+        b = std::min(std::max(b, prev), nb);
+        out.push_back((uint64_t)b << shift);
+        prev = b;
+    }
+    return out;
+}
+
+}  // namespace
+
+void build_graph_sharded(mcaat_ctx *ctx, Comm &comm, const mcaat_reads *r, int k, mcaat_graph *g) {
+    hipStream_t st = ctx->stream;
+    const int N = comm.world, R = comm.rank;
+    StageTimer timer(ctx);
+    CountResult c;
+    node_counter(ctx, r, k, c);
+    timer.mark("node_counter");
+
+    std::vector<uint64_t> hist(1u << kHistBits);
+    counts_histogram(ctx, c, k, kHistBits, hist.data());
+    {
+        const std::vector<uint64_t> all = comm.allgather_vec(hist);
+        std::fill(hist.begin(), hist.end(), 0);
+        for (size_t i = 0; i < all.size(); ++i) hist[i % hist.size()] += all[i];
+    }
+    const std::vector<uint64_t> splits = choose_splits(hist, N, 2 * (k + 1));
+    const uint64_t cap = std::max<uint64_t>(1, 2 * c.n);
+    DevBuf<uint64_t> okeys(cap);
+    DevBuf<uint32_t> ocnt(cap);
+    std::vector<uint64_t> sizes(N);
+    counts_partition(ctx, c, k, N, splits.data(), sizes.data(), okeys.p, ocnt.p, cap);
+    c = CountResult{};
+    timer.mark("shard_partition");
+
+    // sizes[s][d] of every rank s -> what this rank receives
+    const std::vector<uint64_t> mat = comm.allgather_vec(sizes);
+    std::vector<uint64_t> in(N), sb(N), rb(N);
+    uint64_t n_in = 0;
+    for (int s = 0; s < N; ++s) n_in += in[s] = mat[(uint64_t)s * N + R];
+    DevBuf<uint64_t> rk(n_in);
+    DevBuf<uint32_t> rc(n_in);
+    for (int p = 0; p < N; ++p) sb[p] = 8 * sizes[p], rb[p] = 8 * in[p];
+    comm.alltoallv_dev(okeys.p, sb.data(), rk.p, rb.data());
+    for (int p = 0; p < N; ++p) sb[p] = 4 * sizes[p], rb[p] = 4 * in[p];
+    comm.alltoallv_dev(ocnt.p, sb.data(), rc.p, rb.data());
+    okeys.release();
+    ocnt.release();
+    timer.mark("shard_all_to_all");
+
+    DevBuf<uint64_t> uk(n_in);
+    DevBuf<uint16_t> um(n_in);
+    const uint64_t u = edges_reduce(ctx, k, rk.p, rc.p, n_in, uk.p, um.p);
+    rk.release();
+    rc.release();
+    timer.mark("shard_reduce");
+
+    const std::vector<uint64_t> ns = comm.allgather_one(u);
+    uint64_t D = 0;
+    for (uint64_t x : ns) D += x;
+    g->ctx = ctx;
+    g->k = k;
+    g->D = D;
+    g->key.alloc(D ? D : 1);
+    g->mult.alloc(D ? D : 1);
+    std::vector<uint64_t> b8(N), b2(N);
+    for (int p = 0; p < N; ++p) b8[p] = 8 * ns[p], b2[p] = 2 * ns[p];
+    HIP_OK(hipStreamSynchronize(st));
+    comm.allgatherv_dev(uk.p, g->key.p, b8.data());
+    comm.allgatherv_dev(um.p, g->mult.p, b2.data());
+    uk.release();
+    um.release();
+    timer.mark("shard_all_gather");
+    sdbg_finish(ctx, g);
+    timer.mark("sdbg_build");
+    HIP_OK(hipStreamSynchronize(st));
+    timer.finish();
+}
+
+}  // namespace mcaat

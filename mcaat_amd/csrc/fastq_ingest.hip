@@ -302,11 +302,14 @@ struct Source {
     int fd = -1;
     uint64_t off = 0;
     const char *path;
-    explicit Source(const char *p) : path(p) {
+    uint64_t end = ~0ULL;  // plain files: read [off, end) only (a rank's part of the file)
+    // [begin, end) of a plain file; a .gz file is read whole (begin = 0, end = ~0)
+    explicit Source(const char *p, uint64_t begin = 0, uint64_t end_ = ~0ULL) : off(begin), path(p), end(end_) {
         unsigned char magic[2] = {0, 0};
         fd = open(p, O_RDONLY);
         if (fd < 0) throw Error(MCAAT_E_IO, std::string("cannot open ") + p);
         const bool is_gz = pread(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b;
+        if (is_gz && (begin != 0 || end_ != ~0ULL)) throw Error(MCAAT_E_INVALID, "a .gz input cannot be split");
         if (is_gz) {
             close(fd);
             fd = -1;
@@ -325,6 +328,8 @@ struct Source {
     Source &operator=(const Source &) = delete;
     size_t read(uint8_t *dst, size_t n) {
         if (gz) return read_full(gz, dst, n, path);
+        n = (size_t)std::min<uint64_t>(n, end > off ? end - off : 0);
+        if (!n) return 0;
         // 8 by default: the C3 FASTQ (92 GB in tmpfs) reads at 38 GB/s end to end with 8 or 16
         // threads, 12.6 GB/s with 4; MCAAT_FASTQ_THREADS overrides (1..32)
         static const int kThreads = [] {
@@ -377,7 +382,8 @@ size_t fastq_chunk_bytes() {
 
 // All inputs are FASTQ (checked by the caller). Files are concatenated; records of files
 // after the first are reversed and complemented in the mapping view (paired-end R2).
-void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_reads *r) {
+void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_reads *r,
+                  const std::vector<std::pair<uint64_t, uint64_t>> *ranges) {
     const size_t CH = fastq_chunk_bytes();
     const size_t R = std::max<size_t>(CH / 4, 4096);  // carry reserve: the longest record that fits
     const size_t cap = R + CH + 2 * kSeg;
@@ -387,7 +393,11 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
         struct stat st;
         const std::string path(files[i]);
         const bool gz = path.size() > 3 && path.compare(path.size() - 3, 3, ".gz") == 0;
-        if (stat(files[i], &st) == 0) est += (uint64_t)st.st_size * (gz ? 4 : 1);
+        if (stat(files[i], &st) == 0) {
+            uint64_t sz = (uint64_t)st.st_size;
+            if (ranges) sz = std::min(sz, (*ranges)[i].second) - std::min(sz, (*ranges)[i].first);
+            est += sz * (gz ? 4 : 1);
+        }
     }
     DevBuf<uint64_t> packed(est / 64 + 1024), offsets(est / 256 + 1024);
     DevBuf<uint64_t> qpacked(est / 64 + 1024), qoffsets(est / 256 + 1024);
@@ -461,8 +471,16 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
             HIP_OK(hipEventRecord(up_ev[x], cs.s));
         }
     };
+    std::vector<uint64_t> file_records;
     for (int fi = 0; fi < n_files; ++fi) {
-        Source src(files[fi]);
+        const uint64_t rec_before = n_rec;
+        struct FileDone {  // records of this file, however the loop below is left
+            std::vector<uint64_t> &v;
+            const uint64_t &n, before;
+            ~FileDone() { v.push_back(n - before); }
+        } file_done{file_records, n_rec, rec_before};
+        if (ranges && (*ranges)[fi].first >= (*ranges)[fi].second) continue;  // no part of this file
+        Source src(files[fi], ranges ? (*ranges)[fi].first : 0, ranges ? (*ranges)[fi].second : ~0ULL);
         int cur = 0;
         size_t n = src.read(hb[cur] + R, CH);
         bool eof = n < CH;
@@ -590,6 +608,7 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
     r->packed = std::move(packed);
     r->offsets = std::move(offsets);
     r->n_records = n_rec;
+    r->file_records = file_records;
     r->has_records = (flags_all & kDiffer) != 0;
     if (r->has_records) {
         r->rec_packed = std::move(qpacked);
@@ -655,6 +674,84 @@ void write_fastq(const mcaat_reads *r, const char *path, int threads) {
     for (auto &th : pool) th.join();
     close(fd);
     if (failed) throw Error(MCAAT_E_IO, std::string("write failed: ") + path);
+}
+
+}  // namespace mcaat
+
+namespace mcaat {
+
+bool is_gzip_file(const char *path) {
+    unsigned char magic[2] = {0, 0};
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) throw Error(MCAAT_E_IO, std::string("cannot open ") + path);
+    const bool gz = pread(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b;
+    close(fd);
+    return gz;
+}
+
+// A line start q >= pos begins a record when line q starts with '@', line q+2 with '+', and
+// lines q+1 and q+3 (sequence, quality) have the same length. A quality line that starts
+// with '@' is followed by a header and a sequence line, never by '+', so it is not taken.
+// The window grows until four whole lines follow a candidate (records up to 64 MiB).
+uint64_t fastq_record_start(const char *path, uint64_t pos) {
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) throw Error(MCAAT_E_IO, std::string("cannot open ") + path);
+    struct stat st;
+    if (fstat(fd, &st) != 0) {
+        close(fd);
+        throw Error(MCAAT_E_IO, std::string("cannot stat ") + path);
+    }
+    const uint64_t size = (uint64_t)st.st_size;
+    if (pos == 0 || pos >= size) {
+        close(fd);
+        return std::min(pos, size);
+    }
+    std::vector<uint8_t> buf;
+    uint64_t result = size;
+    // the window starts one byte early so a record starting exactly at pos is seen
+    const uint64_t w0 = pos - 1;
+    for (uint64_t win = 1 << 16;; win *= 2) {
+        const uint64_t n = std::min<uint64_t>(win, size - w0);
+        buf.resize(n);
+        uint64_t got = 0;
+        while (got < n) {
+            const ssize_t r = pread(fd, buf.data() + got, n - got, (off_t)(w0 + got));
+            if (r <= 0) break;
+            got += (uint64_t)r;
+        }
+        buf.resize(got);
+        const bool at_eof = w0 + got >= size;
+        // line starts at or after pos (index 0 is byte pos - 1)
+        std::vector<uint64_t> ls;
+        for (uint64_t i = 0; i + 1 < got; ++i)
+            if (buf[i] == '\n') ls.push_back(i + 1);
+        auto line_len = [&](size_t li) -> int64_t {  // -1: line not complete in the window
+            const uint64_t b = ls[li];
+            const uint64_t e = li + 1 < ls.size() ? ls[li + 1] - 1 : (at_eof ? got : ~0ULL);
+            if (e == ~0ULL) return -1;
+            uint64_t len = e - b;
+            if (len && buf[b + len - 1] == '\n') --len;
+            if (len && buf[b + len - 1] == '\r') --len;
+            return (int64_t)len;
+        };
+        bool undecided = false;
+        for (size_t li = 0; li < ls.size(); ++li) {
+            if (buf[ls[li]] != '@') continue;
+            if (li + 3 >= ls.size()) {  // the record's four lines are not all in the window
+                if (!at_eof) undecided = true;
+                break;
+            }
+            if (buf[ls[li + 2]] != '+') continue;
+            const int64_t a = line_len(li + 1), b = line_len(li + 3);
+            if (a < 0 || b < 0) { undecided = true; break; }
+            if (a != b) continue;
+            result = w0 + ls[li];
+            break;
+        }
+        if (result != size || !undecided || at_eof || win >= (64ULL << 20)) break;
+    }
+    close(fd);
+    return result;
 }
 
 }  // namespace mcaat

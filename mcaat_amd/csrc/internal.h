@@ -148,6 +148,7 @@ struct mcaat_reads {
     mcaat::DevBuf<uint64_t> rec_offsets;
     uint64_t n_records = 0;
     bool has_records = false;
+    std::vector<uint64_t> file_records;  // mapping-view records per input file (file order)
 };
 
 struct mcaat_mapped {  // relevant reads: node-id chains in reference order
@@ -276,7 +277,10 @@ void counts_partition(mcaat_ctx *ctx, const CountResult &c, int k, int n_owners,
 uint64_t edges_reduce(mcaat_ctx *ctx, int k, const uint64_t *keys, const uint32_t *cnt, uint64_t n, uint64_t *keys_out,
                       uint16_t *mult_out);
 void graph_from_sorted(mcaat_ctx *ctx, int k, const uint64_t *keys, const uint16_t *mult, uint64_t D, mcaat_graph *g);
-void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out);
+struct Comm;  // comm.h
+// comm: the ranks of a multi-GPU run that each hold this graph (null: one GPU); every rank
+// gets the same results
+void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, Comm *comm = nullptr);
 void synth_reads(mcaat_ctx *ctx, const mcaat_synth_spec &s, mcaat_reads *out, uint64_t first, uint64_t count);
 void synth_genome_host(const mcaat_synth_spec &s, std::vector<uint64_t> &genome);
 void graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, int incoming, uint64_t *out,
@@ -285,7 +289,12 @@ void graph_set_valid(mcaat_graph *g, const uint64_t *ids, size_t n, int valid);
 void graph_download_valid(const mcaat_graph *g, uint8_t *valid);
 void graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n);
 // FASTQ(.gz) inputs parsed on the GPU (fastq_ingest.hip)
-void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_reads *r);
+// ranges: per file, the byte range [first, second) to read (a rank's part; null: whole files)
+void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_reads *r,
+                  const std::vector<std::pair<uint64_t, uint64_t>> *ranges = nullptr);
+// first 4-line FASTQ record start at or after byte pos of a plain file (its size if none)
+uint64_t fastq_record_start(const char *path, uint64_t pos);
+bool is_gzip_file(const char *path);
 void write_fastq(const mcaat_reads *r, const char *path, int threads);
 void graph_save(const mcaat_graph *g, const char *path);
 void graph_load(mcaat_ctx *ctx, const char *path, mcaat_graph *g);

@@ -32,6 +32,11 @@ std::vector<uint64_t> get_read_from_sequence(const SDBG &sdbg,                  
 // reads.cpp:88-130 over the reads resident in HBM (mapping view of the input files)
 std::vector<std::vector<uint64_t>> get_reads(const SDBG &sdbg, const mcaat_reads *reads,
                                              const std::vector<std::vector<uint64_t>> cycles);
+// over the ranks of a multi-GPU run: each maps its own part; every rank gets all relevant
+// reads in input order (n_files: number of input files)
+std::vector<std::vector<uint64_t>> get_reads(const SDBG &sdbg, const mcaat_reads *reads,
+                                             const std::vector<std::vector<uint64_t>> cycles, mcaat_comm *comm,
+                                             int n_files);
 
 // ---------------------------------------------------------------- spacer_ordering.h
 struct Graph {  // spacer_ordering.h:20-46
@@ -115,7 +120,8 @@ double partial_ratio(const std::string &s1, const std::string &s2);
 // ---------------------------------------------------------------- main_run_and_debug.h
 using FoundSystem = std::tuple<std::string, std::string, std::vector<std::string>, float, float>;
 std::vector<std::vector<uint64_t>> run_and_debug_finding_of_relevant_reads(
-    const std::vector<std::vector<uint64_t>> &cycles, const mcaat_reads *reads, const SDBG &sdbg);
+    const std::vector<std::vector<uint64_t>> &cycles, const mcaat_reads *reads, const SDBG &sdbg,
+    mcaat_comm *comm = nullptr, int n_files = 1);
 std::vector<FoundSystem> run_and_debug_spacer_ordering(const std::vector<std::vector<uint64_t>> &reads, SDBG &sdbg,
                                                        const std::vector<std::vector<uint64_t>> &cycles);
 void run_and_debug_benchmark_results(const Settings &settings, const std::vector<FoundSystem> &found_systems);

@@ -3,11 +3,18 @@
 // (step 6), spacer ordering (step 7), results / benchmark (step 8) and CRISPRAnalyzer, which
 // writes settings.output_file (CRISPR_Arrays.txt). The cycles themselves are also written to
 // <cycles_folder>/cycles.txt (not in the reference's release build).
+#include <sys/wait.h>
+#include <unistd.h>
+
 #include <chrono>
+#include <csignal>
 #include <cstdio>
 #include <filesystem>
 #include <fstream>
 #include <iostream>
+#include <random>
+#include <sstream>
+#include <thread>
 
 #include "downstream.h"
 
@@ -35,11 +42,121 @@ static std::string cycle_sequence(const SDBG &sdbg, const std::vector<uint64_t> 
     return s;
 }
 
+// Multi-GPU run (--gpus N): rank 0 forks ranks 1..N-1 before anything touches the GPU, one
+// process per GPU. The RCCL id goes to each child through a pipe; the shared-memory transport
+// needs only the segment name chosen here. Ranks other than 0 print nothing to stdout and end
+// after step 6 (the relevant reads are gathered to every rank); rank 0 writes the outputs. A
+// rank that fails ends the whole run (a watcher thread on rank 0 reaps the children).
+struct Ranks {
+    std::vector<pid_t> children;
+    std::vector<int> to_child;  // rank 0: write ends of the id pipes
+    int from_parent = -1;       // rank > 0: read end
+    std::string shm_name;
+    std::thread watcher;
+
+    ~Ranks() {
+        if (watcher.joinable()) watcher.detach();  // an error path: the process is ending
+    }
+    void kill_children() {
+        for (pid_t p : children) kill(p, SIGTERM);
+    }
+    static void write_all(int fd, const void *p, size_t n) {
+        const char *c = (const char *)p;
+        while (n) {
+            const ssize_t w = write(fd, c, n);
+            if (w <= 0) throw std::runtime_error("multi-GPU: cannot pass the communicator id to a rank");
+            c += w;
+            n -= (size_t)w;
+        }
+    }
+    static void read_all(int fd, void *p, size_t n) {
+        char *c = (char *)p;
+        while (n) {
+            const ssize_t r = read(fd, c, n);
+            if (r <= 0) throw std::runtime_error("multi-GPU: rank 0 ended before passing the communicator id");
+            c += r;
+            n -= (size_t)r;
+        }
+    }
+
+    void fork_ranks(Settings &s) {
+        std::random_device rd;
+        char name[64];
+        snprintf(name, sizeof name, "/mcaat_%d_%08x", (int)getpid(), (unsigned)rd());
+        shm_name = name;
+        std::cout.flush();
+        fflush(stdout);
+        for (int r = 1; r < s.gpus; ++r) {
+            int fds[2];
+            if (pipe(fds) != 0) throw std::runtime_error("multi-GPU: pipe failed");
+            const pid_t pid = fork();
+            if (pid < 0) throw std::runtime_error("multi-GPU: fork failed");
+            if (pid == 0) {
+                close(fds[1]);
+                for (int w : to_child) close(w);
+                to_child.clear();
+                children.clear();
+                from_parent = fds[0];
+                s.rank = r;
+                if (!freopen("/dev/null", "w", stdout)) throw std::runtime_error("multi-GPU: cannot silence a rank");
+                return;
+            }
+            close(fds[0]);
+            children.push_back(pid);
+            to_child.push_back(fds[1]);
+        }
+    }
+
+    // after fork: this rank's context and communicator
+    void connect(Settings &s) {
+        mcaat_ctx *ctx = mcaat_host_ctx(mcaat_rank_device(s));
+        if (s.comm == "rccl") {
+            int n = 0;
+            mcaat_check(mcaat_device_count(&n), "mcaat_device_count");
+            if (s.gpus > n)
+                throw std::runtime_error("--gpus " + std::to_string(s.gpus) + " > " + std::to_string(n) +
+                                         " visible GPUs (RCCL needs one GPU per rank; --comm shm shares GPUs)");
+            uint8_t id[MCAAT_COMM_ID_BYTES];
+            if (s.rank == 0) {
+                mcaat_check(mcaat_comm_unique_id(id), "mcaat_comm_unique_id");
+                for (int w : to_child) write_all(w, id, sizeof id);
+            } else {
+                read_all(from_parent, id, sizeof id);
+            }
+            mcaat_check(mcaat_comm_init_rccl(ctx, s.gpus, s.rank, id, &s.mcomm), "joining the ranks (RCCL)");
+        } else {
+            mcaat_check(mcaat_comm_init_shm(ctx, s.gpus, s.rank, shm_name.c_str(), 0, &s.mcomm),
+                        "joining the ranks (shared memory)");
+        }
+        for (int w : to_child) close(w);
+        to_child.clear();
+        if (from_parent >= 0) close(from_parent);
+        from_parent = -1;
+    }
+
+    void watch() {
+        std::vector<pid_t> kids = children;
+        watcher = std::thread([kids]() {
+            for (size_t i = 0; i < kids.size(); ++i) {
+                int st = 0;
+                if (waitpid(kids[i], &st, 0) < 0) continue;
+                if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) {
+                    std::cerr << "rank " << i + 1 << " failed; ending the run" << std::endl;
+                    for (pid_t p : kids) kill(p, SIGTERM);
+                    _exit(1);
+                }
+            }
+        });
+    }
+};
+
 static void banner(const char *title) {
     std::cout << "\n══════════════════════════════════════════════" << std::endl;
     std::cout << title << std::endl;
     std::cout << "══════════════════════════════════════════════" << std::endl;
 }
+
+static int run(Settings &settings, Ranks &ranks);
 
 int main(int argc, char **argv) {
     try {
@@ -57,12 +174,33 @@ int main(int argc, char **argv) {
             fs::remove_all(settings.output_folder);
             return 1;
         }
-        {
-            // brings the HIP runtime up before the timed span (errors surface in SDBGBuild, after
-            // it has written data.lib as the reference does)
-            int n_dev = 0;
-            (void)mcaat_device_count(&n_dev);
+        Ranks ranks;
+        if (settings.gpus > 1) ranks.fork_ranks(settings);  // before any GPU call
+        try {
+            return run(settings, ranks);
+        } catch (...) {
+            ranks.kill_children();
+            throw;
         }
+    } catch (const std::exception &e) {
+        std::cerr << e.what() << std::endl;
+        return 1;
+    }
+}
+
+static int run(Settings &settings, Ranks &ranks) {
+    const bool rank0 = settings.rank == 0;
+    {
+        // brings the HIP runtime up before the timed span (errors surface in SDBGBuild, after
+        // it has written data.lib as the reference does)
+        int n_dev = 0;
+        (void)mcaat_device_count(&n_dev);
+    }
+    if (settings.gpus > 1) {
+        ranks.connect(settings);
+        if (rank0) ranks.watch();
+    }
+    {
         using clk = std::chrono::steady_clock;
         const auto t_start = clk::now();
         SDBGBuild sdbg_build(settings);                        // main.cpp:517
@@ -86,7 +224,7 @@ int main(int argc, char **argv) {
         auto cycles_map = cycle_finder.results;
         std::cout << "Number of nodes in results: " << cycles_map.size() << std::endl;
         auto cycles = cycles_map_to_cycles(cycles_map);        // main.cpp:542
-        {
+        if (rank0) {
             const std::string out = settings.cycles_folder + "/cycles.txt";
             std::ofstream f(out);
             size_t idx = 0;
@@ -98,7 +236,20 @@ int main(int argc, char **argv) {
         }
 
         banner("🔸STEP 6: Finding relevant reads");             // main.cpp:544-551
-        const auto reads = run_and_debug_finding_of_relevant_reads(cycles, sdbg_build.reads(), sdbg);
+        int n_files = 0;
+        {
+            std::istringstream iss(settings.input_files);
+            std::string t;
+            while (iss >> t) ++n_files;
+        }
+        const auto reads = run_and_debug_finding_of_relevant_reads(cycles, sdbg_build.reads(), sdbg,
+                                                                   settings.gpus > 1 ? settings.mcomm : nullptr,
+                                                                   std::max(1, n_files));
+        if (settings.mcomm) {
+            mcaat_comm_free(settings.mcomm);
+            settings.mcomm = nullptr;
+        }
+        if (!rank0) return 0;  // rank 0 writes the outputs
 
         banner("🔸STEP 7: Order the spacers");                  // main.cpp:553-556
         const auto found_systems = run_and_debug_spacer_ordering(reads, sdbg, cycles);
@@ -124,9 +275,7 @@ int main(int argc, char **argv) {
         } catch (const std::filesystem::filesystem_error &e) {
             std::cerr << "Warning: Could not remove graph folder: " << e.what() << std::endl;
         }
+        if (ranks.watcher.joinable()) ranks.watcher.join();  // every rank ended cleanly
         return 0;
-    } catch (const std::exception &e) {
-        std::cerr << e.what() << std::endl;
-        return 1;
     }
 }

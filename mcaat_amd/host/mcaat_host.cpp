@@ -28,6 +28,15 @@ mcaat_ctx *mcaat_host_ctx(int device) {
     return ctx;
 }
 
+// GPU of this process's rank in a multi-GPU run (rank 0 / one GPU: settings.gpu)
+int mcaat_rank_device(const Settings &s) {
+    if (s.gpus <= 1) return s.gpu;
+    int n = 0;
+    mcaat_check(mcaat_device_count(&n), "mcaat_device_count");
+    if (n < 1) throw std::runtime_error("no HIP device available");
+    return (s.gpu + s.rank) % n;
+}
+
 // ---------------------------------------------------------------- SDBGBuild
 SDBGBuild::SDBGBuild(Settings s) : settings(s) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -68,25 +77,50 @@ std::string SDBGBuild::WriteLibFile() {
 }
 
 void SDBGBuild::BuildLib() {
-    WriteLibFile();
+    if (settings.rank == 0) WriteLibFile();
     std::istringstream iss(settings.input_files);
     std::vector<std::string> files;
     std::string t;
     while (iss >> t) files.push_back(t);
     std::vector<const char *> cf;
     for (auto &x : files) cf.push_back(x.c_str());
-    mcaat_ctx *ctx = mcaat_host_ctx(settings.gpu);
-    mcaat_check(mcaat_reads_from_fastx(ctx, cf.data(), (int)cf.size(), &reads_), "reading input files");
+    mcaat_ctx *ctx = mcaat_host_ctx(mcaat_rank_device(settings));
+    if (settings.gpus <= 1 || !settings.mcomm) {
+        mcaat_check(mcaat_reads_from_fastx(ctx, cf.data(), (int)cf.size(), &reads_), "reading input files");
+        return;
+    }
+    // each rank reads its part of every file; inputs that cannot be split (FASTA, wrapped or
+    // gapped FASTQ) are read whole by rank 0, and the other ranks count nothing
+    const int rc = mcaat_reads_from_fastx_part(ctx, cf.data(), (int)cf.size(), settings.rank, settings.gpus, &reads_);
+    std::vector<uint64_t> sizes(settings.gpus);
+    const uint8_t ok = rc == MCAAT_OK;
+    mcaat_check(mcaat_comm_allgather_sizes(settings.mcomm, 1, sizes.data()), "comm");
+    std::vector<uint8_t> oks(settings.gpus);
+    mcaat_check(mcaat_comm_allgatherv(settings.mcomm, &ok, 1, oks.data(), sizes.data()), "comm");
+    if (std::all_of(oks.begin(), oks.end(), [](uint8_t x) { return x != 0; })) return;
+    if (reads_) mcaat_reads_free(reads_);
+    reads_ = nullptr;
+    if (settings.rank == 0) {
+        std::cout << "Inputs read whole on rank 0 (" << mcaat_last_error() << ")" << std::endl;
+        mcaat_check(mcaat_reads_from_fastx(ctx, cf.data(), (int)cf.size(), &reads_), "reading input files");
+    } else {
+        const uint64_t off0 = 0;
+        mcaat_check(mcaat_reads_from_host(ctx, nullptr, 0, &off0, 0, &reads_), "empty read part");
+    }
 }
 
 void SDBGBuild::BuildSDBG() {
-    mcaat_ctx *ctx = mcaat_host_ctx(settings.gpu);
-    if (!settings.load_graph.empty()) {
+    mcaat_ctx *ctx = mcaat_host_ctx(mcaat_rank_device(settings));
+    if (!settings.load_graph.empty()) {  // every rank loads the whole graph
         mcaat_check(mcaat_graph_load(ctx, settings.load_graph.c_str(), &graph_), "loading the graph");
         std::cout << "Resumed the graph from " << settings.load_graph << std::endl;
     } else {
-        mcaat_check(mcaat_build_graph(ctx, reads_, settings.kmer_k, &graph_), "building the SDBG");
-        if (settings.keep_graph) {
+        if (settings.gpus > 1 && settings.mcomm)
+            mcaat_check(mcaat_build_graph_sharded(ctx, settings.mcomm, reads_, settings.kmer_k, &graph_),
+                        "building the SDBG over the ranks");
+        else
+            mcaat_check(mcaat_build_graph(ctx, reads_, settings.kmer_k, &graph_), "building the SDBG");
+        if (settings.keep_graph && settings.rank == 0) {
             const std::string out = settings.graph_folder + "/graph.mcaat_sdbg";
             mcaat_check(mcaat_graph_save(graph_, out.c_str()), "saving the graph");
             std::cout << "Graph kept in " << out << std::endl;
@@ -253,7 +287,8 @@ CycleFinder::CycleFinder(Settings &s) : settings(s) {
     p.cycle_max_length = settings.cycle_finder_settings.cycle_max_length;
     p.cycle_min_length = settings.cycle_finder_settings.cycle_min_length;
     mcaat_cycles *c = nullptr;
-    mcaat_check(mcaat_cycle_finder(settings.sdbg->device(), &p, &c), "CycleFinder");
+    mcaat_check(mcaat_cycle_finder_comm(settings.sdbg->device(), settings.gpus > 1 ? settings.mcomm : nullptr, &p, &c),
+                "CycleFinder");
     size_t n = 0;
     mcaat_cycles_count(c, &n);
     mcaat_cycles_stats(c, stats);

@@ -18,6 +18,8 @@ void mcaat_check(int rc, const char *what);
 
 // One GPU context per process (one process per GPU).
 mcaat_ctx *mcaat_host_ctx(int device);
+// the GPU of this process's rank (settings.gpu on one GPU)
+int mcaat_rank_device(const Settings &s);
 
 // Reference: SDBGBuild(Settings) writes <graph>/data.lib (sdbg_build.cpp:25-75), builds the
 // read library and the SDBG (MEGAHIT). Here: the same data.lib, FASTQ/FASTA(.gz) -> packed

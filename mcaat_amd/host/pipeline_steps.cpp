@@ -18,9 +18,10 @@ void print_elapsed(std::chrono::high_resolution_clock::time_point t0) {
 
 // main_run_and_debug.cpp:3-30 (the reads come from HBM instead of the FASTQ files)
 std::vector<std::vector<uint64_t>> run_and_debug_finding_of_relevant_reads(
-    const std::vector<std::vector<uint64_t>> &cycles, const mcaat_reads *reads, const SDBG &sdbg) {
+    const std::vector<std::vector<uint64_t>> &cycles, const mcaat_reads *reads, const SDBG &sdbg, mcaat_comm *comm,
+    int n_files) {
     const auto t0 = std::chrono::high_resolution_clock::now();
-    auto relevant = get_reads(sdbg, reads, cycles);
+    auto relevant = get_reads(sdbg, reads, cycles, comm, n_files);
     std::cout << "    ▸ Found " << relevant.size() << " reads" << std::endl;
     if (relevant.empty()) {
         std::cout << "══════════════════════════════════════════════" << std::endl;

@@ -47,6 +47,29 @@ std::vector<uint64_t> get_read_from_sequence(const SDBG &sdbg, const std::unorde
 // against the cycle labels before resolving the relevant reads' k-mers.
 std::vector<std::vector<uint64_t>> get_reads(const SDBG &sdbg, const mcaat_reads *reads,
                                              const std::vector<std::vector<uint64_t>> cycles) {
+    return get_reads(sdbg, reads, cycles, nullptr, 1);
+}
+
+// host allgather of one vector per rank (rank order)
+template <class T>
+static std::vector<T> gather_all(mcaat_comm *comm, int world, const std::vector<T> &mine, std::vector<uint64_t> &counts) {
+    std::vector<uint64_t> sizes(world);
+    mcaat_check(mcaat_comm_allgather_sizes(comm, mine.size() * sizeof(T), sizes.data()), "comm");
+    uint64_t total = 0;
+    for (uint64_t b : sizes) total += b;
+    std::vector<T> all(total / sizeof(T));
+    mcaat_check(mcaat_comm_allgatherv(comm, mine.data(), mine.size() * sizeof(T), all.data(), sizes.data()), "comm");
+    counts.resize(world);
+    for (int r = 0; r < world; ++r) counts[r] = sizes[r] / sizeof(T);
+    return all;
+}
+
+// With comm, every rank maps its own part of the reads (mcaat_reads_from_fastx_part: a
+// contiguous record range of each input file) and the relevant reads of all ranks come back
+// in input order, file by file and, inside a file, the ranks' parts in rank order.
+std::vector<std::vector<uint64_t>> get_reads(const SDBG &sdbg, const mcaat_reads *reads,
+                                             const std::vector<std::vector<uint64_t>> cycles, mcaat_comm *comm,
+                                             int n_files) {
     std::unordered_set<uint64_t> nodes_of_cycles;
     for (const auto &cycle : cycles)
         for (const auto &node : cycle) nodes_of_cycles.insert(node);
@@ -56,10 +79,36 @@ std::vector<std::vector<uint64_t>> get_reads(const SDBG &sdbg, const mcaat_reads
     mcaat_mapped *m = nullptr;
     mcaat_check(mcaat_map_reads(sdbg.device(), reads, nodes.data(), nodes.size(), 0, &m), "mapping the reads");
     uint64_t n = 0;
-    const uint64_t *ids = nullptr, *off = nullptr;
-    mcaat_check(mcaat_mapped_get(m, &n, &ids, &off, nullptr), "mcaat_mapped_get");
-    std::vector<std::vector<uint64_t>> out(n);
-    for (uint64_t i = 0; i < n; ++i) out[i].assign(ids + off[i], ids + off[i + 1]);
+    const uint64_t *ids = nullptr, *off = nullptr, *rec = nullptr;
+    mcaat_check(mcaat_mapped_get(m, &n, &ids, &off, &rec), "mcaat_mapped_get");
+    int world = 1;
+    if (comm) mcaat_check(mcaat_comm_info(comm, &world, nullptr), "mcaat_comm_info");
+    if (world == 1) {
+        std::vector<std::vector<uint64_t>> out(n);
+        for (uint64_t i = 0; i < n; ++i) out[i].assign(ids + off[i], ids + off[i + 1]);
+        mcaat_mapped_free(m);
+        return out;
+    }
+    std::vector<std::vector<uint64_t>> out;
+    uint64_t lo = 0, i = 0;
+    for (int f = 0; f < n_files; ++f) {
+        uint64_t nf = 0;
+        mcaat_check(mcaat_reads_file_records(reads, f, &nf), "mcaat_reads_file_records");
+        std::vector<uint64_t> lens, flat;
+        for (; i < n && rec[i] < lo + nf; ++i) {
+            lens.push_back(off[i + 1] - off[i]);
+            flat.insert(flat.end(), ids + off[i], ids + off[i + 1]);
+        }
+        lo += nf;
+        std::vector<uint64_t> nl, ni;
+        const std::vector<uint64_t> all_lens = gather_all(comm, world, lens, nl);
+        const std::vector<uint64_t> all_ids = gather_all(comm, world, flat, ni);
+        uint64_t a = 0;
+        for (uint64_t len : all_lens) {
+            out.emplace_back(all_ids.begin() + a, all_ids.begin() + a + len);
+            a += len;
+        }
+    }
     mcaat_mapped_free(m);
     return out;
 }

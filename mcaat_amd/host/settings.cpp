@@ -26,6 +26,8 @@ static void print_help() {
               << "  --low-abundance <true|false>    Enable low abundance mode for cycle filtering\n"
               << "  --settings <path>               Path to a key=value settings file (overridden by CLI args)\n"
               << "  --gpu <index>                   GPU to run the hot path on (default 0)\n"
+              << "  --gpus <num>                    GPUs (one process each) sharing the run (default 1)\n"
+              << "  --comm <rccl|shm>               Multi-GPU transport: RCCL over xGMI, or host shared memory\n"
               << "  --keep-graph                    Keep the graph as <graph folder>/graph.mcaat_sdbg (checkpoint)\n"
               << "  --load-graph <file>             Resume from a kept graph instead of building it\n"
               << "  --help, -h                      Show this help message\n";
@@ -100,6 +102,12 @@ Settings parse_arguments(int argc, char *argv[], bool create_dirs) {
         } else if (arg == "--gpu") {
             if (++i < argc) settings.gpu = std::stoi(argv[i]);
             else throw std::runtime_error("Error: Missing value for --gpu");
+        } else if (arg == "--gpus") {
+            if (++i < argc) settings.gpus = std::stoi(argv[i]);
+            else throw std::runtime_error("Error: Missing value for --gpus");
+        } else if (arg == "--comm") {
+            if (++i < argc) settings.comm = argv[i];
+            else throw std::runtime_error("Error: Missing value for --comm");
         } else if (arg == "--keep-graph") {
             settings.keep_graph = true;
         } else if (arg == "--load-graph") {
@@ -149,6 +157,8 @@ Settings parse_arguments(int argc, char *argv[], bool create_dirs) {
             settings.input_files += file;
         }
     }
+    if (settings.gpus < 1 || settings.gpus > 64) throw std::runtime_error("Error: --gpus must be in [1, 64]");
+    if (settings.comm != "rccl" && settings.comm != "shm") throw std::runtime_error("Error: --comm must be rccl or shm");
     if (settings.threads == 0) settings.threads = std::thread::hardware_concurrency() - 2;
     if (settings.ram == 0.0) settings.ram = get_total_system_ram() * 0.95;
     return settings;

@@ -2,7 +2,7 @@
 // (reference include/settings.h:22-221, src/main.cpp:89-301): the same settings.txt keys,
 // defaults, CLI flags and error behaviour (std::runtime_error). Additions, all optional and
 // ignored by the reference as unknown keys: `kmer_k` (k is hard-coded to 23 in the
-// reference, sdbg_build.cpp:217) and `--gpu <index>`.
+// reference, sdbg_build.cpp:217), `--gpu <index>`, and the multi-GPU `gpus` / `comm`.
 #pragma once
 #include <algorithm>
 #include <cctype>
@@ -37,6 +37,14 @@ struct Settings {
     // such a file instead of building (the reads are still read for the downstream steps)
     bool keep_graph = false;
     std::string load_graph;
+    // multi-GPU run (not in the reference): `gpus` ranks, one process per GPU forked by main
+    // before any GPU call; rank r runs on GPU (gpu + r) % device count. comm "rccl" moves data
+    // GPU to GPU over xGMI, "shm" stages it through host shared memory (ranks may share a
+    // GPU). rank / mcomm are filled in per process by main.
+    int gpus = 1;
+    std::string comm = "rccl";
+    int rank = 0;
+    struct mcaat_comm *mcomm = nullptr;
 
     struct CycleFinderSettings {           // settings.h:33-38
         uint64_t threshold_multiplicity = 20;
@@ -173,6 +181,8 @@ struct Settings {
                 std::transform(val.begin(), val.end(), val.begin(), ::tolower);
                 keep_graph = (val == "true" || val == "1" || val == "yes");
             } else if (key == "load_graph") load_graph = val;
+            else if (key == "gpus") gpus = std::stoi(val);
+            else if (key == "comm") comm = val;
             // unknown keys are ignored for forward-compatibility (settings.h:216)
         }
         return true;

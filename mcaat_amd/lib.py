@@ -113,6 +113,19 @@ SIGNATURES = {
     "mcaat_graph_save": (C.c_int, [C.c_void_p, C.c_char_p]),
     "mcaat_graph_load": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_void_p)]),
     "mcaat_graph_download_range": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, _u64p, _u16p, _u8p]),
+    "mcaat_comm_unique_id": (C.c_int, [_u8p]),
+    "mcaat_comm_init_rccl": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p, C.POINTER(C.c_void_p)]),
+    "mcaat_comm_init_shm": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_char_p, C.c_uint64, C.POINTER(C.c_void_p)]),
+    "mcaat_comm_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    "mcaat_comm_barrier": (C.c_int, [C.c_void_p]),
+    "mcaat_comm_allgather_sizes": (C.c_int, [C.c_void_p, C.c_uint64, _u64p]),
+    "mcaat_comm_allgatherv": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, _u64p]),
+    "mcaat_comm_free": (None, [C.c_void_p]),
+    "mcaat_reads_from_fastx_part": (C.c_int, [C.c_void_p, C.POINTER(C.c_char_p), C.c_int, C.c_int, C.c_int,
+                                              C.POINTER(C.c_void_p)]),
+    "mcaat_reads_file_records": (C.c_int, [C.c_void_p, C.c_int, _u64p]),
+    "mcaat_build_graph_sharded": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
+    "mcaat_cycle_finder_comm": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(_CfParams), C.POINTER(C.c_void_p)]),
 }
 
 _lib: Optional[C.CDLL] = None
@@ -256,6 +269,66 @@ class Context:
         return _cm()
 
 
+class Comm:
+    """The ranks of one multi-GPU run (mcaat_comm): RCCL between GPUs, or a POSIX
+    shared-memory segment that stages device data through the host (ranks sharing a GPU,
+    rehearsals; ctx None: host collectives only, no GPU needed)."""
+
+    ID_BYTES = 128
+
+    def __init__(self, h):
+        self._lib = load_library()
+        self.h = h
+        w, r = C.c_int(0), C.c_int(0)
+        _check(self._lib.mcaat_comm_info(h, C.byref(w), C.byref(r)))
+        self.world, self.rank = w.value, r.value
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = np.zeros(Comm.ID_BYTES, dtype=np.uint8)
+        _check(load_library().mcaat_comm_unique_id(_ptr(buf, _u8p)))
+        return buf.tobytes()
+
+    @classmethod
+    def rccl(cls, ctx: "Context", world: int, rank: int, uid: bytes) -> "Comm":
+        buf = np.frombuffer(uid, dtype=np.uint8).copy()
+        h = C.c_void_p()
+        _check(load_library().mcaat_comm_init_rccl(ctx.h, world, rank, _ptr(buf, _u8p), C.byref(h)))
+        return cls(h)
+
+    @classmethod
+    def shm(cls, ctx: Optional["Context"], world: int, rank: int, name: str, slot_bytes: int = 0) -> "Comm":
+        h = C.c_void_p()
+        _check(load_library().mcaat_comm_init_shm(ctx.h if ctx else None, world, rank, name.encode(), slot_bytes,
+                                                  C.byref(h)))
+        return cls(h)
+
+    def barrier(self) -> None:
+        _check(self._lib.mcaat_comm_barrier(self.h))
+
+    def allgather_bytes(self, data: bytes) -> List[bytes]:
+        """Every rank's bytes, in rank order."""
+        sizes = np.zeros(self.world, dtype=np.uint64)
+        _check(self._lib.mcaat_comm_allgather_sizes(self.h, len(data), _ptr(sizes, _u64p)))
+        out = np.zeros(max(int(sizes.sum()), 1), dtype=np.uint8)
+        src = np.frombuffer(data, dtype=np.uint8).copy() if data else np.zeros(1, np.uint8)
+        _check(self._lib.mcaat_comm_allgatherv(self.h, src.ctypes.data_as(C.c_void_p), len(data),
+                                               out.ctypes.data_as(C.c_void_p), _ptr(sizes, _u64p)))
+        offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+        return [out[offs[r]:offs[r + 1]].tobytes() for r in range(self.world)]
+
+    def close(self) -> None:
+        if self.h:
+            self._lib.mcaat_comm_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class Reads:
     """Packed 2-bit reads resident in HBM (mcaat_reads)."""
 
@@ -293,6 +366,19 @@ class Reads:
         h = C.c_void_p()
         _check(ctx._lib.mcaat_reads_from_fastx(ctx.h, arr, len(files), C.byref(h)))
         return cls(ctx, h)
+
+    @classmethod
+    def from_fastx_part(cls, ctx: Context, files: Sequence[str], part: int, n_parts: int) -> "Reads":
+        """Part `part` of n_parts of the FASTQ inputs (cut at record starts; .gz whole on part 0)."""
+        arr = (C.c_char_p * len(files))(*[f.encode() for f in files])
+        h = C.c_void_p()
+        _check(ctx._lib.mcaat_reads_from_fastx_part(ctx.h, arr, len(files), part, n_parts, C.byref(h)))
+        return cls(ctx, h)
+
+    def file_records(self, file: int) -> int:
+        n = C.c_uint64(0)
+        _check(self.ctx._lib.mcaat_reads_file_records(self.h, file, C.byref(n)))
+        return n.value
 
     def info(self) -> Tuple[int, int]:
         n = C.c_uint64(0)
@@ -461,6 +547,13 @@ class Graph:
         return cls(ctx, h)
 
     @classmethod
+    def build_sharded(cls, ctx: Context, comm: Comm, reads: Reads, k: int) -> "Graph":
+        """The graph of every rank's reads (mcaat_build_graph_sharded); each rank passes its own."""
+        h = C.c_void_p()
+        _check(ctx._lib.mcaat_build_graph_sharded(ctx.h, comm.h, reads.h, k, C.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
     def from_sorted(cls, ctx: Context, k: int, keys_dev: int, mult_dev: int, D: int) -> "Graph":
         """Graph from ascending unique BOSS keys and multiplicities in device memory."""
         h = C.c_void_p()
@@ -539,13 +632,18 @@ class Graph:
         ids = np.ascontiguousarray(ids, dtype=np.uint64)
         _check(self.ctx._lib.mcaat_graph_set_valid(self.h, _ptr(ids, _u64p), ids.size, int(valid)))
 
-    def cycle_finder(self, params: Optional[CfParams] = None, as_arrays: bool = False) -> CycleResult:
+    def cycle_finder(self, params: Optional[CfParams] = None, as_arrays: bool = False,
+                     comm: Optional[Comm] = None) -> CycleResult:
         """CycleFinder results in the reference's commit order. as_arrays: each entry is
-        (start, (flat node ids, cycle offsets)) as numpy copies instead of Python lists."""
+        (start, (flat node ids, cycle offsets)) as numpy copies instead of Python lists.
+        comm: the searches are split over the ranks that each hold this graph (same results)."""
         p = (params or CfParams()).to_c()
         h = C.c_void_p()
         lib = self.ctx._lib
-        _check(lib.mcaat_cycle_finder(self.h, C.byref(p), C.byref(h)))
+        if comm is not None:
+            _check(lib.mcaat_cycle_finder_comm(self.h, comm.h, C.byref(p), C.byref(h)))
+        else:
+            _check(lib.mcaat_cycle_finder(self.h, C.byref(p), C.byref(h)))
         try:
             res = CycleResult()
             n = C.c_size_t(0)

@@ -210,9 +210,11 @@ def test_downstream_several_arrays_with_errors(tmp_path):
 
 
 # ---- GPU: the CLI's CRISPR_Arrays.txt equals the oracle-driven one --------------------------
+# gpus > 1: the CLI forks one rank per GPU; on the one-GPU box the ranks share it through the
+# shared-memory transport (FASTQ parts, sharded build, CycleFinder over ranks, gathered reads)
 @pytest.mark.gpu
-@pytest.mark.parametrize("paired", [False, True])
-def test_cli_crispr_arrays_match_oracle_path(tmp_path, paired):
+@pytest.mark.parametrize("paired,gpus", [(False, 1), (True, 1), (False, 3), (True, 2)])
+def test_cli_crispr_arrays_match_oracle_path(tmp_path, paired, gpus):
     spec = M.SynthSpec()
     packed, offs = M.synth_host(spec)
     seqs = [unpack_read(packed, int(offs[i]), int(offs[i + 1])) for i in range(len(offs) - 1)]
@@ -227,8 +229,9 @@ def test_cli_crispr_arrays_match_oracle_path(tmp_path, paired):
             for i, s in enumerate(part):
                 f.write(f"@r{i}\n{s}\n+\n{'I' * len(s)}\n")
         files.append(str(p))
-    out = subprocess.run([CLI, "-i", *files, "--output-folder", str(tmp_path / "o"), "--threads", "2", "--ram", "2G"],
-                         capture_output=True, text=True, timeout=600)
+    multi = ["--gpus", str(gpus), "--comm", "shm"] if gpus > 1 else []
+    out = subprocess.run([CLI, "-i", *files, "--output-folder", str(tmp_path / "o"), "--threads", "2", "--ram", "2G",
+                          *multi], capture_output=True, text=True, timeout=600)
     assert out.returncode == 0, out.stderr + out.stdout[-2000:]
     got = (tmp_path / "o" / "CRISPR_Arrays.txt").read_text()
 

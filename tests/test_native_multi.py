@@ -1,0 +1,164 @@
+"""Native multi-GPU path (include/mcaat_gpu.h "multi-GPU, native"): communicators, the
+sharded build and CycleFinder split over ranks, FASTQ parts.
+
+CPU: the shared-memory communicator's host collectives between processes (no GPU).
+GPU: ranks sharing the one GPU of the box over the shared-memory transport, and RCCL with
+one rank, against the single-GPU graph and CycleFinder results."""
+import os
+import subprocess
+import sys
+import uuid
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import mcaat_amd as M  # noqa: E402
+
+_HOST_RANK = r"""
+import sys, numpy as np
+sys.path.insert(0, {root!r})
+import mcaat_amd as M
+world, rank, name = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+c = M.Comm.shm(None, world, rank, name, 4096)   # 4 KiB slots: large messages move in rounds
+assert (c.world, c.rank) == (world, rank)
+for rnd in range(3):
+    rng = np.random.default_rng(100 * rnd + rank)
+    n = [0, 5000, 13, 20000][(rank + rnd) % 4]
+    mine = rng.integers(0, 256, size=n, dtype=np.uint8).tobytes()
+    got = c.allgather_bytes(mine)
+    for r in range(world):
+        rr = np.random.default_rng(100 * rnd + r)
+        nr = [0, 5000, 13, 20000][(r + rnd) % 4]
+        assert got[r] == rr.integers(0, 256, size=nr, dtype=np.uint8).tobytes(), (rnd, r)
+    c.barrier()
+c.close()
+print("HOST_OK", rank)
+"""
+
+
+def _spawn(argv_list, timeout=300):
+    procs = [subprocess.Popen(a, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for a in argv_list]
+    outs = []
+    try:
+        for p in procs:
+            o, e = p.communicate(timeout=timeout)
+            outs.append((p.returncode, o, e))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return outs
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_shm_comm_host_allgather_between_processes(world):
+    name = f"/mcaat_t_{uuid.uuid4().hex[:12]}"
+    code = _HOST_RANK.format(root=ROOT)
+    outs = _spawn([[sys.executable, "-c", code, str(world), str(r), name] for r in range(world)], timeout=120)
+    for rc, o, e in outs:
+        assert rc == 0, e[-2000:]
+        assert "HOST_OK" in o
+    assert not os.path.exists("/dev/shm" + name), "the segment name must be removed once all ranks attached"
+
+
+def test_shm_comm_rejects_bad_arguments():
+    with pytest.raises(M.McaatError):
+        M.Comm.shm(None, 2, 2, "/mcaat_bad")
+    with pytest.raises(M.McaatError):
+        M.Comm.shm(None, 1, 0, "no_slash")
+
+
+def test_shm_comm_single_rank_is_identity():
+    c = M.Comm.shm(None, 1, 0, f"/mcaat_t_{uuid.uuid4().hex[:12]}")
+    assert c.allgather_bytes(b"abc") == [b"abc"]
+    c.barrier()
+    c.close()
+
+
+def _ranks(world, comm, extra=(), timeout=600):
+    name = f"/mcaat_g_{uuid.uuid4().hex[:12]}"
+    uid = f"/tmp/mcaat_uid_{uuid.uuid4().hex[:12]}"
+    script = os.path.join(ROOT, "tools", "native_multi_check.py")
+    argv = [[sys.executable, script, "--world", str(world), "--rank", str(r), "--comm", comm, "--name", name,
+             "--uid-file", uid, *extra] for r in range(world)]
+    try:
+        return _spawn(argv, timeout=timeout)
+    finally:
+        if os.path.exists(uid):
+            os.unlink(uid)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,extra", [(2, ()), (3, ("--window", "16", "--slot", "65536"))])
+def test_sharded_build_and_cycle_finder_ranks_share_one_gpu(world, extra):
+    outs = _ranks(world, "shm", extra)
+    for rc, o, e in outs:
+        assert rc == 0, (o[-2000:], e[-3000:])
+        assert "NATIVE_MULTI_OK" in o, o
+
+
+@pytest.mark.gpu
+def test_rccl_single_rank_matches_one_gpu():
+    outs = _ranks(1, "rccl")
+    rc, o, e = outs[0]
+    assert rc == 0, (o[-2000:], e[-3000:])
+    assert "NATIVE_MULTI_OK" in o
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("paired", [False, True])
+def test_fastq_parts_partition_the_records(gpu_ctx, tmp_path, paired):
+    spec = M.SynthSpec(seed=7, n_reads=7001, paired=paired, error_rate=1e-3)
+    r = M.Reads.synth(gpu_ctx, spec)
+    p1 = str(tmp_path / "r1.fq")
+    r.write_fastq(p1, threads=2)
+    r.free()
+    files = [p1]
+    if paired:  # a second file with other records (reverse-complemented in the mapping view)
+        r2 = M.Reads.synth(gpu_ctx, M.SynthSpec(seed=8, n_reads=3333))
+        p2 = str(tmp_path / "r2.fq")
+        r2.write_fastq(p2, threads=2)
+        r2.free()
+        files.append(p2)
+    whole = M.Reads.from_fastx(gpu_ctx, files)
+    wp, wo = whole.download()
+    wrp, wro = whole.download_records()
+    n_file = [whole.file_records(f) for f in range(len(files))]
+    whole.free()
+    for n_parts in (2, 3, 5):
+        per_file = np.zeros(len(files), dtype=np.int64)
+        parts = []
+        for part in range(n_parts):
+            pr = M.Reads.from_fastx_part(gpu_ctx, files, part, n_parts)
+            parts.append(pr)
+            per_file += [pr.file_records(f) for f in range(len(files))]
+        assert per_file.tolist() == n_file
+        # mapping views: per file, the parts' records in part order are the whole file's records
+        def view(p, o, lo, hi):  # records [lo, hi): their lengths and their bases
+            return np.diff(o[lo:hi + 1].astype(np.int64)), _bases(p, int(o[lo]), int(o[hi]))
+        wl = 0
+        for f in range(len(files)):
+            want_len, want_b = view(wrp, wro, wl, wl + n_file[f])
+            wl += n_file[f]
+            lens, bases = [], []
+            for pr in parts:
+                rp, ro = pr.download_records()
+                nf = [pr.file_records(x) for x in range(len(files))]
+                lo = sum(nf[:f])
+                ln, bs = view(rp, ro, lo, lo + nf[f])
+                lens.append(ln)
+                bases.append(bs)
+            assert np.array_equal(np.concatenate(lens), want_len), (n_parts, f)
+            assert np.array_equal(np.concatenate(bases), want_b), (n_parts, f)
+        n_all = sum(pr.info()[1] for pr in parts)
+        assert n_all == int(wo[-1])
+        for pr in parts:
+            pr.free()
+
+
+def _bases(packed, a, b):
+    idx = np.arange(a, b, dtype=np.uint64)
+    return ((packed[(idx >> np.uint64(5)).astype(np.int64)] >> (np.uint64(2) * (idx & np.uint64(31)))) & np.uint64(3))

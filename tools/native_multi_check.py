@@ -1,0 +1,99 @@
+"""One rank of a native multi-GPU check (tests/test_native_multi.py starts `world` of these).
+
+Each rank joins a communicator (shm: POSIX shared memory, ranks may share one GPU; rccl:
+one GPU per rank, or world 1), builds the graph of its slice of one synthetic dataset with
+mcaat_build_graph_sharded, runs mcaat_cycle_finder_comm, and compares graph and results
+with the single-GPU path over all the reads (computed by every rank on its own context).
+
+usage: native_multi_check.py --world N --rank R --comm shm|rccl --name /x [--reads N]
+       [--window W] [--uid-file F]
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import mcaat_amd as M  # noqa: E402
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, required=True)
+    ap.add_argument("--rank", type=int, required=True)
+    ap.add_argument("--comm", default="shm", choices=["shm", "rccl"])
+    ap.add_argument("--name", default="/mcaat_check")
+    ap.add_argument("--reads", type=int, default=30000)
+    ap.add_argument("--window", type=int, default=0, help="cf.fc_window knob (small: many rounds)")
+    ap.add_argument("--uid-file", default="")
+    ap.add_argument("--slot", type=int, default=1 << 20, help="shm staging bytes per rank")
+    a = ap.parse_args()
+
+    spec = M.SynthSpec(seed=11, n_genomes=3, genome_len=40_000, arrays_per_genome=2, spacers_per_array=10,
+                       repeat_len_min=30, repeat_len_max=34, spacer_len_min=30, spacer_len_max=36,
+                       n_reads=a.reads, error_rate=2e-3)
+    k = 27
+    dev = a.rank % max(1, M.device_count()) if a.comm == "rccl" else 0
+    ctx = M.Context(dev)
+    if a.window:
+        ctx.set_knob("cf.fc_window", a.window)
+    if a.comm == "shm":
+        comm = M.Comm.shm(ctx, a.world, a.rank, a.name, a.slot)
+    else:
+        if a.rank == 0:
+            uid = M.Comm.unique_id()
+            tmp = a.uid_file + ".tmp"
+            with open(tmp, "wb") as f:
+                f.write(uid)
+            os.replace(tmp, a.uid_file)
+        else:
+            t0 = time.time()
+            while not os.path.exists(a.uid_file):
+                if time.time() - t0 > 120:
+                    raise SystemExit("no unique id file")
+                time.sleep(0.05)
+        with open(a.uid_file, "rb") as f:
+            uid = f.read()
+        comm = M.Comm.rccl(ctx, a.world, a.rank, uid)
+    assert (comm.world, comm.rank) == (a.world, a.rank)
+
+    first = a.rank * spec.n_reads // a.world
+    count = (a.rank + 1) * spec.n_reads // a.world - first
+    mine = M.Reads.synth_range(ctx, spec, first, count)
+    prm = M.CfParams(threshold_multiplicity=20)
+    g = M.Graph.build_sharded(ctx, comm, mine, k)
+    keys, mult, _ = g.download()
+    res = g.cycle_finder(prm, comm=comm)
+    g.free()
+    mine.free()
+
+    whole = M.Reads.synth(ctx, spec)
+    g1 = M.Graph.build(ctx, whole, k)
+    k1, m1, _ = g1.download()
+    r1 = g1.cycle_finder(prm)
+    g1.free()
+    whole.free()
+
+    ok = np.array_equal(keys, k1) and np.array_equal(mult, m1)
+    ok = ok and res.entries == r1.entries and res.stats[:6] == r1.stats[:6]
+    ok = ok and list(res.candidates) == list(r1.candidates) and list(res.buckets) == list(r1.buckets)
+    # every rank holds the same results
+    digest = repr((res.entries, res.stats[:6])).encode()
+    same = len(set(comm.allgather_bytes(digest))) == 1
+    print(f"rank {a.rank}: D={len(keys)} (single {len(k1)}) entries={len(res.entries)} cycles={res.stats[5]} "
+          f"rounds={res.stats[6]} reruns={res.stats[7]} match={ok} ranks_agree={same}", flush=True)
+    comm.barrier()
+    comm.close()
+    ctx.close()
+    if ok and same:
+        print("NATIVE_MULTI_OK", flush=True)
+        return 0
+    return 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
