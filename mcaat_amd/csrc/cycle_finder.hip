@@ -468,22 +468,35 @@ struct FcParams {
     int maxl, minl, cluster;
     int64_t step_cap;
 };
-struct FcScratch {
-    uint64_t *path;     // P
-    int32_t *bl;        // P
-    uint64_t *fr;       // 4P
-    uint8_t *frn;       // P
-    uint64_t *lk;       // CL keys
-    int32_t *lv;        // CL values
-    uint64_t *relax;    // CR
-    uint64_t *out;      // CO
-    uint16_t *olen;     // CC
+// lock / footprint table entry: key and value in one 16-B record (one line per probe)
+struct __attribute__((aligned(16))) LockRec {
+    uint64_t key;
+    int32_t val;
+    uint32_t pad;
 };
+// Per search: the hot state read every step (path, neighbour frames, backtrack lengths) is in
+// the workgroup's LDS; the lock table, relax stack and outputs are in global scratch
+// (fc_per_search bytes per search: lock records, relax stack, output nodes, cycle lengths).
+struct FcScratch {
+    uint64_t *path;     // P      (LDS)
+    int32_t *bl;        // P      (LDS)
+    uint64_t *fr;       // 4P     (LDS)
+    uint8_t *frn;       // P      (LDS)
+    LockRec *lk;        // CL     (global)
+    uint64_t *relax;    // CR     (global)
+    uint64_t *out;      // CO     (global)
+    uint16_t *olen;     // CC     (global)
+};
+__host__ __device__ inline uint64_t fc_per_search(const FcCaps &c) {
+    const uint64_t per = (uint64_t)c.CL * 16 + (uint64_t)c.CR * 8 + (uint64_t)c.CO * 8 + (uint64_t)c.CC * 2;
+    return (per + 255) & ~255ULL;
+}
+__host__ __device__ inline uint32_t fc_lds_bytes(const FcCaps &c) { return c.P * (8 + 32 + 4 + 1) + 16; }
 struct FcStatus {
     int32_t status;     // 0 ok, 1 lock table full, 2 relax stack full, 3 output full
     int32_t ncyc;
     uint32_t nnodes;
-    uint32_t pad;
+    uint32_t steps;  // main-loop iterations (diagnostics: MCAAT_VERBOSE)
 };
 
 struct FcThread {
@@ -501,12 +514,12 @@ struct FcThread {
     __device__ int lock_slot(uint64_t x, int dflt) {
         uint32_t h = (uint32_t)(mix64(x) & (c.CL - 1));
         for (;;) {
-            const uint64_t k = s.lk[h];
+            const uint64_t k = s.lk[h].key;
             if (k == x) return (int)h;
             if (k == kNone) {
                 if (lsize + 1 > c.CL / 4 * 3) { status = 1; return -1; }
-                s.lk[h] = x;
-                s.lv[h] = dflt;
+                s.lk[h].key = x;
+                s.lk[h].val = dflt;
                 ++lsize;
                 return (int)h;
             }
@@ -553,35 +566,36 @@ struct FcThread {
     }
 };
 
-// lpw searches per wave: each search is a divergent pointer-chasing state machine, so lanes
-// of one wave serialise each other's branches; few lanes per wave keep searches independent
 // A/B knob: minimum waves per SIMD (6 or 8 force 80 / 64 VGPRs with spills; measured no
 // faster at C3: the kernel's time is its longest search, not its occupancy)
 #ifndef MCAAT_FC_MINW
 #define MCAAT_FC_MINW 1
 #endif
+// One search per workgroup of one wave: the search itself is sequential (lane 0); the other
+// lanes clear its lock table first. Its path and frames live in LDS (fc_lds_bytes), so every
+// step touches global memory only for the graph, the visited bits and the lock table.
+// (Per-step latency, not occupancy, bounds this kernel: at C3 ~1.5K steps per search, each a
+// chain of dependent loads.)
 __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, const uint64_t *visited, const uint64_t *starts,
                                                   uint64_t n, FcCaps caps, FcParams prm, uint64_t *sbase,
-                                                  FcStatus *stat, int lpw) {
-    if ((int)threadIdx.x >= lpw) return;
-    const uint64_t i = (uint64_t)blockIdx.x * lpw + threadIdx.x;
+                                                  FcStatus *stat) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char fc_lds[];
+    const uint64_t i = blockIdx.x;
     if (i >= n) return;
-    // carve this thread's scratch
-    const uint64_t per = (uint64_t)caps.P * 8 + caps.P * 4 + caps.P * 32 + caps.P + (uint64_t)caps.CL * 12 +
-                         (uint64_t)caps.CR * 8 + (uint64_t)caps.CO * 8 + caps.CC * 2;
-    const uint64_t per_al = (per + 255) & ~255ULL;
-    uint8_t *base = (uint8_t *)sbase + i * per_al;
+    uint8_t *base = (uint8_t *)sbase + i * fc_per_search(caps);
     FcScratch s;
-    s.lk = (uint64_t *)base; base += (uint64_t)caps.CL * 8;
+    s.lk = (LockRec *)base; base += (uint64_t)caps.CL * 16;
     s.relax = (uint64_t *)base; base += (uint64_t)caps.CR * 8;
     s.out = (uint64_t *)base; base += (uint64_t)caps.CO * 8;
-    s.path = (uint64_t *)base; base += (uint64_t)caps.P * 8;
-    s.fr = (uint64_t *)base; base += (uint64_t)caps.P * 32;
-    s.lv = (int32_t *)base; base += (uint64_t)caps.CL * 4;
-    s.bl = (int32_t *)base; base += (uint64_t)caps.P * 4;
-    s.olen = (uint16_t *)base; base += (uint64_t)caps.CC * 2;
-    s.frn = base;
-    for (uint32_t j = 0; j < caps.CL; ++j) s.lk[j] = kNone;
+    s.olen = (uint16_t *)base;
+    unsigned char *lb = fc_lds;
+    s.path = (uint64_t *)lb; lb += (uint64_t)caps.P * 8;
+    s.fr = (uint64_t *)lb; lb += (uint64_t)caps.P * 32;
+    s.bl = (int32_t *)lb; lb += (uint64_t)caps.P * 4;
+    s.frn = lb;
+    for (uint32_t j = threadIdx.x; j < caps.CL; j += blockDim.x) s.lk[j].key = kNone;
+    __syncthreads();  // the workgroup is one wave: lane 0 sees every lane's clear
+    if (threadIdx.x != 0) return;
 
     FcThread t(g, visited, s, caps);
     const int maxl = prm.maxl, minl = prm.minl;
@@ -595,7 +609,7 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
     s.path[plen++] = st;
     {
         const int sl = t.lock_slot(st, maxl);
-        if (sl >= 0) s.lv[sl] = 0;
+        if (sl >= 0) s.lk[sl].val = 0;
     }
     s.frn[0] = (uint8_t)t.get_outgoings(st, rm, s.fr, maxl);
     s.bl[0] = maxl;
@@ -624,7 +638,7 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
             } else {
                 const int sl = t.lock_slot(x, maxl);
                 if (sl < 0) break;
-                if ((int)plen < s.lv[sl]) {
+                if ((int)plen < s.lk[sl].val) {
                     // erase x from the top frame (order of the rest is kept)
                     int m = s.frn[top], q = 0;
                     for (int r = 0; r < m; ++r)
@@ -632,7 +646,7 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
                     s.frn[top] = (uint8_t)q;
                     s.path[plen++] = x;
                     s.bl[depth] = maxl;
-                    s.lv[sl] = (int)plen;
+                    s.lk[sl].val = (int)plen;
                     s.frn[depth] = (uint8_t)t.get_outgoings(x, rm, s.fr + 4 * depth, maxl);
                     ++depth;
                     flag = false;
@@ -658,8 +672,8 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
                     const uint64_t u = e >> 16;
                     const int sl = t.lock_slot(u, maxl);
                     if (sl < 0) break;
-                    if (s.lv[sl] < maxl - blv + 1) {
-                        s.lv[sl] = maxl - blv + 1;
+                    if (s.lk[sl].val < maxl - blv + 1) {
+                        s.lk[sl].val = maxl - blv + 1;
                         uint64_t ins[4];
                         const int ni = t.get_incomings(u, rm, ins, maxl);
                         for (int j = 0; j < ni; ++j) {
@@ -686,7 +700,7 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
     o.status = t.status;
     o.ncyc = ncyc;
     o.nnodes = nnodes;
-    o.pad = 0;
+    o.steps = (uint32_t)(steps < 0xFFFFFFFFLL ? steps : 0xFFFFFFFFLL);
     stat[i] = o;
 }
 
@@ -698,10 +712,8 @@ __global__ void k_fc_gather(const uint64_t *sbase, uint64_t per_al, FcCaps caps,
     if (q >= nsel) return;
     const uint64_t i = sel[q];
     const uint8_t *base = (const uint8_t *)sbase + i * per_al;
-    const uint64_t *out = (const uint64_t *)(base + (uint64_t)caps.CL * 8 + (uint64_t)caps.CR * 8);
-    const uint16_t *olen = (const uint16_t *)(base + (uint64_t)caps.CL * 8 + (uint64_t)caps.CR * 8 +
-                                              (uint64_t)caps.CO * 8 + (uint64_t)caps.P * 8 + (uint64_t)caps.P * 32 +
-                                              (uint64_t)caps.CL * 4 + (uint64_t)caps.P * 4);
+    const uint64_t *out = (const uint64_t *)(base + (uint64_t)caps.CL * 16 + (uint64_t)caps.CR * 8);
+    const uint16_t *olen = (const uint16_t *)(base + (uint64_t)caps.CL * 16 + (uint64_t)caps.CR * 8 + (uint64_t)caps.CO * 8);
     const uint64_t nn = node_off[q + 1] - node_off[q];
     const uint64_t nc = cyc_off[q + 1] - cyc_off[q];
     for (uint64_t j = threadIdx.x; j < nn; j += blockDim.x) nodes[node_off[q] + j] = out[j];
@@ -720,9 +732,112 @@ __global__ void k_fc_conflict(const uint64_t *sbase, uint64_t per_al, uint32_t C
         const uint64_t a = idx / nj, q = idx - a * nj;
         const uint32_t j = jlist[q];
         if (j <= newly_c[a] || conflict[q]) continue;
-        const uint64_t *lk = (const uint64_t *)((const uint8_t *)sbase + (uint64_t)jslot[q] * per_al);
-        if (set_contains(lk, CL, newly[a])) conflict[q] = 1;
+        const LockRec *lk = (const LockRec *)((const uint8_t *)sbase + (uint64_t)jslot[q] * per_al);
+        const uint64_t x = newly[a];
+        for (uint32_t h = (uint32_t)(mix64(x) & (CL - 1));; h = (h + 1) & (CL - 1)) {
+            const uint64_t k = lk[h].key;
+            if (k == x) { conflict[q] = 1; break; }
+            if (k == kNone) break;
+        }
     }
+}
+
+// ---- FindCycle commit on the device (FcRunner::commit_round) ----
+// open-addressing tables keyed by node id (kNone = empty slot), power-of-two capacity
+__device__ __forceinline__ uint32_t node_slot(uint64_t x, uint32_t cap) { return (uint32_t)(mix64(x) & (cap - 1)); }
+
+// the round's start nodes (start j -> j) and whether each was visited before the round
+__global__ void k_fc_starts(const uint64_t *starts, uint32_t n, uint64_t *skeys, uint32_t *svals, uint32_t cap,
+                            const uint64_t *vis, uint8_t *pre_vis) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t x = starts[i];
+    pre_vis[i] = bit_get(vis, x) ? 1 : 0;
+    for (uint32_t h = node_slot(x, cap);; h = (h + 1) & (cap - 1)) {
+        const unsigned long long prev = atomicCAS((unsigned long long *)&skeys[h], kNone, (unsigned long long)x);
+        if (prev == kNone || prev == x) {
+            svals[h] = i;  // start nodes are distinct
+            return;
+        }
+    }
+}
+
+// (j', j) for every start node s_j that an output of an earlier start j' passes through
+__global__ void k_fc_pairs(const uint64_t *nodes, const uint32_t *nodej, uint64_t n, const uint64_t *skeys,
+                           const uint32_t *svals, uint32_t cap, uint64_t *pairs, unsigned long long *np) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t a = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; a < n; a += stride) {
+        const uint64_t x = nodes[a];
+        for (uint32_t h = node_slot(x, cap);; h = (h + 1) & (cap - 1)) {
+            const uint64_t k = skeys[h];
+            if (k == kNone) break;
+            if (k == x) {
+                if (svals[h] > nodej[a]) pairs[atomicAdd(np, 1ull)] = ((uint64_t)nodej[a] << 32) | svals[h];
+                break;
+            }
+        }
+    }
+}
+
+// first[x] = the smallest committing start whose cycles pass through x, for x not yet visited
+__global__ void k_fc_first(const uint64_t *nodes, const uint32_t *nodej, uint64_t n, const uint8_t *active,
+                           const uint64_t *vis, uint64_t *hkeys, uint32_t *hvals, uint32_t cap) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t a = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; a < n; a += stride) {
+        const uint32_t j = nodej[a];
+        const uint64_t x = nodes[a];
+        if (!active[j] || bit_get(vis, x)) continue;
+        for (uint32_t h = node_slot(x, cap);; h = (h + 1) & (cap - 1)) {
+            const unsigned long long prev = atomicCAS((unsigned long long *)&hkeys[h], kNone, (unsigned long long)x);
+            if (prev == kNone || prev == x) {
+                atomicMin(&hvals[h], j);
+                break;
+            }
+        }
+    }
+}
+
+// one wave per start j of jl: j conflicts when its footprint (lock table) holds a node that an
+// earlier start of the round visits first; *first = the smallest conflicting j
+__global__ void k_fc_conf(const uint8_t *sbase, uint64_t per_al, uint32_t CL, const uint32_t *jl, const uint32_t *js,
+                          uint32_t nj, const uint64_t *hkeys, const uint32_t *hvals, uint32_t cap, unsigned int *first) {
+    const uint32_t q = blockIdx.x;
+    if (q >= nj) return;
+    const uint32_t j = jl[q];
+    if (__hip_atomic_load(first, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <= j) return;
+    const LockRec *lk = (const LockRec *)(sbase + (uint64_t)js[q] * per_al);
+    for (uint32_t t = threadIdx.x; t < CL; t += blockDim.x) {
+        const uint64_t x = lk[t].key;
+        if (x == kNone) continue;
+        for (uint32_t h = node_slot(x, cap);; h = (h + 1) & (cap - 1)) {
+            const uint64_t k = hkeys[h];
+            if (k == kNone) break;
+            if (k == x) {
+                if (hvals[h] < j) atomicMin(first, j);
+                break;
+            }
+        }
+    }
+}
+
+// dj[noff[q] .. noff[q+1]) = sel[q] (the start owning each gathered node; one GPU: slot = start)
+__global__ void k_fc_owner(const uint64_t *sel, const uint64_t *noff, uint32_t *dj, uint64_t nsel) {
+    const uint64_t q = blockIdx.x;
+    if (q >= nsel) return;
+    for (uint64_t a = noff[q] + threadIdx.x; a < noff[q + 1]; a += blockDim.x) dj[a] = (uint32_t)sel[q];
+}
+
+// visited |= every node first visited by a start before the commit point f
+__global__ void k_fc_mark(const uint64_t *hkeys, const uint32_t *hvals, uint32_t cap, uint32_t f, uint64_t *vis) {
+    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= cap) return;
+    const uint64_t x = hkeys[h];
+    if (x != kNone && hvals[h] < f) atomicOr((unsigned long long *)&vis[x >> 6], 1ull << (x & 63));
+}
+
+__global__ void k_get_bits(const uint64_t *bm, const uint64_t *ids, uint64_t n, uint8_t *out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = bit_get(bm, ids[i]) ? 1 : 0;
 }
 
 __global__ void k_set_bits(uint64_t *bm, const uint64_t *ids, uint64_t n, int value) {
@@ -772,28 +887,6 @@ uint64_t select_flagged(mcaat_ctx *ctx, const uint8_t *flags, uint64_t n, uint64
 }
 
 
-// host visited mirror: a dense bitmap in the context's pool (faulted in on first use only);
-// the words touched are recorded and zeroed again when the mirror goes away
-struct HostBits {
-    uint64_t *w;
-    std::vector<uint64_t> touched;
-    HostBits(mcaat_ctx *ctx, uint64_t D) {
-        ctx->host_bits.ensure((D + 63) / 64 + 1);
-        w = ctx->host_bits.p;
-    }
-    ~HostBits() {
-        for (uint64_t i : touched) w[i] = 0;
-    }
-    HostBits(const HostBits &) = delete;
-    HostBits &operator=(const HostBits &) = delete;
-    bool get(uint64_t x) const { return (w[x >> 6] >> (x & 63)) & 1; }
-    void set(uint64_t x) {
-        uint64_t &v = w[x >> 6];
-        if (!v) touched.push_back(x >> 6);
-        v |= 1ULL << (x & 63);
-    }
-    void clear(uint64_t x) { w[x >> 6] &= ~(1ULL << (x & 63)); }
-};
 
 }  // namespace
 
@@ -971,12 +1064,11 @@ struct FcRunner {
     FcParams prm;
     FcCaps caps;
     DevBuf<uint64_t> dvis;
-    HostBits hvis;
     mcaat_cycles *out;
     uint64_t rounds = 0, reruns = 0;
 
     FcRunner(mcaat_graph *gr, const mcaat_cf_params &p, mcaat_cycles *o, Comm *cm)
-        : g(gr), comm(cm), hvis(gr->ctx, gr->D), out(o) {
+        : g(gr), comm(cm), out(o) {
         if (comm) {
             N = comm->world;
             R = comm->rank;
@@ -995,11 +1087,7 @@ struct FcRunner {
         dvis.alloc(gr->n_words());
         HIP_OK(hipMemsetAsync(dvis.p, 0, dvis.bytes(), gr->ctx->stream));
     }
-    uint64_t per_al() const {
-        const uint64_t per = (uint64_t)caps.P * 8 + caps.P * 4 + caps.P * 32 + caps.P + (uint64_t)caps.CL * 12 +
-                             (uint64_t)caps.CR * 8 + (uint64_t)caps.CO * 8 + caps.CC * 2;
-        return (per + 255) & ~255ULL;
-    }
+    uint64_t per_al() const { return fc_per_search(caps); }
 
     // One speculative round's outputs as seen by every rank: the window's starts are dealt
     // round-robin (start j runs on rank j % N in its slot j / N), each rank runs its share
@@ -1011,6 +1099,136 @@ struct FcRunner {
         std::vector<uint16_t> lens;
     };
 
+    // Commit of one round on the device, in the reference's threads=1 order:
+    //  (1) start j is skipped when it was visited before the round or when the cycles of an
+    //      earlier committed start pass through it (k_fc_pairs finds the pairs; resolved in
+    //      order on the host, a few per round);
+    //  (2) every node not yet visited gets the smallest committing start whose cycles contain
+    //      it (k_fc_first: atomicMin in a table keyed by node);
+    //  (3) start j (after the first committing one) conflicts when its footprint — its lock
+    //      table holds every node whose visited bit it read — contains a node first visited by
+    //      an earlier start of the round (k_fc_conf, on the rank that ran j);
+    //  the prefix before the first conflict or overflow commits (k_fc_mark sets its visited
+    //  bits) and the rest re-runs. Returns the commit point f; skip[j] for j < f.
+    uint64_t commit_round(const std::vector<uint64_t> &pending, uint64_t W, uint64_t first_bad,
+                          const std::vector<uint32_t> &selj, const std::vector<const uint64_t *> &jn,
+                          const std::vector<const FcStatus *> &hs, uint64_t n_nodes, const uint8_t *scratch,
+                          uint64_t pa, std::vector<uint8_t> &skip, const uint64_t *dev_nodes,
+                          const uint32_t *dev_owner) {
+        hipStream_t st = g->ctx->stream;
+        skip.assign(W, 0);
+        const uint32_t nb = (uint32_t)first_bad;
+        if (nb == 0) return 0;
+        const uint32_t scap = (uint32_t)next_pow2(2ULL * nb + 16);
+        const uint32_t hcap = (uint32_t)next_pow2(2ULL * n_nodes + 16);
+        DevBuf<uint64_t> dstarts(nb), skeys(scap), dnb, hkeys(hcap), dpairs(n_nodes + 1);
+        DevBuf<uint32_t> svals(scap), djb, hvals(hcap);
+        DevBuf<uint8_t> prev(nb), act(nb);
+        DevBuf<unsigned long long> dnp(1);
+        DevBuf<unsigned int> dfirst(1);
+        HIP_OK(hipMemcpyAsync(dstarts.p, pending.data(), 8ULL * nb, hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemsetAsync(skeys.p, 0xFF, skeys.bytes(), st));
+        HIP_OK(hipMemsetAsync(dnp.p, 0, 8, st));
+        // node lists of the starts with cycles, in start order, and each node's start (one GPU:
+        // already on the device from the gather; several: assembled from every rank's outputs)
+        const uint64_t *dn = dev_nodes;
+        const uint32_t *dj = dev_owner;
+        if (n_nodes && (!dn || !dj)) {
+            std::vector<uint64_t> hn(n_nodes);
+            std::vector<uint32_t> hj(n_nodes);
+            uint64_t a = 0;
+            for (uint32_t j : selj) {
+                const uint64_t nn = hs[j]->nnodes;
+                std::copy(jn[j], jn[j] + nn, hn.begin() + a);
+                std::fill(hj.begin() + a, hj.begin() + a + nn, j);
+                a += nn;
+            }
+            dnb.alloc(n_nodes);
+            djb.alloc(n_nodes);
+            HIP_OK(hipMemcpyAsync(dnb.p, hn.data(), 8 * n_nodes, hipMemcpyHostToDevice, st));
+            HIP_OK(hipMemcpyAsync(djb.p, hj.data(), 4 * n_nodes, hipMemcpyHostToDevice, st));
+            dn = dnb.p;
+            dj = djb.p;
+            HIP_OK(hipStreamSynchronize(st));  // hn/hj go out of scope
+        }
+        hipLaunchKernelGGL(k_fc_starts, dim3(grid_for(nb, kBlock)), dim3(kBlock), 0, st, dstarts.p, nb, skeys.p,
+                           svals.p, scap, dvis.p, prev.p);
+        LAUNCH_OK();
+        if (n_nodes) {
+            hipLaunchKernelGGL(k_fc_pairs, dim3(grid_for(n_nodes, kBlock)), dim3(kBlock), 0, st, dn, dj, n_nodes,
+                               skeys.p, svals.p, scap, dpairs.p, dnp.p);
+            LAUNCH_OK();
+        }
+        std::vector<uint8_t> pv(nb);
+        unsigned long long np = 0;
+        HIP_OK(hipMemcpyAsync(pv.data(), prev.p, nb, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipMemcpyAsync(&np, dnp.p, 8, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        std::vector<uint64_t> pairs(np);
+        if (np) {
+            HIP_OK(hipMemcpy(pairs.data(), dpairs.p, 8 * np, hipMemcpyDeviceToHost));
+            std::sort(pairs.begin(), pairs.end(), [](uint64_t a, uint64_t b) {
+                return (uint32_t)a != (uint32_t)b ? (uint32_t)a < (uint32_t)b : a < b;
+            });
+        }
+        // (1) skips, in start order (pairs sorted by the start they reach)
+        std::vector<uint8_t> active(nb, 0);
+        for (uint32_t j = 0, q = 0; j < nb; ++j) {
+            bool sk = pv[j] != 0;
+            for (; q < pairs.size() && (uint32_t)pairs[q] == j; ++q)
+                if (!skip[pairs[q] >> 32]) sk = true;
+            skip[j] = sk ? 1 : 0;
+            active[j] = sk ? 0 : 1;
+        }
+        // (2) first visitor of each node
+        HIP_OK(hipMemcpyAsync(act.p, active.data(), nb, hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemsetAsync(hkeys.p, 0xFF, hkeys.bytes(), st));
+        HIP_OK(hipMemsetAsync(hvals.p, 0xFF, hvals.bytes(), st));
+        if (n_nodes) {
+            hipLaunchKernelGGL(k_fc_first, dim3(grid_for(n_nodes, kBlock)), dim3(kBlock), 0, st, dn, dj, n_nodes,
+                               act.p, dvis.p, hkeys.p, hvals.p, hcap);
+            LAUNCH_OK();
+        }
+        // (3) conflicts: only starts that commit after some other start can conflict
+        uint64_t f = first_bad;
+        std::vector<uint32_t> jm, js;
+        bool seen_commit = false;
+        for (uint32_t j = 0; j < nb; ++j) {
+            if (skip[j]) continue;
+            if (seen_commit && (int)(j % N) == R) {
+                jm.push_back(j);
+                js.push_back(j / N);
+            }
+            seen_commit = true;
+        }
+        uint64_t my_first = W;
+        if (n_nodes && !jm.empty()) {
+            DevBuf<uint32_t> djm(jm.size()), djs(js.size());
+            const unsigned int none = 0xFFFFFFFFu;
+            HIP_OK(hipMemcpyAsync(dfirst.p, &none, 4, hipMemcpyHostToDevice, st));
+            HIP_OK(hipMemcpyAsync(djm.p, jm.data(), 4 * jm.size(), hipMemcpyHostToDevice, st));
+            HIP_OK(hipMemcpyAsync(djs.p, js.data(), 4 * js.size(), hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(k_fc_conf, dim3((unsigned)jm.size()), dim3(64), 0, st, scratch, pa, caps.CL, djm.p,
+                               djs.p, (uint32_t)jm.size(), hkeys.p, hvals.p, hcap, dfirst.p);
+            LAUNCH_OK();
+            unsigned int h = none;
+            HIP_OK(hipMemcpyAsync(&h, dfirst.p, 4, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipStreamSynchronize(st));
+            if (h != none) my_first = h;
+        }
+        if (N > 1)
+            for (uint64_t x : comm->allgather_one(my_first)) my_first = std::min(my_first, x);
+        f = std::min(f, my_first);
+        // commit [0, f): visited bits of the nodes its starts visit first
+        if (n_nodes && f > 0) {
+            hipLaunchKernelGGL(k_fc_mark, dim3(grid_for(hcap, kBlock)), dim3(kBlock), 0, st, hkeys.p, hvals.p, hcap,
+                               (uint32_t)f, dvis.p);
+            LAUNCH_OK();
+        }
+        HIP_OK(hipStreamSynchronize(st));
+        return f;
+    }
+
     void run_bucket(const std::vector<uint64_t> &bucket) {
         hipStream_t st = g->ctx->stream;
         std::vector<uint64_t> pending(bucket);
@@ -1018,11 +1236,22 @@ struct FcRunner {
         if (N > 1) window *= (uint64_t)N;  // each rank keeps the single-GPU window of searches
         while (!pending.empty()) {
             // starts already visited are skipped by the reference (:476) -> no entry
-            std::vector<uint64_t> keep;
-            keep.reserve(pending.size());
-            for (uint64_t s : pending)
-                if (!hvis.get(s)) keep.push_back(s);
-            pending.swap(keep);
+            {
+                DevBuf<uint64_t> ids(pending.size());
+                DevBuf<uint8_t> bits(pending.size());
+                std::vector<uint8_t> hb(pending.size());
+                HIP_OK(hipMemcpyAsync(ids.p, pending.data(), 8 * pending.size(), hipMemcpyHostToDevice, st));
+                hipLaunchKernelGGL(k_get_bits, dim3(grid_for(pending.size(), kBlock)), dim3(kBlock), 0, st, dvis.p, ids.p,
+                                   (uint64_t)pending.size(), bits.p);
+                LAUNCH_OK();
+                HIP_OK(hipMemcpyAsync(hb.data(), bits.p, pending.size(), hipMemcpyDeviceToHost, st));
+                HIP_OK(hipStreamSynchronize(st));
+                std::vector<uint64_t> keep;
+                keep.reserve(pending.size());
+                for (size_t i = 0; i < pending.size(); ++i)
+                    if (!hb[i]) keep.push_back(pending[i]);
+                pending.swap(keep);
+            }
             if (pending.empty()) break;
             ++rounds;
             const uint64_t W = std::min<uint64_t>(window, pending.size());
@@ -1037,15 +1266,35 @@ struct FcRunner {
                 std::vector<uint64_t> ls(Wl);
                 for (uint64_t i = 0; i < Wl; ++i) ls[i] = pending[R + N * i];
                 HIP_OK(hipMemcpyAsync(dst.p, ls.data(), 8 * Wl, hipMemcpyHostToDevice, st));
-                static const int lpw = getenv("MCAAT_FC_LPW") ? atoi(getenv("MCAAT_FC_LPW")) : 1;  // measured: 64 lanes 93 ms, 16: 44, 4: 30, 1: 23 (C3)
-                hipLaunchKernelGGL(k_findcycle, dim3(grid_for(Wl, (unsigned)lpw)), dim3(64), 0, st, g->view(), dvis.p,
-                                   dst.p, Wl, caps, prm, (uint64_t *)scratch.p, dstat.p, lpw);
+                // one search per one-wave workgroup (more searches per wave serialise each
+                // other's divergent branches: measured 64 per wave 93 ms, 16: 44, 4: 30, 1: 23 at C3)
+                hipLaunchKernelGGL(k_findcycle, dim3((unsigned)Wl), dim3(64), fc_lds_bytes(caps), st, g->view(), dvis.p,
+                                   dst.p, Wl, caps, prm, (uint64_t *)scratch.p, dstat.p);
                 LAUNCH_OK();
                 HIP_OK(hipMemcpyAsync(mine.st.data(), dstat.p, Wl * sizeof(FcStatus), hipMemcpyDeviceToHost, st));
                 HIP_OK(hipStreamSynchronize(st));
             }
             verbose_mark(g->ctx, "fc.round_kernel");
-            // this rank's finished searches (status 0) with cycles, in slot order
+            static const bool verbose = getenv("MCAAT_VERBOSE") && getenv("MCAAT_VERBOSE")[0] == '1';
+            if (verbose && Wl) {
+                std::vector<uint64_t> ord(Wl);
+                for (uint64_t i = 0; i < Wl; ++i) ord[i] = i;
+                const size_t top = std::min<size_t>(5, ord.size());
+                std::partial_sort(ord.begin(), ord.begin() + top, ord.end(),
+                                  [&](uint64_t a, uint64_t b) { return mine.st[a].steps > mine.st[b].steps; });
+                uint64_t tot = 0;
+                for (const auto &x : mine.st) tot += x.steps;
+                fprintf(stderr, "[mcaat] fc: %llu searches, %llu steps; longest:", (unsigned long long)Wl,
+                        (unsigned long long)tot);
+                for (size_t q = 0; q < top; ++q)
+                    fprintf(stderr, " %u (ncyc %d, nodes %u)", mine.st[ord[q]].steps, mine.st[ord[q]].ncyc,
+                            mine.st[ord[q]].nnodes);
+                fprintf(stderr, "\n");
+            }
+            // this rank's finished searches (status 0) with cycles, in slot order; on one GPU
+            // their nodes stay on the device for the commit (dn_keep, node -> start in dj_keep)
+            DevBuf<uint64_t> dn_keep;
+            DevBuf<uint32_t> dj_keep;
             {
                 std::vector<uint64_t> sel, noff{0}, coff{0};
                 for (uint64_t i = 0; i < Wl; ++i) {
@@ -1069,6 +1318,13 @@ struct FcRunner {
                     LAUNCH_OK();
                     HIP_OK(hipMemcpyAsync(mine.nodes.data(), dn.p, 8 * mine.nodes.size(), hipMemcpyDeviceToHost, st));
                     HIP_OK(hipMemcpyAsync(mine.lens.data(), dl.p, 2 * mine.lens.size(), hipMemcpyDeviceToHost, st));
+                    if (N == 1) {  // one GPU: slot i is start i
+                        dj_keep.alloc(noff.back());
+                        hipLaunchKernelGGL(k_fc_owner, dim3((unsigned)sel.size()), dim3(256), 0, st, dsel.p, dno.p,
+                                           dj_keep.p, (uint64_t)sel.size());
+                        LAUNCH_OK();
+                        dn_keep = std::move(dn);
+                    }
                     HIP_OK(hipStreamSynchronize(st));
                 }
             }
@@ -1103,6 +1359,8 @@ struct FcRunner {
             }
             std::vector<const uint64_t *> jn(W, nullptr);
             std::vector<const uint16_t *> jc(W, nullptr);
+            std::vector<uint32_t> selj;  // starts before the first overflow that found cycles
+            uint64_t n_nodes = 0;
             {
                 // each rank's outputs are in slot order; only starts before the first overflow
                 // are used (one GPU gathers nothing past it)
@@ -1114,77 +1372,17 @@ struct FcRunner {
                         jc[j] = ro[o]->lens.data() + cptr[o];
                         nptr[o] += hs[j]->nnodes;
                         cptr[o] += hs[j]->ncyc;
+                        selj.push_back((uint32_t)j);
+                        n_nodes += hs[j]->nnodes;
                     }
                 }
             }
             verbose_mark(g->ctx, "fc.round_gather");
-            // tentative sequential commit (threads=1 semantics), applied directly to the
-            // host visited bitmap and rolled back past the first conflicting start
-            std::vector<uint64_t> newly;
-            std::vector<uint32_t> newly_c;
-            std::vector<uint8_t> skip(W, 0);
-            for (uint64_t j = 0; j < first_bad; ++j) {
-                const uint64_t s = pending[j];
-                if (hvis.get(s)) { skip[j] = 1; continue; }
-                if (jn[j]) {
-                    const uint64_t nn = hs[j]->nnodes;
-                    for (uint64_t a = 0; a < nn; ++a) {
-                        // random bits of a D-bit map: keep a few misses in flight
-                        if (a + 16 < nn) __builtin_prefetch(hvis.w + (jn[j][a + 16] >> 6), 1);
-                        const uint64_t x = jn[j][a];
-                        if (!hvis.get(x)) {
-                            hvis.set(x);
-                            newly.push_back(x);
-                            newly_c.push_back((uint32_t)j);
-                        }
-                    }
-                }
-            }
-            verbose_mark(g->ctx, "fc.commit_tentative");
-            uint64_t f = first_bad;
-            // only starts that would commit after some tentative commit can conflict
-            std::vector<uint32_t> jl;
-            bool seen_commit = false;
-            for (uint64_t j = 0; j < first_bad; ++j) {
-                if (skip[j]) continue;
-                if (seen_commit) jl.push_back((uint32_t)j);
-                seen_commit = true;
-            }
-            if (!newly.empty() && !jl.empty()) {
-                // each rank checks the footprints of its own starts
-                std::vector<uint32_t> jm, js;
-                for (uint32_t j : jl)
-                    if ((int)(j % N) == R) {
-                        jm.push_back(j);
-                        js.push_back(j / N);
-                    }
-                uint64_t my_first = W;
-                if (!jm.empty()) {
-                    DevBuf<uint64_t> dnw(newly.size());
-                    DevBuf<uint32_t> dnc(newly.size()), djl(jm.size()), djs(js.size());
-                    DevBuf<int> dconf(jm.size());
-                    HIP_OK(hipMemsetAsync(dconf.p, 0, 4 * jm.size(), st));
-                    HIP_OK(hipMemcpyAsync(dnw.p, newly.data(), 8 * newly.size(), hipMemcpyHostToDevice, st));
-                    HIP_OK(hipMemcpyAsync(dnc.p, newly_c.data(), 4 * newly.size(), hipMemcpyHostToDevice, st));
-                    HIP_OK(hipMemcpyAsync(djl.p, jm.data(), 4 * jm.size(), hipMemcpyHostToDevice, st));
-                    HIP_OK(hipMemcpyAsync(djs.p, js.data(), 4 * js.size(), hipMemcpyHostToDevice, st));
-                    hipLaunchKernelGGL(k_fc_conflict, dim3(grid_for((uint64_t)newly.size() * jm.size(), kBlock)),
-                                       dim3(kBlock), 0, st, (uint64_t *)scratch.p, pa, caps.CL, dnw.p, dnc.p,
-                                       (uint64_t)newly.size(), djl.p, djs.p, (uint64_t)jm.size(), dconf.p);
-                    LAUNCH_OK();
-                    std::vector<int> conf(jm.size());
-                    HIP_OK(hipMemcpyAsync(conf.data(), dconf.p, 4 * jm.size(), hipMemcpyDeviceToHost, st));
-                    HIP_OK(hipStreamSynchronize(st));
-                    for (size_t q = 0; q < jm.size(); ++q)
-                        if (conf[q]) { my_first = jm[q]; break; }
-                }
-                if (N > 1)
-                    for (uint64_t x : comm->allgather_one(my_first)) my_first = std::min(my_first, x);
-                f = std::min(f, my_first);
-            }
-            verbose_mark(g->ctx, "fc.commit_conflicts");
-            // commit the prefix [0, f)
-            std::vector<uint64_t> setv;
+            std::vector<uint8_t> skip;
+            const uint64_t f = commit_round(pending, W, first_bad, selj, jn, hs, n_nodes, scratch.p, pa, skip,
+                                            dn_keep.p ? dn_keep.p : nullptr, dj_keep.p ? dj_keep.p : nullptr);
+            verbose_mark(g->ctx, "fc.commit_device");
+            // results of the committed prefix [0, f)
             for (uint64_t j = 0; j < f; ++j) {
                 if (skip[j]) continue;
                 out->starts.push_back(pending[j]);
@@ -1196,19 +1394,6 @@ struct FcRunner {
                 out->stats[5] += of.size() - 1;
                 out->flat.push_back(std::move(fl));
                 out->offsets.push_back(std::move(of));
-            }
-            for (size_t a = 0; a < newly.size(); ++a) {
-                if (newly_c[a] < f) setv.push_back(newly[a]);
-                else hvis.clear(newly[a]);  // roll back tentative marks past the commit prefix
-            }
-            verbose_mark(g->ctx, "fc.commit_results");
-            if (!setv.empty()) {
-                DevBuf<uint64_t> ds(setv.size());
-                HIP_OK(hipMemcpyAsync(ds.p, setv.data(), 8 * setv.size(), hipMemcpyHostToDevice, st));
-                hipLaunchKernelGGL(k_set_bits, dim3(grid_for(setv.size(), kBlock)), dim3(kBlock), 0, st, dvis.p, ds.p,
-                                   (uint64_t)setv.size(), 1);
-                LAUNCH_OK();
-                HIP_OK(hipStreamSynchronize(st));
             }
             verbose_mark(g->ctx, "fc.round_commit");
             if (f < W) ++reruns;
