@@ -107,6 +107,21 @@ __device__ __forceinline__ int dev_incoming(const GraphView &g, uint64_t e, uint
     }
     return n;
 }
+// bits [lo, lo + 16) of a bitmap from its words lo/64 and lo/64 + 1
+__device__ __forceinline__ uint32_t bits16(uint64_t w0, uint64_t w1, uint64_t lo) {
+    const int sh = (int)(lo & 63);
+    return (uint32_t)(((w0 >> sh) | (sh ? w1 << (64 - sh) : 0)) & 0xFFFFu);
+}
+// index of lo's word and of the word after it, clamped to the bitmap (an edge without
+// neighbours may carry any lo: the loads stay in bounds, the mask discards their bits)
+__device__ __forceinline__ uint64_t this_word(uint64_t lo, uint64_t nw) {
+    const uint64_t w = lo >> 6;
+    return w < nw ? w : nw - 1;
+}
+__device__ __forceinline__ uint64_t next_word(uint64_t lo, uint64_t nw) {
+    const uint64_t w = (lo >> 6) + 1;
+    return w < nw ? w : nw - 1;
+}
 __device__ __forceinline__ int dev_outdeg(const GraphView &g, uint64_t e) {
     uint64_t t[4];
     return dev_outgoing(g, e, t);

@@ -32,20 +32,39 @@ constexpr uint64_t kNone = ~0ULL;
 constexpr uint8_t kUnk = 0, kRem = 1, kSurv = 2;
 
 // ------------------------------- scans -------------------------------------
-// one wave per 64-edge bitmap word
+// one wave per 64-edge bitmap word, kScanU words per iteration with all their loads in flight
+// together: the out-edges of e are the consecutive ids [lo, lo + cnt), so its valid out-degree
+// is a popcount of at most two bitmap words (no per-successor loads)
+constexpr int kScanU = 4;
 __global__ void __launch_bounds__(kBlock) k_tips(GraphView g, uint64_t *tip_bm, unsigned long long *count) {
     const int lane = threadIdx.x & 63;
     const uint64_t nw = (g.D + 63) / 64;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     unsigned long long acc = 0;
-    for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nw; w += wstride) {
-        const uint64_t e = w * 64 + lane;
-        bool t = false;
-        if (e < g.D && bit_get(g.valid, e)) t = dev_outdeg(g, e) == 0;
-        const unsigned long long m = __ballot(t);
-        if (lane == 0) {
-            if (tip_bm) tip_bm[w] = m;
-            acc += __popcll(m);
+    for (uint64_t wb = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; wb < nw; wb += kScanU * wstride) {
+        uint64_t sv[kScanU], oi[kScanU], a0[kScanU], a1[kScanU];
+#pragma unroll
+        for (int u = 0; u < kScanU; ++u) {
+            const uint64_t w = wb + u * wstride, e = w * 64 + lane;
+            sv[u] = w < nw ? g.valid[w] : 0;
+            oi[u] = e < g.D ? g.out_info[e] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kScanU; ++u) {
+            const uint64_t lo = oi[u] & kIdxMask;
+            a0[u] = g.valid[this_word(lo, nw)];
+            a1[u] = g.valid[next_word(lo, nw)];
+        }
+#pragma unroll
+        for (int u = 0; u < kScanU; ++u) {
+            const uint64_t w = wb + u * wstride;
+            const uint32_t cnt = __popc((unsigned)(oi[u] >> kIdxBits) & 0xF);
+            const bool t = ((sv[u] >> lane) & 1) && (bits16(a0[u], a1[u], oi[u] & kIdxMask) & ((1u << cnt) - 1)) == 0;
+            const unsigned long long m = __ballot(t);
+            if (lane == 0 && w < nw) {
+                if (tip_bm) tip_bm[w] = m;
+                acc += __popcll(m);
+            }
         }
     }
     block_add(count, acc);
@@ -363,28 +382,46 @@ __global__ void __launch_bounds__(kBlock) k_ids_to_bits(const uint64_t *ids, uin
 }
 
 // --------------------------- start candidates --------------------------------
-// ids [lo, hi) (a rank's share of the scan; [0, D) on one GPU)
+// ids [lo, hi) (a rank's share of the scan; [0, D) on one GPU). The in-edges of e are the
+// positions of a 16-bit mask inside the group starting at in_lo, so the valid in-degree and the
+// self-loop test are two bitmap words; kScanU blocks of edges per iteration, loads in flight
+// together
 __global__ void __launch_bounds__(kBlock) k_candidates(GraphView g, uint64_t thr, uint64_t lo, uint64_t hi,
                                                        uint64_t *list, unsigned long long *cursor) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     const int lane = threadIdx.x & 63;
-    for (uint64_t base = lo + (uint64_t)blockIdx.x * blockDim.x; base < hi; base += stride) {
-        const uint64_t e = base + threadIdx.x;
-        bool c = false;
-        if (e < hi && bit_get(g.valid, e) && (uint64_t)g.mult[e] > thr) {
-            uint64_t in[4];
-            const int n = dev_incoming(g, e, in);
-            if (n >= 2) {
-                c = true;
-                for (int j = 0; j < n; ++j)
-                    if (in[j] == e) c = false;  // _IncomingNotEqualToCurrentNode
-            }
+    const uint64_t nw = (g.D + 63) / 64;
+    for (uint64_t base = lo + (uint64_t)blockIdx.x * blockDim.x; base < hi; base += kScanU * stride) {
+        uint64_t sv[kScanU], ii[kScanU], a0[kScanU], a1[kScanU];
+        uint32_t mu[kScanU];
+#pragma unroll
+        for (int u = 0; u < kScanU; ++u) {
+            const uint64_t e = base + u * stride + threadIdx.x;
+            const bool in = e < hi;
+            sv[u] = in ? g.valid[e >> 6] : 0;
+            mu[u] = in ? g.mult[e] : 0;
+            ii[u] = in ? g.in_info[e] : 0;
         }
-        const unsigned long long m = __ballot(c);
-        unsigned long long off = 0;
-        if (lane == 0 && m) off = atomicAdd(cursor, (unsigned long long)__popcll(m));
-        off = __shfl(off, 0);
-        if (c) list[off + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = e;
+#pragma unroll
+        for (int u = 0; u < kScanU; ++u) {
+            const uint64_t l = ii[u] & kIdxMask;
+            a0[u] = g.valid[this_word(l, nw)];
+            a1[u] = g.valid[next_word(l, nw)];
+        }
+#pragma unroll
+        for (int u = 0; u < kScanU; ++u) {
+            const uint64_t e = base + u * stride + threadIdx.x;
+            const uint64_t l = ii[u] & kIdxMask;
+            const uint32_t in = bits16(a0[u], a1[u], l) & (uint32_t)((ii[u] >> kIdxBits) & 0xFFFF);  // valid in-edges
+            // _IncomingNotEqualToCurrentNode: e must not be one of its own in-edges
+            const bool self = e >= l && e - l < 16 && ((in >> (e - l)) & 1);
+            const bool c = e < hi && ((sv[u] >> (e & 63)) & 1) && (uint64_t)mu[u] > thr && __popc(in) >= 2 && !self;
+            const unsigned long long m = __ballot(c);
+            unsigned long long off = 0;
+            if (lane == 0 && m) off = atomicAdd(cursor, (unsigned long long)__popcll(m));
+            off = __shfl(off, 0);
+            if (c) list[off + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = e;
+        }
     }
 }
 
@@ -526,42 +563,118 @@ struct FcThread {
             h = (h + 1) & (c.CL - 1);
         }
     }
-    // _BackgroundCheck (cycle_finder.cpp:40-52); records x in the footprint
-    __device__ bool background(uint64_t node, uint64_t rm, uint64_t x, int maxl) {
-        if (lock_slot(x, maxl) < 0) return false;
-        const uint64_t nm = g.mult[x];
-        if (bit_get(visited, x)) return false;
-        if (rm / nm > 500) return false;
-        if (node == x) return false;
-        return true;
-    }
-    // _GetOutgoings(node, set, rm) + libstdc++ unordered_set insertion order
-    __device__ int get_outgoings(uint64_t node, uint64_t rm, uint64_t *f, int maxl) {
-        uint64_t nb[4];
-        const int od = dev_outgoing(g, node, nb);
-        int n = 0;
-        if (od == 0 || !bit_get(g.valid, node)) return 0;
-        for (int i = 0; i < od; ++i) {
-            const uint64_t x = nb[i];
-            if (background(node, rm, x, maxl) && bit_get(g.valid, x)) {
-                // 13 buckets, hash(x)=x: before the first element of x's bucket, else at front
-                int pos = 0;
-                for (int j = 0; j < n; ++j)
-                    if (f[j] % 13 == x % 13) { pos = j; break; }
-                for (int j = n; j > pos; --j) f[j] = f[j - 1];
-                f[pos] = x;
-                ++n;
+    // lock_slot(x) whose first probe record (slot h0, key k0) was loaded ahead of this call's
+    // insertions: a prefetched slot filled since (wr[0..nwr)) is read again
+    __device__ int lock_from(uint64_t x, int dflt, uint32_t h0, uint64_t k0, uint32_t *wr, int &nwr) {
+        uint32_t h = h0;
+        uint64_t k = k0;
+        for (int w = 0; w < nwr; ++w)
+            if (wr[w] == h) k = s.lk[h].key;
+        for (;;) {
+            if (k == x) return (int)h;
+            if (k == kNone) {
+                if (lsize + 1 > c.CL / 4 * 3) { status = 1; return -1; }
+                s.lk[h].key = x;
+                s.lk[h].val = dflt;
+                ++lsize;
+                wr[nwr++] = h;
+                return (int)h;
             }
+            h = (h + 1) & (c.CL - 1);
+            k = s.lk[h].key;
+        }
+    }
+    // _BackgroundCheck (cycle_finder.cpp:40-52) for up to 4 neighbours ids[0..n) of node, in
+    // that order (each is recorded in the footprint first). Every neighbour's multiplicity,
+    // visited bit (vis_bits: bit i for ids[i]) and first lock record are loaded together before
+    // the first insertion, so a step waits for one round of loads, not one per neighbour.
+    // ok[i] = the check passed.
+    __device__ void background_all(uint64_t node, uint64_t rm, const uint64_t *ids, int n, uint32_t vis_bits, int maxl,
+                                   bool *ok) {
+        uint16_t mu[4];
+        uint32_t h0[4];
+        uint64_t k0[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (i < n) {
+                mu[i] = g.mult[ids[i]];
+                h0[i] = (uint32_t)(mix64(ids[i]) & (c.CL - 1));
+                k0[i] = s.lk[h0[i]].key;
+            }
+        }
+        uint32_t wr[4];
+        int nwr = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            if (i >= n) break;
+            ok[i] = false;
+            if (lock_from(ids[i], maxl, h0[i], k0[i], wr, nwr) < 0) continue;
+            if ((vis_bits >> i) & 1) continue;
+            if (rm / mu[i] > 500) continue;
+            if (node == ids[i]) continue;
+            ok[i] = true;
+        }
+    }
+    // _GetOutgoings(node, set, rm) + libstdc++ unordered_set insertion order. The successors
+    // are the consecutive ids [lo, lo + cnt): their valid and visited bits are one window each.
+    __device__ int get_outgoings(uint64_t node, uint64_t rm, uint64_t *f, int maxl) {
+        const uint64_t nw = (g.D + 63) / 64;
+        const uint64_t oi = g.out_info[node];
+        const uint64_t nv = g.valid[node >> 6];
+        const uint64_t lo = oi & kIdxMask;
+        const uint32_t cnt = __popc((unsigned)(oi >> kIdxBits) & 0xF);
+        if (cnt == 0 || !((nv >> (node & 63)) & 1)) return 0;
+        const uint32_t vb = bits16(g.valid[this_word(lo, nw)], g.valid[next_word(lo, nw)], lo) & ((1u << cnt) - 1);
+        const uint32_t qb = bits16(visited[this_word(lo, nw)], visited[next_word(lo, nw)], lo);
+        // valid successors in descending id order (OutgoingEdges)
+        uint64_t ids[4];
+        uint32_t vis = 0;
+        int m = 0;
+        for (int i = (int)cnt - 1; i >= 0; --i)
+            if ((vb >> i) & 1) {
+                vis |= ((qb >> i) & 1) << m;
+                ids[m++] = lo + i;
+            }
+        bool ok[4];
+        background_all(node, rm, ids, m, vis, maxl, ok);
+        int n = 0;
+        for (int i = 0; i < m; ++i) {
+            if (!ok[i]) continue;
+            const uint64_t x = ids[i];
+            // 13 buckets, hash(x)=x: before the first element of x's bucket, else at front
+            int pos = 0;
+            for (int j = 0; j < n; ++j)
+                if (f[j] % 13 == x % 13) { pos = j; break; }
+            for (int j = n; j > pos; --j) f[j] = f[j - 1];
+            f[pos] = x;
+            ++n;
         }
         return n;
     }
+    // valid predecessors (ascending ids: positions of the 16-bit mask inside the group at lo)
     __device__ int get_incomings(uint64_t node, uint64_t rm, uint64_t *f, int maxl) {
-        uint64_t in[4];
-        const int id = dev_incoming(g, node, in);
+        const uint64_t nw = (g.D + 63) / 64;
+        const uint64_t ii = g.in_info[node];
+        const uint64_t nv = g.valid[node >> 6];
+        const uint64_t lo = ii & kIdxMask;
+        const uint32_t mask = (uint32_t)(ii >> kIdxBits) & 0xFFFF;
+        if (mask == 0 || !((nv >> (node & 63)) & 1)) return 0;
+        uint32_t vb = bits16(g.valid[this_word(lo, nw)], g.valid[next_word(lo, nw)], lo) & mask;
+        const uint32_t qb = bits16(visited[this_word(lo, nw)], visited[next_word(lo, nw)], lo);
+        uint64_t ids[4];
+        uint32_t vis = 0;
+        int m = 0;
+        while (vb && m < 4) {
+            const int j = __ffs(vb) - 1;
+            vb &= vb - 1;
+            vis |= ((qb >> j) & 1) << m;
+            ids[m++] = lo + j;
+        }
+        bool ok[4];
+        background_all(node, rm, ids, m, vis, maxl, ok);
         int n = 0;
-        if (id == 0 || !bit_get(g.valid, node)) return 0;
-        for (int i = 0; i < id; ++i)
-            if (background(node, rm, in[i], maxl) && bit_get(g.valid, in[i])) f[n++] = in[i];
+        for (int i = 0; i < m; ++i)
+            if (ok[i]) f[n++] = ids[i];
         return n;
     }
 };
@@ -1484,7 +1597,7 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
         DevBuf<uint64_t> list(hi > lo ? hi - lo : 1);
         zero();
         if (hi > lo) {
-            hipLaunchKernelGGL(k_candidates, dim3(grid_for(hi - lo, kBlock)), dim3(kBlock), 0, st, v,
+            hipLaunchKernelGGL(k_candidates, dim3(grid_for(hi - lo, kBlock * kScanU, (unsigned)ctx->n_cu * 16)), dim3(kBlock), 0, st, v,
                                p.threshold_multiplicity, lo, hi, list.p, cnt.p);
             LAUNCH_OK();
         }
