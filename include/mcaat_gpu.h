@@ -54,7 +54,8 @@ int mcaat_device_count(int *n);
  * offsets[n_reads+1] are base offsets of each read in the stream. */
 int mcaat_reads_from_host(mcaat_ctx *ctx, const uint64_t *packed, uint64_t n_words,
                           const uint64_t *offsets, uint64_t n_reads, mcaat_reads **out);
-/* Non-ACGT symbols split a read (k-mers spanning them are dropped). gz via zlib.
+/* Non-ACGT symbols split a read (k-mers spanning them are dropped). gzip via zlib, bzip2 via
+ * libbz2 (opened at run time; concatenated members / streams read in sequence).
  * FASTQ inputs (4-line records) are parsed on the GPU in chunks (csrc/fastq_ingest.hip;
  * chunk size MCAAT_FASTQ_CHUNK bytes, default 256 MiB); FASTA (multi-line) on the host.
  * Blank lines are accepted only before the first and after the last record. */

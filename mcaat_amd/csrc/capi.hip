@@ -154,15 +154,16 @@ void upload_records(mcaat_ctx *ctx, const Stream &rec, mcaat_reads *r) {
     HIP_OK(hipStreamSynchronize(ctx->stream));
 }
 
-// first non-blank byte of a (possibly gzipped) file: '@' FASTQ, '>' FASTA
+// first non-blank byte of a (possibly compressed) file: '@' FASTQ, '>' FASTA
 int sniff_format(const char *path) {
-    gzFile f = gzopen(path, "rb");
-    if (!f) throw Error(MCAAT_E_IO, std::string("cannot open ") + path);
-    int c;
-    while ((c = gzgetc(f)) != -1 && (c == '\n' || c == '\r' || c == ' ' || c == '\t')) {
+    InStream f(path);
+    uint8_t buf[4096];
+    for (;;) {
+        const size_t n = f.read(buf, sizeof buf);
+        for (size_t i = 0; i < n; ++i)
+            if (buf[i] != '\n' && buf[i] != '\r' && buf[i] != ' ' && buf[i] != '\t') return buf[i];
+        if (n < sizeof buf) return -1;
     }
-    gzclose(f);
-    return c;
 }
 
 // Host reader with the reference's kseq semantics (klib kseq_read, as MEGAHIT buildlib and
@@ -173,28 +174,18 @@ int sniff_format(const char *path) {
 // starts with '>', '@' or '+'; after '+' the rest of that line is skipped and quality lines are
 // read until they hold at least as many characters as the sequence (at least one line); any
 // other count is an error. Restated for the tests in oracle/fastx.py kseq_sequences.
-struct GzChars {
-    gzFile f;
-    std::vector<char> buf = std::vector<char>(1 << 20);
-    int pos = 0, len = 0;
-    const char *path;
-    GzChars(const char *p) : path(p) {
-        f = gzopen(p, "rb");
-        if (!f) throw Error(MCAAT_E_IO, std::string("cannot open ") + p);
-        gzbuffer(f, 1u << 20);
-    }
-    ~GzChars() { gzclose(f); }
+struct GzChars {  // characters of a plain, gzip or bzip2 input
+    InStream f;
+    std::vector<uint8_t> buf = std::vector<uint8_t>(1 << 20);
+    size_t pos = 0, len = 0;
+    explicit GzChars(const char *p) : f(p) {}
     int peek() {
         if (pos == len) {
-            len = gzread(f, buf.data(), (unsigned)buf.size());
+            len = f.read(buf.data(), buf.size());
             pos = 0;
-            if (len < 0) {
-                int errnum = 0;
-                throw Error(MCAAT_E_IO, std::string("read error in ") + path + ": " + gzerror(f, &errnum));
-            }
             if (len == 0) return -1;
         }
-        return (unsigned char)buf[pos];
+        return buf[pos];
     }
     int get() {
         const int c = peek();
@@ -1004,8 +995,8 @@ int mcaat_reads_from_fastx_part(mcaat_ctx *ctx, const char *const *files, int n_
         for (int i = 0; i < n_files; ++i) {
             const int c = sniff_format(files[i]);
             if (c == '>') throw Error(MCAAT_E_IO, std::string("FASTA inputs are not split over ranks: ") + files[i]);
-            if (is_gzip_file(files[i])) {
-                // one inflate stream cannot be split: part 0 reads the whole file
+            if (is_compressed_file(files[i])) {
+                // one compressed stream cannot be split: part 0 reads the whole file
                 ranges.push_back(part == 0 ? std::make_pair(0ULL, ~0ULL) : std::make_pair(0ULL, 0ULL));
                 continue;
             }

@@ -1,9 +1,9 @@
-// fastq_ingest.hip — FASTQ(.gz) -> 2-bit read library in HBM.
+// fastq_ingest.hip — FASTQ(.gz/.bz2) -> 2-bit read library in HBM.
 //
 // Replaces SDBGBuild::BuildLib / SequenceLibCollection::Build (sdbg_build.cpp:82-115, the
 // MEGAHIT buildlib step) for FASTQ inputs, and builds in the same pass the mapping view that
 // get_reads re-parses the FASTQ for (reads.cpp:20-52, 88-130). The host only moves bytes: a
-// reader task fills pinned chunks (zlib inflates .gz; plain files are copied straight into
+// reader task fills pinned chunks (zlib / libbz2 inflate .gz / .bz2; plain files are copied straight into
 // the chunk by four pread() threads) while the GPU parses the previous chunk:
 //
 //  1. k_fq_nlcount   one lane per 64-byte segment (4 x 16-B loads): number of '\n' bytes
@@ -31,6 +31,7 @@
 #include <cstring>
 #include <atomic>
 #include <future>
+#include <memory>
 #include <string>
 #include <fcntl.h>
 #include <sys/stat.h>
@@ -280,54 +281,32 @@ void grow(mcaat_ctx *ctx, DevBuf<uint64_t> &b, uint64_t used, uint64_t need) {
     b = std::move(nb);
 }
 
-size_t read_full(gzFile f, uint8_t *dst, size_t n, const char *path) {
-    size_t got = 0;
-    while (got < n) {
-        const unsigned want = (unsigned)std::min<size_t>(n - got, 1u << 30);
-        const int r = gzread(f, dst + got, want);
-        if (r < 0) {
-            int errnum = 0;
-            throw Error(MCAAT_E_IO, std::string("read error in ") + path + ": " + gzerror(f, &errnum));
-        }
-        if (r == 0) break;
-        got += (size_t)r;
-    }
-    return got;
-}
-
-// Source of input bytes: zlib for .gz (one inflate stream), parallel pread() for plain
-// files (one thread copies page-cache data at ~13 GB/s; eight reach ~38 GB/s end to end).
+// Source of input bytes: InStream for compressed files (one inflate stream), parallel pread()
+// for plain files (one thread copies page-cache data at ~13 GB/s; eight reach ~38 GB/s end to end).
 struct Source {
-    gzFile gz = nullptr;
+    std::unique_ptr<InStream> z;  // gzip / bzip2
     int fd = -1;
     uint64_t off = 0;
     const char *path;
     uint64_t end = ~0ULL;  // plain files: read [off, end) only (a rank's part of the file)
-    // [begin, end) of a plain file; a .gz file is read whole (begin = 0, end = ~0)
+    // [begin, end) of a plain file; a compressed file is read whole (begin = 0, end = ~0)
     explicit Source(const char *p, uint64_t begin = 0, uint64_t end_ = ~0ULL) : off(begin), path(p), end(end_) {
-        unsigned char magic[2] = {0, 0};
+        if (is_compressed_file(p)) {
+            if (begin != 0 || end_ != ~0ULL) throw Error(MCAAT_E_INVALID, "a compressed input cannot be split");
+            z.reset(new InStream(p));
+            return;
+        }
         fd = open(p, O_RDONLY);
         if (fd < 0) throw Error(MCAAT_E_IO, std::string("cannot open ") + p);
-        const bool is_gz = pread(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b;
-        if (is_gz && (begin != 0 || end_ != ~0ULL)) throw Error(MCAAT_E_INVALID, "a .gz input cannot be split");
-        if (is_gz) {
-            close(fd);
-            fd = -1;
-            gz = gzopen(p, "rb");
-            if (!gz) throw Error(MCAAT_E_IO, std::string("cannot open ") + p);
-            gzbuffer(gz, 1u << 20);
-        } else {
-            posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
-        }
+        posix_fadvise(fd, 0, 0, POSIX_FADV_SEQUENTIAL);
     }
     ~Source() {
-        if (gz) gzclose(gz);
         if (fd >= 0) close(fd);
     }
     Source(const Source &) = delete;
     Source &operator=(const Source &) = delete;
     size_t read(uint8_t *dst, size_t n) {
-        if (gz) return read_full(gz, dst, n, path);
+        if (z) return z->read(dst, n);
         n = (size_t)std::min<uint64_t>(n, end > off ? end - off : 0);
         if (!n) return 0;
         // 8 by default: the C3 FASTQ (92 GB in tmpfs) reads at 38 GB/s end to end with 8 or 16
@@ -392,7 +371,8 @@ void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_r
     for (int i = 0; i < n_files; ++i) {
         struct stat st;
         const std::string path(files[i]);
-        const bool gz = path.size() > 3 && path.compare(path.size() - 3, 3, ".gz") == 0;
+        const bool gz = (path.size() > 3 && path.compare(path.size() - 3, 3, ".gz") == 0) ||
+                        (path.size() > 4 && path.compare(path.size() - 4, 4, ".bz2") == 0);
         if (stat(files[i], &st) == 0) {
             uint64_t sz = (uint64_t)st.st_size;
             if (ranges) sz = std::min(sz, (*ranges)[i].second) - std::min(sz, (*ranges)[i].first);
@@ -680,13 +660,15 @@ void write_fastq(const mcaat_reads *r, const char *path, int threads) {
 
 namespace mcaat {
 
-bool is_gzip_file(const char *path) {
-    unsigned char magic[2] = {0, 0};
+bool is_compressed_file(const char *path) {
+    unsigned char m[4] = {0, 0, 0, 0};
     const int fd = open(path, O_RDONLY);
     if (fd < 0) throw Error(MCAAT_E_IO, std::string("cannot open ") + path);
-    const bool gz = pread(fd, magic, 2, 0) == 2 && magic[0] == 0x1f && magic[1] == 0x8b;
+    const ssize_t n = pread(fd, m, 4, 0);
     close(fd);
-    return gz;
+    const bool gz = n >= 2 && m[0] == 0x1f && m[1] == 0x8b;
+    const bool bz = n >= 4 && m[0] == 'B' && m[1] == 'Z' && m[2] == 'h' && m[3] >= '1' && m[3] <= '9';
+    return gz || bz;
 }
 
 // A line start q >= pos begins a record when line q starts with '@', line q+2 with '+', and

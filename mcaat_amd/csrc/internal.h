@@ -292,9 +292,26 @@ void graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n);
 // ranges: per file, the byte range [first, second) to read (a rank's part; null: whole files)
 void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_reads *r,
                   const std::vector<std::pair<uint64_t, uint64_t>> *ranges = nullptr);
+// Decompressed sequential bytes of an input file (instream.hip): gzip (zlib), bzip2 (libbz2,
+// opened at run time) or plain; concatenated members / streams are read in sequence.
+class InStream {
+   public:
+    enum class Kind { Plain, Gzip, Bzip2 };
+    explicit InStream(const char *path);
+    ~InStream();
+    InStream(const InStream &) = delete;
+    InStream &operator=(const InStream &) = delete;
+    size_t read(uint8_t *dst, size_t n);  // < n only at the end of the input
+    Kind kind() const { return kind_; }
+
+   private:
+    struct Impl;
+    Impl *impl_;
+    Kind kind_ = Kind::Plain;
+};
 // first 4-line FASTQ record start at or after byte pos of a plain file (its size if none)
 uint64_t fastq_record_start(const char *path, uint64_t pos);
-bool is_gzip_file(const char *path);
+bool is_compressed_file(const char *path);  // gzip or bzip2: read whole, never split
 void write_fastq(const mcaat_reads *r, const char *path, int threads);
 void graph_save(const mcaat_graph *g, const char *path);
 void graph_load(mcaat_ctx *ctx, const char *path, mcaat_graph *g);

@@ -14,7 +14,7 @@ double get_total_system_ram() {
 static void print_help() {
     std::cout << "Usage: ./mcaat --input-files <file1> [file2] [options]\n"
               << "\nRequired:\n"
-              << "  --input-files, -i <file1> [file2]  One or two input FASTA/FASTQ files (.gz ok)\n"
+              << "  --input-files, -i <file1> [file2]  One or two input FASTA/FASTQ files (.gz, .bz2 ok)\n"
               << "\nOptional:\n"
               << "  --ram <amount>                  RAM to use (e.g., 4G, 500M). Default: 95% of system RAM\n"
               << "  --threads <num>                 Number of threads. Default: CPU cores - 2\n"

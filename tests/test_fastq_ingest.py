@@ -5,8 +5,10 @@ mapping view (one entry per record, second file reverse-complemented, reads.cpp:
 Bar: bit-exact packed streams and offsets. The chunk size is forced down (MCAAT_FASTQ_CHUNK) so
 records straddle chunk boundaries and the carry path runs many times. Edge cases: N and IUPAC
 symbols, lowercase, CRLF, empty sequences, no final newline, blank lines around the records,
-gzip input, paired-end, records longer than the carry reserve and malformed input (loud errors).
+gzip and bzip2 input (concatenated members / streams), paired-end, records longer than the
+carry reserve and malformed input (loud errors).
 """
+import bz2
 import gzip
 import os
 
@@ -38,7 +40,11 @@ def _fastq_text(seqs, crlf=False, final_newline=True, lead="", trail=""):
 
 def _write(path, text, gz=False):
     data = text.encode()
-    if gz:
+    if gz == "bz2":  # two concatenated bzip2 streams (as pbzip2 writes), split mid-record
+        h = len(data) // 2
+        with open(path, "wb") as f:
+            f.write(bz2.compress(data[:h]) + bz2.compress(data[h:]))
+    elif gz:
         with gzip.open(path, "wb") as f:
             f.write(data)
     else:
@@ -101,12 +107,12 @@ def test_single_end_chunked(gpu_ctx, tmp_path, monkeypatch, chunk):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gz", [False, True])
+@pytest.mark.parametrize("gz", [False, True, "bz2"])
 def test_paired_end_crlf_gzip(gpu_ctx, tmp_path, monkeypatch, gz):
     rng = np.random.default_rng(5)
     t1 = _fastq_text(_rand_records(rng, 300), crlf=True)
     t2 = _fastq_text(_rand_records(rng, 300), final_newline=False)
-    sfx = ".fq.gz" if gz else ".fq"
+    sfx = ".fq.bz2" if gz == "bz2" else ".fq.gz" if gz else ".fq"
     files = [_write(tmp_path / ("r1" + sfx), t1, gz), _write(tmp_path / ("r2" + sfx), t2, gz)]
     _check(gpu_ctx, files, [t1, t2], monkeypatch, 777)
 
@@ -213,3 +219,21 @@ def test_fasta_still_parsed(gpu_ctx, tmp_path):
     p, o = reads.download()
     wp, wo = FX.pack_bases(["ACGT", "ACG", "TTTT"])
     assert np.array_equal(o, wo) and np.array_equal(p[:1], wp[:1])
+
+
+@pytest.mark.gpu
+def test_bzip2_fasta_wrapped_and_truncated(gpu_ctx, tmp_path, monkeypatch):
+    """bzip2 through the host kseq-style reader (FASTA, wrapped FASTQ), and a truncated stream
+    fails loudly instead of reading short."""
+    import mcaat_amd as M
+
+    monkeypatch.delenv("MCAAT_FASTQ_CHUNK", raising=False)
+    texts = [">a\nACGTN\nACG\n>b\nTTTT\n", "@a\nACGTAC\nGTTT\n+\nIIIIII\nIIII\n@b\nGGA\n+\n@@@\n"]
+    for i, t in enumerate(texts):
+        f = _write(tmp_path / f"k{i}.bz2", t, "bz2")
+        _check_kseq(gpu_ctx, [f], [t])
+    good = bz2.compress(_fastq_text(["ACGT" * 40] * 50).encode())
+    cut = tmp_path / "cut.fq.bz2"
+    cut.write_bytes(good[: len(good) // 2])
+    with pytest.raises(RuntimeError):
+        M.Reads.from_fastx(gpu_ctx, [str(cut)])

@@ -109,6 +109,28 @@ def test_rccl_single_rank_matches_one_gpu():
 
 
 @pytest.mark.gpu
+def test_fastq_parts_compressed_inputs_go_whole_to_part_zero(gpu_ctx, tmp_path):
+    import bz2
+    import gzip
+
+    r = M.Reads.synth(gpu_ctx, M.SynthSpec(seed=9, n_reads=3000))
+    plain = str(tmp_path / "r.fq")
+    r.write_fastq(plain, threads=2)
+    r.free()
+    data = open(plain, "rb").read()
+    for name, blob in (("r.fq.gz", gzip.compress(data)), ("r.fq.bz2", bz2.compress(data))):
+        p = tmp_path / name
+        p.write_bytes(blob)
+        whole = M.Reads.from_fastx(gpu_ctx, [plain])
+        want = whole.info()
+        whole.free()
+        parts = [M.Reads.from_fastx_part(gpu_ctx, [str(p)], i, 3) for i in range(3)]
+        assert parts[0].info() == want and parts[1].info() == (0, 0) and parts[2].info() == (0, 0)
+        for q in parts:
+            q.free()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("paired", [False, True])
 def test_fastq_parts_partition_the_records(gpu_ctx, tmp_path, paired):
     spec = M.SynthSpec(seed=7, n_reads=7001, paired=paired, error_rate=1e-3)
