@@ -54,11 +54,12 @@ CONFIGS = {
                sample=M.SynthSpec(seed=3, n_genomes=20, genome_len=100_000, arrays_per_genome=2, spacers_per_array=12,
                                   repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
                                   read_len=150, n_reads=2_000_000, error_rate=2.0e-4)),
-    # C2-shaped, smaller: 50M PE reads over a 400 Mbp community
-    "c2": dict(spec=M.SynthSpec(seed=2, n_genomes=200, genome_len=2_000_000, arrays_per_genome=2,
+    # C2: 50M PE reads (25M pairs) over a 400 Mbp community with 500 CRISPR arrays, 0.5 % errors
+    # (250 genomes x 1.6 Mbp x 2 arrays: the generator places whole arrays per genome)
+    "c2": dict(spec=M.SynthSpec(seed=2, n_genomes=250, genome_len=1_600_000, arrays_per_genome=2,
                                 spacers_per_array=12, repeat_len_min=30, repeat_len_max=36, spacer_len_min=30,
                                 spacer_len_max=36, read_len=150, n_reads=50_000_000, error_rate=5.0e-3, paired=True),
-               k=27, thr=20, name="C2 50M PE synthetic metagenome (k=27)",
+               k=27, thr=20, name="C2 50M PE synthetic metagenome (400 Mbp, 500 arrays, e=0.5%, k=27)",
                sample=M.SynthSpec(seed=2, n_genomes=40, genome_len=200_000, arrays_per_genome=2, spacers_per_array=12,
                                   repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
                                   read_len=150, n_reads=1_000_000, error_rate=5.0e-3, paired=True)),

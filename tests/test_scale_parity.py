@@ -162,8 +162,8 @@ def test_bench_regime_sample_matches_oracle(gpu_ctx, name):
 
 # ---- full-size properties (bench configs) ---------------------------------------------
 FULL = {
-    # bench.py "c2": 50M PE reads, 0.5 % errors -> D ~ 2.4e9 > 2^31
-    "c2_full": (M.SynthSpec(seed=2, n_genomes=200, genome_len=2_000_000, arrays_per_genome=2, spacers_per_array=12,
+    # bench.py "c2": 50M PE reads over 400 Mbp (500 arrays), 0.5 % errors -> D > 2^31
+    "c2_full": (M.SynthSpec(seed=2, n_genomes=250, genome_len=1_600_000, arrays_per_genome=2, spacers_per_array=12,
                             repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
                             read_len=150, n_reads=50_000_000, error_rate=5.0e-3, paired=True), 27, 20),
     # bench.py "c3": 300M reads, D ~ 1.0e9
