@@ -455,13 +455,22 @@ __device__ __forceinline__ bool set_contains(const uint64_t *tab, uint32_t cap, 
 __global__ void __launch_bounds__(kBlock) k_dls(GraphView g, const uint64_t *cand, uint64_t n, int limit,
                                                 uint64_t *stack_all, uint32_t cs, uint64_t *vis_all, uint32_t cv,
                                                 int8_t *res, int lpw) {
-    // lpw searches per wave (divergent searches serialise each other's branches)
+    // lpw searches per wave (divergent searches serialise each other's branches); the whole
+    // wave first clears their visited sets, then lanes >= lpw leave
+    const uint64_t w0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64 * lpw;
+    {
+        const uint64_t nw_s = w0 < n ? (n - w0 < (uint64_t)lpw ? n - w0 : (uint64_t)lpw) : 0;
+        uint64_t *v0 = vis_all + w0 * cv;
+        for (uint64_t j = threadIdx.x & 63; j < nw_s * cv; j += 64) v0[j] = kNone;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
     if ((int)(threadIdx.x & 63) >= lpw) return;
-    const uint64_t i = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64 * lpw + (threadIdx.x & 63);
+    const uint64_t i = w0 + (threadIdx.x & 63);
     if (i >= n) return;
     uint64_t *stk = stack_all + i * cs;
     uint64_t *vis = vis_all + i * cv;
-    for (uint32_t j = 0; j < cv; ++j) vis[j] = kNone;
     const uint64_t start = cand[i];
     uint32_t sp = 0, vsize = 0;
     bool over = false;
@@ -1135,7 +1144,9 @@ static std::vector<uint64_t> run_dls(mcaat_graph *g, const std::vector<uint64_t>
     uint32_t cs = (uint32_t)std::max<int64_t>(1, knob(ctx, "cf.dls_stack", 1024));
     uint32_t cv = (uint32_t)next_pow2((uint64_t)std::max<int64_t>(2, knob(ctx, "cf.dls_visited", 2048)));
     while (!todo.empty()) {
-        const uint64_t batch_cap = std::max<uint64_t>(64, (512ULL << 20) / (8ULL * (cs + cv)));
+        // scratch for every candidate at once (C3: 65K candidates x 24 KB = 1.6 GB): one launch,
+        // whose time is its longest search (512 MB batches made C3 three launches, 6.6 ms)
+        const uint64_t batch_cap = std::max<uint64_t>(64, (8ULL << 30) / (8ULL * (cs + cv)));
         std::vector<uint64_t> next;
         for (size_t b0 = 0; b0 < todo.size(); b0 += batch_cap) {
             const uint64_t n = std::min<uint64_t>(batch_cap, todo.size() - b0);
@@ -1151,6 +1162,13 @@ static std::vector<uint64_t> run_dls(mcaat_graph *g, const std::vector<uint64_t>
             std::vector<int8_t> h(n);
             HIP_OK(hipMemcpyAsync(h.data(), dres.p, n, hipMemcpyDeviceToHost, st));
             HIP_OK(hipStreamSynchronize(st));
+            static const bool verbose = getenv("MCAAT_VERBOSE") && getenv("MCAAT_VERBOSE")[0] == '1';
+            if (verbose) {
+                uint64_t over = 0, found = 0;
+                for (int8_t x : h) over += x < 0, found += x > 0;
+                fprintf(stderr, "[mcaat] dls: batch of %llu (stack %u, visited %u): found %llu, overflow %llu\n",
+                        (unsigned long long)n, cs, cv, (unsigned long long)found, (unsigned long long)over);
+            }
             for (uint64_t j = 0; j < n; ++j) {
                 if (h[j] < 0) next.push_back(todo[b0 + j]);
                 else res[todo[b0 + j]] = h[j];
