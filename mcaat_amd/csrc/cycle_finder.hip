@@ -627,12 +627,15 @@ struct FcThread {
     // _GetOutgoings(node, set, rm) + libstdc++ unordered_set insertion order. The successors
     // are the consecutive ids [lo, lo + cnt): their valid and visited bits are one window each.
     __device__ int get_outgoings(uint64_t node, uint64_t rm, uint64_t *f, int maxl) {
+        return get_outgoings_oi(node, g.out_info[node], ((g.valid[node >> 6] >> (node & 63)) & 1) != 0, rm, f, maxl);
+    }
+    // the same with node's out_info word and validity already loaded (a frame candidate's
+    // out_info is loaded together with its lock record, one round trip earlier)
+    __device__ int get_outgoings_oi(uint64_t node, uint64_t oi, bool node_valid, uint64_t rm, uint64_t *f, int maxl) {
         const uint64_t nw = (g.D + 63) / 64;
-        const uint64_t oi = g.out_info[node];
-        const uint64_t nv = g.valid[node >> 6];
         const uint64_t lo = oi & kIdxMask;
         const uint32_t cnt = __popc((unsigned)(oi >> kIdxBits) & 0xF);
-        if (cnt == 0 || !((nv >> (node & 63)) & 1)) return 0;
+        if (cnt == 0 || !node_valid) return 0;
         const uint32_t vb = bits16(g.valid[this_word(lo, nw)], g.valid[next_word(lo, nw)], lo) & ((1u << cnt) - 1);
         const uint32_t qb = bits16(visited[this_word(lo, nw)], visited[next_word(lo, nw)], lo);
         // valid successors in descending id order (OutgoingEdges)
@@ -661,10 +664,9 @@ struct FcThread {
         return n;
     }
     // valid predecessors (ascending ids: positions of the 16-bit mask inside the group at lo)
-    __device__ int get_incomings(uint64_t node, uint64_t rm, uint64_t *f, int maxl) {
+    // (node's in_info word and validity word loaded by the caller, beside its lock record)
+    __device__ int get_incomings_ii(uint64_t node, uint64_t ii, uint64_t nv, uint64_t rm, uint64_t *f, int maxl) {
         const uint64_t nw = (g.D + 63) / 64;
-        const uint64_t ii = g.in_info[node];
-        const uint64_t nv = g.valid[node >> 6];
         const uint64_t lo = ii & kIdxMask;
         const uint32_t mask = (uint32_t)(ii >> kIdxBits) & 0xFFFF;
         if (mask == 0 || !((nv >> (node & 63)) & 1)) return 0;
@@ -744,6 +746,9 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
         uint64_t N[4];
         const int nN = s.frn[top];
         for (int j = 0; j < nN; ++j) N[j] = s.fr[4 * top + j];
+        // the first candidate is the one usually pushed: its out_info is loaded now, beside its
+        // lock record (frame entries are valid edges)
+        const uint64_t oi0 = nN > 0 ? g.out_info[N[0]] : 0;
         bool flag = true, pushed = false;
         for (int j = 0; j < nN; ++j) {
             const uint64_t x = N[j];
@@ -769,7 +774,8 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
                     s.path[plen++] = x;
                     s.bl[depth] = maxl;
                     s.lk[sl].val = (int)plen;
-                    s.frn[depth] = (uint8_t)t.get_outgoings(x, rm, s.fr + 4 * depth, maxl);
+                    s.frn[depth] = (uint8_t)(j == 0 ? t.get_outgoings_oi(x, oi0, true, rm, s.fr + 4 * depth, maxl)
+                                                    : t.get_outgoings(x, rm, s.fr + 4 * depth, maxl));
                     ++depth;
                     flag = false;
                     pushed = true;
@@ -792,12 +798,13 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
                     const uint64_t e = s.relax[--rs];
                     const int blv = (int)(e & 0xFFFF);
                     const uint64_t u = e >> 16;
+                    const uint64_t uii = g.in_info[u], unv = g.valid[u >> 6];  // beside the lock probe
                     const int sl = t.lock_slot(u, maxl);
                     if (sl < 0) break;
                     if (s.lk[sl].val < maxl - blv + 1) {
                         s.lk[sl].val = maxl - blv + 1;
                         uint64_t ins[4];
-                        const int ni = t.get_incomings(u, rm, ins, maxl);
+                        const int ni = t.get_incomings_ii(u, uii, unv, rm, ins, maxl);
                         for (int j = 0; j < ni; ++j) {
                             bool on_path = false;
                             for (uint32_t q = 0; q < plen; ++q)
