@@ -518,7 +518,7 @@ struct FcParams {
 struct __attribute__((aligned(16))) LockRec {
     uint64_t key;
     int32_t val;
-    uint32_t pad;
+    uint32_t onpath;  // 1 while the node is on the search path (path nodes are distinct)
 };
 // Per search: the hot state read every step (path, neighbour frames, backtrack lengths) is in
 // the workgroup's LDS; the lock table, relax stack and outputs are in global scratch
@@ -526,6 +526,7 @@ struct __attribute__((aligned(16))) LockRec {
 struct FcScratch {
     uint64_t *path;     // P      (LDS)
     int32_t *bl;        // P      (LDS)
+    int32_t *psl;       // P      (LDS) lock slot of each path node
     uint64_t *fr;       // 4P     (LDS)
     uint8_t *frn;       // P      (LDS)
     LockRec *lk;        // CL     (global)
@@ -537,7 +538,7 @@ __host__ __device__ inline uint64_t fc_per_search(const FcCaps &c) {
     const uint64_t per = (uint64_t)c.CL * 16 + (uint64_t)c.CR * 8 + (uint64_t)c.CO * 8 + (uint64_t)c.CC * 2;
     return (per + 255) & ~255ULL;
 }
-__host__ __device__ inline uint32_t fc_lds_bytes(const FcCaps &c) { return c.P * (8 + 32 + 4 + 1) + 16; }
+__host__ __device__ inline uint32_t fc_lds_bytes(const FcCaps &c) { return c.P * (8 + 32 + 4 + 4 + 1) + 16; }
 struct FcStatus {
     int32_t status;     // 0 ok, 1 lock table full, 2 relax stack full, 3 output full
     int32_t ncyc;
@@ -566,6 +567,7 @@ struct FcThread {
                 if (lsize + 1 > c.CL / 4 * 3) { status = 1; return -1; }
                 s.lk[h].key = x;
                 s.lk[h].val = dflt;
+                s.lk[h].onpath = 0;
                 ++lsize;
                 return (int)h;
             }
@@ -585,6 +587,7 @@ struct FcThread {
                 if (lsize + 1 > c.CL / 4 * 3) { status = 1; return -1; }
                 s.lk[h].key = x;
                 s.lk[h].val = dflt;
+                s.lk[h].onpath = 0;
                 ++lsize;
                 wr[nwr++] = h;
                 return (int)h;
@@ -599,7 +602,7 @@ struct FcThread {
     // the first insertion, so a step waits for one round of loads, not one per neighbour.
     // ok[i] = the check passed.
     __device__ void background_all(uint64_t node, uint64_t rm, const uint64_t *ids, int n, uint32_t vis_bits, int maxl,
-                                   bool *ok) {
+                                   bool *ok, int *slot = nullptr) {
         uint16_t mu[4];
         uint32_t h0[4];
         uint64_t k0[4];
@@ -617,7 +620,9 @@ struct FcThread {
         for (int i = 0; i < 4; ++i) {
             if (i >= n) break;
             ok[i] = false;
-            if (lock_from(ids[i], maxl, h0[i], k0[i], wr, nwr) < 0) continue;
+            const int sl = lock_from(ids[i], maxl, h0[i], k0[i], wr, nwr);
+            if (slot) slot[i] = sl;
+            if (sl < 0) continue;
             if ((vis_bits >> i) & 1) continue;
             if (rm / mu[i] > 500) continue;
             if (node == ids[i]) continue;
@@ -665,7 +670,8 @@ struct FcThread {
     }
     // valid predecessors (ascending ids: positions of the 16-bit mask inside the group at lo)
     // (node's in_info word and validity word loaded by the caller, beside its lock record)
-    __device__ int get_incomings_ii(uint64_t node, uint64_t ii, uint64_t nv, uint64_t rm, uint64_t *f, int maxl) {
+    __device__ int get_incomings_ii(uint64_t node, uint64_t ii, uint64_t nv, uint64_t rm, uint64_t *f, int *fslot,
+                                    int maxl) {
         const uint64_t nw = (g.D + 63) / 64;
         const uint64_t lo = ii & kIdxMask;
         const uint32_t mask = (uint32_t)(ii >> kIdxBits) & 0xFFFF;
@@ -682,10 +688,14 @@ struct FcThread {
             ids[m++] = lo + j;
         }
         bool ok[4];
-        background_all(node, rm, ids, m, vis, maxl, ok);
+        int sl[4];
+        background_all(node, rm, ids, m, vis, maxl, ok, sl);
         int n = 0;
         for (int i = 0; i < m; ++i)
-            if (ok[i]) f[n++] = ids[i];
+            if (ok[i]) {
+                fslot[n] = sl[i];
+                f[n++] = ids[i];
+            }
         return n;
     }
 };
@@ -716,6 +726,7 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
     s.path = (uint64_t *)lb; lb += (uint64_t)caps.P * 8;
     s.fr = (uint64_t *)lb; lb += (uint64_t)caps.P * 32;
     s.bl = (int32_t *)lb; lb += (uint64_t)caps.P * 4;
+    s.psl = (int32_t *)lb; lb += (uint64_t)caps.P * 4;
     s.frn = lb;
     for (uint32_t j = threadIdx.x; j < caps.CL; j += blockDim.x) s.lk[j].key = kNone;
     __syncthreads();  // the workgroup is one wave: lane 0 sees every lane's clear
@@ -730,11 +741,15 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
     int64_t counter = 0, steps = 0;
 
     // FindCycleUtil (cycle_finder.cpp:231-243)
-    s.path[plen++] = st;
     {
         const int sl = t.lock_slot(st, maxl);
-        if (sl >= 0) s.lk[sl].val = 0;
+        if (sl >= 0) {
+            s.lk[sl].val = 0;
+            s.lk[sl].onpath = 1;
+        }
+        s.psl[plen] = sl;
     }
+    s.path[plen++] = st;
     s.frn[0] = (uint8_t)t.get_outgoings(st, rm, s.fr, maxl);
     s.bl[0] = maxl;
     depth = 1;
@@ -771,9 +786,11 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
                     for (int r = 0; r < m; ++r)
                         if (s.fr[4 * top + r] != x) s.fr[4 * top + q++] = s.fr[4 * top + r];
                     s.frn[top] = (uint8_t)q;
+                    s.psl[plen] = sl;
                     s.path[plen++] = x;
                     s.bl[depth] = maxl;
                     s.lk[sl].val = (int)plen;
+                    s.lk[sl].onpath = 1;
                     s.frn[depth] = (uint8_t)(j == 0 ? t.get_outgoings_oi(x, oi0, true, rm, s.fr + 4 * depth, maxl)
                                                     : t.get_outgoings(x, rm, s.fr + 4 * depth, maxl));
                     ++depth;
@@ -787,6 +804,7 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
         if (flag) {
             --depth;
             const uint64_t v = s.path[--plen];
+            if (s.psl[plen] >= 0) s.lk[s.psl[plen]].onpath = 0;
             const int b = s.bl[depth];
             if (depth > 0) s.bl[depth - 1] = min(s.bl[depth - 1], b);
             if (b < maxl) {
@@ -804,11 +822,11 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
                     if (s.lk[sl].val < maxl - blv + 1) {
                         s.lk[sl].val = maxl - blv + 1;
                         uint64_t ins[4];
-                        const int ni = t.get_incomings_ii(u, uii, unv, rm, ins, maxl);
+                        int isl[4];
+                        const int ni = t.get_incomings_ii(u, uii, unv, rm, ins, isl, maxl);
                         for (int j = 0; j < ni; ++j) {
-                            bool on_path = false;
-                            for (uint32_t q = 0; q < plen; ++q)
-                                if (s.path[q] == ins[j]) { on_path = true; break; }
+                            // std::find(path, ins[j]): the path flag of its lock record
+                            const bool on_path = s.lk[isl[j]].onpath != 0;
                             if (!on_path) {
                                 if (rs >= caps.CR) { t.status = 2; break; }
                                 s.relax[rs++] = (ins[j] << 16) | (uint64_t)(blv + 1);
