@@ -355,6 +355,8 @@ void mcaat_finalize(mcaat_ctx *ctx) {
     mcaat::dev_trim();
     for (auto *&p : ctx->pinned)
         if (p) (void)hipHostFree(p);
+    for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
+    if (ctx->bounce) (void)hipHostFree(ctx->bounce);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -547,10 +549,13 @@ int mcaat_build_graph(mcaat_ctx *ctx, const mcaat_reads *r, int k, mcaat_graph *
         require(ctx && r && out, "null argument");
         require(k >= 2 && k <= kMaxK, "k must be in [2, 30]");
         HIP_OK(hipSetDevice(ctx->device));
+        verbose_mark(ctx, "build.enter");
         auto *g = new mcaat_graph;
         g->ctx = ctx;
         try {
+            verbose_mark(ctx, "build.new");
             StageTimer timer(ctx);
+            verbose_mark(ctx, "build.timer");
             CountResult c;
             node_counter(ctx, r, k, c);
             timer.mark("node_counter");
@@ -634,6 +639,7 @@ int mcaat_graph_from_sorted(mcaat_ctx *ctx, int k, const uint64_t *keys_dev, con
         require(ctx && out && (D == 0 || (keys_dev && mult_dev)), "null argument");
         require(k >= 2 && k <= kMaxK, "k must be in [2, 30]");
         HIP_OK(hipSetDevice(ctx->device));
+        verbose_mark(ctx, "build.enter");
         auto *g = new mcaat_graph;
         g->ctx = ctx;
         try {
@@ -738,7 +744,12 @@ int mcaat_graph_load(mcaat_ctx *ctx, const char *path, mcaat_graph **out) {
     });
 }
 
-void mcaat_graph_free(mcaat_graph *g) { delete g; }
+void mcaat_graph_free(mcaat_graph *g) {
+    mcaat_ctx *ctx = g ? g->ctx : nullptr;
+    if (ctx) verbose_mark(ctx, "graph.enter_free");
+    delete g;
+    if (ctx) verbose_mark(ctx, "graph.free");
+}
 
 int mcaat_reads_records_info(const mcaat_reads *r, uint64_t *n_records, int *separate) {
     return guarded([&] {
@@ -1063,6 +1074,7 @@ int mcaat_cycle_finder_comm(mcaat_graph *g, mcaat_comm *comm, const mcaat_cf_par
         auto *c = new mcaat_cycles;
         try {
             cycle_finder(g, *p, c, comm ? comm->c.get() : nullptr);
+            verbose_mark(g->ctx, "cf.return");
         } catch (...) {
             delete c;
             throw;

@@ -544,6 +544,8 @@ struct FcStatus {
     int32_t ncyc;
     uint32_t nnodes;
     uint32_t steps;  // main-loop iterations (diagnostics: MCAAT_VERBOSE)
+    uint32_t relax;  // lock-relaxation expansions (diagnostics)
+    uint32_t locks;  // lock-table entries at the end (diagnostics)
 };
 
 struct FcThread {
@@ -739,6 +741,7 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
     uint32_t plen = 0, depth = 0, nnodes = 0;
     int32_t ncyc = 0;
     int64_t counter = 0, steps = 0;
+    uint32_t relaxed = 0;
 
     // FindCycleUtil (cycle_finder.cpp:231-243)
     {
@@ -821,6 +824,7 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
                     if (sl < 0) break;
                     if (s.lk[sl].val < maxl - blv + 1) {
                         s.lk[sl].val = maxl - blv + 1;
+                        ++relaxed;
                         uint64_t ins[4];
                         int isl[4];
                         const int ni = t.get_incomings_ii(u, uii, unv, rm, ins, isl, maxl);
@@ -848,6 +852,8 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
     o.ncyc = ncyc;
     o.nnodes = nnodes;
     o.steps = (uint32_t)(steps < 0xFFFFFFFFLL ? steps : 0xFFFFFFFFLL);
+    o.relax = relaxed;
+    o.locks = t.lsize;
     stat[i] = o;
 }
 
@@ -1179,7 +1185,7 @@ static std::vector<uint64_t> run_dls(mcaat_graph *g, const std::vector<uint64_t>
             for (uint64_t j = 0; j < n; ++j) ids[j] = cand[todo[b0 + j]];
             DevBuf<uint64_t> dids(n), dstk(n * cs), dvis(n * cv);
             DevBuf<int8_t> dres(n);
-            HIP_OK(hipMemcpyAsync(dids.p, ids.data(), 8 * n, hipMemcpyHostToDevice, st));
+            h2d(g->ctx, dids.p, ids.data(), 8 * n);
             constexpr int kDlsLanes = 4;
             hipLaunchKernelGGL(k_dls, dim3(grid_for(n, kDlsLanes)), dim3(64), 0, st, g->view(), dids.p, n, limit, dstk.p,
                                cs, dvis.p, cv, dres.p, kDlsLanes);
@@ -1322,7 +1328,8 @@ struct FcRunner {
         HIP_OK(hipStreamSynchronize(st));
         std::vector<uint64_t> pairs(np);
         if (np) {
-            HIP_OK(hipMemcpy(pairs.data(), dpairs.p, 8 * np, hipMemcpyDeviceToHost));
+            HIP_OK(hipMemcpyAsync(pairs.data(), dpairs.p, 8 * np, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipStreamSynchronize(st));
             std::sort(pairs.begin(), pairs.end(), [](uint64_t a, uint64_t b) {
                 return (uint32_t)a != (uint32_t)b ? (uint32_t)a < (uint32_t)b : a < b;
             });
@@ -1427,8 +1434,7 @@ struct FcRunner {
                 hipLaunchKernelGGL(k_findcycle, dim3((unsigned)Wl), dim3(64), fc_lds_bytes(caps), st, g->view(), dvis.p,
                                    dst.p, Wl, caps, prm, (uint64_t *)scratch.p, dstat.p);
                 LAUNCH_OK();
-                HIP_OK(hipMemcpyAsync(mine.st.data(), dstat.p, Wl * sizeof(FcStatus), hipMemcpyDeviceToHost, st));
-                HIP_OK(hipStreamSynchronize(st));
+                d2h(g->ctx, mine.st.data(), dstat.p, Wl * sizeof(FcStatus));
             }
             verbose_mark(g->ctx, "fc.round_kernel");
             static const bool verbose = getenv("MCAAT_VERBOSE") && getenv("MCAAT_VERBOSE")[0] == '1';
@@ -1438,13 +1444,18 @@ struct FcRunner {
                 const size_t top = std::min<size_t>(5, ord.size());
                 std::partial_sort(ord.begin(), ord.begin() + top, ord.end(),
                                   [&](uint64_t a, uint64_t b) { return mine.st[a].steps > mine.st[b].steps; });
-                uint64_t tot = 0;
-                for (const auto &x : mine.st) tot += x.steps;
-                fprintf(stderr, "[mcaat] fc: %llu searches, %llu steps; longest:", (unsigned long long)Wl,
-                        (unsigned long long)tot);
+                uint64_t tot = 0, trl = 0, mlk = 0;
+                for (const auto &x : mine.st) {
+                    tot += x.steps;
+                    trl += x.relax;
+                    mlk = std::max<uint64_t>(mlk, x.locks);
+                }
+                fprintf(stderr, "[mcaat] fc: %llu searches, %llu steps, %llu relaxations, max locks %llu; longest:",
+                        (unsigned long long)Wl, (unsigned long long)tot, (unsigned long long)trl,
+                        (unsigned long long)mlk);
                 for (size_t q = 0; q < top; ++q)
-                    fprintf(stderr, " %u (ncyc %d, nodes %u)", mine.st[ord[q]].steps, mine.st[ord[q]].ncyc,
-                            mine.st[ord[q]].nnodes);
+                    fprintf(stderr, " %u (relax %u, locks %u, ncyc %d, nodes %u)", mine.st[ord[q]].steps,
+                            mine.st[ord[q]].relax, mine.st[ord[q]].locks, mine.st[ord[q]].ncyc, mine.st[ord[q]].nnodes);
                 fprintf(stderr, "\n");
             }
             // this rank's finished searches (status 0) with cycles, in slot order; on one GPU
@@ -1472,8 +1483,8 @@ struct FcRunner {
                     hipLaunchKernelGGL(k_fc_gather, dim3((unsigned)sel.size()), dim3(256), 0, st, (uint64_t *)scratch.p,
                                        pa, caps, dsel.p, dno.p, dco.p, dn.p, dl.p, (uint64_t)sel.size());
                     LAUNCH_OK();
-                    HIP_OK(hipMemcpyAsync(mine.nodes.data(), dn.p, 8 * mine.nodes.size(), hipMemcpyDeviceToHost, st));
-                    HIP_OK(hipMemcpyAsync(mine.lens.data(), dl.p, 2 * mine.lens.size(), hipMemcpyDeviceToHost, st));
+                    d2h(g->ctx, mine.nodes.data(), dn.p, 8 * mine.nodes.size());
+                    d2h(g->ctx, mine.lens.data(), dl.p, 2 * mine.lens.size());
                     if (N == 1) {  // one GPU: slot i is start i
                         dj_keep.alloc(noff.back());
                         hipLaunchKernelGGL(k_fc_owner, dim3((unsigned)sel.size()), dim3(256), 0, st, dsel.p, dno.p,
@@ -1646,7 +1657,9 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
         }
         const uint64_t nc = read_counter(ctx, cnt.p);
         cand.resize(nc);
-        if (nc) HIP_OK(hipMemcpy(cand.data(), list.p, 8 * nc, hipMemcpyDeviceToHost));
+        if (nc) {
+            d2h(ctx, cand.data(), list.p, 8 * nc);
+        }
     }
     std::sort(cand.begin(), cand.end());
     if (comm) cand = gather_sorted(comm, cand);

@@ -133,6 +133,14 @@ struct mcaat_ctx {
     // tuning/test knobs (mcaat_set_knob): size limits that decide which code path a stage
     // takes, so small parity inputs can drive the branches that only large inputs reach
     std::map<std::string, int64_t> knobs;
+    // timing events reused across calls (stage and kernel timers take them from here)
+    std::vector<hipEvent_t> events;
+    // pinned bounce buffer for device-to-host result copies (mcaat::d2h). A copy straight into
+    // a large pageable vector pins it for the transfer, and freeing it afterwards (munmap) makes
+    // the driver evict and later restore the process's queues: the next step's first
+    // submission then waited ~20-28 ms on an idle GPU.
+    uint8_t *bounce = nullptr;
+    size_t bounce_bytes = 0;
 };
 
 struct mcaat_reads {
@@ -186,14 +194,66 @@ struct mcaat_cycles {
 
 namespace mcaat {
 
+inline hipEvent_t event_get(mcaat_ctx *ctx) {
+    if (!ctx->events.empty()) {
+        hipEvent_t e = ctx->events.back();
+        ctx->events.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    HIP_OK(hipEventCreate(&e));
+    return e;
+}
+inline void event_put(mcaat_ctx *ctx, hipEvent_t e) {
+    if (e) ctx->events.push_back(e);
+}
+
+// device -> host copy of n bytes through the ctx's pinned bounce buffer (stream-synchronous)
+inline void d2h(mcaat_ctx *ctx, void *dst, const void *src, size_t n) {
+    if (!n) return;
+    if (ctx->bounce_bytes < n) {
+        if (ctx->bounce) {
+            HIP_OK(hipStreamSynchronize(ctx->stream));
+            HIP_OK(hipHostFree(ctx->bounce));
+            ctx->bounce = nullptr;
+            ctx->bounce_bytes = 0;
+        }
+        const size_t want = std::max<size_t>(n, 4u << 20);
+        HIP_OK(hipHostMalloc((void **)&ctx->bounce, want, hipHostMallocDefault));
+        ctx->bounce_bytes = want;
+    }
+    HIP_OK(hipMemcpyAsync(ctx->bounce, src, n, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    memcpy(dst, ctx->bounce, n);
+}
+
+// host -> device copy of n bytes through the same bounce buffer (stream-synchronous)
+inline void h2d(mcaat_ctx *ctx, void *dst, const void *src, size_t n) {
+    if (!n) return;
+    if (ctx->bounce_bytes < n) {
+        if (ctx->bounce) {
+            HIP_OK(hipStreamSynchronize(ctx->stream));
+            HIP_OK(hipHostFree(ctx->bounce));
+            ctx->bounce = nullptr;
+            ctx->bounce_bytes = 0;
+        }
+        const size_t want = std::max<size_t>(n, 4u << 20);
+        HIP_OK(hipHostMalloc((void **)&ctx->bounce, want, hipHostMallocDefault));
+        ctx->bounce_bytes = want;
+    }
+    HIP_OK(hipStreamSynchronize(ctx->stream));  // an earlier copy out of the bounce buffer is done
+    memcpy(ctx->bounce, src, n);
+    HIP_OK(hipMemcpyAsync(dst, ctx->bounce, n, hipMemcpyHostToDevice, ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+}
+
 // event-bracketed stage timer on the ctx stream
 struct StageTimer {
     mcaat_ctx *ctx;
     std::vector<std::pair<const char *, hipEvent_t>> marks;
     explicit StageTimer(mcaat_ctx *c) : ctx(c) { ctx->stages.clear(); mark("begin"); }
     void mark(const char *name) {
-        hipEvent_t e;
-        HIP_OK(hipEventCreate(&e));
+        hipEvent_t e = event_get(ctx);
         HIP_OK(hipEventRecord(e, ctx->stream));
         marks.push_back({name, e});
     }
@@ -205,10 +265,11 @@ struct StageTimer {
             HIP_OK(hipEventElapsedTime(&ms, marks[i - 1].second, marks[i].second));
             ctx->stages.push_back({marks[i].first, (double)ms});
         }
-        for (auto &m : marks) (void)hipEventDestroy(m.second);
+        for (auto &m : marks) event_put(ctx, m.second);
         marks.clear();
     }
     ~StageTimer() {
+        // an unfinished timer (an error unwinding): its events may still be pending
         for (auto &m : marks) (void)hipEventDestroy(m.second);
     }
 };
@@ -220,8 +281,8 @@ struct KernelTimer {
     double bytes;
     hipEvent_t a = nullptr, b = nullptr;
     KernelTimer(mcaat_ctx *c, const char *n, double algorithmic_bytes) : ctx(c), name(n), bytes(algorithmic_bytes) {
-        HIP_OK(hipEventCreate(&a));
-        HIP_OK(hipEventCreate(&b));
+        a = event_get(ctx);
+        b = event_get(ctx);
         HIP_OK(hipEventRecord(a, ctx->stream));
     }
     void stop() {
@@ -233,8 +294,11 @@ struct KernelTimer {
         s.total_ms += ms;
         s.launches += 1;
         s.total_bytes += bytes;
+        event_put(ctx, a);
+        event_put(ctx, b);
+        a = b = nullptr;
     }
-    ~KernelTimer() {
+    ~KernelTimer() {  // not stopped (an error unwinding)
         if (a) (void)hipEventDestroy(a);
         if (b) (void)hipEventDestroy(b);
     }

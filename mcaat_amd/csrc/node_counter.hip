@@ -1173,6 +1173,13 @@ __global__ void k_items_fill(const uint64_t *offsets, uint64_t n_reads, int E, c
     }
 }
 
+__global__ void k_sum_u32(const uint32_t *v, uint64_t n, unsigned long long *sum) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    unsigned long long acc = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) acc += v[i];
+    block_add(sum, acc);
+}
+
 template <class T>
 void exclusive_scan(mcaat_ctx *ctx, const T *in, T *out, uint64_t n) {
     size_t tmp = 0;
@@ -1188,11 +1195,13 @@ void verbose_mark(mcaat_ctx *ctx, const char *what) {
     static const bool on = getenv("MCAAT_VERBOSE") && getenv("MCAAT_VERBOSE")[0] == '1';
     static double last = 0;
     if (!on) return;
-    (void)hipStreamSynchronize(ctx->stream);
     timespec ts;
     clock_gettime(CLOCK_MONOTONIC, &ts);
+    const double pre = ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
+    (void)hipStreamSynchronize(ctx->stream);
+    clock_gettime(CLOCK_MONOTONIC, &ts);
     const double now = ts.tv_sec * 1e3 + ts.tv_nsec / 1e6;
-    fprintf(stderr, "[mcaat] %-28s %10.2f ms\n", what, last ? now - last : 0.0);
+    fprintf(stderr, "[mcaat] %-28s %10.2f ms (sync %.2f)\n", what, last ? now - last : 0.0, now - pre);
     last = now;
 }
 
@@ -1251,10 +1260,17 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
         hipLaunchKernelGGL(k_items_fill, dim3(grid_for(r->n_reads, kBlock)), dim3(kBlock), 0, st, r->offsets.p,
                            r->n_reads, E, start.p, item_base.p, item_np.p);
         LAUNCH_OK();
-        std::vector<uint32_t> hn(n_items);
-        HIP_OK(hipMemcpyAsync(hn.data(), item_np.p, 4 * n_items, hipMemcpyDeviceToHost, st));
-        HIP_OK(hipStreamSynchronize(st));
-        for (uint32_t v : hn) n_occ += v;
+        {  // occurrences = sum of the items' positions (reduced on the device)
+            DevBuf<unsigned long long> socc(1);
+            HIP_OK(hipMemsetAsync(socc.p, 0, 8, st));
+            hipLaunchKernelGGL(k_sum_u32, dim3(grid_for(n_items, kBlock, (unsigned)ctx->n_cu * 8)), dim3(kBlock), 0, st,
+                               item_np.p, n_items, socc.p);
+            LAUNCH_OK();
+            unsigned long long h = 0;
+            HIP_OK(hipMemcpyAsync(&h, socc.p, 8, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipStreamSynchronize(st));
+            n_occ = h;
+        }
         src.item_base = item_base.p;
         src.item_np = item_np.p;
         src.n_items = n_items;
@@ -1367,8 +1383,8 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
             LAUNCH_OK();
         }
         exclusive_scan(ctx, (const uint64_t *)dtot.p, dfine.p, F + 1);
-        HIP_OK(hipMemcpyAsync(hfine.data(), dfine.p, 8 * (F + 1), hipMemcpyDeviceToHost, st));
         HIP_OK(hipMemcpyAsync(dcursor.p, dfine.p, 8 * (F + 1), hipMemcpyDeviceToDevice, st));
+        d2h(ctx, hfine.data(), dfine.p, 8 * (F + 1));
         kt.stop();
     }
     const uint64_t n_live = hfine[F];
@@ -1429,9 +1445,8 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
                 LAUNCH_OK();
                 std::vector<uint64_t> occ_h(n_ovf);
                 std::vector<uint32_t> parts_h(n_ovf);
-                HIP_OK(hipMemcpyAsync(occ_h.data(), occ.p, 8 * n_ovf, hipMemcpyDeviceToHost, st));
-                HIP_OK(hipMemcpyAsync(parts_h.data(), ovf_list.p, 4 * n_ovf, hipMemcpyDeviceToHost, st));
-                HIP_OK(hipStreamSynchronize(st));
+                d2h(ctx, occ_h.data(), occ.p, 8 * n_ovf);
+                d2h(ctx, parts_h.data(), ovf_list.p, 4 * n_ovf);
                 const uint64_t budget =
                     (uint64_t)std::max<int64_t>(1, knob(ctx, "nc.fallback_budget", 1LL << 30));  // occurrences per batch (table <= 32 GB)
                 DevBuf<unsigned long long> nn(1);
