@@ -284,7 +284,11 @@ void mcaat_reset_timing(mcaat_ctx *ctx);
  *   cf.fc_lock / cf.fc_relax / cf.fc_out   initial FindCycle scratch (grows on overflow)
  *   cf.fc_window       initial FindCycle speculation window
  *   cf.walk_budget     > 0: counter-driven peel walks of this many steps before the
- *                      list-ranking peel (default 0: the list-ranking peel alone) */
+ *                      list-ranking peel (default 0: the list-ranking peel alone)
+ *   sdbg.adj_lds       0: adjacency by per-edge directory searches in global memory
+ *                      (default 1: per-run target key ranges staged in LDS)
+ *   sdbg.adj_cap       largest target key range staged in LDS (default and maximum 1024;
+ *                      larger ranges take the global search) */
 int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value);
 
 #ifdef __cplusplus

@@ -521,24 +521,38 @@ struct __attribute__((aligned(16))) LockRec {
     uint32_t onpath;  // 1 while the node is on the search path (path nodes are distinct)
 };
 // Per search: the hot state read every step (path, neighbour frames, backtrack lengths) is in
-// the workgroup's LDS; the lock table, relax stack and outputs are in global scratch
-// (fc_per_search bytes per search: lock records, relax stack, output nodes, cycle lengths).
+// the workgroup's LDS; the lock table, relax stack, the frames' out_info words and the outputs
+// are in global scratch (fc_per_search bytes per search).
+// A frame keeps, per candidate, the lock slot and out_info word loaded when the frame was
+// built, and a relax record keeps its node's lock slot and in_info word, so a push or a
+// relaxation waits for one round of graph loads (every load of it issued together), not three.
+struct RelaxRec {
+    uint64_t ub;    // node << 16 | backtrack length
+    uint64_t ii;    // node's in_info word (0: no predecessors to visit)
+    int32_t slot;   // node's lock slot
+    uint32_t pad;
+};
 struct FcScratch {
     uint64_t *path;     // P      (LDS)
     int32_t *bl;        // P      (LDS)
     int32_t *psl;       // P      (LDS) lock slot of each path node
-    uint64_t *fr;       // 4P     (LDS)
-    uint8_t *frn;       // P      (LDS)
+    uint64_t *fr;       // 4P     (LDS) frame candidates
+    int32_t *frs;       // 4P     (LDS) their lock slots
+    uint8_t *frm;       // P      (LDS) live-candidate mask of each frame
     LockRec *lk;        // CL     (global)
-    uint64_t *relax;    // CR     (global)
+    RelaxRec *relax;    // CR     (global)
+    uint64_t *froi;     // 4P     (global) frame candidates' out_info words
     uint64_t *out;      // CO     (global)
     uint16_t *olen;     // CC     (global)
 };
+__host__ __device__ inline uint64_t fc_out_offset(const FcCaps &c) {
+    return (uint64_t)c.CL * 16 + (uint64_t)c.CR * sizeof(RelaxRec) + (uint64_t)c.P * 32;
+}
 __host__ __device__ inline uint64_t fc_per_search(const FcCaps &c) {
-    const uint64_t per = (uint64_t)c.CL * 16 + (uint64_t)c.CR * 8 + (uint64_t)c.CO * 8 + (uint64_t)c.CC * 2;
+    const uint64_t per = fc_out_offset(c) + (uint64_t)c.CO * 8 + (uint64_t)c.CC * 2;
     return (per + 255) & ~255ULL;
 }
-__host__ __device__ inline uint32_t fc_lds_bytes(const FcCaps &c) { return c.P * (8 + 32 + 4 + 4 + 1) + 16; }
+__host__ __device__ inline uint32_t fc_lds_bytes(const FcCaps &c) { return c.P * (8 + 4 + 4 + 32 + 16 + 1) + 16; }
 struct FcStatus {
     int32_t status;     // 0 ok, 1 lock table full, 2 relax stack full, 3 output full
     int32_t ncyc;
@@ -547,6 +561,11 @@ struct FcStatus {
     uint32_t relax;  // lock-relaxation expansions (diagnostics)
     uint32_t locks;  // lock-table entries at the end (diagnostics)
 };
+
+// x % 13 with 32-bit arithmetic (2^32 = 9 mod 13)
+__device__ __forceinline__ uint32_t mod13(uint64_t x) {
+    return (((uint32_t)(x >> 32) % 13u) * 9u + (uint32_t)x % 13u) % 13u;
+}
 
 struct FcThread {
     const GraphView &g;
@@ -598,106 +617,139 @@ struct FcThread {
             k = s.lk[h].key;
         }
     }
-    // _BackgroundCheck (cycle_finder.cpp:40-52) for up to 4 neighbours ids[0..n) of node, in
-    // that order (each is recorded in the footprint first). Every neighbour's multiplicity,
-    // visited bit (vis_bits: bit i for ids[i]) and first lock record are loaded together before
-    // the first insertion, so a step waits for one round of loads, not one per neighbour.
-    // ok[i] = the check passed.
-    __device__ void background_all(uint64_t node, uint64_t rm, const uint64_t *ids, int n, uint32_t vis_bits, int maxl,
-                                   bool *ok, int *slot = nullptr) {
-        uint16_t mu[4];
+    // _BackgroundCheck (cycle_finder.cpp:40-52) of neighbour x (multiplicity mu, visited bit
+    // q) after its footprint record: integer rm / mu > 500 rejects (mu = 0 as well: the
+    // device's division by zero is all ones)
+    __device__ static bool background_ok(uint64_t node, uint64_t x, uint64_t rm, uint32_t mu, bool q) {
+        if (q) return false;
+        if (mu == 0 || rm / mu > 500) return false;
+        return node != x;
+    }
+
+    // Frame of node (out_info oi, node valid): _GetOutgoings(node, set, rm) in the libstdc++
+    // unordered_set insertion order, each candidate with its lock slot and out_info word. The
+    // successors are the consecutive ids [lo, lo + cnt): their valid and visited windows and,
+    // per id, the multiplicity, out_info word and first lock record are one round of loads.
+    // Written to frame d; returns its live mask.
+    __device__ uint8_t build_frame(uint64_t node, uint64_t oi, uint64_t rm, int maxl, uint32_t d) {
+        const uint64_t nw = (g.D + 63) / 64;
+        const uint64_t lo = oi & kIdxMask;
+        const int cnt = __popc((unsigned)(oi >> kIdxBits) & 0xF);
+        if (cnt == 0) return 0;
+        const uint64_t v0 = g.valid[this_word(lo, nw)], v1 = g.valid[next_word(lo, nw)];
+        const uint64_t q0 = visited[this_word(lo, nw)], q1 = visited[next_word(lo, nw)];
+        uint32_t mu[4];
+        uint64_t no[4], k0[4];
         uint32_t h0[4];
-        uint64_t k0[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-            if (i < n) {
-                mu[i] = g.mult[ids[i]];
-                h0[i] = (uint32_t)(mix64(ids[i]) & (c.CL - 1));
+            mu[i] = 0;
+            no[i] = 0;
+            h0[i] = 0;
+            k0[i] = 0;
+            if (i < cnt) {
+                const uint64_t x = lo + i;
+                mu[i] = g.mult[x];
+                no[i] = g.out_info[x];
+                h0[i] = (uint32_t)(mix64(x) & (c.CL - 1));
                 k0[i] = s.lk[h0[i]].key;
             }
         }
+        const uint32_t vb = bits16(v0, v1, lo) & ((1u << cnt) - 1);
+        const uint32_t qb = bits16(q0, q1, lo);
+        uint64_t fx[4] = {0, 0, 0, 0}, fo[4] = {0, 0, 0, 0};
+        int32_t fs[4] = {0, 0, 0, 0};
+        uint32_t fm[4] = {0, 0, 0, 0};
         uint32_t wr[4];
-        int nwr = 0;
+        int nwr = 0, n = 0;
+        // valid successors in descending id order (OutgoingEdges), each recorded in the
+        // footprint before its check
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if (i >= n) break;
-            ok[i] = false;
-            const int sl = lock_from(ids[i], maxl, h0[i], k0[i], wr, nwr);
-            if (slot) slot[i] = sl;
+        for (int i = 3; i >= 0; --i) {
+            if (i >= cnt || !((vb >> i) & 1)) continue;
+            const uint64_t x = lo + i;
+            const int sl = lock_from(x, maxl, h0[i], k0[i], wr, nwr);
             if (sl < 0) continue;
-            if ((vis_bits >> i) & 1) continue;
-            if (rm / mu[i] > 500) continue;
-            if (node == ids[i]) continue;
-            ok[i] = true;
-        }
-    }
-    // _GetOutgoings(node, set, rm) + libstdc++ unordered_set insertion order. The successors
-    // are the consecutive ids [lo, lo + cnt): their valid and visited bits are one window each.
-    __device__ int get_outgoings(uint64_t node, uint64_t rm, uint64_t *f, int maxl) {
-        return get_outgoings_oi(node, g.out_info[node], ((g.valid[node >> 6] >> (node & 63)) & 1) != 0, rm, f, maxl);
-    }
-    // the same with node's out_info word and validity already loaded (a frame candidate's
-    // out_info is loaded together with its lock record, one round trip earlier)
-    __device__ int get_outgoings_oi(uint64_t node, uint64_t oi, bool node_valid, uint64_t rm, uint64_t *f, int maxl) {
-        const uint64_t nw = (g.D + 63) / 64;
-        const uint64_t lo = oi & kIdxMask;
-        const uint32_t cnt = __popc((unsigned)(oi >> kIdxBits) & 0xF);
-        if (cnt == 0 || !node_valid) return 0;
-        const uint32_t vb = bits16(g.valid[this_word(lo, nw)], g.valid[next_word(lo, nw)], lo) & ((1u << cnt) - 1);
-        const uint32_t qb = bits16(visited[this_word(lo, nw)], visited[next_word(lo, nw)], lo);
-        // valid successors in descending id order (OutgoingEdges)
-        uint64_t ids[4];
-        uint32_t vis = 0;
-        int m = 0;
-        for (int i = (int)cnt - 1; i >= 0; --i)
-            if ((vb >> i) & 1) {
-                vis |= ((qb >> i) & 1) << m;
-                ids[m++] = lo + i;
-            }
-        bool ok[4];
-        background_all(node, rm, ids, m, vis, maxl, ok);
-        int n = 0;
-        for (int i = 0; i < m; ++i) {
-            if (!ok[i]) continue;
-            const uint64_t x = ids[i];
-            // 13 buckets, hash(x)=x: before the first element of x's bucket, else at front
+            if (!background_ok(node, x, rm, mu[i], (qb >> i) & 1)) continue;
+            // 13 buckets, hash(x) = x: before the first element of x's bucket, else at front
+            const uint32_t xm = mod13(x);
             int pos = 0;
-            for (int j = 0; j < n; ++j)
-                if (f[j] % 13 == x % 13) { pos = j; break; }
-            for (int j = n; j > pos; --j) f[j] = f[j - 1];
-            f[pos] = x;
+            bool hit = false;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (!hit && j < n && fm[j] == xm) { pos = j; hit = true; }
+#pragma unroll
+            for (int j = 3; j > 0; --j)
+                if (j <= n && j > pos) { fx[j] = fx[j - 1]; fo[j] = fo[j - 1]; fs[j] = fs[j - 1]; fm[j] = fm[j - 1]; }
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (j == pos) { fx[j] = x; fo[j] = no[i]; fs[j] = sl; fm[j] = xm; }
             ++n;
         }
-        return n;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (j < n) {
+                s.fr[4 * d + j] = fx[j];
+                s.frs[4 * d + j] = fs[j];
+                s.froi[4 * d + j] = fo[j];
+            }
+        return (uint8_t)((1u << n) - 1);
     }
-    // valid predecessors (ascending ids: positions of the 16-bit mask inside the group at lo)
-    // (node's in_info word and validity word loaded by the caller, beside its lock record)
-    __device__ int get_incomings_ii(uint64_t node, uint64_t ii, uint64_t nv, uint64_t rm, uint64_t *f, int *fslot,
-                                    int maxl) {
+
+    // valid predecessors of node (in_info ii; node valid) passing the background check, in
+    // ascending ids, with their lock slots and in_info words; one round of loads as above.
+    __device__ int preds_of(uint64_t node, uint64_t ii, uint64_t rm, uint64_t *f, int32_t *fs, uint64_t *fii, int maxl) {
         const uint64_t nw = (g.D + 63) / 64;
         const uint64_t lo = ii & kIdxMask;
-        const uint32_t mask = (uint32_t)(ii >> kIdxBits) & 0xFFFF;
-        if (mask == 0 || !((nv >> (node & 63)) & 1)) return 0;
-        uint32_t vb = bits16(g.valid[this_word(lo, nw)], g.valid[next_word(lo, nw)], lo) & mask;
-        const uint32_t qb = bits16(visited[this_word(lo, nw)], visited[next_word(lo, nw)], lo);
-        uint64_t ids[4];
-        uint32_t vis = 0;
+        uint32_t mask = (uint32_t)(ii >> kIdxBits) & 0xFFFF;
+        if (mask == 0) return 0;
+        // positions of the mask (an in-group holds one edge per source node: at most 4)
+        int pj[4];
         int m = 0;
-        while (vb && m < 4) {
-            const int j = __ffs(vb) - 1;
-            vb &= vb - 1;
-            vis |= ((qb >> j) & 1) << m;
-            ids[m++] = lo + j;
-        }
-        bool ok[4];
-        int sl[4];
-        background_all(node, rm, ids, m, vis, maxl, ok, sl);
-        int n = 0;
-        for (int i = 0; i < m; ++i)
-            if (ok[i]) {
-                fslot[n] = sl[i];
-                f[n++] = ids[i];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            pj[q] = 0;
+            if (mask) {
+                pj[q] = __ffs(mask) - 1;
+                mask &= mask - 1;
+                m = q + 1;
             }
+        }
+        const uint64_t v0 = g.valid[this_word(lo, nw)], v1 = g.valid[next_word(lo, nw)];
+        const uint64_t q0 = visited[this_word(lo, nw)], q1 = visited[next_word(lo, nw)];
+        uint32_t mu[4];
+        uint64_t ni[4], k0[4];
+        uint32_t h0[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            mu[q] = 0;
+            ni[q] = 0;
+            h0[q] = 0;
+            k0[q] = 0;
+            if (q < m) {
+                const uint64_t x = lo + pj[q];
+                mu[q] = g.mult[x];
+                ni[q] = g.in_info[x];
+                h0[q] = (uint32_t)(mix64(x) & (c.CL - 1));
+                k0[q] = s.lk[h0[q]].key;
+            }
+        }
+        const uint32_t vb = bits16(v0, v1, lo);
+        const uint32_t qb = bits16(q0, q1, lo);
+        uint32_t wr[4];
+        int nwr = 0, n = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (q >= m || !((vb >> pj[q]) & 1)) continue;
+            const uint64_t x = lo + pj[q];
+            const int sl = lock_from(x, maxl, h0[q], k0[q], wr, nwr);
+            if (sl < 0) continue;
+            if (!background_ok(node, x, rm, mu[q], (qb >> pj[q]) & 1)) continue;
+            f[n] = x;
+            fs[n] = sl;
+            fii[n] = ni[q];
+            ++n;
+        }
         return n;
     }
 };
@@ -709,7 +761,8 @@ struct FcThread {
 #endif
 // One search per workgroup of one wave: the search itself is sequential (lane 0); the other
 // lanes clear its lock table first. Its path and frames live in LDS (fc_lds_bytes), so every
-// step touches global memory only for the graph, the visited bits and the lock table.
+// step touches global memory only for the graph, the visited bits, the lock table and the
+// frames' out_info words.
 // (Per-step latency, not occupancy, bounds this kernel: at C3 ~1.5K steps per search, each a
 // chain of dependent loads.)
 __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, const uint64_t *visited, const uint64_t *starts,
@@ -721,15 +774,17 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
     uint8_t *base = (uint8_t *)sbase + i * fc_per_search(caps);
     FcScratch s;
     s.lk = (LockRec *)base; base += (uint64_t)caps.CL * 16;
-    s.relax = (uint64_t *)base; base += (uint64_t)caps.CR * 8;
+    s.relax = (RelaxRec *)base; base += (uint64_t)caps.CR * sizeof(RelaxRec);
+    s.froi = (uint64_t *)base; base += (uint64_t)caps.P * 32;
     s.out = (uint64_t *)base; base += (uint64_t)caps.CO * 8;
     s.olen = (uint16_t *)base;
     unsigned char *lb = fc_lds;
     s.path = (uint64_t *)lb; lb += (uint64_t)caps.P * 8;
     s.fr = (uint64_t *)lb; lb += (uint64_t)caps.P * 32;
+    s.frs = (int32_t *)lb; lb += (uint64_t)caps.P * 16;
     s.bl = (int32_t *)lb; lb += (uint64_t)caps.P * 4;
     s.psl = (int32_t *)lb; lb += (uint64_t)caps.P * 4;
-    s.frn = lb;
+    s.frm = lb;
     for (uint32_t j = threadIdx.x; j < caps.CL; j += blockDim.x) s.lk[j].key = kNone;
     __syncthreads();  // the workgroup is one wave: lane 0 sees every lane's clear
     if (threadIdx.x != 0) return;
@@ -753,7 +808,11 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
         s.psl[plen] = sl;
     }
     s.path[plen++] = st;
-    s.frn[0] = (uint8_t)t.get_outgoings(st, rm, s.fr, maxl);
+    {
+        const uint64_t oi = g.out_info[st];
+        const bool vst = (g.valid[st >> 6] >> (st & 63)) & 1;
+        s.frm[0] = vst ? t.build_frame(st, oi, rm, maxl, 0) : 0;
+    }
     s.bl[0] = maxl;
     depth = 1;
 
@@ -761,14 +820,27 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
     while (depth > 0 && t.status == 0) {
         if (++steps > prm.step_cap) break;
         const uint32_t top = depth - 1;
-        uint64_t N[4];
-        const int nN = s.frn[top];
-        for (int j = 0; j < nN; ++j) N[j] = s.fr[4 * top + j];
-        // the first candidate is the one usually pushed: its out_info is loaded now, beside its
-        // lock record (frame entries are valid edges)
-        const uint64_t oi0 = nN > 0 ? g.out_info[N[0]] : 0;
+        const uint32_t live = s.frm[top];
+        // the live candidates, their lock values and out_info words: one round of loads
+        uint64_t N[4], OI[4];
+        int32_t SL[4], VAL[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            N[j] = 0;
+            OI[j] = 0;
+            SL[j] = 0;
+            VAL[j] = 0;
+            if ((live >> j) & 1) {
+                N[j] = s.fr[4 * top + j];
+                SL[j] = s.frs[4 * top + j];
+                OI[j] = s.froi[4 * top + j];
+                VAL[j] = s.lk[SL[j]].val;
+            }
+        }
         bool flag = true, pushed = false;
-        for (int j = 0; j < nN; ++j) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (!((live >> j) & 1)) continue;
             const uint64_t x = N[j];
             if (x == st) {
                 s.bl[top] = 1;
@@ -780,61 +852,66 @@ __global__ void __launch_bounds__(64, MCAAT_FC_MINW) k_findcycle(GraphView g, co
                     counter += 1;
                     if (counter >= prm.cluster) { ncyc = 0; nnodes = 0; flag = false; }
                 }
-            } else {
-                const int sl = t.lock_slot(x, maxl);
-                if (sl < 0) break;
-                if ((int)plen < s.lk[sl].val) {
-                    // erase x from the top frame (order of the rest is kept)
-                    int m = s.frn[top], q = 0;
-                    for (int r = 0; r < m; ++r)
-                        if (s.fr[4 * top + r] != x) s.fr[4 * top + q++] = s.fr[4 * top + r];
-                    s.frn[top] = (uint8_t)q;
-                    s.psl[plen] = sl;
-                    s.path[plen++] = x;
-                    s.bl[depth] = maxl;
-                    s.lk[sl].val = (int)plen;
-                    s.lk[sl].onpath = 1;
-                    s.frn[depth] = (uint8_t)(j == 0 ? t.get_outgoings_oi(x, oi0, true, rm, s.fr + 4 * depth, maxl)
-                                                    : t.get_outgoings(x, rm, s.fr + 4 * depth, maxl));
-                    ++depth;
-                    flag = false;
-                    pushed = true;
-                    break;
-                }
+            } else if ((int)plen < VAL[j]) {
+                // erase x from the top frame (the rest keep their order) and push it
+                const int sl = SL[j];
+                s.frm[top] = (uint8_t)(live & ~(1u << j));
+                s.psl[plen] = sl;
+                s.path[plen++] = x;
+                s.bl[depth] = maxl;
+                s.lk[sl].val = (int)plen;
+                s.lk[sl].onpath = 1;
+                s.frm[depth] = t.build_frame(x, OI[j], rm, maxl, depth);
+                ++depth;
+                flag = false;
+                pushed = true;
+                break;
             }
         }
         if (t.status) break;
         if (flag) {
             --depth;
             const uint64_t v = s.path[--plen];
-            if (s.psl[plen] >= 0) s.lk[s.psl[plen]].onpath = 0;
+            const int vsl = s.psl[plen];
+            if (vsl >= 0) s.lk[vsl].onpath = 0;
             const int b = s.bl[depth];
             if (depth > 0) s.bl[depth - 1] = min(s.bl[depth - 1], b);
             if (b < maxl) {
                 // lock relaxation (cycle_finder.cpp:191-209); its fixpoint does not depend on
                 // the processing order, so a plain stack is used.
+                const uint64_t vii = g.in_info[v];
+                const bool vv = (g.valid[v >> 6] >> (v & 63)) & 1;
                 uint32_t rs = 0;
-                s.relax[rs++] = (v << 16) | (uint64_t)b;
+                {
+                    RelaxRec r0;
+                    r0.ub = (v << 16) | (uint64_t)b;
+                    r0.ii = vv ? vii : 0;  // an invalid node has no predecessors to visit
+                    r0.slot = vsl;
+                    r0.pad = 0;
+                    s.relax[rs++] = r0;
+                }
                 while (rs > 0 && t.status == 0) {
-                    const uint64_t e = s.relax[--rs];
-                    const int blv = (int)(e & 0xFFFF);
-                    const uint64_t u = e >> 16;
-                    const uint64_t uii = g.in_info[u], unv = g.valid[u >> 6];  // beside the lock probe
-                    const int sl = t.lock_slot(u, maxl);
+                    const RelaxRec e = s.relax[--rs];
+                    const int blv = (int)(e.ub & 0xFFFF);
+                    const uint64_t u = e.ub >> 16;
+                    const int sl = e.slot;
                     if (sl < 0) break;
                     if (s.lk[sl].val < maxl - blv + 1) {
                         s.lk[sl].val = maxl - blv + 1;
                         ++relaxed;
-                        uint64_t ins[4];
-                        int isl[4];
-                        const int ni = t.get_incomings_ii(u, uii, unv, rm, ins, isl, maxl);
+                        uint64_t ins[4], iii[4];
+                        int32_t isl[4];
+                        const int ni = t.preds_of(u, e.ii, rm, ins, isl, iii, maxl);
                         for (int j = 0; j < ni; ++j) {
                             // std::find(path, ins[j]): the path flag of its lock record
-                            const bool on_path = s.lk[isl[j]].onpath != 0;
-                            if (!on_path) {
-                                if (rs >= caps.CR) { t.status = 2; break; }
-                                s.relax[rs++] = (ins[j] << 16) | (uint64_t)(blv + 1);
-                            }
+                            if (s.lk[isl[j]].onpath) continue;
+                            if (rs >= caps.CR) { t.status = 2; break; }
+                            RelaxRec r;
+                            r.ub = (ins[j] << 16) | (uint64_t)(blv + 1);
+                            r.ii = iii[j];
+                            r.slot = isl[j];
+                            r.pad = 0;
+                            s.relax[rs++] = r;
                         }
                     }
                 }
@@ -865,8 +942,8 @@ __global__ void k_fc_gather(const uint64_t *sbase, uint64_t per_al, FcCaps caps,
     if (q >= nsel) return;
     const uint64_t i = sel[q];
     const uint8_t *base = (const uint8_t *)sbase + i * per_al;
-    const uint64_t *out = (const uint64_t *)(base + (uint64_t)caps.CL * 16 + (uint64_t)caps.CR * 8);
-    const uint16_t *olen = (const uint16_t *)(base + (uint64_t)caps.CL * 16 + (uint64_t)caps.CR * 8 + (uint64_t)caps.CO * 8);
+    const uint64_t *out = (const uint64_t *)(base + fc_out_offset(caps));
+    const uint16_t *olen = (const uint16_t *)(base + fc_out_offset(caps) + (uint64_t)caps.CO * 8);
     const uint64_t nn = node_off[q + 1] - node_off[q];
     const uint64_t nc = cyc_off[q + 1] - cyc_off[q];
     for (uint64_t j = threadIdx.x; j < nn; j += blockDim.x) nodes[node_off[q] + j] = out[j];

@@ -116,6 +116,78 @@ __global__ void __launch_bounds__(kBlock) k_adjacency(const uint64_t *key, uint6
     }
 }
 
+// The same for the block's run of kAdjB consecutive edges, with the target searches in LDS.
+// Sources are sorted, so for each W the targets (W, s[1..k-1]) of the run lie in one key
+// range, bounded by the run's first and last source; the four ranges (~kAdjB/4 keys each)
+// are loaded once, coalesced, and every search and degree scan of the run reads LDS. A range
+// larger than kAdjCap (skewed key spaces) falls back to the directory search in global memory.
+constexpr int kAdjB = 2048;
+constexpr int kAdjCap = 1024;
+__global__ void __launch_bounds__(kBlock) k_adjacency_lds(const uint64_t *key, uint64_t D, int k, const uint64_t *dir,
+                                                          int shift, uint32_t cap, uint64_t *out_info,
+                                                          uint64_t *in_info) {
+    __shared__ uint64_t rng[4][kAdjCap];
+    __shared__ uint64_t rlo[4];
+    __shared__ uint32_t rn[4];
+    const uint64_t e0 = (uint64_t)blockIdx.x * kAdjB;
+    if (e0 >= D) return;
+    const uint64_t e1 = e0 + kAdjB < D ? e0 + kAdjB : D;
+    const uint64_t top = (uint64_t)1 << (2 * (k - 1));
+    if (threadIdx.x < 4) {
+        const uint64_t W = threadIdx.x;
+        const uint64_t a = (W * top) | (key[e0] >> 4), b = (W * top) | (key[e1 - 1] >> 4);
+        const uint64_t lo = lower_bound_dir(key, dir, shift, a << 2);
+        const uint64_t qb = (b + 1) << 2;  // past the key space when b is the last label
+        const uint64_t hi = qb >> (2 * (k + 1)) ? D : lower_bound_dir(key, dir, shift, qb);
+        rlo[W] = lo;
+        rn[W] = hi - lo <= (uint64_t)cap ? (uint32_t)(hi - lo) : 0xFFFFFFFFu;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int W = 0; W < 4; ++W) {
+        const uint32_t n = rn[W];
+        if (n == 0xFFFFFFFFu) continue;
+        for (uint32_t i = threadIdx.x; i < n; i += kBlock) rng[W][i] = key[rlo[W] + i];
+    }
+    __syncthreads();
+    for (uint64_t e = e0 + threadIdx.x; e < e1; e += kBlock) {
+        const uint64_t K = key[e];
+        const uint64_t W = K & 3, R = K >> 2;
+        const uint64_t Rt = (W << (2 * (k - 1))) | (R >> 2);
+        uint64_t lo;
+        unsigned m = 0;
+        const uint32_t n = rn[W];
+        if (n != 0xFFFFFFFFu) {
+            const uint64_t *r = rng[W];
+            const uint64_t q = Rt << 2;
+            uint32_t a = 0, b = n;
+            while (a < b) {
+                const uint32_t mid = (a + b) >> 1;
+                if (r[mid] < q) a = mid + 1; else b = mid;
+            }
+            lo = rlo[W] + a;
+            // the range holds every key below (last target + 1) << 2: all of Rt's edges
+            for (uint32_t i = a; i < n && (r[i] >> 2) == Rt; ++i) m |= 1u << (r[i] & 3);
+        } else {
+            lo = lower_bound_dir(key, dir, shift, Rt << 2);
+            for (uint64_t i = lo; i < D && (key[i] >> 2) == Rt; ++i) m |= 1u << (key[i] & 3);
+        }
+        out_info[e] = lo | ((uint64_t)m << kIdxBits);
+        if (!m) continue;
+        const uint64_t gk = K >> 4;
+        uint64_t gs = e;
+        while (gs > 0 && (key[gs - 1] >> 4) == gk) --gs;
+        unsigned pm = 0;
+        int j = 0;
+        for (uint64_t i = gs; i < D && (key[i] >> 4) == gk && j < 16; ++i, ++j)
+            if ((key[i] & 3) == W) pm |= 1u << j;
+        if ((uint64_t)(__ffs(pm) - 1) != e - gs) continue;
+        const uint64_t v = gs | ((uint64_t)pm << kIdxBits);
+        const int deg = __popc(m);
+        for (int r = 0; r < deg; ++r) in_info[lo + r] = v;
+    }
+}
+
 __global__ void __launch_bounds__(kBlock) k_valid_init(uint64_t *valid, uint64_t D) {
     const uint64_t nw = (D + 63) / 64;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -649,8 +721,14 @@ void sdbg_finish(mcaat_ctx *ctx, mcaat_graph *g) {
         // searches' loads share lines across the wave (a thread-per-run merge walk that
         // loses this was 5x slower)
         HIP_OK(hipMemsetAsync(g->in_info.p, 0, 8 * D, st));
-        hipLaunchKernelGGL(k_adjacency, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, g->key.p, D, k, dir.p, shift,
-                           g->out_info.p, g->in_info.p);
+        if (knob(ctx, "sdbg.adj_lds", 1)) {
+            const uint32_t cap = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(kAdjCap, knob(ctx, "sdbg.adj_cap", kAdjCap)));
+            hipLaunchKernelGGL(k_adjacency_lds, dim3((unsigned)((D + kAdjB - 1) / kAdjB)), dim3(kBlock), 0, st, g->key.p,
+                               D, k, dir.p, shift, cap, g->out_info.p, g->in_info.p);
+        } else {
+            hipLaunchKernelGGL(k_adjacency, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, g->key.p, D, k, dir.p,
+                               shift, g->out_info.p, g->in_info.p);
+        }
         LAUNCH_OK();
         kt.stop();
     }

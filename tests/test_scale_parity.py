@@ -56,6 +56,11 @@ KNOBS = {
     # (nearly) unbounded walks that finish every chain themselves
     "peel_walk1": {"cf.walk_budget": 1},
     "peel_kahn": {"cf.walk_budget": 1 << 30},
+    # adjacency: per-edge global directory searches, and the LDS-range kernel with every range
+    # (cap 0) or the larger ones (cap 200) sent to its global fallback
+    "adj_global": {"sdbg.adj_lds": 0},
+    "adj_cap0": {"sdbg.adj_cap": 0},
+    "adj_cap200": {"sdbg.adj_cap": 200},
 }
 
 _oracle_cache = {}
