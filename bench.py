@@ -404,6 +404,10 @@ def main() -> int:
             local = local % max(1, torch.cuda.device_count())
             torch.cuda.set_device(local)
         ctx = M.Context(local)
+        # tuning aid: MCAAT_KNOBS="name=value,..." sets path-selecting knobs (mcaat_set_knob)
+        for kv in filter(None, os.environ.get("MCAAT_KNOBS", "").split(",")):
+            kn, kval = kv.split("=")
+            ctx.set_knob(kn.strip(), int(kval))
         reads = M.Reads.synth_range(ctx, spec, first, count) if sharded else M.Reads.synth(ctx, spec)
     comm = None
     if native and not args.dry_run:

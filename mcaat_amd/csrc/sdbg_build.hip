@@ -116,17 +116,21 @@ __global__ void __launch_bounds__(kBlock) k_adjacency(const uint64_t *key, uint6
     }
 }
 
-// The same for the block's run of kAdjB consecutive edges, with the target searches in LDS.
+// The same for the block's run of kAdjB consecutive edges, with every search and scan in LDS.
 // Sources are sorted, so for each W the targets (W, s[1..k-1]) of the run lie in one key
 // range, bounded by the run's first and last source; the four ranges (~kAdjB/4 keys each)
-// are loaded once, coalesced, and every search and degree scan of the run reads LDS. A range
-// larger than kAdjCap (skewed key spaces) falls back to the directory search in global memory.
+// and the run's own keys (with a group-sized halo on each side, for the in-group scans) are
+// loaded once, coalesced. A range larger than cap (skewed key spaces) falls back to the
+// directory search in global memory.
 constexpr int kAdjB = 2048;
+constexpr int kAdjT = 1024;   // threads per run: two edges each
 constexpr int kAdjCap = 1024;
-__global__ void __launch_bounds__(kBlock) k_adjacency_lds(const uint64_t *key, uint64_t D, int k, const uint64_t *dir,
-                                                          int shift, uint32_t cap, uint64_t *out_info,
-                                                          uint64_t *in_info) {
+constexpr int kAdjHalo = 16;  // an in-group holds at most 16 edges
+__global__ void __launch_bounds__(kAdjT) k_adjacency_lds(const uint64_t *key, uint64_t D, int k, const uint64_t *dir,
+                                                         int shift, uint32_t cap, uint64_t *out_info,
+                                                         uint64_t *in_info) {
     __shared__ uint64_t rng[4][kAdjCap];
+    __shared__ uint64_t own[kAdjB + 2 * kAdjHalo];
     __shared__ uint64_t rlo[4];
     __shared__ uint32_t rn[4];
     const uint64_t e0 = (uint64_t)blockIdx.x * kAdjB;
@@ -142,16 +146,24 @@ __global__ void __launch_bounds__(kBlock) k_adjacency_lds(const uint64_t *key, u
         rlo[W] = lo;
         rn[W] = hi - lo <= (uint64_t)cap ? (uint32_t)(hi - lo) : 0xFFFFFFFFu;
     }
+    // own[j] = key[e0 - kAdjHalo + j]; outside [0, D): a value no group matches
+    const uint64_t olo = e0 >= (uint64_t)kAdjHalo ? e0 - kAdjHalo : 0;
+    const uint32_t opad = (uint32_t)(e0 - olo);  // halo entries actually before e0
+    for (uint32_t j = threadIdx.x; j < kAdjB + 2 * kAdjHalo; j += kAdjT) {
+        const uint64_t x = e0 + j - kAdjHalo;  // wraps below 0 for the first run
+        own[j] = (j >= (uint32_t)kAdjHalo - opad && x < D) ? key[x] : ~0ULL;
+    }
     __syncthreads();
 #pragma unroll
     for (int W = 0; W < 4; ++W) {
         const uint32_t n = rn[W];
         if (n == 0xFFFFFFFFu) continue;
-        for (uint32_t i = threadIdx.x; i < n; i += kBlock) rng[W][i] = key[rlo[W] + i];
+        for (uint32_t i = threadIdx.x; i < n; i += kAdjT) rng[W][i] = key[rlo[W] + i];
     }
     __syncthreads();
-    for (uint64_t e = e0 + threadIdx.x; e < e1; e += kBlock) {
-        const uint64_t K = key[e];
+    for (uint64_t e = e0 + threadIdx.x; e < e1; e += kAdjT) {
+        const uint32_t oe = (uint32_t)(e - e0) + kAdjHalo;
+        const uint64_t K = own[oe];
         const uint64_t W = K & 3, R = K >> 2;
         const uint64_t Rt = (W << (2 * (k - 1))) | (R >> 2);
         uint64_t lo;
@@ -174,15 +186,18 @@ __global__ void __launch_bounds__(kBlock) k_adjacency_lds(const uint64_t *key, u
         }
         out_info[e] = lo | ((uint64_t)m << kIdxBits);
         if (!m) continue;
+        // e's in-group (labels sharing s[1..k-1], key >> 4) from the staged keys; a group cut
+        // by the halo's edge cannot occur (groups hold at most kAdjHalo edges) except at the
+        // ends of the key array, where the ~0 fill stops the scans
         const uint64_t gk = K >> 4;
-        uint64_t gs = e;
-        while (gs > 0 && (key[gs - 1] >> 4) == gk) --gs;
+        uint32_t gs = oe;
+        while (gs > 0 && (own[gs - 1] >> 4) == gk) --gs;
         unsigned pm = 0;
         int j = 0;
-        for (uint64_t i = gs; i < D && (key[i] >> 4) == gk && j < 16; ++i, ++j)
-            if ((key[i] & 3) == W) pm |= 1u << j;
-        if ((uint64_t)(__ffs(pm) - 1) != e - gs) continue;
-        const uint64_t v = gs | ((uint64_t)pm << kIdxBits);
+        for (uint32_t q = gs; q < (uint32_t)(kAdjB + 2 * kAdjHalo) && (own[q] >> 4) == gk && j < 16; ++q, ++j)
+            if ((own[q] & 3) == W) pm |= 1u << j;
+        if ((uint32_t)(__ffs(pm) - 1) != oe - gs) continue;
+        const uint64_t v = (e0 - kAdjHalo + gs) | ((uint64_t)pm << kIdxBits);
         const int deg = __popc(m);
         for (int r = 0; r < deg; ++r) in_info[lo + r] = v;
     }
@@ -723,7 +738,7 @@ void sdbg_finish(mcaat_ctx *ctx, mcaat_graph *g) {
         HIP_OK(hipMemsetAsync(g->in_info.p, 0, 8 * D, st));
         if (knob(ctx, "sdbg.adj_lds", 1)) {
             const uint32_t cap = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(kAdjCap, knob(ctx, "sdbg.adj_cap", kAdjCap)));
-            hipLaunchKernelGGL(k_adjacency_lds, dim3((unsigned)((D + kAdjB - 1) / kAdjB)), dim3(kBlock), 0, st, g->key.p,
+            hipLaunchKernelGGL(k_adjacency_lds, dim3((unsigned)((D + kAdjB - 1) / kAdjB)), dim3(kAdjT), 0, st, g->key.p,
                                D, k, dir.p, shift, cap, g->out_info.p, g->in_info.p);
         } else {
             hipLaunchKernelGGL(k_adjacency, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, g->key.p, D, k, dir.p,
