@@ -147,8 +147,8 @@ __global__ void __launch_bounds__(kBlock) k_peel_mark(GraphView g, PeelArrays pa
 // rulers: unary nodes without a unary predecessor (chain heads) plus 1/64 of the others;
 // compacted into list by wave ballots, one cursor atomic per 4096-edge tile
 constexpr int kTileJ = 16;  // 64-edge words per wave per tile
-__global__ void __launch_bounds__(kBlock) k_peel_rulers(uint64_t D, PeelArrays pa, uint64_t *list,
-                                                        unsigned long long *cursor) {
+__global__ void __launch_bounds__(kBlock) k_peel_rulers(uint64_t D, PeelArrays pa, uint64_t ruler_mask,
+                                                        uint64_t *list, unsigned long long *cursor) {
     __shared__ uint32_t wcnt[kBlock / 64];
     __shared__ unsigned long long tbase;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -161,7 +161,7 @@ __global__ void __launch_bounds__(kBlock) k_peel_rulers(uint64_t D, PeelArrays p
             const uint64_t e = t0 + (uint64_t)j * kBlock + threadIdx.x;
             bool r = false;
             if (e < D && kind_chain(pa.kind[e])) {
-                r = pa.upred[e] == 0 || (mix64(e ^ 0x5eed) & 63) == 0;
+                r = pa.upred[e] == 0 || (mix64(e ^ 0x5eed) & ruler_mask) == 0;
                 if (r) pa.kind[e] |= kRulerBit;
             }
             m[j] = __ballot(r);
@@ -1138,7 +1138,12 @@ static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm) {
     DevBuf<unsigned long long> cur(1);
     DevBuf<uint64_t> list(D);
     HIP_OK(hipMemsetAsync(cur.p, 0, 8, st));
-    hipLaunchKernelGGL(k_peel_rulers, dim3(grid_for(D, kBlock * kTileJ)), dim3(kBlock), 0, st, D, pa, list.p, cur.p);
+    // 1 in (ruler_mask + 1) unary nodes is a ruler besides the chain heads: a walk costs one
+    // random read per node whatever the spacing, pointer jumping ~log2(rulers per chain) rounds
+    // over the rulers
+    const uint64_t ruler_mask = (uint64_t)std::max<int64_t>(0, knob(ctx, "cf.ruler_mask", 63));
+    hipLaunchKernelGGL(k_peel_rulers, dim3(grid_for(D, kBlock * kTileJ)), dim3(kBlock), 0, st, D, pa, ruler_mask,
+                       list.p, cur.p);
     LAUNCH_OK();
     hipLaunchKernelGGL(k_peel_pack, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, D, pa);
     LAUNCH_OK();
