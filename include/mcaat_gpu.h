@@ -277,6 +277,8 @@ void mcaat_reset_timing(mcaat_ctx *ctx);
  *   nc.fine_bits       log2 fine partitions (8..19)
  *   nc.edge_cap        distinct edges per LDS partition before the class split / fallback
  *   nc.desc_cap        distinct super-k-mers per LDS partition before the class split / raw path
+ *   nc.overlap         0: passes B and C of successive groups in turn on one stream (default
+ *                      1: the next group's pass B on a second stream while C counts this one)
  *   sort.msd           0: radix sort only, 1: MSD sort whenever k <= 28 (default: D >= 2^16)
  *   sort.wave_limit / sort.mid_limit / sort.block_limit   level-3 bucket size limits of the
  *                      one-wave, 256-thread and 1024-thread LDS sorts (above the last: radix)

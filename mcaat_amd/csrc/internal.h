@@ -119,6 +119,9 @@ struct mcaat_ctx {
     int device = 0;
     int n_cu = 256;  // compute units (persistent-grid sizing)
     hipStream_t stream = nullptr;
+    // second stream (created on first use): node_counter partitions the next group of L1
+    // buckets (pass B) on it while pass C counts the current group
+    hipStream_t side = nullptr;
     std::vector<std::pair<const char *, double>> stages;
     std::map<std::string, mcaat::KernelStat> kstats;
     bool timing = true;
@@ -280,13 +283,21 @@ struct KernelTimer {
     const char *name;
     double bytes;
     hipEvent_t a = nullptr, b = nullptr;
-    KernelTimer(mcaat_ctx *c, const char *n, double algorithmic_bytes) : ctx(c), name(n), bytes(algorithmic_bytes) {
+    hipStream_t s = nullptr;
+    KernelTimer(mcaat_ctx *c, const char *n, double algorithmic_bytes, hipStream_t on = nullptr)
+        : ctx(c), name(n), bytes(algorithmic_bytes), s(on ? on : c->stream) {
         a = event_get(ctx);
         b = event_get(ctx);
-        HIP_OK(hipEventRecord(a, ctx->stream));
+        HIP_OK(hipEventRecord(a, s));
     }
     void stop() {
-        HIP_OK(hipEventRecord(b, ctx->stream));
+        mark();
+        finish();
+    }
+    // mark() closes the timed span on the stream; finish() waits for it, so work launched on
+    // other streams in between is not held up by the host
+    void mark() { HIP_OK(hipEventRecord(b, s)); }
+    void finish() {
         HIP_OK(hipEventSynchronize(b));
         float ms = 0;
         HIP_OK(hipEventElapsedTime(&ms, a, b));
@@ -309,6 +320,8 @@ inline int64_t knob(const mcaat_ctx *ctx, const char *name, int64_t dflt) {
     auto it = ctx->knobs.find(name);
     return it == ctx->knobs.end() ? dflt : it->second;
 }
+
+inline bool knob_set(const mcaat_ctx *ctx, const char *name) { return ctx->knobs.count(name) != 0; }
 
 inline unsigned grid_for(uint64_t n, unsigned block, unsigned cap = 65535u * 16) {
     uint64_t g = (n + block - 1) / block;

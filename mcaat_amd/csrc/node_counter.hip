@@ -1403,23 +1403,63 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
         (uint64_t)knob(ctx, "nc.group_budget", (int64_t)std::max<uint64_t>(n_live / 4 + 1, 1ULL << 28));  // descriptors per group
     const uint32_t cap_max = (uint32_t)std::min<int64_t>(kCapMax, std::max<int64_t>(1, knob(ctx, "nc.edge_cap", kCapMax)));
     const uint32_t dmax = (uint32_t)std::min<int64_t>(kDMax, std::max<int64_t>(1, knob(ctx, "nc.desc_cap", kDMax)));
-    uint64_t n_out = 0;
+    // groups of L1 buckets; with the overlap knob (default on) group g+1's pass B runs on the
+    // side stream while group g's pass C counts on the main stream (two groups' fine
+    // partitions alive at once, so groups are half the size)
+    const bool overlap = knob(ctx, "nc.overlap", 1) != 0;
+    struct Group {
+        int b0, b1;
+        DevBuf<uint4> fine;
+        hipEvent_t done = nullptr;
+    };
+    std::vector<Group> groups;
     for (int b0 = 0; b0 < 256;) {
         int b1 = b0 + 1;
-        while (b1 < 256 && hfine[(uint64_t)(b1 + 1) * S] - hfine[(uint64_t)b0 * S] <= group_budget) ++b1;
+        const uint64_t gb = overlap && !knob_set(ctx, "nc.group_budget") ? group_budget / 2 + 1 : group_budget;
+        while (b1 < 256 && hfine[(uint64_t)(b1 + 1) * S] - hfine[(uint64_t)b0 * S] <= gb) ++b1;
+        groups.push_back(Group{b0, b1, {}, nullptr});
+        b0 = b1;
+    }
+    if (overlap && !ctx->side) HIP_OK(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+    hipStream_t sb = overlap ? ctx->side : st;
+    if (overlap) {  // the side stream starts after everything queued so far (pass A, offsets)
+        hipEvent_t ev = event_get(ctx);
+        HIP_OK(hipEventRecord(ev, st));
+        HIP_OK(hipStreamWaitEvent(sb, ev, 0));
+        event_put(ctx, ev);
+    }
+    std::vector<KernelTimer *> btimers;
+    auto launch_b = [&](Group &g) {
+        const uint64_t p0 = (uint64_t)g.b0 * S, p1 = (uint64_t)g.b1 * S;
+        const uint64_t gbase = hfine[p0], gn = hfine[p1] - gbase;
+        const uint64_t c0 = bchunk[g.b0], c1 = bchunk[g.b1];
+        g.fine.alloc(gn ? gn : 1);
+        auto *kt = new KernelTimer(ctx, "l2_partition", 34.0 * (double)gn, sb);  // sub rows + descriptors read, descriptors written
+        if (c1 > c0) {
+            hipLaunchKernelGGL(k_l2_scatter, dim3((unsigned)(c1 - c0)), dim3(kBThreads), 0, sb, l1.p, l1s.p,
+                               dcs.p + c0, dcl.p + c0, dcb.p + c0, P.l2_bits, dcursor.p, g.fine.p, gbase);
+            LAUNCH_OK();
+        }
+        kt->mark();
+        g.done = event_get(ctx);
+        HIP_OK(hipEventRecord(g.done, sb));
+        btimers.push_back(kt);
+    };
+    struct TimerGuard {  // timers of launched B passes, freed on every exit
+        std::vector<KernelTimer *> &v;
+        ~TimerGuard() { for (auto *t : v) delete t; }
+    } tguard{btimers};
+    uint64_t n_out = 0;
+    if (!groups.empty()) launch_b(groups[0]);
+    for (size_t gi = 0; gi < groups.size(); ++gi) {
+        Group &grp = groups[gi];
+        const int b0 = grp.b0, b1 = grp.b1;
         const uint64_t p0 = (uint64_t)b0 * S, p1 = (uint64_t)b1 * S;
         const uint64_t gbase = hfine[p0], gn = hfine[p1] - gbase;
-        const uint64_t c0 = bchunk[b0], c1 = bchunk[b1];
-        DevBuf<uint4> fine(gn ? gn : 1);
-        {
-            KernelTimer kt(ctx, "l2_partition", 34.0 * (double)gn);  // sub rows + descriptors read, descriptors written
-            if (c1 > c0) {
-                hipLaunchKernelGGL(k_l2_scatter, dim3((unsigned)(c1 - c0)), dim3(kBThreads), 0, st, l1.p, l1s.p,
-                                       dcs.p + c0, dcl.p + c0, dcb.p + c0, P.l2_bits, dcursor.p, fine.p, gbase);
-                LAUNCH_OK();
-            }
-            kt.stop();
-        }
+        HIP_OK(hipStreamWaitEvent(st, grp.done, 0));
+        // the next group's partitioning overlaps this group's counting
+        if (overlap && gi + 1 < groups.size()) launch_b(groups[gi + 1]);
+        DevBuf<uint4> &fine = grp.fine;
         // C; a group whose output overflows the key buffers is counted again after they grow
         for (int attempt = 0;; ++attempt) {
             HIP_OK(hipMemsetAsync(dcnt.p + 1, 0, 8, st));
@@ -1503,8 +1543,12 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
             const unsigned long long keep = n_out;
             HIP_OK(hipMemcpyAsync(dcnt.p, &keep, 8, hipMemcpyHostToDevice, st));
         }
-        b0 = b1;
+        if (!overlap && gi + 1 < groups.size()) launch_b(groups[gi + 1]);
+        fine.release();
+        event_put(ctx, grp.done);
+        grp.done = nullptr;
     }
+    for (auto *t : btimers) t->finish();
     if (prof_c) {
         unsigned long long hp[8];
         HIP_OK(hipMemcpy(hp, dprof.p, 64, hipMemcpyDeviceToHost));
