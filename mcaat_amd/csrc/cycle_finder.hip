@@ -109,13 +109,21 @@ __device__ __forceinline__ bool kind_chain(uint8_t k) { return (k & 0xBF) == 1; 
 struct PeelArrays {
     uint8_t *kind;
     uint8_t *upred;   // 1: some unary node points here
+    uint8_t *bpred;   // 1: some branch node (out-degree >= 2) points here
     uint8_t *st;      // kUnk / kRem / kSurv (non-unary nodes)
     uint64_t *nxk;    // successor | successor kind << 56 (unary nodes)
-    uint64_t *owner;  // ruler whose walk passed this node (kNone: none)
-    uint64_t *jump;   // for rulers: terminal reached (kNone: cycle)
+    uint64_t *owner;  // non-rulers: ruler whose walk passed this node; rulers: the super ruler
+                      // whose walk over rulers passed it (kNone: none)
+    uint64_t *jump;   // rulers: next ruler or terminal | its kind << 56, then the terminal (kNone: cycle)
     const uint64_t *seed;  // tips bitmap collected before the multiplicity filter
 };
 
+// super rulers: chain heads and 1 in 64 of the other rulers (a ruler reached from another
+// ruler has a unary predecessor, so for it the hash alone decides)
+constexpr uint64_t kSuperMask = 63;
+__device__ __forceinline__ bool peel_super_hash(uint64_t r) { return (mix64(r ^ 0xbeefULL) & kSuperMask) == 0; }
+
+// pass 1 (D-wide): out-degree, the unary successor, unary- and branch-predecessor flags
 __global__ void __launch_bounds__(kBlock) k_peel_init(GraphView g, PeelArrays pa) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < g.D; e += stride) {
@@ -126,49 +134,95 @@ __global__ void __launch_bounds__(kBlock) k_peel_init(GraphView g, PeelArrays pa
         if (n == 1) {
             pa.nxk[e] = out[0];
             pa.upred[out[0]] = 1;
+        } else {
+            for (int j = 0; j < n; ++j) pa.bpred[out[j]] = 1;
         }
     }
 }
 
-__global__ void __launch_bounds__(kBlock) k_peel_mark(GraphView g, PeelArrays pa) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < g.D; e += stride) {
-        const int od = kind_od(pa.kind[e]);
-        if (od < 2 || od == kInvalid) continue;
-        uint64_t out[4];
-        const int n = dev_outgoing(g, e, out);
-        for (int j = 0; j < n; ++j) {
-            const uint64_t y = out[j];
-            atomicOr((unsigned int *)(pa.kind + (y & ~3ULL)), (unsigned)kBranchSucc << (8 * (y & 3)));
-        }
-    }
-}
-
-// rulers: unary nodes without a unary predecessor (chain heads) plus 1/64 of the others;
-// compacted into list by wave ballots, one cursor atomic per 4096-edge tile
+// pass 2 (D-wide): final kind bytes (ruler, branch-successor), each unary node's successor
+// packed with the successor's final kind (computed here from its flags, so the walk pays
+// one dependent load per step), non-unary states; rulers (unary chain heads plus 1 in
+// ruler_mask + 1 others) compacted into list with one cursor atomic per 4096-edge tile,
+// branch nodes and removed seeds into blist
 constexpr int kTileJ = 16;  // 64-edge words per wave per tile
-__global__ void __launch_bounds__(kBlock) k_peel_rulers(uint64_t D, PeelArrays pa, uint64_t ruler_mask,
-                                                        uint64_t *list, unsigned long long *cursor) {
+__global__ void __launch_bounds__(kBlock) k_peel_prep(uint64_t D, PeelArrays pa, uint64_t ruler_mask, uint64_t *list,
+                                                      unsigned long long *cursor, uint64_t *blist,
+                                                      unsigned long long *bcursor) {
     __shared__ uint32_t wcnt[kBlock / 64];
     __shared__ unsigned long long tbase;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const uint64_t tile = (uint64_t)kBlock * kTileJ;
     for (uint64_t t0 = (uint64_t)blockIdx.x * tile; t0 < D; t0 += (uint64_t)gridDim.x * tile) {
         unsigned long long m[kTileJ];
         uint32_t c = 0;
+        // kPB edges per thread at a time: their own bytes and successors are loaded first (all
+        // in flight together), then their successors' flags, then everything is written
+        constexpr int kPB = 8;
+        static_assert(kTileJ % kPB == 0, "whole batches per tile");
 #pragma unroll
-        for (int j = 0; j < kTileJ; ++j) {
-            const uint64_t e = t0 + (uint64_t)j * kBlock + threadIdx.x;
-            bool r = false;
-            if (e < D && kind_chain(pa.kind[e])) {
-                r = pa.upred[e] == 0 || (mix64(e ^ 0x5eed) & ruler_mask) == 0;
-                if (r) pa.kind[e] |= kRulerBit;
+        for (int h = 0; h < kTileJ; h += kPB) {
+            uint8_t od[kPB], bp[kPB], up[kPB], oy[kPB], by[kPB], uy[kPB];
+            uint64_t y[kPB];
+#pragma unroll
+            for (int q = 0; q < kPB; ++q) {
+                const uint64_t e = t0 + (uint64_t)(h + q) * kBlock + threadIdx.x;
+                // other lanes may already have set their own kind bits: the low 6 are the degree
+                od[q] = e < D ? (uint8_t)(pa.kind[e] & 0x3F) : kInvalid;
+                bp[q] = e < D ? pa.bpred[e] : 0;
+                up[q] = e < D ? pa.upred[e] : 0;
             }
-            m[j] = __ballot(r);
-            c += __popcll(m[j]);
-            // only unary non-ruler successors of branch nodes have their owner read (peel_res);
-            // their owner starts empty here instead of a D-wide fill
-            if (e < D && !r && kind_chain(pa.kind[e]) && (pa.kind[e] & kBranchSucc)) pa.owner[e] = kNone;
+#pragma unroll
+            for (int q = 0; q < kPB; ++q) {
+                const uint64_t e = t0 + (uint64_t)(h + q) * kBlock + threadIdx.x;
+                y[q] = od[q] == 1 ? pa.nxk[e] : 0;
+            }
+#pragma unroll
+            for (int q = 0; q < kPB; ++q) {
+                oy[q] = by[q] = uy[q] = 0;
+                if (od[q] == 1) {
+                    oy[q] = pa.kind[y[q]] & 0x3F;
+                    by[q] = pa.bpred[y[q]];
+                    uy[q] = pa.upred[y[q]];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < kPB; ++q) {
+                const int j = h + q;
+                const uint64_t e = t0 + (uint64_t)j * kBlock + threadIdx.x;
+                bool r = false, br = false;
+                if (od[q] != kInvalid) {
+                    uint8_t k = od[q] | (bp[q] ? kBranchSucc : 0);
+                    if (od[q] == 1) {
+                        r = up[q] == 0 || (mix64(e ^ 0x5eed) & ruler_mask) == 0;
+                        if (r) k |= kRulerBit;
+                        // owners: rulers' start empty (super-ruler walk), and of the others only
+                        // branch successors' are ever read (peel_res)
+                        if (r || bp[q]) pa.owner[e] = kNone;
+                        uint8_t ky = oy[q] | (by[q] ? kBranchSucc : 0);
+                        if (oy[q] == 1 && (uy[q] == 0 || (mix64(y[q] ^ 0x5eed) & ruler_mask) == 0)) ky |= kRulerBit;
+                        pa.nxk[e] = y[q] | ((uint64_t)ky << 56);
+                    } else if (od[q] == 0) {
+                        const bool rm = bit_get(pa.seed, e);
+                        pa.st[e] = rm ? kRem : kSurv;
+                        br = rm;
+                    } else {
+                        pa.st[e] = kUnk;
+                        br = true;
+                    }
+                    pa.kind[e] = k;
+                }
+                m[j] = __ballot(r);
+                c += __popcll(m[j]);
+                const unsigned long long mb = __ballot(br);
+                if (mb) {  // branch nodes are rare: one atomic per wave that has any
+                    unsigned long long off = 0;
+                    if (lane == 0) off = atomicAdd(bcursor, (unsigned long long)__popcll(mb));
+                    off = __shfl(off, 0);
+                    if (br) blist[off + __popcll(mb & lt)] = e;
+                }
+            }
         }
         if (lane == 0) wcnt[wave] = c;
         __syncthreads();
@@ -183,7 +237,6 @@ __global__ void __launch_bounds__(kBlock) k_peel_rulers(uint64_t D, PeelArrays p
         }
         __syncthreads();
         uint64_t off = tbase + wcnt[wave];
-        const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
 #pragma unroll
         for (int j = 0; j < kTileJ; ++j) {
             if ((m[j] >> lane) & 1) list[off + __popcll(m[j] & lt)] = t0 + (uint64_t)j * kBlock + threadIdx.x;
@@ -193,16 +246,8 @@ __global__ void __launch_bounds__(kBlock) k_peel_rulers(uint64_t D, PeelArrays p
     }
 }
 
-__global__ void __launch_bounds__(kBlock) k_peel_pack(uint64_t D, PeelArrays pa) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < D; e += stride)
-        if (kind_od(pa.kind[e]) == 1) {
-            const uint64_t y = pa.nxk[e];
-            pa.nxk[e] = y | ((uint64_t)pa.kind[y] << 56);
-        }
-}
-
-// each ruler walks its chain to the next ruler or non-unary node (Brent cycle check)
+// each ruler walks its chain to the next ruler or non-unary node (Brent cycle check); jump
+// keeps what it reached with that node's kind byte
 __global__ void __launch_bounds__(kBlock) k_peel_walk(PeelArrays pa, const uint64_t *list, uint64_t nr) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nr; i += stride) {
@@ -212,7 +257,7 @@ __global__ void __launch_bounds__(kBlock) k_peel_walk(PeelArrays pa, const uint6
         uint64_t res = kNone;
         for (;;) {
             const uint64_t y = w & kNodeMask;
-            if (!kind_chain((uint8_t)(w >> 56))) { res = y; break; }
+            if (!kind_chain((uint8_t)(w >> 56))) { res = w; break; }
             if (y == tort) { res = kNone; break; }  // ruler-less unary cycle reached
             if ((w >> 56) & kBranchSucc) pa.owner[y] = r;
             if (power == lam) { tort = y; power <<= 1; lam = 0; }
@@ -223,20 +268,79 @@ __global__ void __launch_bounds__(kBlock) k_peel_walk(PeelArrays pa, const uint6
     }
 }
 
-// one pointer-jumping round; *changed is raised when some ruler still pointed at a unary
-// node (a round that changes nothing proves every jump final)
-__global__ void __launch_bounds__(kBlock) k_peel_jump(PeelArrays pa, const uint64_t *list, uint64_t nr, int *changed) {
+// list ranking one level up: each super ruler walks the rulers of its chain (one jump load per
+// ruler) to the next super ruler or terminal, marking itself as their owner, and is listed
+__global__ void __launch_bounds__(kBlock) k_peel_super(PeelArrays pa, const uint64_t *list, uint64_t nr,
+                                                       uint64_t *slist, unsigned long long *scursor) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < nr; i0 += stride) {
+        const uint64_t i = i0 + threadIdx.x;
+        bool sup = false;
+        uint64_t r = 0;
+        if (i < nr) {
+            r = list[i];
+            sup = pa.upred[r] == 0 || peel_super_hash(r);
+        }
+        const unsigned long long m = __ballot(sup);
+        if (m) {
+            unsigned long long off = 0;
+            if (lane == 0) off = atomicAdd(scursor, (unsigned long long)__popcll(m));
+            off = __shfl(off, 0);
+            if (sup) slist[off + __popcll(m & lt)] = r;
+        }
+        if (!sup) continue;
+        uint64_t w = pa.jump[r], tort = r, power = 1, lam = 1;
+        for (;;) {
+            if (w == kNone) break;
+            const uint64_t x = w & kNodeMask;
+            if (kind_od((uint8_t)(w >> 56)) != 1 || peel_super_hash(x)) break;  // terminal or super ruler
+            if (x == tort) { w = kNone; break; }  // a cycle of rulers without a super ruler
+            pa.owner[x] = r;
+            if (power == lam) { tort = x; power <<= 1; lam = 0; }
+            w = pa.jump[x];
+            ++lam;
+        }
+        // a super ruler's jump is only read by its own walks from here on (walks stop at it)
+        pa.jump[r] = w;
+    }
+}
+
+// one pointer-jumping round over the super rulers; *changed is raised when some super ruler
+// still pointed at a unary node (a round that changes nothing proves every jump final)
+__global__ void __launch_bounds__(kBlock) k_peel_jump(PeelArrays pa, const uint64_t *slist, uint64_t ns, int *changed) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     bool ch = false;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nr; i += stride) {
-        const uint64_t r = list[i];
-        const uint64_t j = pa.jump[r];
-        if (j != kNone && kind_od(pa.kind[j]) == 1) {
-            pa.jump[r] = pa.jump[j];
-            ch = true;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride) {
+        const uint64_t s = slist[i];
+        const uint64_t j = pa.jump[s];
+        if (j != kNone && kind_od((uint8_t)(j >> 56)) == 1) {
+            const uint64_t t = pa.jump[j & kNodeMask];
+            if (t != j) {
+                pa.jump[s] = t;
+                ch = true;
+            }
         }
     }
     if (__ballot(ch) && (threadIdx.x & 63) == 0) *changed = 1;
+}
+
+// every ruler's terminal: a super ruler's own jump, another ruler's through its owner (kNone:
+// on a cycle); the kind byte is dropped (a super ruler's word is the same node either way)
+__global__ void __launch_bounds__(kBlock) k_peel_final(PeelArrays pa, const uint64_t *list, uint64_t nr) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nr; i += stride) {
+        const uint64_t r = list[i];
+        uint64_t v;
+        if (pa.upred[r] == 0 || peel_super_hash(r)) {
+            v = pa.jump[r];
+        } else {
+            const uint64_t o = pa.owner[r];
+            v = o == kNone ? kNone : pa.jump[o];
+        }
+        pa.jump[r] = v == kNone ? kNone : (v & kNodeMask);
+    }
 }
 
 __device__ __forceinline__ uint8_t peel_res(const PeelArrays &pa, uint64_t y) {
@@ -247,34 +351,6 @@ __device__ __forceinline__ uint8_t peel_res(const PeelArrays &pa, uint64_t y) {
     const uint64_t t = pa.jump[o];
     if (t == kNone || kind_od(pa.kind[t]) == 1) return kSurv;  // chain ends in a unary cycle
     return pa.st[t];
-}
-
-// non-unary valid nodes: seeds without successors are removed, the rest wait for their
-// successors; branch nodes (out-degree >= 2) and removed seeds are listed
-__global__ void __launch_bounds__(kBlock) k_peel_term(uint64_t D, PeelArrays pa, uint64_t *blist,
-                                                      unsigned long long *cursor) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    const int lane = threadIdx.x & 63;
-    for (uint64_t base = (uint64_t)blockIdx.x * blockDim.x; base < D; base += stride) {
-        const uint64_t e = base + threadIdx.x;
-        bool br = false;
-        if (e < D) {
-            const uint8_t o = pa.kind[e];
-            if (kind_od(o) == 0) {
-                const bool rm = bit_get(pa.seed, e);
-                pa.st[e] = rm ? kRem : kSurv;
-                br = rm;
-            } else {
-                pa.st[e] = kUnk;
-                br = kind_od(o) != kInvalid && kind_od(o) >= 2;
-            }
-        }
-        const unsigned long long m = __ballot(br);
-        unsigned long long off = 0;
-        if (lane == 0 && m) off = atomicAdd(cursor, (unsigned long long)__popcll(m));
-        off = __shfl(off, 0);
-        if (br) blist[off + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = e;
-    }
 }
 
 __global__ void __launch_bounds__(kBlock) k_peel_branch(GraphView g, PeelArrays pa, const uint64_t *blist,
@@ -1127,40 +1203,45 @@ static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm) {
     const uint64_t D = g->D;
     if (!D) return;
     GraphView v = g->view();
-    DevBuf<uint8_t> kind(D), upred(D), stt(D);
+    DevBuf<uint8_t> kind(D), upred(D), bpred(D), stt(D);
     DevBuf<uint64_t> nxk(D), owner(D), jump(D);
     HIP_OK(hipMemsetAsync(upred.p, 0, D, st));
-    PeelArrays pa{kind.p, upred.p, stt.p, nxk.p, owner.p, jump.p, seed_bm};
+    HIP_OK(hipMemsetAsync(bpred.p, 0, D, st));
+    PeelArrays pa{kind.p, upred.p, bpred.p, stt.p, nxk.p, owner.p, jump.p, seed_bm};
     hipLaunchKernelGGL(k_peel_init, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, v, pa);
     LAUNCH_OK();
-    hipLaunchKernelGGL(k_peel_mark, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, v, pa);
-    LAUNCH_OK();
-    DevBuf<unsigned long long> cur(1);
-    DevBuf<uint64_t> list(D);
-    HIP_OK(hipMemsetAsync(cur.p, 0, 8, st));
+    DevBuf<unsigned long long> cur(4);
+    DevBuf<uint64_t> list(D), blist(D);
+    HIP_OK(hipMemsetAsync(cur.p, 0, cur.bytes(), st));
     // 1 in (ruler_mask + 1) unary nodes is a ruler besides the chain heads: a walk costs one
-    // random read per node whatever the spacing, pointer jumping ~log2(rulers per chain) rounds
-    // over the rulers
+    // random read per node whatever the spacing; the rulers are then ranked one level up
+    // (1 in 64 of them, plus the heads, are super rulers) before pointer jumping
     const uint64_t ruler_mask = (uint64_t)std::max<int64_t>(0, knob(ctx, "cf.ruler_mask", 63));
-    hipLaunchKernelGGL(k_peel_rulers, dim3(grid_for(D, kBlock * kTileJ)), dim3(kBlock), 0, st, D, pa, ruler_mask,
-                       list.p, cur.p);
+    hipLaunchKernelGGL(k_peel_prep, dim3(grid_for(D, kBlock * kTileJ)), dim3(kBlock), 0, st, D, pa, ruler_mask,
+                       list.p, cur.p, blist.p, cur.p + 1);
     LAUNCH_OK();
-    hipLaunchKernelGGL(k_peel_pack, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, D, pa);
-    LAUNCH_OK();
-    const uint64_t nr = read_counter(ctx, cur.p);
+    unsigned long long hc[2];
+    HIP_OK(hipMemcpyAsync(hc, cur.p, 16, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    const uint64_t nr = hc[0], nb = hc[1];
     if (nr) {
         hipLaunchKernelGGL(k_peel_walk, dim3(grid_for(nr, kBlock)), dim3(kBlock), 0, st, pa, list.p, nr);
         LAUNCH_OK();
+        DevBuf<uint64_t> slist(nr);
+        hipLaunchKernelGGL(k_peel_super, dim3(grid_for(nr, kBlock)), dim3(kBlock), 0, st, pa, list.p, nr, slist.p,
+                           cur.p + 2);
+        LAUNCH_OK();
+        const uint64_t ns = read_counter(ctx, cur.p + 2);
         int rounds = 2;
-        while ((1ULL << rounds) < nr + 1) ++rounds;
+        while ((1ULL << rounds) < ns + 1) ++rounds;
         rounds += 1;
-        // log2(nr)+1 rounds bound the chain depth; most inputs converge far earlier, which
+        // log2(ns)+1 rounds bound the chain depth; most inputs converge far earlier, which
         // a round without changes proves (checked from the fourth round on)
         DevBuf<int> chg(1);
         int hchg = 1;
-        for (int r = 0; r < rounds; ++r) {
+        for (int r = 0; ns && r < rounds; ++r) {
             if (r >= 4) HIP_OK(hipMemsetAsync(chg.p, 0, 4, st));
-            hipLaunchKernelGGL(k_peel_jump, dim3(grid_for(nr, kBlock)), dim3(kBlock), 0, st, pa, list.p, nr, chg.p);
+            hipLaunchKernelGGL(k_peel_jump, dim3(grid_for(ns, kBlock)), dim3(kBlock), 0, st, pa, slist.p, ns, chg.p);
             LAUNCH_OK();
             if (r >= 4) {
                 HIP_OK(hipMemcpyAsync(&hchg, chg.p, 4, hipMemcpyDeviceToHost, st));
@@ -1168,12 +1249,9 @@ static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm) {
                 if (!hchg) break;
             }
         }
+        hipLaunchKernelGGL(k_peel_final, dim3(grid_for(nr, kBlock)), dim3(kBlock), 0, st, pa, list.p, nr);
+        LAUNCH_OK();
     }
-    DevBuf<uint64_t> blist(D);
-    HIP_OK(hipMemsetAsync(cur.p, 0, 8, st));
-    hipLaunchKernelGGL(k_peel_term, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, D, pa, blist.p, cur.p);
-    LAUNCH_OK();
-    const uint64_t nb = read_counter(ctx, cur.p);
     DevBuf<int> changed(1);
     for (uint64_t it = 0; nb && it < D + 1; ++it) {
         HIP_OK(hipMemsetAsync(changed.p, 0, 4, st));

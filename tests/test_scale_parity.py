@@ -56,6 +56,12 @@ KNOBS = {
     # (nearly) unbounded walks that finish every chain themselves
     "peel_walk1": {"cf.walk_budget": 1},
     "peel_kahn": {"cf.walk_budget": 1 << 30},
+    # list-ranking peel with every unary node a ruler (one-step walks, deep super-ruler chains)
+    # and with sparse rulers (long walks, few super rulers)
+    "peel_dense_rulers": {"cf.ruler_mask": 0},
+    "peel_sparse_rulers": {"cf.ruler_mask": 4095},
+    # passes B and C of successive groups in turn on one stream
+    "nc_no_overlap": {"nc.overlap": 0, "nc.group_budget": 1 << 14},
     # adjacency: per-edge global directory searches, and the LDS-range kernel with every range
     # (cap 0) or the larger ones (cap 200) sent to its global fallback
     "adj_global": {"sdbg.adj_lds": 0},
