@@ -282,6 +282,8 @@ void mcaat_reset_timing(mcaat_ctx *ctx);
  *   sort.msd           0: radix sort only, 1: MSD sort whenever k <= 28 (default: D >= 2^16)
  *   sort.wave_limit / sort.mid_limit / sort.block_limit   level-3 bucket size limits of the
  *                      one-wave, 256-thread and 1024-thread LDS sorts (above the last: radix)
+ *   sort.l3_counting   0: one-wave level-3 buckets by the bitonic network only (default 1: LDS
+ *                      counting sort by the next key bits, bitonic for clustered buckets)
  *   cf.dls_stack / cf.dls_visited   initial DepthLevelSearch scratch (grows x8 on overflow)
  *   cf.fc_lock / cf.fc_relax / cf.fc_out   initial FindCycle scratch (grows on overflow)
  *   cf.fc_window       initial FindCycle speculation window

@@ -906,7 +906,7 @@ int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value) {
         "nc.edge_cap",     "nc.desc_cap",        "sort.msd",   "sort.wave_limit", "sort.mid_limit",
         "sort.block_limit", "cf.dls_stack",      "cf.dls_visited", "cf.fc_lock", "cf.fc_relax",
         "cf.fc_out",       "cf.fc_window",       "cf.walk_budget", "sdbg.adj_lds",   "sdbg.adj_cap",       "cf.ruler_mask",
-        "nc.overlap"};
+        "nc.overlap",      "sort.l3_counting"};
     return guarded([&] {
         require(ctx && name, "null argument");
         bool ok = false;

@@ -447,19 +447,36 @@ __device__ __forceinline__ void msd_emit(const uint64_t *s, uint32_t nreal, uint
     }
 }
 
-// one wave per level-2 bucket of <= kWaveSort items; larger ones are listed
+// one wave per level-2 bucket of <= kWaveSort items; larger ones are listed. A bucket is
+// counting-sorted by the next lg(P) key bits (P = its size rounded up to a power of two, so
+// about one item per bin): each item's rank inside its bin comes from the LDS histogram atomic,
+// a wave scan turns counts into bin starts, items go to their bins in LDS, and each then finds
+// its final rank among the few items of its own bin and is written straight to HBM (ranks
+// are nearly the LDS order, so the writes stay coalesced). A bucket whose largest bin holds
+// more than kMaxBin items (clustered keys) takes the bitonic network instead.
 constexpr int kL3Waves = 4;
+constexpr uint32_t kMaxBin = 16;
 __global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in, const uint64_t *off2,
                                                              const uint64_t *real2, const uint64_t *base3, int k,
                                                              uint64_t *key, uint16_t *mult, uint32_t *big,
-                                                             unsigned long long *nbig, uint32_t limit) {
+                                                             unsigned long long *nbig, uint32_t limit, int counting) {
     __shared__ uint64_t sm[kL3Waves][kWaveSort];
+    __shared__ uint64_t so[kL3Waves][kWaveSort];
+    __shared__ uint32_t sc[kL3Waves][kWaveSort];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    uint64_t *s = sm[wave];
+    uint64_t *s = sm[wave], *o = so[wave];
+    uint32_t *cnt = sc[wave];
     const int E = k + 1;
+    const int rb = 2 * E - 2 * kMB;  // key bits below the two MSD levels (item bits 16 .. 16 + rb)
     const uint64_t nb = (uint64_t)kMS * kMS;
     const uint64_t bstride = (uint64_t)gridDim.x * kL3Waves;
     constexpr int NL = 10;  // loads per lane: buckets of up to 640 padded items
+    constexpr int NR = kWaveSort / 64;  // items per lane once compacted
+    auto wave_sync = [] {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
     uint64_t b = (uint64_t)blockIdx.x * kL3Waves + wave;
     // bucket metadata one bucket ahead
     uint64_t m_lo = 0, m_hi = 0, m_real = 0, m_base = 0;
@@ -484,7 +501,7 @@ __global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in,
             continue;
         }
         // load the bucket (all loads in flight together), compacted: line padding dropped, so
-        // the network is sized by the real items
+        // the sort is sized by the real items
         const uint32_t nreal = (uint32_t)nr64;
         uint64_t v[NL];
 #pragma unroll
@@ -492,8 +509,6 @@ __global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in,
             const uint32_t i = t * 64 + lane;
             v[t] = i < n ? in[lo + i] : kPad;
         }
-        uint32_t P = 8;
-        while (P < nreal) P <<= 1;
         uint32_t fill = 0;
 #pragma unroll
         for (int t = 0; t < NL; ++t) {
@@ -502,16 +517,80 @@ __global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in,
                 s[fill + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = v[t];
             fill += (uint32_t)__popcll(m);
         }
-        for (uint32_t i = nreal + lane; i < P; i += 64) s[i] = kPad;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        lds_bitonic(s, P, lane, 64, true);
         const uint64_t hi = (b >> kMB) << (2 * E - kMB);
-        msd_emit(s, nreal, lane, 64, hi, key, mult, base);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // bins: P >= nreal, at least 64 (one per lane), at most 2^rb
+        uint32_t lgb = 6;
+        while ((1u << lgb) < nreal) ++lgb;
+        bool sorted = false;
+        if (counting && lgb <= (uint32_t)rb) {
+            const uint32_t nbins = 1u << lgb, per = nbins / 64, sh = 16 + rb - lgb;
+            for (uint32_t i = lane; i < nbins; i += 64) cnt[i] = 0;
+            wave_sync();
+            uint32_t rk[NR];
+#pragma unroll
+            for (int t = 0; t < NR; ++t) {
+                const uint32_t i = t * 64 + lane;
+                rk[t] = i < nreal ? atomicAdd(&cnt[(uint32_t)(s[i] >> sh) & (nbins - 1)], 1u) : 0;
+            }
+            wave_sync();
+            // bin counts -> bin starts (each lane owns `per` consecutive bins)
+            uint32_t loc = 0, mx = 0;
+            for (uint32_t j = 0; j < per; ++j) {
+                const uint32_t c = cnt[lane * per + j];
+                loc += c;
+                mx = c > mx ? c : mx;
+            }
+            uint32_t incl = loc;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t u = __shfl_up(incl, d);
+                if (lane >= d) incl += u;
+            }
+            for (int d = 32; d > 0; d >>= 1) {
+                const uint32_t u = __shfl_xor(mx, d);
+                mx = u > mx ? u : mx;
+            }
+            if (mx <= kMaxBin) {
+                uint32_t run = incl - loc;
+                for (uint32_t j = 0; j < per; ++j) {
+                    const uint32_t c = cnt[lane * per + j];
+                    cnt[lane * per + j] = run;
+                    run += c;
+                }
+                wave_sync();
+#pragma unroll
+                for (int t = 0; t < NR; ++t) {
+                    const uint32_t i = t * 64 + lane;
+                    if (i < nreal) {
+                        const uint64_t x = s[i];
+                        o[cnt[(uint32_t)(x >> sh) & (nbins - 1)] + rk[t]] = x;
+                    }
+                }
+                wave_sync();
+#pragma unroll
+                for (int t = 0; t < NR; ++t) {
+                    const uint32_t p = t * 64 + lane;
+                    if (p < nreal) {
+                        const uint64_t x = o[p];
+                        const uint32_t bi = (uint32_t)(x >> sh) & (nbins - 1);
+                        const uint32_t bs = cnt[bi], be = bi + 1 < nbins ? cnt[bi + 1] : nreal;
+                        uint32_t r = bs;
+                        for (uint32_t q = bs; q < be; ++q) r += o[q] < x;
+                        key[base + r] = hi | (x >> 16);
+                        mult[base + r] = (uint16_t)(x & 0xFFFF);
+                    }
+                }
+                sorted = true;
+            }
+        }
+        if (!sorted) {
+            uint32_t P = 8;
+            while (P < nreal) P <<= 1;
+            for (uint32_t i = nreal + lane; i < P; i += 64) s[i] = kPad;
+            wave_sync();
+            lds_bitonic(s, P, lane, 64, true);
+            msd_emit(s, nreal, lane, 64, hi, key, mult, base);
+        }
+        wave_sync();
     }
 }
 
@@ -614,9 +693,11 @@ bool msd_sort(mcaat_ctx *ctx, const uint64_t *ckeys, const uint32_t *ccnt, uint6
     DevBuf<int> too(1);
     HIP_OK(hipMemsetAsync(nbig.p, 0, 8, st));
     HIP_OK(hipMemsetAsync(too.p, 0, 4, st));
-    hipLaunchKernelGGL(k_msd3_wave, dim3((unsigned)ctx->n_cu * 16), dim3(kL3Waves * 64), 0, st, l2.p, off2.p,
+    // 40 KB of LDS per workgroup: four resident per CU
+    hipLaunchKernelGGL(k_msd3_wave, dim3((unsigned)ctx->n_cu * 4), dim3(kL3Waves * 64), 0, st, l2.p, off2.p,
                        (const uint64_t *)real2.p, (const uint64_t *)base3.p, k, key, mult, big.p, nbig.p,
-                       (uint32_t)std::min<int64_t>(kWaveSort, knob(ctx, "sort.wave_limit", kWaveSort)));
+                       (uint32_t)std::min<int64_t>(kWaveSort, knob(ctx, "sort.wave_limit", kWaveSort)),
+                       (int)knob(ctx, "sort.l3_counting", 1));
     LAUNCH_OK();
     unsigned long long hb = 0;
     HIP_OK(hipMemcpyAsync(&hb, nbig.p, 8, hipMemcpyDeviceToHost, st));

@@ -49,6 +49,8 @@ KNOBS = {
     "sort_block": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_limit": 0},
     "sort_radix": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_limit": 0, "sort.block_limit": 0},
     "sort_radix_only": {"sort.msd": 0},
+    # one-wave level-3 buckets by the bitonic network instead of the LDS counting sort
+    "sort_l3_bitonic": {"sort.msd": 1, "sort.l3_counting": 0},
     # scratch regrowth in DepthLevelSearch and FindCycle, one speculative start per round
     "cf_scratch": {"cf.dls_stack": 1, "cf.dls_visited": 2, "cf.fc_lock": 4, "cf.fc_relax": 1, "cf.fc_out": 1,
                    "cf.fc_window": 1},
