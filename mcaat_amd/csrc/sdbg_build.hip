@@ -311,11 +311,25 @@ __global__ void __launch_bounds__(kSBlock) k_msd1_scatter(const uint64_t *ckeys,
     const uint64_t c0 = (uint64_t)blockIdx.x * kCh1, c1 = c0 + kCh1 < n ? c0 + kCh1 : n;
     for (int i = threadIdx.x; i < kMS; i += kSBlock) lc[i] = 0;
     __syncthreads();
-    for (uint64_t i = c0 + threadIdx.x; i < c1; i += kSBlock) {
-        uint32_t bk[2];
-        uint64_t it[2];
-        const int no = msd_items(ckeys[i], ccnt[i], k, bk, it);
-        for (int j = 0; j < no; ++j) atomicAdd(&lc[bk[j]], 1u);
+    // counting: kCL entries per thread have their loads in flight together
+    constexpr int kCL = 4;
+    for (uint64_t i0 = c0 + threadIdx.x; i0 < c1; i0 += (uint64_t)kSBlock * kCL) {
+        uint64_t a[kCL];
+        uint32_t cc[kCL];
+#pragma unroll
+        for (int q = 0; q < kCL; ++q) {
+            const uint64_t i = i0 + (uint64_t)q * kSBlock;
+            a[q] = i < c1 ? ckeys[i] : 0;
+            cc[q] = i < c1 ? ccnt[i] : 0;
+        }
+#pragma unroll
+        for (int q = 0; q < kCL; ++q) {
+            if (i0 + (uint64_t)q * kSBlock >= c1) break;
+            uint32_t bk[2];
+            uint64_t it[2];
+            const int no = msd_items(a[q], cc[q], k, bk, it);
+            for (int j = 0; j < no; ++j) atomicAdd(&lc[bk[j]], 1u);
+        }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kMS; i += kSBlock) {
@@ -326,13 +340,26 @@ __global__ void __launch_bounds__(kSBlock) k_msd1_scatter(const uint64_t *ckeys,
     }
     __syncthreads();
     LinePlace lp{buf, lb, lc, bl, out, 0};
+    // the next round's entry is loaded while this round places its items
+    uint64_t na = 0;
+    uint32_t nc = 0;
+    if (c0 + threadIdx.x < c1) {
+        na = ckeys[c0 + threadIdx.x];
+        nc = ccnt[c0 + threadIdx.x];
+    }
     for (uint64_t i0 = c0; i0 < c1; i0 += kSBlock) {
         const uint64_t i = i0 + threadIdx.x;
+        const uint64_t a = na;
+        const uint32_t cn = nc;
+        if (i + kSBlock < c1) {
+            na = ckeys[i + kSBlock];
+            nc = ccnt[i + kSBlock];
+        }
         uint32_t bk[2] = {0, 0}, r[2] = {0, 0}, line[2] = {0, 0}, nl[2] = {0, 0};
         uint64_t it[2] = {0, 0};
         bool bf[2] = {false, false};
         int no = 0;
-        if (i < c1) no = msd_items(ckeys[i], ccnt[i], k, bk, it);
+        if (i < c1) no = msd_items(a, cn, k, bk, it);
         for (int j = 0; j < no; ++j) lp.put(bk[j], it[j], r[j], line[j], bf[j]);
         lds_barrier();
         for (int j = 0; j < no; ++j) lp.flush(bk[j], r[j], line[j], bf[j], nl[j]);
@@ -381,9 +408,14 @@ __global__ void __launch_bounds__(kSBlock) k_msd2_scatter(const uint64_t *in, co
     __syncthreads();
     const uint64_t s0 = cstart[c];
     const uint32_t n = clen[c];
-    for (uint32_t i = threadIdx.x; i < n; i += kSBlock) {
-        const uint64_t it = in[s0 + i];
-        if (it != kPad) atomicAdd(&lc[msd_sub(it, k)], 1u);
+    constexpr int kCL = 4;  // counting loads in flight per thread
+    for (uint32_t i0 = threadIdx.x; i0 < n; i0 += kSBlock * kCL) {
+        uint64_t v[kCL];
+#pragma unroll
+        for (int q = 0; q < kCL; ++q) v[q] = i0 + q * kSBlock < n ? in[s0 + i0 + q * kSBlock] : kPad;
+#pragma unroll
+        for (int q = 0; q < kCL; ++q)
+            if (v[q] != kPad) atomicAdd(&lc[msd_sub(v[q], k)], 1u);
     }
     __syncthreads();
     const uint64_t fb = (uint64_t)cbucket[c] * kMS;
