@@ -106,11 +106,18 @@ constexpr uint64_t kNodeMask = (1ULL << 56) - 1;
 __device__ __forceinline__ int kind_od(uint8_t k) { return k & 0x3F; }
 __device__ __forceinline__ bool kind_chain(uint8_t k) { return (k & 0xBF) == 1; }  // unary, not a ruler
 
+// a node's four flag bytes share one word (nf[4e + field]), so a walk or a successor check
+// touches one line per node instead of one per byte array
+enum : int { kFKind = 0, kFUpred = 1, kFBpred = 2, kFSt = 3 };
 struct PeelArrays {
-    uint8_t *kind;
-    uint8_t *upred;   // 1: some unary node points here
-    uint8_t *bpred;   // 1: some branch node (out-degree >= 2) points here
-    uint8_t *st;      // kUnk / kRem / kSurv (non-unary nodes)
+    uint8_t *nf;      // per node: kind; upred (1: some unary node points here); bpred (1: some
+                      // branch node, out-degree >= 2, points here); st (kUnk / kRem / kSurv,
+                      // non-unary nodes)
+    __device__ __forceinline__ uint8_t &kind(uint64_t e) const { return nf[4 * e + kFKind]; }
+    __device__ __forceinline__ uint8_t &upred(uint64_t e) const { return nf[4 * e + kFUpred]; }
+    __device__ __forceinline__ uint8_t &bpred(uint64_t e) const { return nf[4 * e + kFBpred]; }
+    __device__ __forceinline__ uint8_t &st(uint64_t e) const { return nf[4 * e + kFSt]; }
+    __device__ __forceinline__ uchar4 flags(uint64_t e) const { return *(const uchar4 *)(nf + 4 * e); }
     uint64_t *nxk;    // successor | successor kind << 56 (unary nodes)
     uint64_t *owner;  // non-rulers: ruler whose walk passed this node; rulers: the super ruler
                       // whose walk over rulers passed it (kNone: none)
@@ -127,15 +134,15 @@ __device__ __forceinline__ bool peel_super_hash(uint64_t r) { return (mix64(r ^ 
 __global__ void __launch_bounds__(kBlock) k_peel_init(GraphView g, PeelArrays pa) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < g.D; e += stride) {
-        if (!bit_get(g.valid, e)) { pa.kind[e] = kInvalid; continue; }
+        if (!bit_get(g.valid, e)) { pa.kind(e) = kInvalid; continue; }
         uint64_t out[4];
         const int n = dev_outgoing(g, e, out);
-        pa.kind[e] = (uint8_t)n;
+        pa.kind(e) = (uint8_t)n;
         if (n == 1) {
             pa.nxk[e] = out[0];
-            pa.upred[out[0]] = 1;
+            pa.upred(out[0]) = 1;
         } else {
-            for (int j = 0; j < n; ++j) pa.bpred[out[j]] = 1;
+            for (int j = 0; j < n; ++j) pa.bpred(out[j]) = 1;
         }
     }
 }
@@ -169,9 +176,10 @@ __global__ void __launch_bounds__(kBlock) k_peel_prep(uint64_t D, PeelArrays pa,
             for (int q = 0; q < kPB; ++q) {
                 const uint64_t e = t0 + (uint64_t)(h + q) * kBlock + threadIdx.x;
                 // other lanes may already have set their own kind bits: the low 6 are the degree
-                od[q] = e < D ? (uint8_t)(pa.kind[e] & 0x3F) : kInvalid;
-                bp[q] = e < D ? pa.bpred[e] : 0;
-                up[q] = e < D ? pa.upred[e] : 0;
+                const uchar4 f = e < D ? pa.flags(e) : make_uchar4(kInvalid, 0, 0, 0);
+                od[q] = (uint8_t)(f.x & 0x3F);
+                up[q] = f.y;
+                bp[q] = f.z;
             }
 #pragma unroll
             for (int q = 0; q < kPB; ++q) {
@@ -182,9 +190,10 @@ __global__ void __launch_bounds__(kBlock) k_peel_prep(uint64_t D, PeelArrays pa,
             for (int q = 0; q < kPB; ++q) {
                 oy[q] = by[q] = uy[q] = 0;
                 if (od[q] == 1) {
-                    oy[q] = pa.kind[y[q]] & 0x3F;
-                    by[q] = pa.bpred[y[q]];
-                    uy[q] = pa.upred[y[q]];
+                    const uchar4 f = pa.flags(y[q]);
+                    oy[q] = f.x & 0x3F;
+                    uy[q] = f.y;
+                    by[q] = f.z;
                 }
             }
 #pragma unroll
@@ -205,13 +214,13 @@ __global__ void __launch_bounds__(kBlock) k_peel_prep(uint64_t D, PeelArrays pa,
                         pa.nxk[e] = y[q] | ((uint64_t)ky << 56);
                     } else if (od[q] == 0) {
                         const bool rm = bit_get(pa.seed, e);
-                        pa.st[e] = rm ? kRem : kSurv;
+                        pa.st(e) = rm ? kRem : kSurv;
                         br = rm;
                     } else {
-                        pa.st[e] = kUnk;
+                        pa.st(e) = kUnk;
                         br = true;
                     }
-                    pa.kind[e] = k;
+                    pa.kind(e) = k;
                 }
                 m[j] = __ballot(r);
                 c += __popcll(m[j]);
@@ -281,7 +290,7 @@ __global__ void __launch_bounds__(kBlock) k_peel_super(PeelArrays pa, const uint
         uint64_t r = 0;
         if (i < nr) {
             r = list[i];
-            sup = pa.upred[r] == 0 || peel_super_hash(r);
+            sup = pa.upred(r) == 0 || peel_super_hash(r);
         }
         const unsigned long long m = __ballot(sup);
         if (m) {
@@ -333,7 +342,7 @@ __global__ void __launch_bounds__(kBlock) k_peel_final(PeelArrays pa, const uint
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nr; i += stride) {
         const uint64_t r = list[i];
         uint64_t v;
-        if (pa.upred[r] == 0 || peel_super_hash(r)) {
+        if (pa.upred(r) == 0 || peel_super_hash(r)) {
             v = pa.jump[r];
         } else {
             const uint64_t o = pa.owner[r];
@@ -344,13 +353,16 @@ __global__ void __launch_bounds__(kBlock) k_peel_final(PeelArrays pa, const uint
 }
 
 __device__ __forceinline__ uint8_t peel_res(const PeelArrays &pa, uint64_t y) {
-    const uint8_t k = pa.kind[y];
-    if (kind_od(k) != 1) return pa.st[y];
+    const uchar4 f = pa.flags(y);
+    const uint8_t k = f.x;
+    if (kind_od(k) != 1) return f.w;
     const uint64_t o = (k & kRulerBit) ? y : pa.owner[y];
     if (o == kNone) return kSurv;  // unary node on a ruler-less cycle
     const uint64_t t = pa.jump[o];
-    if (t == kNone || kind_od(pa.kind[t]) == 1) return kSurv;  // chain ends in a unary cycle
-    return pa.st[t];
+    if (t == kNone) return kSurv;
+    const uchar4 ft = pa.flags(t);
+    if (kind_od(ft.x) == 1) return kSurv;  // chain ends in a unary cycle
+    return ft.w;
 }
 
 __global__ void __launch_bounds__(kBlock) k_peel_branch(GraphView g, PeelArrays pa, const uint64_t *blist,
@@ -358,7 +370,7 @@ __global__ void __launch_bounds__(kBlock) k_peel_branch(GraphView g, PeelArrays 
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += stride) {
         const uint64_t b = blist[i];
-        if (pa.st[b] != kUnk) continue;
+        if (pa.st(b) != kUnk) continue;
         uint64_t out[4];
         const int n = dev_outgoing(g, b, out);
         bool all_rem = true, any_surv = false;
@@ -367,8 +379,8 @@ __global__ void __launch_bounds__(kBlock) k_peel_branch(GraphView g, PeelArrays 
             if (r == kSurv) any_surv = true;
             if (r != kRem) all_rem = false;
         }
-        if (any_surv) { pa.st[b] = kSurv; *changed = 1; }
-        else if (all_rem) { pa.st[b] = kRem; *changed = 1; }
+        if (any_surv) { pa.st(b) = kSurv; *changed = 1; }
+        else if (all_rem) { pa.st(b) = kRem; *changed = 1; }
     }
 }
 
@@ -382,7 +394,7 @@ __global__ void __launch_bounds__(kBlock) k_peel_apply_list(GraphView g, PeelArr
                                                             uint64_t nb) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += stride)
-        if (pa.st[blist[i]] == kRem) clear_valid(g, blist[i]);
+        if (pa.st(blist[i]) == kRem) clear_valid(g, blist[i]);
 }
 
 __global__ void __launch_bounds__(kBlock) k_peel_apply_rulers(GraphView g, PeelArrays pa, const uint64_t *list,
@@ -1203,11 +1215,10 @@ static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm) {
     const uint64_t D = g->D;
     if (!D) return;
     GraphView v = g->view();
-    DevBuf<uint8_t> kind(D), upred(D), bpred(D), stt(D);
+    DevBuf<uint8_t> nf(4 * D);
     DevBuf<uint64_t> nxk(D), owner(D), jump(D);
-    HIP_OK(hipMemsetAsync(upred.p, 0, D, st));
-    HIP_OK(hipMemsetAsync(bpred.p, 0, D, st));
-    PeelArrays pa{kind.p, upred.p, bpred.p, stt.p, nxk.p, owner.p, jump.p, seed_bm};
+    HIP_OK(hipMemsetAsync(nf.p, 0, nf.bytes(), st));  // the flag bytes other nodes set
+    PeelArrays pa{nf.p, nxk.p, owner.p, jump.p, seed_bm};
     hipLaunchKernelGGL(k_peel_init, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, v, pa);
     LAUNCH_OK();
     DevBuf<unsigned long long> cur(4);
@@ -1798,12 +1809,9 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
     LAUNCH_OK();
     out->stats[3] = read_counter(ctx, cnt.p);
     timer.mark("recount");
-    // 5. ChunkStartNodes
-    if (!p.low_abundance) {
-        zero();
-        hipLaunchKernelGGL(k_mult_filter, dim3(wgrid), dim3(kBlock), 0, st, v, cnt.p);
-        LAUNCH_OK();
-    }
+    // 5. ChunkStartNodes. Its InvalidateMultiplicityOneNodes (cycle_finder.cpp:391-393) is a
+    // no-op here: step 2 already cleared every mult <= 1 edge and nothing since sets a valid
+    // bit, and the count it would print is stats[1] (every mult <= 1 edge, valid or not)
     std::vector<uint64_t> cand;
     {
         // rank R scans ids [R*D/N, (R+1)*D/N)

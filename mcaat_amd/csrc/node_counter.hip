@@ -743,9 +743,13 @@ constexpr int kDCap = 2048;                                // descriptor slots
 constexpr int kDMax = kDCap * 3 / 4;                       // distinct descriptors before going raw
 constexpr int kDProbe = 128;                               // probe bound of the descriptor table
 #ifndef MCAAT_CB
-#define MCAAT_CB 2
+#define MCAAT_CB 1
 #endif
 constexpr int kCB = MCAAT_CB;                              // descriptor loads in flight per thread
+#ifndef MCAAT_CPF
+#define MCAAT_CPF 1
+#endif
+constexpr bool kCPF = MCAAT_CPF != 0;                      // next round's loads issued before the probes
 constexpr int kDefer = 64;                                 // descriptors with w0 == kEmpty before going raw
 #ifndef MCAAT_CPERCU
 #define MCAAT_CPERCU 2
@@ -897,19 +901,34 @@ __global__ void __launch_bounds__(kCThreads, kCPerCu * kCThreads / 256) k_lds_co
             dovf = 1;
             if (PROF) atomicAdd(&prof[5], 1ull);
         };
-        // kCB descriptors per thread per round: their loads are all in flight together
-        for (uint64_t d0 = beg + threadIdx.x; d0 < end; d0 += (uint64_t)kCThreads * kCB) {
-            if (__hip_atomic_load(&dovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-            uint4 q[kCB];
+        // kCB descriptors per thread per round: their loads are all in flight together, and
+        // with kCPF the next round's are issued before this round's probes
+        uint4 q[kCB];
+        if (kCPF) {
 #pragma unroll
             for (int k = 0; k < kCB; ++k) {
-                const uint64_t d = d0 + (uint64_t)k * kCThreads;
+                const uint64_t d = beg + threadIdx.x + (uint64_t)k * kCThreads;
                 q[k] = d < end ? data[d] : make_uint4(0, 0, 0, 0);
+            }
+        }
+        for (uint64_t d0 = beg + threadIdx.x; d0 < end; d0 += (uint64_t)kCThreads * kCB) {
+            if (__hip_atomic_load(&dovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+            uint4 cq[kCB];
+#pragma unroll
+            for (int k = 0; k < kCB; ++k) {
+                if (kCPF) {
+                    cq[k] = q[k];
+                    const uint64_t d = d0 + (uint64_t)(k + kCB) * kCThreads;
+                    q[k] = d < end ? data[d] : make_uint4(0, 0, 0, 0);
+                } else {
+                    const uint64_t d = d0 + (uint64_t)k * kCThreads;
+                    cq[k] = d < end ? data[d] : make_uint4(0, 0, 0, 0);
+                }
             }
 #pragma unroll
             for (int k = 0; k < kCB; ++k)
                 if (d0 + (uint64_t)k * kCThreads < end)
-                    collapse((uint64_t)q[k].x | ((uint64_t)q[k].y << 32), (uint64_t)q[k].z | ((uint64_t)q[k].w << 32));
+                    collapse((uint64_t)cq[k].x | ((uint64_t)cq[k].y << 32), (uint64_t)cq[k].z | ((uint64_t)cq[k].w << 32));
         }
         __syncthreads();
         tick(1);
