@@ -63,6 +63,18 @@ CONFIGS = {
                sample=M.SynthSpec(seed=2, n_genomes=40, genome_len=200_000, arrays_per_genome=2, spacers_per_array=12,
                                   repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
                                   read_len=150, n_reads=1_000_000, error_rate=5.0e-3, paired=True)),
+    # C5: the low-abundance regime (include/settings.h:33-38 with threshold_multiplicity=2,
+    # low_abundance=true, cycle min/max 27/77) on the C3 community, substitution errors raised
+    # until the graph passes 2^31 edges (D ~ 4e9 is BASELINE's 8-GPU figure; this is the
+    # largest D one GPU's 288 GB holds through the build)
+    "c5": dict(spec=M.SynthSpec(seed=5, n_genomes=200, genome_len=1_500_000, arrays_per_genome=2,
+                                spacers_per_array=12, repeat_len_min=30, repeat_len_max=36, spacer_len_min=30,
+                                spacer_len_max=36, read_len=150, n_reads=300_000_000, error_rate=1.7e-3),
+               k=27, thr=2, name="C5 low-abundance regime on one GPU (300M x 150bp SE, e=0.17%, k=27, thr=2, "
+                                 "low_abundance, 27/77)",
+               sample=M.SynthSpec(seed=5, n_genomes=20, genome_len=100_000, arrays_per_genome=2, spacers_per_array=12,
+                                  repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
+                                  read_len=150, n_reads=2_000_000, error_rate=1.7e-3)),
     "tiny": dict(spec=M.SynthSpec(), k=27, thr=20, name="C1 tiny (10k x 150bp, 50 kbp genome, k=27)",
                  sample=M.SynthSpec()),
 }
@@ -204,11 +216,20 @@ def measure_e2e(cfg: dict, spec, fastq: str, threads: int, n_kmers: int) -> dict
         p = subprocess.run([exe, "--settings", st, "--input-files", fastq, "--output-folder",
                             os.path.join(work, "out")], capture_output=True, text=True, timeout=900)
         wall = time.perf_counter() - t0
+        if os.environ.get("MCAAT_E2E_LOG"):  # keep the CLI's own output (per-step timers) for study
+            with open(os.environ["MCAAT_E2E_LOG"], "w") as f:
+                f.write(p.stdout + "\n---- stderr ----\n" + p.stderr)
         m = re.search(r"TIMING span_s=([0-9.]+) sdbg_build_s=([0-9.]+) build_lib_s=([0-9.]+) cycle_finder_s=([0-9.]+)",
                       p.stdout)
         if p.returncode != 0 or not m:
             return {"error": f"CLI rc={p.returncode}: {(p.stderr or p.stdout)[-400:]}"}
         span, build, lib, cf = (float(x) for x in m.groups())
+        # the rest of the wall, from the CLI's own phase timers (main.cpp TIMING_TAIL)
+        tail = {}
+        mt = re.search(r"TIMING_TAIL (.*)", p.stdout)
+        if mt:
+            tail = {kv.split("=")[0]: round(float(kv.split("=")[1]), 3) for kv in mt.group(1).split()}
+            tail["process_start_and_exit_s"] = round(wall - tail.get("main_s", 0.0), 3)
         arrays = os.path.join(work, "out", "CRISPR_Arrays.txt")
         n_arr = None
         if os.path.exists(arrays):
@@ -219,7 +240,7 @@ def measure_e2e(cfg: dict, spec, fastq: str, threads: int, n_kmers: int) -> dict
             "value": n_kmers / span, "unit": "k-mers/s", "T_s": round(span, 3),
             "build_lib_s": round(lib, 3), "sdbg_build_s": round(build, 3), "cycle_finder_s": round(cf, 3),
             "fastq_bytes": os.path.getsize(fastq), "fastq_GBps": round(os.path.getsize(fastq) / lib / 1e9, 2),
-            "cli_wall_s": round(wall, 3), "crispr_systems": n_arr,
+            "cli_wall_s": round(wall, 3), "cli_phases_s": tail, "crispr_systems": n_arr,
             "note": "fresh CLI process on a GPU no earlier process of this job used, FASTQ in tmpfs (/dev/shm, "
                     "pages settled by one untimed read); the span excludes process start, HIP runtime init (input "
                     "check) and the downstream steps 6-8 (cli_wall_s includes them)",
@@ -471,6 +492,10 @@ def main() -> int:
     sync()
     barrier()
     dt = (time.perf_counter() - t0) / max(1, args.steps)
+    hbm_used = None
+    if not args.dry_run:
+        free_b, total_b = torch.cuda.mem_get_info(local)
+        hbm_used = round((total_b - free_b) / 1e9, 1)  # the arena keeps its chunks: ~ the step's peak
     if dist is not None:
         t = torch.tensor([dt], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -559,6 +584,7 @@ def main() -> int:
                 "cycles": res.stats[5] if res else 0,
                 "cf_stats": list(res.stats) if res else None,
                 "start_candidates": len(res.candidates) if res else 0,
+                "hbm_used_GB": hbm_used,
             },
             "roofline": {
                 "kernel": kern,

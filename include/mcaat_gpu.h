@@ -44,6 +44,9 @@ typedef struct mcaat_comm mcaat_comm;
 /* Replaces: nothing in the reference (single process, OpenMP). Binds one GPU. */
 int mcaat_init(int device, mcaat_ctx **out);
 void mcaat_finalize(mcaat_ctx *ctx);
+/* release the device memory the context's arena holds but no live object uses (the arena keeps
+ * freed blocks for the next step; another process on the same GPU may need them) */
+void mcaat_trim(mcaat_ctx *ctx);
 const char *mcaat_last_error(void);
 int mcaat_device_count(int *n);
 
@@ -99,6 +102,11 @@ int mcaat_reads_synth_range(mcaat_ctx *ctx, const mcaat_synth_spec *spec, uint64
 int mcaat_synth_host(const mcaat_synth_spec *spec, uint64_t *packed, uint64_t *offsets);
 /* the genome sequences (n_genomes*genome_len bases, packed) and array truth */
 int mcaat_synth_genome_host(const mcaat_synth_spec *spec, uint64_t *packed);
+/* the planted CRISPR arrays as text, one line per array: "genome<TAB>index<TAB>repeat<TAB>
+ * spacer1,spacer2,...\n" (ACGT, genome strand). *len = the full length; at most cap-1 bytes and
+ * a terminating 0 are written to text (text may be null to ask the length). The ground truth a
+ * reference run would take as its benchmark file (settings benchmark_file, main.cpp:559-569). */
+int mcaat_synth_arrays_host(const mcaat_synth_spec *spec, char *text, uint64_t cap, uint64_t *len);
 
 /* ---- node_counter ----------------------------------------------------------
  * Replaces: the multiplicity counting inside MEGAHIT Read2SdbgS2::Run
@@ -289,6 +297,11 @@ void mcaat_reset_timing(mcaat_ctx *ctx);
  *   cf.fc_window       initial FindCycle speculation window
  *   cf.walk_budget     > 0: counter-driven peel walks of this many steps before the
  *                      list-ranking peel (default 0: the list-ranking peel alone)
+ *   cf.ruler_mask      1 in (mask + 1) unary nodes is a peel ruler besides the chain heads
+ *   cf.peel_list_div   first ruler-list capacity D / div (default 16; the prep pass runs again
+ *                      with the counted size when it overflows)
+ *   cf.peel_list_cap / cf.cand_cap   first capacity of the ruler and branch lists / of the
+ *                      start-candidate list (regrowth test knobs)
  *   sdbg.adj_lds       0: adjacency by per-edge directory searches in global memory
  *                      (default 1: per-run target key ranges staged in LDS)
  *   sdbg.adj_cap       largest target key range staged in LDS (default and maximum 1024;

@@ -17,6 +17,7 @@ from .lib import (  # noqa: F401
     count_edges,
     device_count,
     load_library,
+    synth_arrays,
     synth_genome_host,
     synth_host,
 )

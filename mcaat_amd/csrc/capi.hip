@@ -252,6 +252,41 @@ namespace mcaat {
 
 // genome of the synthetic community: iid bases, arrays R S1 R S2 ... R Sn R written
 // into disjoint slots (one slot per array) of each genome
+// the planted arrays of the community (what synth_genome_host writes into each slot): per
+// array its genome, index, repeat and spacers as base codes 0..3
+struct PlantedArray {
+    uint64_t g;
+    uint32_t a;
+    std::vector<int> repeat;
+    std::vector<std::vector<int>> spacers;
+};
+static void synth_arrays(const mcaat_synth_spec &s, std::vector<PlantedArray> *arrays, std::vector<uint64_t> *pos_out) {
+    for (uint64_t g = 0; g < s.n_genomes; ++g) {
+        for (uint32_t a = 0; a < s.arrays_per_genome; ++a) {
+            const uint64_t h0 = hash3(s.seed ^ 0xC415, g, a);
+            const uint32_t lr = s.repeat_len_min + (uint32_t)(h0 % (s.repeat_len_max - s.repeat_len_min + 1));
+            const uint32_t ls_max = s.spacer_len_max;
+            const uint64_t slot = s.genome_len / s.arrays_per_genome;
+            uint64_t len = (uint64_t)(s.spacers_per_array + 1) * lr + (uint64_t)s.spacers_per_array * ls_max;
+            const uint64_t room = slot > len ? slot - len : 0;
+            PlantedArray pa;
+            pa.g = g;
+            pa.a = a;
+            pa.repeat.resize(lr);
+            for (uint32_t i = 0; i < lr; ++i) pa.repeat[i] = (int)(hash3(s.seed ^ 0x4e9, g * 1000003 + a, i) & 3);
+            for (uint32_t c = 0; c < s.spacers_per_array; ++c) {
+                const uint64_t hs = hash3(s.seed ^ 0x5ACE, g * 1000003 + a, c);
+                const uint32_t ls = s.spacer_len_min + (uint32_t)(hs % (s.spacer_len_max - s.spacer_len_min + 1));
+                std::vector<int> sp(ls);
+                for (uint32_t i = 0; i < ls; ++i) sp[i] = (int)(hash3(hs, c, i) & 3);
+                pa.spacers.push_back(std::move(sp));
+            }
+            if (pos_out) pos_out->push_back(g * s.genome_len + a * slot + (room ? hash3(s.seed ^ 0x9051, g, a) % room : 0));
+            arrays->push_back(std::move(pa));
+        }
+    }
+}
+
 void synth_genome_host(const mcaat_synth_spec &s, std::vector<uint64_t> &genome) {
     check_spec(s);
     const uint64_t total = (uint64_t)s.n_genomes * s.genome_len;
@@ -263,24 +298,17 @@ void synth_genome_host(const mcaat_synth_spec &s, std::vector<uint64_t> &genome)
     };
     for (uint64_t g = 0; g < s.n_genomes; ++g)
         for (uint64_t i = 0; i < s.genome_len; ++i) setb(g * s.genome_len + i, (int)(hash3(s.seed, g, i ^ 0xA11) & 3));
-    for (uint64_t g = 0; g < s.n_genomes; ++g) {
-        for (uint32_t a = 0; a < s.arrays_per_genome; ++a) {
-            const uint64_t h0 = hash3(s.seed ^ 0xC415, g, a);
-            const uint32_t lr = s.repeat_len_min + (uint32_t)(h0 % (s.repeat_len_max - s.repeat_len_min + 1));
-            const uint32_t ls_max = s.spacer_len_max;
-            const uint64_t slot = s.genome_len / s.arrays_per_genome;
-            uint64_t len = (uint64_t)(s.spacers_per_array + 1) * lr + (uint64_t)s.spacers_per_array * ls_max;
-            const uint64_t room = slot > len ? slot - len : 0;
-            uint64_t pos = g * s.genome_len + a * slot + (room ? hash3(s.seed ^ 0x9051, g, a) % room : 0);
-            std::vector<int> rep(lr);
-            for (uint32_t i = 0; i < lr; ++i) rep[i] = (int)(hash3(s.seed ^ 0x4e9, g * 1000003 + a, i) & 3);
-            for (uint32_t c = 0; c <= s.spacers_per_array; ++c) {
-                for (uint32_t i = 0; i < lr; ++i) setb(pos++, rep[i]);
-                if (c == s.spacers_per_array) break;
-                const uint64_t hs = hash3(s.seed ^ 0x5ACE, g * 1000003 + a, c);
-                const uint32_t ls = s.spacer_len_min + (uint32_t)(hs % (s.spacer_len_max - s.spacer_len_min + 1));
-                for (uint32_t i = 0; i < ls; ++i) setb(pos++, (int)(hash3(hs, c, i) & 3));
-            }
+    // arrays R S1 R S2 ... R Sn R, one per slot
+    std::vector<PlantedArray> arrays;
+    std::vector<uint64_t> starts;
+    synth_arrays(s, &arrays, &starts);
+    for (size_t j = 0; j < arrays.size(); ++j) {
+        uint64_t pos = starts[j];
+        const PlantedArray &pa = arrays[j];
+        for (size_t c = 0; c <= pa.spacers.size(); ++c) {
+            for (int b : pa.repeat) setb(pos++, b);
+            if (c == pa.spacers.size()) break;
+            for (int b : pa.spacers[c]) setb(pos++, b);
         }
     }
 }
@@ -521,6 +549,41 @@ int mcaat_synth_genome_host(const mcaat_synth_spec *spec, uint64_t *packed) {
         const uint64_t total = (uint64_t)spec->n_genomes * spec->genome_len;
         memcpy(packed, genome.data(), 8 * ((total + 31) / 32));
     });
+}
+
+int mcaat_synth_arrays_host(const mcaat_synth_spec *spec, char *text, uint64_t cap, uint64_t *len) {
+    return guarded([&] {
+        require(spec && len, "null argument");
+        check_spec(*spec);
+        std::vector<PlantedArray> arrays;
+        synth_arrays(*spec, &arrays, nullptr);
+        std::string t;
+        auto seq = [&](const std::vector<int> &v) {
+            for (int b : v) t += "ACGT"[b];
+        };
+        for (const auto &pa : arrays) {
+            t += std::to_string(pa.g) + "\t" + std::to_string(pa.a) + "\t";
+            seq(pa.repeat);
+            t += "\t";
+            for (size_t c = 0; c < pa.spacers.size(); ++c) {
+                if (c) t += ",";
+                seq(pa.spacers[c]);
+            }
+            t += "\n";
+        }
+        *len = t.size();
+        if (text && cap) {
+            const size_t n = std::min<size_t>(cap - 1, t.size());
+            memcpy(text, t.data(), n);
+            text[n] = 0;
+        }
+    });
+}
+
+void mcaat_trim(mcaat_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    mcaat::dev_trim();
 }
 
 int mcaat_count_edges(mcaat_ctx *ctx, const mcaat_reads *r, int k, uint64_t *n_distinct, uint64_t **keys,
@@ -906,7 +969,7 @@ int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value) {
         "nc.edge_cap",     "nc.desc_cap",        "sort.msd",   "sort.wave_limit", "sort.mid_limit",
         "sort.block_limit", "cf.dls_stack",      "cf.dls_visited", "cf.fc_lock", "cf.fc_relax",
         "cf.fc_out",       "cf.fc_window",       "cf.walk_budget", "sdbg.adj_lds",   "sdbg.adj_cap",       "cf.ruler_mask",
-        "nc.overlap",      "sort.l3_counting"};
+        "nc.overlap",      "sort.l3_counting",   "cf.peel_list_div", "cf.peel_list_cap", "cf.cand_cap"};
     return guarded([&] {
         require(ctx && name, "null argument");
         bool ok = false;

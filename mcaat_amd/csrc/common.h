@@ -143,6 +143,7 @@ __device__ __forceinline__ void block_add(unsigned long long *counter, unsigned 
         for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += part[i];
         if (t) atomicAdd(counter, t);
     }
+    __syncthreads();  // part[] is reused by the next call in the same kernel
 }
 
 // workgroup barrier for LDS hand-offs only: __syncthreads() also drains every outstanding

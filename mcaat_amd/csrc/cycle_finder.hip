@@ -34,20 +34,30 @@ constexpr uint8_t kUnk = 0, kRem = 1, kSurv = 2;
 // ------------------------------- scans -------------------------------------
 // one wave per 64-edge bitmap word, kScanU words per iteration with all their loads in flight
 // together: the out-edges of e are the consecutive ids [lo, lo + cnt), so its valid out-degree
-// is a popcount of at most two bitmap words (no per-successor loads)
+// is a popcount of at most two bitmap words (no per-successor loads); the in-edges of e are the
+// positions of a 16-bit mask inside the group starting at in_lo, so the valid in-degree and the
+// self-loop test of the candidate filter are two bitmap words as well
 constexpr int kScanU = 4;
-__global__ void __launch_bounds__(kBlock) k_tips(GraphView g, uint64_t *tip_bm, unsigned long long *count) {
+
+// CollectTips and InvalidateMultiplicityOneNodes in one pass: tips from the valid bits as they
+// were before the filter (every successor window is read from `valid`, which this pass does not
+// write), the filtered bits into `post` (swapped in by the driver); counts[0] tips, counts[1]
+// every mult <= 1 edge (the reference counts valid or not)
+__global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t *tip_bm, uint64_t *post,
+                                                        unsigned long long *counts) {
     const int lane = threadIdx.x & 63;
     const uint64_t nw = (g.D + 63) / 64;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    unsigned long long acc = 0;
+    unsigned long long acc = 0, low_n = 0;
     for (uint64_t wb = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; wb < nw; wb += kScanU * wstride) {
         uint64_t sv[kScanU], oi[kScanU], a0[kScanU], a1[kScanU];
+        uint32_t mu[kScanU];
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
             const uint64_t w = wb + u * wstride, e = w * 64 + lane;
             sv[u] = w < nw ? g.valid[w] : 0;
             oi[u] = e < g.D ? g.out_info[e] : 0;
+            mu[u] = e < g.D ? g.mult[e] : 0xFFFFu;
         }
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
@@ -61,39 +71,81 @@ __global__ void __launch_bounds__(kBlock) k_tips(GraphView g, uint64_t *tip_bm, 
             const uint32_t cnt = __popc((unsigned)(oi[u] >> kIdxBits) & 0xF);
             const bool t = ((sv[u] >> lane) & 1) && (bits16(a0[u], a1[u], oi[u] & kIdxMask) & ((1u << cnt) - 1)) == 0;
             const unsigned long long m = __ballot(t);
+            const unsigned long long lowm = __ballot(mu[u] <= 1);
             if (lane == 0 && w < nw) {
-                if (tip_bm) tip_bm[w] = m;
+                tip_bm[w] = m;
+                post[w] = sv[u] & ~lowm;
                 acc += __popcll(m);
+                low_n += __popcll(lowm);
             }
         }
     }
-    block_add(count, acc);
+    block_add(counts, acc);
+    block_add(counts + 1, low_n);
 }
 
-__global__ void __launch_bounds__(kBlock) k_mult_filter(GraphView g, unsigned long long *count) {
+// the recount after the reduction (valid edges, tips) and ChunkStartNodes' candidate filter in
+// one pass: counts[0] valid, counts[1] tips (whole graph), candidates only in [lo, hi) (a rank's
+// share), appended to list while they fit in cap (counts[2] counts them all)
+__global__ void __launch_bounds__(kBlock) k_recount_candidates(GraphView g, uint64_t thr, uint64_t lo, uint64_t hi,
+                                                               uint64_t *list, uint64_t cap,
+                                                               unsigned long long *counts) {
     const int lane = threadIdx.x & 63;
+    const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const uint64_t nw = (g.D + 63) / 64;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    unsigned long long acc = 0;
-    for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nw; w += wstride) {
-        const uint64_t e = w * 64 + lane;
-        const bool low = e < g.D && g.mult[e] <= 1;
-        const unsigned long long m = __ballot(low);
-        if (lane == 0) {
-            const uint64_t old = g.valid[w];
-            g.valid[w] = old & ~m;
-            acc += __popcll(m);  // reference counts every mult<=1 edge
+    unsigned long long nvalid = 0, ntips = 0;
+    for (uint64_t wb = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; wb < nw; wb += kScanU * wstride) {
+        uint64_t sv[kScanU], oi[kScanU], ii[kScanU], a0[kScanU], a1[kScanU], b0[kScanU], b1[kScanU];
+        uint32_t mu[kScanU];
+#pragma unroll
+        for (int u = 0; u < kScanU; ++u) {
+            const uint64_t w = wb + u * wstride, e = w * 64 + lane;
+            const bool in = e < g.D;
+            sv[u] = w < nw ? g.valid[w] : 0;
+            oi[u] = in ? g.out_info[e] : 0;
+            const bool cr = in && e >= lo && e < hi && ((sv[u] >> lane) & 1);
+            ii[u] = cr ? g.in_info[e] : 0;
+            mu[u] = cr ? g.mult[e] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kScanU; ++u) {
+            const uint64_t l = oi[u] & kIdxMask, m = ii[u] & kIdxMask;
+            a0[u] = g.valid[this_word(l, nw)];
+            a1[u] = g.valid[next_word(l, nw)];
+            b0[u] = g.valid[this_word(m, nw)];
+            b1[u] = g.valid[next_word(m, nw)];
+        }
+#pragma unroll
+        for (int u = 0; u < kScanU; ++u) {
+            const uint64_t w = wb + u * wstride, e = w * 64 + lane;
+            const bool v = (sv[u] >> lane) & 1;
+            const uint32_t cnt = __popc((unsigned)(oi[u] >> kIdxBits) & 0xF);
+            const bool t = v && (bits16(a0[u], a1[u], oi[u] & kIdxMask) & ((1u << cnt) - 1)) == 0;
+            const unsigned long long tm = __ballot(t);
+            if (lane == 0 && w < nw) {
+                ntips += __popcll(tm);
+                nvalid += __popcll(sv[u]);
+            }
+            const uint64_t l = ii[u] & kIdxMask;
+            const uint32_t in = bits16(b0[u], b1[u], l) & (uint32_t)((ii[u] >> kIdxBits) & 0xFFFF);  // valid in-edges
+            // _IncomingNotEqualToCurrentNode: e must not be one of its own in-edges
+            const bool self = e >= l && e - l < 16 && ((in >> (e - l)) & 1);
+            const bool c = v && e >= lo && e < hi && (uint64_t)mu[u] > thr && __popc(in) >= 2 && !self;
+            const unsigned long long cm = __ballot(c);
+            if (cm) {
+                unsigned long long off = 0;
+                if (lane == 0) off = atomicAdd(counts + 2, (unsigned long long)__popcll(cm));
+                off = __shfl(off, 0);
+                if (c && off + __popcll(cm & lt) < cap) list[off + __popcll(cm & lt)] = e;
+            }
         }
     }
-    block_add(count, acc);
+    block_add(counts, nvalid);
+    block_add(counts + 1, ntips);
 }
 
-__global__ void __launch_bounds__(kBlock) k_popcount(const uint64_t *bm, uint64_t nw, unsigned long long *count) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    unsigned long long s = 0;
-    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) s += __popcll(bm[w]);
-    block_add(count, s);
-}
+
 
 // ------------------------------- peel --------------------------------------
 // kind[e]: low 6 bits the valid out-degree (0..4; 0x3F invalid edge), 0x80 when e is a
@@ -105,6 +157,14 @@ constexpr uint8_t kInvalid = 0x3F, kRulerBit = 0x80, kBranchSucc = 0x40;
 constexpr uint64_t kNodeMask = (1ULL << 56) - 1;
 __device__ __forceinline__ int kind_od(uint8_t k) { return k & 0x3F; }
 __device__ __forceinline__ bool kind_chain(uint8_t k) { return (k & 0xBF) == 1; }  // unary, not a ruler
+
+// Per-ruler words live in arrays indexed by the ruler's position in the ruler list, so the
+// only D-sized arrays are the flag words (4 B), nxk (8 B) and owner (4 B): 16 B per edge
+// (the graph itself is 26 B per edge; C5's ~4e9-edge graph must fit beside it).
+// jump[i]: kRRef | index of the next ruler (kRSuper when that ruler is a super ruler), or the
+// terminal node id (a non-unary node), or kNone (a ruler-less unary cycle)
+constexpr uint64_t kRRef = 1ULL << 62, kRSuper = 1ULL << 61, kRIdx = (1ULL << 40) - 1;
+constexpr uint32_t kNoOwner = 0xFFFFFFFFu;
 
 // a node's four flag bytes share one word (nf[4e + field]), so a walk or a successor check
 // touches one line per node instead of one per byte array
@@ -119,9 +179,11 @@ struct PeelArrays {
     __device__ __forceinline__ uint8_t &st(uint64_t e) const { return nf[4 * e + kFSt]; }
     __device__ __forceinline__ uchar4 flags(uint64_t e) const { return *(const uchar4 *)(nf + 4 * e); }
     uint64_t *nxk;    // successor | successor kind << 56 (unary nodes)
-    uint64_t *owner;  // non-rulers: ruler whose walk passed this node; rulers: the super ruler
-                      // whose walk over rulers passed it (kNone: none)
-    uint64_t *jump;   // rulers: next ruler or terminal | its kind << 56, then the terminal (kNone: cycle)
+    uint32_t *owner;  // rulers: their own list index; non-ruler branch successors: the list index
+                      // of the ruler whose walk passed them (kNoOwner: none); others unused
+    uint64_t *jump;   // per ruler (list index), see kRRef; after k_peel_final: terminal or kNone
+    uint32_t *sowner; // per ruler: the super ruler whose walk over rulers passed it (itself for a
+                      // super ruler, kNoOwner: none)
     const uint64_t *seed;  // tips bitmap collected before the multiplicity filter
 };
 
@@ -153,9 +215,11 @@ __global__ void __launch_bounds__(kBlock) k_peel_init(GraphView g, PeelArrays pa
 // ruler_mask + 1 others) compacted into list with one cursor atomic per 4096-edge tile,
 // branch nodes and removed seeds into blist
 constexpr int kTileJ = 16;  // 64-edge words per wave per tile
+// (list / blist hold cap / bcap entries; the cursors count past them, and the driver then
+// runs the pass again with larger lists: it is idempotent)
 __global__ void __launch_bounds__(kBlock) k_peel_prep(uint64_t D, PeelArrays pa, uint64_t ruler_mask, uint64_t *list,
-                                                      unsigned long long *cursor, uint64_t *blist,
-                                                      unsigned long long *bcursor) {
+                                                      uint64_t cap, unsigned long long *cursor, uint64_t *blist,
+                                                      uint64_t bcap, unsigned long long *bcursor) {
     __shared__ uint32_t wcnt[kBlock / 64];
     __shared__ unsigned long long tbase;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -184,7 +248,7 @@ __global__ void __launch_bounds__(kBlock) k_peel_prep(uint64_t D, PeelArrays pa,
 #pragma unroll
             for (int q = 0; q < kPB; ++q) {
                 const uint64_t e = t0 + (uint64_t)(h + q) * kBlock + threadIdx.x;
-                y[q] = od[q] == 1 ? pa.nxk[e] : 0;
+                y[q] = od[q] == 1 ? (pa.nxk[e] & kNodeMask) : 0;  // masked: prep may run again
             }
 #pragma unroll
             for (int q = 0; q < kPB; ++q) {
@@ -206,9 +270,9 @@ __global__ void __launch_bounds__(kBlock) k_peel_prep(uint64_t D, PeelArrays pa,
                     if (od[q] == 1) {
                         r = up[q] == 0 || (mix64(e ^ 0x5eed) & ruler_mask) == 0;
                         if (r) k |= kRulerBit;
-                        // owners: rulers' start empty (super-ruler walk), and of the others only
-                        // branch successors' are ever read (peel_res)
-                        if (r || bp[q]) pa.owner[e] = kNone;
+                        // owners: rulers get their list index below; of the others only branch
+                        // successors' are ever read (peel_res)
+                        if (!r && bp[q]) pa.owner[e] = kNoOwner;
                         uint8_t ky = oy[q] | (by[q] ? kBranchSucc : 0);
                         if (oy[q] == 1 && (uy[q] == 0 || (mix64(y[q] ^ 0x5eed) & ruler_mask) == 0)) ky |= kRulerBit;
                         pa.nxk[e] = y[q] | ((uint64_t)ky << 56);
@@ -229,7 +293,7 @@ __global__ void __launch_bounds__(kBlock) k_peel_prep(uint64_t D, PeelArrays pa,
                     unsigned long long off = 0;
                     if (lane == 0) off = atomicAdd(bcursor, (unsigned long long)__popcll(mb));
                     off = __shfl(off, 0);
-                    if (br) blist[off + __popcll(mb & lt)] = e;
+                    if (br && off + __popcll(mb & lt) < bcap) blist[off + __popcll(mb & lt)] = e;
                 }
             }
         }
@@ -248,15 +312,21 @@ __global__ void __launch_bounds__(kBlock) k_peel_prep(uint64_t D, PeelArrays pa,
         uint64_t off = tbase + wcnt[wave];
 #pragma unroll
         for (int j = 0; j < kTileJ; ++j) {
-            if ((m[j] >> lane) & 1) list[off + __popcll(m[j] & lt)] = t0 + (uint64_t)j * kBlock + threadIdx.x;
+            if ((m[j] >> lane) & 1) {
+                const uint64_t i = off + __popcll(m[j] & lt), e = t0 + (uint64_t)j * kBlock + threadIdx.x;
+                if (i < cap) {
+                    list[i] = e;
+                    pa.owner[e] = (uint32_t)i;
+                }
+            }
             off += __popcll(m[j]);
         }
         __syncthreads();
     }
 }
 
-// each ruler walks its chain to the next ruler or non-unary node (Brent cycle check); jump
-// keeps what it reached with that node's kind byte
+// each ruler walks its chain to the next ruler or non-unary node (Brent cycle check) and
+// records what it reached in jump (a ruler by its list index, read from its owner word)
 __global__ void __launch_bounds__(kBlock) k_peel_walk(PeelArrays pa, const uint64_t *list, uint64_t nr) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nr; i += stride) {
@@ -266,30 +336,36 @@ __global__ void __launch_bounds__(kBlock) k_peel_walk(PeelArrays pa, const uint6
         uint64_t res = kNone;
         for (;;) {
             const uint64_t y = w & kNodeMask;
-            if (!kind_chain((uint8_t)(w >> 56))) { res = w; break; }
+            const uint8_t ky = (uint8_t)(w >> 56);
+            if (!kind_chain(ky)) {
+                if (kind_od(ky) == 1)  // a ruler, reached from a unary node: super by the hash alone
+                    res = kRRef | (peel_super_hash(y) ? kRSuper : 0) | (uint64_t)pa.owner[y];
+                else
+                    res = y;
+                break;
+            }
             if (y == tort) { res = kNone; break; }  // ruler-less unary cycle reached
-            if ((w >> 56) & kBranchSucc) pa.owner[y] = r;
+            if (ky & kBranchSucc) pa.owner[y] = (uint32_t)i;
             if (power == lam) { tort = y; power <<= 1; lam = 0; }
             w = pa.nxk[y];
             ++lam;
         }
-        pa.jump[r] = res;
+        pa.jump[i] = res;
     }
 }
 
 // list ranking one level up: each super ruler walks the rulers of its chain (one jump load per
 // ruler) to the next super ruler or terminal, marking itself as their owner, and is listed
 __global__ void __launch_bounds__(kBlock) k_peel_super(PeelArrays pa, const uint64_t *list, uint64_t nr,
-                                                       uint64_t *slist, unsigned long long *scursor) {
+                                                       uint32_t *slist, unsigned long long *scursor) {
     const int lane = threadIdx.x & 63;
     const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < nr; i0 += stride) {
         const uint64_t i = i0 + threadIdx.x;
         bool sup = false;
-        uint64_t r = 0;
         if (i < nr) {
-            r = list[i];
+            const uint64_t r = list[i];
             sup = pa.upred(r) == 0 || peel_super_hash(r);
         }
         const unsigned long long m = __ballot(sup);
@@ -297,35 +373,35 @@ __global__ void __launch_bounds__(kBlock) k_peel_super(PeelArrays pa, const uint
             unsigned long long off = 0;
             if (lane == 0) off = atomicAdd(scursor, (unsigned long long)__popcll(m));
             off = __shfl(off, 0);
-            if (sup) slist[off + __popcll(m & lt)] = r;
+            if (sup) slist[off + __popcll(m & lt)] = (uint32_t)i;
         }
         if (!sup) continue;
-        uint64_t w = pa.jump[r], tort = r, power = 1, lam = 1;
+        pa.sowner[i] = (uint32_t)i;
+        uint64_t w = pa.jump[i], tort = i, power = 1, lam = 1;
         for (;;) {
-            if (w == kNone) break;
-            const uint64_t x = w & kNodeMask;
-            if (kind_od((uint8_t)(w >> 56)) != 1 || peel_super_hash(x)) break;  // terminal or super ruler
+            if (w == kNone || !(w & kRRef) || (w & kRSuper)) break;  // cycle, terminal or super ruler
+            const uint64_t x = w & kRIdx;
             if (x == tort) { w = kNone; break; }  // a cycle of rulers without a super ruler
-            pa.owner[x] = r;
+            pa.sowner[x] = (uint32_t)i;
             if (power == lam) { tort = x; power <<= 1; lam = 0; }
             w = pa.jump[x];
             ++lam;
         }
         // a super ruler's jump is only read by its own walks from here on (walks stop at it)
-        pa.jump[r] = w;
+        pa.jump[i] = w;
     }
 }
 
 // one pointer-jumping round over the super rulers; *changed is raised when some super ruler
-// still pointed at a unary node (a round that changes nothing proves every jump final)
-__global__ void __launch_bounds__(kBlock) k_peel_jump(PeelArrays pa, const uint64_t *slist, uint64_t ns, int *changed) {
+// still pointed at a ruler (a round that changes nothing proves every jump final)
+__global__ void __launch_bounds__(kBlock) k_peel_jump(PeelArrays pa, const uint32_t *slist, uint64_t ns, int *changed) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     bool ch = false;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride) {
-        const uint64_t s = slist[i];
+        const uint32_t s = slist[i];
         const uint64_t j = pa.jump[s];
-        if (j != kNone && kind_od((uint8_t)(j >> 56)) == 1) {
-            const uint64_t t = pa.jump[j & kNodeMask];
+        if (j != kNone && (j & kRRef)) {
+            const uint64_t t = pa.jump[j & kRIdx];
             if (t != j) {
                 pa.jump[s] = t;
                 ch = true;
@@ -335,20 +411,14 @@ __global__ void __launch_bounds__(kBlock) k_peel_jump(PeelArrays pa, const uint6
     if (__ballot(ch) && (threadIdx.x & 63) == 0) *changed = 1;
 }
 
-// every ruler's terminal: a super ruler's own jump, another ruler's through its owner (kNone:
-// on a cycle); the kind byte is dropped (a super ruler's word is the same node either way)
-__global__ void __launch_bounds__(kBlock) k_peel_final(PeelArrays pa, const uint64_t *list, uint64_t nr) {
+// every ruler's terminal: a super ruler's own jump, another ruler's through its super owner
+// (kNone: on a cycle); only non-super entries are written, only super entries read
+__global__ void __launch_bounds__(kBlock) k_peel_final(PeelArrays pa, uint64_t nr) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nr; i += stride) {
-        const uint64_t r = list[i];
-        uint64_t v;
-        if (pa.upred(r) == 0 || peel_super_hash(r)) {
-            v = pa.jump[r];
-        } else {
-            const uint64_t o = pa.owner[r];
-            v = o == kNone ? kNone : pa.jump[o];
-        }
-        pa.jump[r] = v == kNone ? kNone : (v & kNodeMask);
+        const uint32_t o = pa.sowner[i];
+        if (o == (uint32_t)i) continue;
+        pa.jump[i] = o == kNoOwner ? kNone : pa.jump[o];
     }
 }
 
@@ -356,10 +426,10 @@ __device__ __forceinline__ uint8_t peel_res(const PeelArrays &pa, uint64_t y) {
     const uchar4 f = pa.flags(y);
     const uint8_t k = f.x;
     if (kind_od(k) != 1) return f.w;
-    const uint64_t o = (k & kRulerBit) ? y : pa.owner[y];
-    if (o == kNone) return kSurv;  // unary node on a ruler-less cycle
+    const uint32_t o = pa.owner[y];
+    if (o == kNoOwner) return kSurv;  // unary node on a ruler-less cycle
     const uint64_t t = pa.jump[o];
-    if (t == kNone) return kSurv;
+    if (t == kNone || (t & kRRef)) return kSurv;
     const uchar4 ft = pa.flags(t);
     if (kind_od(ft.x) == 1) return kSurv;  // chain ends in a unary cycle
     return ft.w;
@@ -467,50 +537,6 @@ __global__ void __launch_bounds__(kBlock) k_ids_to_bits(const uint64_t *ids, uin
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
         atomicOr((unsigned long long *)&bm[ids[i] >> 6], 1ull << (ids[i] & 63));
-}
-
-// --------------------------- start candidates --------------------------------
-// ids [lo, hi) (a rank's share of the scan; [0, D) on one GPU). The in-edges of e are the
-// positions of a 16-bit mask inside the group starting at in_lo, so the valid in-degree and the
-// self-loop test are two bitmap words; kScanU blocks of edges per iteration, loads in flight
-// together
-__global__ void __launch_bounds__(kBlock) k_candidates(GraphView g, uint64_t thr, uint64_t lo, uint64_t hi,
-                                                       uint64_t *list, unsigned long long *cursor) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    const int lane = threadIdx.x & 63;
-    const uint64_t nw = (g.D + 63) / 64;
-    for (uint64_t base = lo + (uint64_t)blockIdx.x * blockDim.x; base < hi; base += kScanU * stride) {
-        uint64_t sv[kScanU], ii[kScanU], a0[kScanU], a1[kScanU];
-        uint32_t mu[kScanU];
-#pragma unroll
-        for (int u = 0; u < kScanU; ++u) {
-            const uint64_t e = base + u * stride + threadIdx.x;
-            const bool in = e < hi;
-            sv[u] = in ? g.valid[e >> 6] : 0;
-            mu[u] = in ? g.mult[e] : 0;
-            ii[u] = in ? g.in_info[e] : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < kScanU; ++u) {
-            const uint64_t l = ii[u] & kIdxMask;
-            a0[u] = g.valid[this_word(l, nw)];
-            a1[u] = g.valid[next_word(l, nw)];
-        }
-#pragma unroll
-        for (int u = 0; u < kScanU; ++u) {
-            const uint64_t e = base + u * stride + threadIdx.x;
-            const uint64_t l = ii[u] & kIdxMask;
-            const uint32_t in = bits16(a0[u], a1[u], l) & (uint32_t)((ii[u] >> kIdxBits) & 0xFFFF);  // valid in-edges
-            // _IncomingNotEqualToCurrentNode: e must not be one of its own in-edges
-            const bool self = e >= l && e - l < 16 && ((in >> (e - l)) & 1);
-            const bool c = e < hi && ((sv[u] >> (e & 63)) & 1) && (uint64_t)mu[u] > thr && __popc(in) >= 2 && !self;
-            const unsigned long long m = __ballot(c);
-            unsigned long long off = 0;
-            if (lane == 0 && m) off = atomicAdd(cursor, (unsigned long long)__popcll(m));
-            off = __shfl(off, 0);
-            if (c) list[off + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))))] = e;
-        }
-    }
 }
 
 // ------------------------------ DLS ------------------------------------------
@@ -1216,29 +1242,51 @@ static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm) {
     if (!D) return;
     GraphView v = g->view();
     DevBuf<uint8_t> nf(4 * D);
-    DevBuf<uint64_t> nxk(D), owner(D), jump(D);
+    DevBuf<uint64_t> nxk(D);
+    DevBuf<uint32_t> owner(D);
     HIP_OK(hipMemsetAsync(nf.p, 0, nf.bytes(), st));  // the flag bytes other nodes set
-    PeelArrays pa{nf.p, nxk.p, owner.p, jump.p, seed_bm};
+    PeelArrays pa{nf.p, nxk.p, owner.p, nullptr, nullptr, seed_bm};
     hipLaunchKernelGGL(k_peel_init, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, v, pa);
     LAUNCH_OK();
-    DevBuf<unsigned long long> cur(4);
-    DevBuf<uint64_t> list(D), blist(D);
-    HIP_OK(hipMemsetAsync(cur.p, 0, cur.bytes(), st));
     // 1 in (ruler_mask + 1) unary nodes is a ruler besides the chain heads: a walk costs one
     // random read per node whatever the spacing; the rulers are then ranked one level up
     // (1 in 64 of them, plus the heads, are super rulers) before pointer jumping
     const uint64_t ruler_mask = (uint64_t)std::max<int64_t>(0, knob(ctx, "cf.ruler_mask", 63));
-    hipLaunchKernelGGL(k_peel_prep, dim3(grid_for(D, kBlock * kTileJ)), dim3(kBlock), 0, st, D, pa, ruler_mask,
-                       list.p, cur.p, blist.p, cur.p + 1);
-    LAUNCH_OK();
-    unsigned long long hc[2];
-    HIP_OK(hipMemcpyAsync(hc, cur.p, 16, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    const uint64_t nr = hc[0], nb = hc[1];
+    // the ruler and branch lists start at a fraction of D (rulers: the chain heads plus 1 in 64
+    // unary nodes; branch nodes are rarer still) and the pass runs again if either overflowed
+    const int64_t div = std::max<int64_t>(1, knob(ctx, "cf.peel_list_div", 16));
+    uint64_t cap = std::min<uint64_t>(D, D / (uint64_t)div + (1u << 16)), bcap = std::min<uint64_t>(D, D / 64 + (1u << 16));
+    if (knob_set(ctx, "cf.peel_list_cap"))  // test knob: both lists start this small
+        cap = bcap = (uint64_t)std::max<int64_t>(1, knob(ctx, "cf.peel_list_cap", 1));
+    DevBuf<unsigned long long> cur(4);
+    DevBuf<uint64_t> list, blist;
+    uint64_t nr = 0, nb = 0;
+    for (;;) {
+        list.alloc(cap);
+        blist.alloc(bcap);
+        HIP_OK(hipMemsetAsync(cur.p, 0, cur.bytes(), st));
+        hipLaunchKernelGGL(k_peel_prep, dim3(grid_for(D, kBlock * kTileJ)), dim3(kBlock), 0, st, D, pa, ruler_mask,
+                           list.p, cap, cur.p, blist.p, bcap, cur.p + 1);
+        LAUNCH_OK();
+        unsigned long long hc[2];
+        HIP_OK(hipMemcpyAsync(hc, cur.p, 16, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        nr = hc[0];
+        nb = hc[1];
+        if (nr <= cap && nb <= bcap) break;
+        cap = std::max<uint64_t>(cap, nr);
+        bcap = std::max<uint64_t>(bcap, nb);
+    }
+    if (nr >= kNoOwner) throw Error(MCAAT_E_CAPACITY, "peel: 2^32 or more rulers");
+    DevBuf<uint64_t> jump(nr ? nr : 1);
+    DevBuf<uint32_t> sowner(nr ? nr : 1);
+    pa.jump = jump.p;
+    pa.sowner = sowner.p;
     if (nr) {
         hipLaunchKernelGGL(k_peel_walk, dim3(grid_for(nr, kBlock)), dim3(kBlock), 0, st, pa, list.p, nr);
         LAUNCH_OK();
-        DevBuf<uint64_t> slist(nr);
+        HIP_OK(hipMemsetAsync(sowner.p, 0xFF, 4 * nr, st));
+        DevBuf<uint32_t> slist(nr);
         hipLaunchKernelGGL(k_peel_super, dim3(grid_for(nr, kBlock)), dim3(kBlock), 0, st, pa, list.p, nr, slist.p,
                            cur.p + 2);
         LAUNCH_OK();
@@ -1260,7 +1308,7 @@ static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm) {
                 if (!hchg) break;
             }
         }
-        hipLaunchKernelGGL(k_peel_final, dim3(grid_for(nr, kBlock)), dim3(kBlock), 0, st, pa, list.p, nr);
+        hipLaunchKernelGGL(k_peel_final, dim3(grid_for(nr, kBlock)), dim3(kBlock), 0, st, pa, nr);
         LAUNCH_OK();
     }
     DevBuf<int> changed(1);
@@ -1769,8 +1817,6 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
     StageTimer timer(ctx);
     if (comm && comm->world == 1) comm = nullptr;
     const int N = comm ? comm->world : 1, R = comm ? comm->rank : 0;
-    DevBuf<unsigned long long> cnt(1);
-    auto zero = [&]() { HIP_OK(hipMemsetAsync(cnt.p, 0, 8, st)); };
     // grid-stride scans whose per-block totals meet in one counter: a capped grid keeps that
     // counter's atomics to a few thousand
     const unsigned wgrid = grid_for(nw * 64, kBlock, (unsigned)ctx->n_cu * 16);
@@ -1778,57 +1824,62 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
     // Steps 1-4 change the valid bits every later step reads, so every rank runs them on its
     // replica of the graph (the peel is a global fixpoint); the scans of step 5 and the
     // searches of steps 5-6 are split over the ranks.
-    // 1. CollectTips (before the multiplicity filter) -> seeds of the reduction
+    // 1-2. CollectTips (before the multiplicity filter) -> seeds of the reduction, and
+    // InvalidateMultiplicityOneNodes, in one pass (the filtered bits go to a second bitmap)
     DevBuf<uint64_t> seeds(nw);
-    zero();
-    hipLaunchKernelGGL(k_tips, dim3(wgrid), dim3(kBlock), 0, st, v, seeds.p, cnt.p);
-    LAUNCH_OK();
-    out->stats[0] = read_counter(ctx, cnt.p);
-    timer.mark("collect_tips");
-    verbose_mark(ctx, "cf.collect_tips");
-    // 2. InvalidateMultiplicityOneNodes
-    zero();
-    hipLaunchKernelGGL(k_mult_filter, dim3(wgrid), dim3(kBlock), 0, st, v, cnt.p);
-    LAUNCH_OK();
-    out->stats[1] = read_counter(ctx, cnt.p);
-    timer.mark("mult_filter");
+    {
+        DevBuf<uint64_t> post(nw);
+        DevBuf<unsigned long long> c2(2);
+        HIP_OK(hipMemsetAsync(c2.p, 0, 16, st));
+        hipLaunchKernelGGL(k_tips_filter, dim3(wgrid), dim3(kBlock), 0, st, v, seeds.p, post.p, c2.p);
+        LAUNCH_OK();
+        unsigned long long hc[2];
+        HIP_OK(hipMemcpyAsync(hc, c2.p, 16, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        out->stats[0] = hc[0];
+        out->stats[1] = hc[1];
+        std::swap(g->valid, post);  // the pre-filter bitmap is released here
+        v = g->view();
+    }
+    timer.mark("tips_filter");
+    verbose_mark(ctx, "cf.tips_filter");
     // 3. RecursiveReduction from every seed
-    verbose_mark(ctx, "cf.mult_filter");
     run_peel(g, seeds.p);
     seeds.release();
     timer.mark("peel");
     verbose_mark(ctx, "cf.peel");
-    // 4. valid count + tips after pruning
-    zero();
-    hipLaunchKernelGGL(k_popcount, dim3(grid_for(nw, kBlock, (unsigned)ctx->n_cu * 16)), dim3(kBlock), 0, st,
-                       g->valid.p, nw, cnt.p);
-    LAUNCH_OK();
-    out->stats[2] = read_counter(ctx, cnt.p);
-    zero();
-    hipLaunchKernelGGL(k_tips, dim3(wgrid), dim3(kBlock), 0, st, v, (uint64_t *)nullptr, cnt.p);
-    LAUNCH_OK();
-    out->stats[3] = read_counter(ctx, cnt.p);
-    timer.mark("recount");
-    // 5. ChunkStartNodes. Its InvalidateMultiplicityOneNodes (cycle_finder.cpp:391-393) is a
-    // no-op here: step 2 already cleared every mult <= 1 edge and nothing since sets a valid
-    // bit, and the count it would print is stats[1] (every mult <= 1 edge, valid or not)
+    // 4-5. valid count + tips after pruning, and ChunkStartNodes' candidate filter (its
+    // InvalidateMultiplicityOneNodes, cycle_finder.cpp:391-393, is a no-op here: step 2 already
+    // cleared every mult <= 1 edge and nothing since sets a valid bit, and the count it would
+    // print is stats[1], every mult <= 1 edge, valid or not)
     std::vector<uint64_t> cand;
     {
-        // rank R scans ids [R*D/N, (R+1)*D/N)
+        // rank R takes the candidates among ids [R*D/N, (R+1)*D/N)
         const uint64_t lo = (uint64_t)((unsigned __int128)D * R / N), hi = (uint64_t)((unsigned __int128)D * (R + 1) / N);
-        DevBuf<uint64_t> list(hi > lo ? hi - lo : 1);
-        zero();
-        if (hi > lo) {
-            hipLaunchKernelGGL(k_candidates, dim3(grid_for(hi - lo, kBlock * kScanU, (unsigned)ctx->n_cu * 16)), dim3(kBlock), 0, st, v,
-                               p.threshold_multiplicity, lo, hi, list.p, cnt.p);
+        uint64_t cap = std::min<uint64_t>(hi - lo, (hi - lo) / 64 + (1u << 20));
+        if (knob_set(ctx, "cf.cand_cap")) cap = (uint64_t)std::max<int64_t>(1, knob(ctx, "cf.cand_cap", 1));  // test knob
+        DevBuf<unsigned long long> c3(3);
+        for (;;) {
+            DevBuf<uint64_t> list(cap ? cap : 1);
+            HIP_OK(hipMemsetAsync(c3.p, 0, 24, st));
+            hipLaunchKernelGGL(k_recount_candidates, dim3(wgrid), dim3(kBlock), 0, st, v, (uint64_t)p.threshold_multiplicity,
+                               lo, hi, list.p, cap, c3.p);
             LAUNCH_OK();
-        }
-        const uint64_t nc = read_counter(ctx, cnt.p);
-        cand.resize(nc);
-        if (nc) {
-            d2h(ctx, cand.data(), list.p, 8 * nc);
+            unsigned long long hc[3];
+            HIP_OK(hipMemcpyAsync(hc, c3.p, 24, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipStreamSynchronize(st));
+            out->stats[2] = hc[0];
+            out->stats[3] = hc[1];
+            if (hc[2] > cap) {  // more candidates than the first list held: the pass again, sized
+                cap = hc[2];
+                continue;
+            }
+            cand.resize(hc[2]);
+            if (hc[2]) d2h(ctx, cand.data(), list.p, 8 * hc[2]);
+            break;
         }
     }
+    timer.mark("recount");
     std::sort(cand.begin(), cand.end());
     if (comm) cand = gather_sorted(comm, cand);
     timer.mark("candidates");

@@ -6,6 +6,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <cerrno>
 #include <chrono>
 #include <csignal>
 #include <cstdio>
@@ -137,12 +138,22 @@ struct Ranks {
     void watch() {
         std::vector<pid_t> kids = children;
         watcher = std::thread([kids]() {
-            for (size_t i = 0; i < kids.size(); ++i) {
+            // whichever rank ends first is reaped first: a failure of rank 3 is seen while
+            // rank 1 is still running
+            for (size_t left = kids.size(); left > 0;) {
                 int st = 0;
-                if (waitpid(kids[i], &st, 0) < 0) continue;
+                const pid_t p = waitpid(-1, &st, 0);
+                if (p < 0) {
+                    if (errno == EINTR) continue;
+                    break;
+                }
+                size_t r = 0;
+                while (r < kids.size() && kids[r] != p) ++r;
+                if (r == kids.size()) continue;
+                --left;
                 if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) {
-                    std::cerr << "rank " << i + 1 << " failed; ending the run" << std::endl;
-                    for (pid_t p : kids) kill(p, SIGTERM);
+                    std::cerr << "rank " << r + 1 << " failed; ending the run" << std::endl;
+                    for (pid_t q : kids) kill(q, SIGTERM);
                     _exit(1);
                 }
             }
@@ -158,7 +169,12 @@ static void banner(const char *title) {
 
 static int run(Settings &settings, Ranks &ranks);
 
+using Clock = std::chrono::steady_clock;
+static Clock::time_point g_main_start;
+static double since(Clock::time_point t) { return std::chrono::duration<double>(Clock::now() - t).count(); }
+
 int main(int argc, char **argv) {
+    g_main_start = Clock::now();
     try {
         Settings settings = parse_arguments(argc, argv);
         if (check_for_error(settings)) {  // main.cpp:499-513
@@ -175,7 +191,12 @@ int main(int argc, char **argv) {
             return 1;
         }
         Ranks ranks;
-        if (settings.gpus > 1) ranks.fork_ranks(settings);  // before any GPU call
+        if (settings.gpus > 1) {
+            ranks.fork_ranks(settings);  // before any GPU call
+            // rank 0 reaps the children from here on: a rank that dies before it joins the
+            // communicator (ncclCommInitRank has no timeout) ends the run instead of hanging it
+            if (settings.rank == 0) ranks.watch();
+        }
         try {
             return run(settings, ranks);
         } catch (...) {
@@ -197,11 +218,13 @@ static int run(Settings &settings, Ranks &ranks) {
         (void)mcaat_device_count(&n_dev);
     }
     if (settings.gpus > 1) {
+        if (const char *e = getenv("MCAAT_TEST_RANK_EXIT"))  // test hook: this rank dies before joining
+            if (atoi(e) == settings.rank && settings.rank > 0) _exit(3);
         ranks.connect(settings);
-        if (rank0) ranks.watch();
     }
     {
         using clk = std::chrono::steady_clock;
+        const double t_span_start = since(g_main_start);
         const auto t_start = clk::now();
         SDBGBuild sdbg_build(settings);                        // main.cpp:517
         const auto t_built = clk::now();
@@ -221,6 +244,7 @@ static int run(Settings &settings, Ranks &ranks) {
                      sec(t_end - t_start), sec(t_built - t_start), sdbg_build.lib_seconds, sec(t_end - t_built));
             std::cout << line << std::endl;
         }
+        const double t_span_end = since(g_main_start);
         auto cycles_map = cycle_finder.results;
         std::cout << "Number of nodes in results: " << cycles_map.size() << std::endl;
         auto cycles = cycles_map_to_cycles(cycles_map);        // main.cpp:542
@@ -235,6 +259,7 @@ static int run(Settings &settings, Ranks &ranks) {
                 }
         }
 
+        const double t_cycles_out = since(g_main_start);
         banner("🔸STEP 6: Finding relevant reads");             // main.cpp:544-551
         int n_files = 0;
         {
@@ -250,10 +275,12 @@ static int run(Settings &settings, Ranks &ranks) {
             settings.mcomm = nullptr;
         }
         if (!rank0) return 0;  // rank 0 writes the outputs
+        const double t_step6 = since(g_main_start);
 
         banner("🔸STEP 7: Order the spacers");                  // main.cpp:553-556
         const auto found_systems = run_and_debug_spacer_ordering(reads, sdbg, cycles);
 
+        const double t_step7 = since(g_main_start);
         if (settings.benchmark_file != "") {                   // main.cpp:559-569
             banner("🔸STEP 8: Compare to ground of truth using benchmark file");
             run_and_debug_benchmark_results(settings, found_systems);
@@ -263,6 +290,7 @@ static int run(Settings &settings, Ranks &ranks) {
         }
         std::cout << "══════════════════════════════════════════════" << std::endl;
 
+        const double t_step8 = since(g_main_start);
         std::cout << "POST PROCESSING START:" << std::endl;    // main.cpp:573-581
         std::unordered_map<std::string, std::vector<std::string>> all_systems;
         for (const auto &[_sequence, repeat, spacers, _conf_a, _conf_b] : found_systems) all_systems[repeat] = spacers;
@@ -276,6 +304,18 @@ static int run(Settings &settings, Ranks &ranks) {
             std::cerr << "Warning: Could not remove graph folder: " << e.what() << std::endl;
         }
         if (ranks.watcher.joinable()) ranks.watcher.join();  // every rank ended cleanly
+        {
+            // where the rest of the wall goes (seconds since main; process start and exit are
+            // outside): runtime init before the span, the span, cycles.txt, steps 6/7/8 and
+            // CRISPRAnalyzer
+            char line[320];
+            snprintf(line, sizeof line,
+                     "TIMING_TAIL init_s=%.6f span_end_s=%.6f cycles_out_s=%.6f step6_s=%.6f step7_s=%.6f "
+                     "step8_s=%.6f analyzer_s=%.6f main_s=%.6f",
+                     t_span_start, t_span_end, t_cycles_out - t_span_end, t_step6 - t_cycles_out,
+                     t_step7 - t_step6, t_step8 - t_step7, since(g_main_start) - t_step8, since(g_main_start));
+            std::cout << line << std::endl;
+        }
         return 0;
     }
 }

@@ -70,6 +70,8 @@ SIGNATURES = {
     "mcaat_reads_synth": (C.c_int, [C.c_void_p, C.POINTER(_SynthSpec), C.POINTER(C.c_void_p)]),
     "mcaat_synth_host": (C.c_int, [C.POINTER(_SynthSpec), _u64p, _u64p]),
     "mcaat_synth_genome_host": (C.c_int, [C.POINTER(_SynthSpec), _u64p]),
+    "mcaat_synth_arrays_host": (C.c_int, [C.POINTER(_SynthSpec), C.c_char_p, C.c_uint64, _u64p]),
+    "mcaat_trim": (None, [C.c_void_p]),
     "mcaat_count_edges": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, _u64p, C.POINTER(_u64p), C.POINTER(_u32p)]),
     "mcaat_free": (None, [C.c_void_p]),
     "mcaat_build_graph": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
@@ -207,6 +209,22 @@ def synth_genome_host(spec: SynthSpec) -> np.ndarray:
     return packed
 
 
+def synth_arrays(spec: SynthSpec) -> List[Tuple[int, int, str, List[str]]]:
+    """The planted CRISPR arrays of the synthetic community: (genome, index, repeat, spacers),
+    genome strand (mcaat_synth_arrays_host)."""
+    lib = load_library()
+    s = spec.to_c()
+    n = C.c_uint64(0)
+    _check(lib.mcaat_synth_arrays_host(C.byref(s), None, 0, C.byref(n)))
+    buf = C.create_string_buffer(n.value + 1)
+    _check(lib.mcaat_synth_arrays_host(C.byref(s), buf, n.value + 1, C.byref(n)))
+    out = []
+    for line in buf.value.decode().splitlines():
+        g, a, rep, sp = line.split("\t")
+        out.append((int(g), int(a), rep, sp.split(",") if sp else []))
+    return out
+
+
 class Context:
     """One GPU, one HIP stream (mcaat_ctx)."""
 
@@ -244,6 +262,10 @@ class Context:
 
     def reset_timing(self) -> None:
         self._lib.mcaat_reset_timing(self.h)
+
+    def trim(self) -> None:
+        """Release device memory the arena keeps but nothing uses (mcaat_trim)."""
+        self._lib.mcaat_trim(self.h)
 
     def set_knob(self, name: str, value: int) -> None:
         """Size limit that picks a code path (include/mcaat_gpu.h, mcaat_set_knob); value < 0

@@ -62,6 +62,9 @@ KNOBS = {
     # and with sparse rulers (long walks, few super rulers)
     "peel_dense_rulers": {"cf.ruler_mask": 0},
     "peel_sparse_rulers": {"cf.ruler_mask": 4095},
+    # the ruler / branch lists and the candidate list start with one entry: the passes that
+    # fill them run again with the counted sizes
+    "list_regrow": {"cf.peel_list_cap": 1, "cf.cand_cap": 1},
     # passes B and C of successive groups in turn on one stream
     "nc_no_overlap": {"nc.overlap": 0, "nc.group_budget": 1 << 14},
     # adjacency: per-edge global directory searches, and the LDS-range kernel with every range
