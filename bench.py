@@ -44,40 +44,7 @@ PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 # node_counter kernels timed with HIP events on the library stream (mcaat_kernel_timing)
 HOT_KERNELS = ("sk_scatter", "l2_hist", "l2_partition", "lds_count")
 
-CONFIGS = {
-    # C3: 300 Mbp community (200 genomes x 1.5 Mbp, 2 arrays each), 300M SE reads, k=27
-    "c3": dict(spec=M.SynthSpec(seed=3, n_genomes=200, genome_len=1_500_000, arrays_per_genome=2,
-                                spacers_per_array=12, repeat_len_min=30, repeat_len_max=36, spacer_len_min=30,
-                                spacer_len_max=36, read_len=150, n_reads=300_000_000, error_rate=2.0e-4),
-               k=27, thr=20, name="C3 1B-node synthetic metagenome (300M x 150bp SE, k=27, thr=20)",
-               # CPU-baseline sample in the same regime: 150x coverage, D/N_occ ~ 0.027 as at C3
-               sample=M.SynthSpec(seed=3, n_genomes=20, genome_len=100_000, arrays_per_genome=2, spacers_per_array=12,
-                                  repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
-                                  read_len=150, n_reads=2_000_000, error_rate=2.0e-4)),
-    # C2: 50M PE reads (25M pairs) over a 400 Mbp community with 500 CRISPR arrays, 0.5 % errors
-    # (250 genomes x 1.6 Mbp x 2 arrays: the generator places whole arrays per genome)
-    "c2": dict(spec=M.SynthSpec(seed=2, n_genomes=250, genome_len=1_600_000, arrays_per_genome=2,
-                                spacers_per_array=12, repeat_len_min=30, repeat_len_max=36, spacer_len_min=30,
-                                spacer_len_max=36, read_len=150, n_reads=50_000_000, error_rate=5.0e-3, paired=True),
-               k=27, thr=20, name="C2 50M PE synthetic metagenome (400 Mbp, 500 arrays, e=0.5%, k=27)",
-               sample=M.SynthSpec(seed=2, n_genomes=40, genome_len=200_000, arrays_per_genome=2, spacers_per_array=12,
-                                  repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
-                                  read_len=150, n_reads=1_000_000, error_rate=5.0e-3, paired=True)),
-    # C5: the low-abundance regime (include/settings.h:33-38 with threshold_multiplicity=2,
-    # low_abundance=true, cycle min/max 27/77) on the C3 community, substitution errors raised
-    # until the graph passes 2^31 edges (D ~ 4e9 is BASELINE's 8-GPU figure; this is the
-    # largest D one GPU's 288 GB holds through the build)
-    "c5": dict(spec=M.SynthSpec(seed=5, n_genomes=200, genome_len=1_500_000, arrays_per_genome=2,
-                                spacers_per_array=12, repeat_len_min=30, repeat_len_max=36, spacer_len_min=30,
-                                spacer_len_max=36, read_len=150, n_reads=300_000_000, error_rate=1.7e-3),
-               k=27, thr=2, name="C5 low-abundance regime on one GPU (300M x 150bp SE, e=0.17%, k=27, thr=2, "
-                                 "low_abundance, 27/77)",
-               sample=M.SynthSpec(seed=5, n_genomes=20, genome_len=100_000, arrays_per_genome=2, spacers_per_array=12,
-                                  repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
-                                  read_len=150, n_reads=2_000_000, error_rate=1.7e-3)),
-    "tiny": dict(spec=M.SynthSpec(), k=27, thr=20, name="C1 tiny (10k x 150bp, 50 kbp genome, k=27)",
-                 sample=M.SynthSpec()),
-}
+from mcaat_amd.configs import CONFIGS  # noqa: E402
 
 
 def n_occ(spec: M.SynthSpec, k: int) -> int:
@@ -348,7 +315,8 @@ def measure_ingest(ctx, spec, n_reads: int) -> dict:
         ok = ok and bool(n_rec == n_reads and np.array_equal(rp[:nw], want[:nw]) and int(ro[-1]) == nb)
         gpu_ms = 0.0
         kern = {}
-        for n in ("fq_parse", "fq_records", "fq_emit"):
+        host_pack = ctx.kernel_timing("fq_concat")[1] > 0
+        for n in ("fq_parse", "fq_records", "fq_emit", "fq_concat"):
             a, l, by = ctx.kernel_timing(n)
             gpu_ms += a * l
             kern[n] = {"ms": round(a * l, 3), "GBps": round(by / (a * 1e-3) / 1e9, 1) if a > 0 else None}
@@ -359,6 +327,7 @@ def measure_ingest(ctx, spec, n_reads: int) -> dict:
         "reads": n_reads, "file_bytes": size, "wall_s": round(wall, 3), "first_call_s": round(first, 3),
         "text_GBps": round(size / first / 1e9, 2), "text_GBps_warm_context": round(size / wall / 1e9, 2),
         "reads_per_s": n_reads / first, "gpu_parse_ms": round(gpu_ms, 3), "kernels": kern, "library_matches": ok,
+        "path": "host 2-bit packer (csrc/fastq_pack.hip)" if host_pack else "GPU text parser (csrc/fastq_ingest.hip)",
         "note": "page-cached plain FASTQ; text_GBps = first call on the context (includes allocating the "
                 "reader's pinned chunks), warm = second call reusing them; wall includes host read, PCIe upload "
                 "and GPU parse",

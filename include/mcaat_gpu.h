@@ -302,6 +302,8 @@ void mcaat_reset_timing(mcaat_ctx *ctx);
  *                      with the counted size when it overflows)
  *   cf.peel_list_cap / cf.cand_cap   first capacity of the ruler and branch lists / of the
  *                      start-candidate list (regrowth test knobs)
+ *   fq.hostpack        0: FASTQ always through the GPU text parser (default 1: plain files of
+ *                      upper-case ACGT 4-line records packed to 2 bits by host threads first)
  *   sdbg.adj_lds       0: adjacency by per-edge directory searches in global memory
  *                      (default 1: per-run target key ranges staged in LDS)
  *   sdbg.adj_cap       largest target key range staged in LDS (default and maximum 1024;

@@ -385,6 +385,7 @@ void mcaat_finalize(mcaat_ctx *ctx) {
         if (p) (void)hipHostFree(p);
     for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
     if (ctx->bounce) (void)hipHostFree(ctx->bounce);
+    if (ctx->pack_pinned) (void)hipHostFree(ctx->pack_pinned);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -969,7 +970,8 @@ int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value) {
         "nc.edge_cap",     "nc.desc_cap",        "sort.msd",   "sort.wave_limit", "sort.mid_limit",
         "sort.block_limit", "cf.dls_stack",      "cf.dls_visited", "cf.fc_lock", "cf.fc_relax",
         "cf.fc_out",       "cf.fc_window",       "cf.walk_budget", "sdbg.adj_lds",   "sdbg.adj_cap",       "cf.ruler_mask",
-        "nc.overlap",      "sort.l3_counting",   "cf.peel_list_div", "cf.peel_list_cap", "cf.cand_cap"};
+        "nc.overlap",      "sort.l3_counting",   "cf.peel_list_div", "cf.peel_list_cap", "cf.cand_cap",
+        "fq.hostpack"};
     return guarded([&] {
         require(ctx && name, "null argument");
         bool ok = false;

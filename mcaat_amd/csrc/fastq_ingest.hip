@@ -363,6 +363,9 @@ size_t fastq_chunk_bytes() {
 // after the first are reversed and complemented in the mapping view (paired-end R2).
 void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_reads *r,
                   const std::vector<std::pair<uint64_t, uint64_t>> *ranges) {
+    // plain files of well-formed upper-case ACGT records: packed by host threads (PCIe carries
+    // 2 bits per base); any other input falls through to the text parser below
+    if (fastq_hostpack(ctx, files, n_files, ranges, r)) return;
     const size_t CH = fastq_chunk_bytes();
     const size_t R = std::max<size_t>(CH / 4, 4096);  // carry reserve: the longest record that fits
     const size_t cap = R + CH + 2 * kSeg;

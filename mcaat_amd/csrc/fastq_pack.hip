@@ -1,0 +1,496 @@
+// fastq_pack.hip — BuildLib's fast path: host threads pack 4-line FASTQ straight to 2 bits.
+//
+// Replaces the text upload of the GPU parser (fastq_ingest.hip) for plain files whose records
+// are all well-formed 4-line records with non-empty, upper-case A/C/G/T sequences and LF line
+// ends — the form simulators and most pipelines write. Such a record is exactly one read of the
+// counting view and one record of the mapping view (oracle/fastx.py), so the library is the
+// packed sequences in file order. PCIe then carries 2 bits per base instead of ~16 bits of
+// text per base (C3: 11.5 GB instead of 92 GB), and the bound moves to the host threads' read
+// of the page cache. Any other input (N or IUPAC symbols, lower case, CR line ends, blank or
+// wrapped lines, empty sequences, compressed files) declines before anything is returned, and
+// the caller runs the GPU text parser, which handles all of them.
+//
+// Each file is cut into one part per thread at record starts (fastq_record_start). A thread
+// reads its part with pread() into a private block, checks and packs every record (AVX2 + BMI2
+// where the CPU has them: 32 bases per compare/shift/multiply-add step), and uploads its packed
+// stream from two pinned staging buffers on a stream of its own into a region of device memory
+// reserved for it. One kernel then concatenates the regions (they start at arbitrary base
+// offsets, so every output word is a funnel shift of at most a few region words); the offsets
+// are i * L when every read has length L, else uploaded; the mapping view of paired inputs
+// (files after the first reverse-complemented, reads.cpp:20-31) is built on the device from
+// the counting view.
+#include <fcntl.h>
+#include <immintrin.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <thread>
+
+#include "internal.h"
+
+namespace mcaat {
+
+namespace {
+
+constexpr size_t kBlk = 16u << 20;        // bytes read per pread() block
+constexpr size_t kMaxRecord = 1u << 20;   // longest record the fast path takes
+constexpr size_t kStageWords = 1u << 20;  // packed words per pinned staging buffer (8 MB)
+constexpr int kPB = 256;
+
+// ---------------------------------------------------------------- packing
+// 2-bit code of an upper-case A/C/G/T byte: ((c >> 1) ^ (c >> 2)) & 3 maps A C G T -> 0 1 2 3.
+inline bool scalar_pack(const uint8_t *s, uint32_t n, uint64_t &v) {
+    v = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint8_t c = s[i];
+        if (c != 'A' && c != 'C' && c != 'G' && c != 'T') return false;
+        v |= (uint64_t)(((c >> 1) ^ (c >> 2)) & 3) << (2 * i);
+    }
+    return true;
+}
+
+// 32 bytes (the first n valid) -> 64 bits of codes; false if one of the n is not A/C/G/T
+__attribute__((target("avx2,bmi2"))) inline bool avx2_pack32(const uint8_t *s, uint32_t n, uint64_t &v) {
+    const __m256i x = _mm256_loadu_si256((const __m256i *)s);
+    const __m256i ok = _mm256_or_si256(_mm256_or_si256(_mm256_cmpeq_epi8(x, _mm256_set1_epi8('A')),
+                                                       _mm256_cmpeq_epi8(x, _mm256_set1_epi8('C'))),
+                                       _mm256_or_si256(_mm256_cmpeq_epi8(x, _mm256_set1_epi8('G')),
+                                                       _mm256_cmpeq_epi8(x, _mm256_set1_epi8('T'))));
+    const uint32_t m = (uint32_t)_mm256_movemask_epi8(ok);
+    const uint32_t need = n >= 32 ? 0xFFFFFFFFu : ((1u << n) - 1);
+    if ((m & need) != need) return false;
+    const __m256i c = _mm256_and_si256(_mm256_xor_si256(_mm256_srli_epi16(x, 1), _mm256_srli_epi16(x, 2)),
+                                       _mm256_set1_epi8(3));
+    // byte pairs -> 4 bits, then 16-bit pairs -> 8 bits: each 32-bit lane holds 4 codes in its low byte
+    const __m256i t = _mm256_maddubs_epi16(c, _mm256_set1_epi16(0x0401));
+    const __m256i u = _mm256_madd_epi16(t, _mm256_set1_epi32(0x00100001));
+    const __m256i g = _mm256_shuffle_epi8(u, _mm256_setr_epi8(0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
+                                                              -1, 0, 4, 8, 12, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1,
+                                                              -1, -1));
+    const __m256i h = _mm256_permutevar8x32_epi32(g, _mm256_setr_epi32(0, 4, 1, 1, 1, 1, 1, 1));
+    v = (uint64_t)_mm_cvtsi128_si64(_mm256_castsi256_si128(h));
+    if (n < 32) v &= (1ULL << (2 * n)) - 1;
+    return true;
+}
+
+bool cpu_has_avx2() {
+    static const bool ok = __builtin_cpu_supports("avx2") && __builtin_cpu_supports("bmi2");
+    return ok;
+}
+
+// ---------------------------------------------------------------- one thread's part
+struct PartOut {
+    uint64_t region = 0;  // first word of this part's device region
+    uint64_t cap = 0;     // words in the region
+    uint64_t bases = 0, reads = 0;
+    uint32_t L0 = 0;      // length of every read so far (fixed-length input), 0 = none yet
+    bool varlen = false;
+    std::vector<uint32_t> lengths;  // every read's length once lengths differ
+    std::string error;
+};
+
+struct Shared {
+    std::atomic<bool> decline{false};
+};
+
+class PartPacker {
+   public:
+    PartPacker(uint64_t *dregion, uint64_t *stage0, uint64_t *stage1, hipStream_t st, PartOut &o)
+        : dst_(dregion), st_(st), o_(o) {
+        stage_[0] = stage0;
+        stage_[1] = stage1;
+        for (auto &e : ev_) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        stage_[0][0] = 0;
+    }
+    ~PartPacker() {
+        for (auto &e : ev_) {
+            (void)hipEventSynchronize(e);
+            (void)hipEventDestroy(e);
+        }
+    }
+
+    // record sequence of n bases -> the stream; false: not upper-case ACGT (declines)
+    bool append(const uint8_t *s, uint32_t n) {
+        if ((pos_ + n) / 32 + 2 >= w0_ + kStageWords) flush(false);
+        if ((pos_ + n) / 32 + 2 > o_.cap) return fail("part region full");
+        const bool simd = cpu_has_avx2();
+        for (uint32_t i = 0; i < n; i += 32) {
+            const uint32_t m = std::min<uint32_t>(32, n - i);
+            uint64_t v;
+            const bool ok = simd ? avx2_pack32(s + i, m, v) : scalar_pack(s + i, m, v);
+            if (!ok) return false;
+            const uint64_t w = (pos_ >> 5) - w0_;
+            const int sh = 2 * (int)(pos_ & 31);
+            uint64_t *q = stage_[cur_];
+            q[w] |= v << sh;
+            q[w + 1] = sh ? v >> (64 - sh) : 0;
+            pos_ += m;
+        }
+        ++o_.reads;
+        if (!o_.varlen) {
+            if (o_.L0 == 0) o_.L0 = n;
+            if (n != o_.L0) {
+                o_.varlen = true;
+                o_.lengths.assign(o_.reads - 1, o_.L0);
+            }
+        }
+        if (o_.varlen) o_.lengths.push_back(n);
+        return true;
+    }
+
+    void finish() {
+        flush(true);
+        for (auto &e : ev_) HIP_OK(hipEventSynchronize(e));
+        o_.bases = pos_;
+    }
+
+   private:
+    bool fail(const char *why) {
+        o_.error = why;
+        return false;
+    }
+    // uploads the complete words [w0_, pos_/32) (and the partial last one at the end); the
+    // partial word moves to the front of the other staging buffer
+    void flush(bool last) {
+        const uint64_t wend = last ? (pos_ + 31) / 32 : pos_ / 32;
+        const uint64_t nw = wend - w0_;
+        if (nw) {
+            HIP_OK(hipMemcpyAsync(dst_ + w0_, stage_[cur_], 8 * nw, hipMemcpyHostToDevice, st_));
+            HIP_OK(hipEventRecord(ev_[cur_], st_));
+        }
+        if (last) return;
+        const int nx = cur_ ^ 1;
+        HIP_OK(hipEventSynchronize(ev_[nx]));  // its previous upload is done
+        stage_[nx][0] = stage_[cur_][nw];      // the partial word (0 when pos_ is word-aligned)
+        cur_ = nx;
+        w0_ = wend;
+    }
+
+    uint64_t *dst_;
+    hipStream_t st_;
+    PartOut &o_;
+    uint64_t *stage_[2];
+    hipEvent_t ev_[2] = {nullptr, nullptr};
+    int cur_ = 0;
+    uint64_t pos_ = 0, w0_ = 0;
+};
+
+// parse [b, e) of a plain file: 4-line records, each sequence packed; false = declined
+bool pack_part(const char *path, uint64_t b, uint64_t e, bool file_end, PartPacker &pk, Shared &sh, PartOut &o) {
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) {
+        o.error = std::string("cannot open ") + path;
+        return false;
+    }
+    struct Fd {
+        int fd;
+        ~Fd() { close(fd); }
+    } guard{fd};
+    std::vector<uint8_t> buf(kBlk + kMaxRecord + 64);
+    uint8_t *B = buf.data();
+    size_t have = 0;  // bytes in B
+    uint64_t off = b;
+    size_t i = 0;     // parse position in B
+    bool eof = b >= e;
+    auto refill = [&]() -> bool {
+        // keep the unparsed tail, read the next block behind it
+        if (i) {
+            memmove(B, B + i, have - i);
+            have -= i;
+            i = 0;
+        }
+        const size_t want = (size_t)std::min<uint64_t>(kBlk, e - off);
+        size_t got = 0;
+        while (got < want) {
+            const ssize_t r = pread(fd, B + have + got, want - got, (off_t)(off + got));
+            if (r < 0) return false;
+            if (r == 0) break;
+            got += (size_t)r;
+        }
+        have += got;
+        off += got;
+        eof = off >= e || got < want;
+        memset(B + have, 0, 64);  // the packer reads up to 31 bytes past a line
+        return true;
+    };
+    if (!refill()) return false;
+    auto line_end = [&](size_t from) -> size_t {  // index of the '\n' ending the line at from, or ~0
+        const void *p = memchr(B + from, '\n', have - from);
+        return p ? (size_t)((const uint8_t *)p - B) : ~(size_t)0;
+    };
+    for (;;) {
+        if (sh.decline.load(std::memory_order_relaxed)) return false;
+        if (i == have) {
+            if (eof) break;
+            if (!refill()) return false;
+            continue;
+        }
+        // one record: header, sequence, '+', quality
+        size_t h = line_end(i), s = h == ~(size_t)0 ? h : line_end(h + 1);
+        size_t p = s == ~(size_t)0 ? s : line_end(s + 1);
+        size_t q = p == ~(size_t)0 ? p : line_end(p + 1);
+        if (q == ~(size_t)0) {
+            // the record continues past the block (or the file ends without a final newline)
+            if (!eof) {
+                if (have - i > kMaxRecord) return false;
+                if (!refill()) return false;
+                continue;
+            }
+            if (p != ~(size_t)0 && file_end && e == off) {
+                q = have;  // last record of the file, no final newline
+                if (q == p + 1) return false;
+            } else {
+                return false;  // truncated record
+            }
+        }
+        if (B[i] != '@' || B[h + 1] == '\n' || B[s + 1] != '+') return false;
+        const size_t n = s - (h + 1);
+        if (n == 0 || q - (p + 1) != n) return false;
+        if (B[s - 1] == '\r' || B[h - 1] == '\r' || B[q - 1] == '\r' || B[p - 1] == '\r') return false;
+        if (!pk.append(B + h + 1, (uint32_t)n)) return false;
+        i = q < have ? q + 1 : have;
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------- device kernels
+// out word W = bases [32W, 32W + 32) of the concatenation of the parts (part t: n_t bases at
+// base offset start[t], stored from word region[t] of src)
+__global__ void k_concat_parts(const uint64_t *src, const uint64_t *region, const uint64_t *start, int T,
+                               uint64_t n_words, uint64_t total, uint64_t *out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t W = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; W < n_words; W += stride) {
+        uint64_t j = 32 * W;
+        const uint64_t jend = min(j + 32, total);
+        int t = 0;
+        while (t + 1 < T && start[t + 1] <= j) ++t;  // T is small (threads per file)
+        uint64_t v = 0;
+        int filled = 0;
+        while (j < jend) {
+            while (start[t + 1] <= j) ++t;
+            const uint64_t lp = j - start[t];           // position inside part t
+            const uint64_t take = min(jend, start[t + 1]) - j;
+            const uint64_t w = region[t] + (lp >> 5);
+            const int sh = 2 * (int)(lp & 31);
+            uint64_t x = src[w] >> sh;
+            if (sh) x |= src[w + 1] << (64 - sh);
+            if (take < 32) x &= (1ULL << (2 * take)) - 1;
+            v |= x << (2 * filled);
+            filled += (int)take;
+            j += take;
+        }
+        out[W] = v;
+    }
+}
+
+__global__ void k_offsets_fixed(uint64_t *off, uint64_t n, uint64_t L) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += stride) off[i] = i * L;
+}
+
+// mapping view of paired inputs: reads before first_rc as they are, the others reversed and
+// complemented (one record per read in this path)
+__global__ void k_mapping_view(const uint64_t *packed, const uint64_t *off, uint64_t n_reads, uint64_t first_rc,
+                               uint64_t n_words, uint64_t total, uint64_t *out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t W = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; W < n_words; W += stride) {
+        const uint64_t j0 = 32 * W, j1 = min(j0 + 32, total);
+        // the read holding j0: last i with off[i] <= j0
+        uint64_t lo = 0, hi = n_reads;
+        while (hi - lo > 1) {
+            const uint64_t mid = (lo + hi) / 2;
+            if (off[mid] <= j0) lo = mid;
+            else hi = mid;
+        }
+        uint64_t i = lo, v = 0;
+        for (uint64_t j = j0; j < j1; ++j) {
+            while (off[i + 1] <= j) ++i;
+            uint64_t src = j, flip = 0;
+            if (i >= first_rc) {
+                src = off[i] + off[i + 1] - 1 - j;
+                flip = 3;
+            }
+            const uint64_t b = ((packed[src >> 5] >> (2 * (src & 31))) & 3) ^ flip;
+            v |= b << (2 * (j - j0));
+        }
+        out[W] = v;
+    }
+}
+
+int pack_threads() {
+    if (const char *e = getenv("MCAAT_PACK_THREADS")) return std::max(1, std::min(64, atoi(e)));
+    if (const char *e = getenv("OMP_NUM_THREADS")) {
+        const int v = atoi(e);
+        if (v > 0) return std::min(64, v);
+    }
+    return (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+}
+
+}  // namespace
+
+bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
+                    const std::vector<std::pair<uint64_t, uint64_t>> *ranges, mcaat_reads *r) {
+    if (const char *e = getenv("MCAAT_HOSTPACK"))
+        if (e[0] == '0') return false;
+    if (knob(ctx, "fq.hostpack", 1) == 0) return false;
+    for (int f = 0; f < n_files; ++f)
+        if (is_compressed_file(files[f])) return false;
+    const int T = pack_threads();
+    hipStream_t st = ctx->stream;
+
+    // parts: per file, T byte ranges cut at record starts
+    struct Part {
+        int file;
+        uint64_t b, e;
+        bool file_end;
+    };
+    std::vector<Part> parts;
+    for (int f = 0; f < n_files; ++f) {
+        struct stat sb;
+        if (stat(files[f], &sb) != 0) throw Error(MCAAT_E_IO, std::string("cannot stat ") + files[f]);
+        const uint64_t S = (uint64_t)sb.st_size;
+        const uint64_t b = ranges ? std::min(S, (*ranges)[f].first) : 0;
+        const uint64_t e = ranges ? std::min(S, (*ranges)[f].second) : S;
+        if (b >= e) continue;
+        // a file must start with a record (leading blank lines: the GPU parser trims them)
+        std::vector<uint64_t> cut{b};
+        for (int t = 1; t < T; ++t) {
+            const uint64_t c = fastq_record_start(files[f], b + (uint64_t)((unsigned __int128)(e - b) * t / T));
+            cut.push_back(std::max(cut.back(), std::min(c, e)));
+        }
+        cut.push_back(e);
+        for (int t = 0; t < T; ++t)
+            if (cut[t + 1] > cut[t]) parts.push_back({f, cut[t], cut[t + 1], cut[t + 1] == S});
+    }
+    if (parts.empty()) return false;  // empty inputs: the GPU path's conventions
+    const int P = (int)parts.size();
+
+    // device regions (bases <= bytes / 2 for 4-line records) and pinned staging on the context
+    std::vector<PartOut> outs(P);
+    uint64_t rw = 0;
+    for (int t = 0; t < P; ++t) {
+        outs[t].region = rw;
+        outs[t].cap = (parts[t].e - parts[t].b) / 64 + 64;
+        rw += outs[t].cap;
+    }
+    DevBuf<uint64_t> regions(rw);
+    const size_t stage_bytes = (size_t)P * 2 * kStageWords * 8;
+    if (ctx->pack_pinned_bytes < stage_bytes) {
+        if (ctx->pack_pinned) HIP_OK(hipHostFree(ctx->pack_pinned));
+        ctx->pack_pinned = nullptr;
+        ctx->pack_pinned_bytes = 0;
+        HIP_OK(hipHostMalloc((void **)&ctx->pack_pinned, stage_bytes, hipHostMallocDefault));
+        ctx->pack_pinned_bytes = stage_bytes;
+    }
+    std::vector<hipStream_t> streams(P, nullptr);
+    struct Streams {
+        std::vector<hipStream_t> &s;
+        ~Streams() {
+            for (auto x : s)
+                if (x) {
+                    (void)hipStreamSynchronize(x);
+                    (void)hipStreamDestroy(x);
+                }
+        }
+    } sguard{streams};
+    for (auto &s : streams) HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+
+    Shared sh;
+    std::vector<int> ok(P, 0);
+    std::vector<std::string> err(P);
+    auto job = [&](int t) {
+        try {
+            uint64_t *s0 = (uint64_t *)ctx->pack_pinned + (size_t)t * 2 * kStageWords;
+            PartPacker pk(regions.p + outs[t].region, s0, s0 + kStageWords, streams[t], outs[t]);
+            const bool good = pack_part(files[parts[t].file], parts[t].b, parts[t].e, parts[t].file_end, pk, sh, outs[t]);
+            if (good) pk.finish();
+            ok[t] = good;
+            if (!good) sh.decline.store(true);
+        } catch (const std::exception &x) {
+            err[t] = x.what();
+            sh.decline.store(true);
+        }
+    };
+    {
+        std::vector<std::thread> pool;
+        for (int t = 1; t < P; ++t) pool.emplace_back(job, t);
+        job(0);
+        for (auto &th : pool) th.join();
+    }
+    for (int t = 0; t < P; ++t)
+        if (!err[t].empty()) throw Error(MCAAT_E_HIP, "FASTQ packing: " + err[t]);
+    for (int t = 0; t < P; ++t)
+        if (!ok[t]) return false;  // not the fast path's input: the GPU text parser takes it
+
+    // concatenate the parts
+    std::vector<uint64_t> start(P + 1, 0), region(P);
+    uint64_t n_reads = 0;
+    bool fixed = true;
+    uint32_t L = 0;
+    std::vector<uint64_t> file_records(n_files, 0);
+    for (int t = 0; t < P; ++t) {
+        start[t + 1] = start[t] + outs[t].bases;
+        region[t] = outs[t].region;
+        n_reads += outs[t].reads;
+        file_records[parts[t].file] += outs[t].reads;
+        if (outs[t].reads) {
+            if (outs[t].varlen || (L && outs[t].L0 != L)) fixed = false;
+            if (!L) L = outs[t].L0;
+        }
+    }
+    const uint64_t n_bases = start[P], n_words = (n_bases + 31) / 32;
+    DevBuf<uint64_t> dstart(P + 1), dregion(P);
+    HIP_OK(hipMemcpyAsync(dstart.p, start.data(), 8 * (P + 1), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(dregion.p, region.data(), 8 * P, hipMemcpyHostToDevice, st));
+    r->packed.alloc(n_words + 64);
+    HIP_OK(hipMemsetAsync(r->packed.p + n_words, 0, 8 * 64, st));
+    if (n_words) {
+        KernelTimer kt(ctx, "fq_concat", 16.0 * (double)n_words);
+        hipLaunchKernelGGL(k_concat_parts, dim3(grid_for(n_words, kPB)), dim3(kPB), 0, st, regions.p, dregion.p,
+                           dstart.p, P, n_words, n_bases, r->packed.p);
+        LAUNCH_OK();
+        kt.stop();
+    }
+    r->offsets.alloc(n_reads + 1);
+    if (fixed) {
+        hipLaunchKernelGGL(k_offsets_fixed, dim3(grid_for(n_reads + 1, kPB)), dim3(kPB), 0, st, r->offsets.p, n_reads,
+                           (uint64_t)L);
+        LAUNCH_OK();
+    } else {
+        std::vector<uint64_t> off(n_reads + 1, 0);
+        uint64_t k = 0;
+        for (int t = 0; t < P; ++t) {
+            for (uint64_t j = 0; j < outs[t].reads; ++j, ++k)
+                off[k + 1] = off[k] + (outs[t].varlen ? outs[t].lengths[j] : outs[t].L0);
+        }
+        h2d(ctx, r->offsets.p, off.data(), 8 * off.size());
+    }
+    HIP_OK(hipStreamSynchronize(st));
+    regions.release();
+    r->ctx = ctx;
+    r->n_reads = n_reads;
+    r->n_bases = n_bases;
+    r->n_words = n_words;
+    r->fixed_len = fixed && n_reads ? L : 0;
+    r->n_records = n_reads;
+    r->file_records = file_records;
+    r->has_records = n_files > 1;
+    if (r->has_records) {
+        r->rec_packed.alloc(n_words + 64);
+        HIP_OK(hipMemsetAsync(r->rec_packed.p + n_words, 0, 8 * 64, st));
+        if (n_words) {
+            hipLaunchKernelGGL(k_mapping_view, dim3(grid_for(n_words, kPB)), dim3(kPB), 0, st, r->packed.p,
+                               r->offsets.p, n_reads, file_records[0], n_words, n_bases, r->rec_packed.p);
+            LAUNCH_OK();
+        }
+        r->rec_offsets.alloc(n_reads + 1);
+        HIP_OK(hipMemcpyAsync(r->rec_offsets.p, r->offsets.p, 8 * (n_reads + 1), hipMemcpyDeviceToDevice, st));
+        HIP_OK(hipStreamSynchronize(st));
+    }
+    return true;
+}
+
+}  // namespace mcaat

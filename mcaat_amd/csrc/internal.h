@@ -144,6 +144,9 @@ struct mcaat_ctx {
     // submission then waited ~20-28 ms on an idle GPU.
     uint8_t *bounce = nullptr;
     size_t bounce_bytes = 0;
+    // pinned staging of the host FASTQ packer (two buffers per packing thread), kept
+    uint8_t *pack_pinned = nullptr;
+    size_t pack_pinned_bytes = 0;
 };
 
 struct mcaat_reads {
@@ -386,6 +389,10 @@ class InStream {
     Impl *impl_;
     Kind kind_ = Kind::Plain;
 };
+// plain 4-line FASTQ with upper-case ACGT sequences packed by host threads (fastq_pack.hip);
+// false (nothing changed) when an input is outside that form: the GPU text parser takes it
+bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
+                    const std::vector<std::pair<uint64_t, uint64_t>> *ranges, mcaat_reads *r);
 // first 4-line FASTQ record start at or after byte pos of a plain file (its size if none)
 uint64_t fastq_record_start(const char *path, uint64_t pos);
 bool is_compressed_file(const char *path);  // gzip or bzip2: read whole, never split

@@ -237,3 +237,92 @@ def test_bzip2_fasta_wrapped_and_truncated(gpu_ctx, tmp_path, monkeypatch):
     cut.write_bytes(good[: len(good) // 2])
     with pytest.raises(RuntimeError):
         M.Reads.from_fastx(gpu_ctx, [str(cut)])
+
+
+# ---- host packer (csrc/fastq_pack.hip): the fast path for upper-case ACGT 4-line records ----
+
+def _acgt_records(rng, n, lens):
+    return ["".join(rng.choice(list("ACGT"), size=int(lens[i % len(lens)]))) for i in range(n)]
+
+
+def _packed_by_host(ctx):
+    """True when the last ingest ran the host packer (its concatenation kernel was timed)."""
+    return ctx.kernel_timing("fq_concat")[1] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("threads,lens,final_nl", [("16", [150], True), ("3", [150], False),
+                                                     ("7", [1, 31, 32, 33, 64, 150, 251, 1000], True),
+                                                     ("1", [77], True)])
+def test_host_pack_single_end(gpu_ctx, tmp_path, monkeypatch, threads, lens, final_nl):
+    """Fixed and variable read lengths (words shared by reads, 32-base boundaries), parts cut
+    at record starts for 1..16 threads, a final record without its newline: the same library
+    as the text parser's restatement, and the host packer is the path that ran."""
+    monkeypatch.setenv("MCAAT_PACK_THREADS", threads)
+    rng = np.random.default_rng(int(threads) * 7 + len(lens))
+    seqs = _acgt_records(rng, 3001, lens)
+    text = _fastq_text(seqs, final_newline=final_nl)
+    gpu_ctx.reset_timing()
+    reads = _check(gpu_ctx, [_write(tmp_path / "a.fq", text)], [text], monkeypatch, 0)
+    assert _packed_by_host(gpu_ctx)
+    n, b = reads.info()
+    assert n == 3001 and b == sum(len(s) for s in seqs)
+    reads.free()
+
+
+@pytest.mark.gpu
+def test_host_pack_paired_end(gpu_ctx, tmp_path, monkeypatch):
+    """Two files: counting view in file order, mapping view with the second file reverse-
+    complemented (built on the device from the counting view)."""
+    monkeypatch.setenv("MCAAT_PACK_THREADS", "5")
+    rng = np.random.default_rng(3)
+    t1 = _fastq_text(_acgt_records(rng, 1200, [150, 149]))
+    t2 = _fastq_text(_acgt_records(rng, 1100, [150]))
+    files = [_write(tmp_path / "r1.fq", t1), _write(tmp_path / "r2.fq", t2)]
+    gpu_ctx.reset_timing()
+    reads = _check(gpu_ctx, files, [t1, t2], monkeypatch, 0)
+    assert _packed_by_host(gpu_ctx)
+    assert reads.records_info() == (2300, True)
+    reads.free()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bad", ["N", "lower", "crlf", "empty", "blank_end"])
+def test_host_pack_declines_to_the_text_parser(gpu_ctx, tmp_path, monkeypatch, bad):
+    """Inputs outside the fast path's form go to the GPU text parser, with its results."""
+    monkeypatch.setenv("MCAAT_PACK_THREADS", "4")
+    rng = np.random.default_rng(9)
+    seqs = _acgt_records(rng, 800, [150])
+    if bad == "N":
+        seqs[700] = seqs[700][:50] + "N" + seqs[700][51:]
+    elif bad == "lower":
+        seqs[3] = seqs[3].lower()
+    elif bad == "empty":
+        seqs[400] = ""
+    text = _fastq_text(seqs, crlf=bad == "crlf", trail="\n\n" if bad == "blank_end" else "")
+    gpu_ctx.reset_timing()
+    reads = _check(gpu_ctx, [_write(tmp_path / "a.fq", text)], [text], monkeypatch, 0)
+    assert not _packed_by_host(gpu_ctx)
+    reads.free()
+
+
+@pytest.mark.gpu
+def test_host_pack_off_matches_on(gpu_ctx, tmp_path, monkeypatch):
+    """fq.hostpack=0 forces the text parser: both paths give the same library."""
+    import mcaat_amd as M
+
+    rng = np.random.default_rng(21)
+    text = _fastq_text(_acgt_records(rng, 5000, [150]))
+    path = _write(tmp_path / "a.fq", text)
+    got = []
+    for on in (1, 0):
+        with gpu_ctx.knobs(fq__hostpack=on):
+            gpu_ctx.reset_timing()
+            r = M.Reads.from_fastx(gpu_ctx, [path])
+            assert _packed_by_host(gpu_ctx) == bool(on)
+            got.append((r.download(), r.info(), r.records_info()))
+            r.free()
+    (p1, o1), i1, q1 = got[0]
+    (p0, o0), i0, q0 = got[1]
+    nw = (int(o1[-1]) + 31) // 32
+    assert i1 == i0 and q1 == q0 and np.array_equal(o1, o0) and np.array_equal(p1[:nw], p0[:nw])

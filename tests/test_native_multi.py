@@ -101,6 +101,34 @@ def test_sharded_build_and_cycle_finder_ranks_share_one_gpu(world, extra):
 
 
 @pytest.mark.gpu
+@pytest.mark.timeout(1500)
+def test_c3_full_dataset_two_shm_ranks_equal_one_gpu(gpu_ctx, tmp_path):
+    """The C4 data path at full size: the whole C3 dataset (300M reads, D ~ 1e9) through
+    mcaat_build_graph_sharded + mcaat_cycle_finder_comm with 2 shared-memory ranks sharing the
+    GPU; keys, multiplicities, post-CycleFinder valid bits (order-sensitive checksums) and the
+    full CycleFinder results (entries, candidates, buckets, stats) equal the one-GPU path's."""
+    import json
+
+    gpu_ctx.trim()  # the ranks need the memory this process's arena keeps from earlier tests
+    dig = str(tmp_path / "rank{rank}.json")
+    outs = _ranks(2, "shm", ("--config", "c3", "--digest", dig, "--slot", "0"), timeout=900)
+    for rc, o, e in outs:
+        assert rc == 0, (o[-2000:], e[-3000:])
+        assert "NATIVE_MULTI_DIGEST" in o, o
+    single = str(tmp_path / "single.json")
+    script = os.path.join(ROOT, "tools", "native_multi_check.py")
+    (rc, o, e), = _spawn([[sys.executable, script, "--world", "1", "--rank", "0", "--single", "--config", "c3",
+                           "--digest", single]], timeout=600)
+    assert rc == 0, (o[-2000:], e[-3000:])
+    want = json.load(open(single))
+    assert want["D"] > 9e8 and want["cycles"] > 0
+    for r in range(2):
+        got = json.load(open(dig.format(rank=r)))
+        for key in ("D", "keys", "mult", "valid", "stats", "results", "entries", "cycles"):
+            assert got[key] == want[key], (r, key, got[key], want[key])
+
+
+@pytest.mark.gpu
 def test_rccl_single_rank_matches_one_gpu():
     outs = _ranks(1, "rccl")
     rc, o, e = outs[0]

@@ -7,6 +7,9 @@ with the single-GPU path over all the reads (computed by every rank on its own c
 
 usage: native_multi_check.py --world N --rank R --comm shm|rccl --name /x [--reads N]
        [--window W] [--uid-file F]
+       native_multi_check.py ... --config c3 --digest FILE   (a bench config at full size: the
+           rank writes checksums of its graph and results instead of comparing in-process)
+       native_multi_check.py --single --config c3 --digest FILE   (the one-GPU path's checksums)
 """
 import argparse
 import os
@@ -21,6 +24,29 @@ sys.path.insert(0, ROOT)
 import mcaat_amd as M  # noqa: E402
 
 
+def digest(g, res) -> dict:
+    """Order-sensitive checksums of the graph (keys, multiplicities, valid bits after
+    CycleFinder) and the full CycleFinder results; two runs agree iff these agree (up to
+    64-bit checksum collisions)."""
+    import hashlib
+
+    D = g.size
+    ks = ms = vs = 0
+    chunk = 1 << 27
+    mask = (1 << 64) - 1
+    with np.errstate(over="ignore"):
+        for a in range(0, D, chunk):
+            n = min(chunk, D - a)
+            kk, mm, vv = g.download_range(a, n, valid=True)
+            idx = np.arange(a, a + n, dtype=np.uint64) * np.uint64(0x9E3779B97F4A7C15) + np.uint64(1)
+            ks = (ks + int((kk * idx).sum(dtype=np.uint64))) & mask
+            ms = (ms + int((mm.astype(np.uint64) * idx).sum(dtype=np.uint64))) & mask
+            vs = (vs + int((vv.astype(np.uint64) * idx).sum(dtype=np.uint64))) & mask
+    h = hashlib.sha256(repr((res.entries, list(res.candidates), list(res.buckets))).encode()).hexdigest()
+    return {"D": D, "keys": ks, "mult": ms, "valid": vs, "stats": list(res.stats[:6]), "results": h,
+            "entries": len(res.entries), "cycles": res.stats[5]}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, required=True)
@@ -31,7 +57,47 @@ def main() -> int:
     ap.add_argument("--window", type=int, default=0, help="cf.fc_window knob (small: many rounds)")
     ap.add_argument("--uid-file", default="")
     ap.add_argument("--slot", type=int, default=1 << 20, help="shm staging bytes per rank")
+    ap.add_argument("--config", default="", help="a bench config (mcaat_amd/configs.py) at full size")
+    ap.add_argument("--digest", default="", help="write checksums here (JSON) instead of comparing")
+    ap.add_argument("--single", action="store_true", help="the one-GPU path alone (with --digest)")
     a = ap.parse_args()
+
+    if a.config:
+        import json
+
+        from mcaat_amd.configs import CONFIGS
+
+        cfg = CONFIGS[a.config]
+        spec, k, prm = cfg["spec"], cfg["k"], M.CfParams(threshold_multiplicity=cfg["thr"])
+        ctx = M.Context(a.rank % max(1, M.device_count()) if a.comm == "rccl" else 0)
+        t0 = time.time()
+        if a.single:
+            reads = M.Reads.synth(ctx, spec)
+            g = M.Graph.build(ctx, reads, k)
+            reads.free()
+            res = g.cycle_finder(prm, as_arrays=False)
+            comm = None
+        else:
+            comm = M.Comm.shm(ctx, a.world, a.rank, a.name, a.slot) if a.comm == "shm" else None
+            assert comm is not None, "--config runs use the shared-memory transport"
+            first = a.rank * spec.n_reads // a.world
+            count = (a.rank + 1) * spec.n_reads // a.world - first
+            mine = M.Reads.synth_range(ctx, spec, first, count)
+            g = M.Graph.build_sharded(ctx, comm, mine, k)
+            mine.free()
+            res = g.cycle_finder(prm, comm=comm)
+        d = digest(g, res)
+        d["seconds"] = round(time.time() - t0, 1)
+        g.free()
+        if comm is not None:
+            comm.barrier()
+            comm.close()
+        ctx.close()
+        with open(a.digest.format(rank=a.rank), "w") as f:
+            json.dump(d, f)
+        print(f"rank {a.rank}: {d}", flush=True)
+        print("NATIVE_MULTI_DIGEST", flush=True)
+        return 0
 
     spec = M.SynthSpec(seed=11, n_genomes=3, genome_len=40_000, arrays_per_genome=2, spacers_per_array=10,
                        repeat_len_min=30, repeat_len_max=34, spacer_len_min=30, spacer_len_max=36,
