@@ -199,15 +199,21 @@ def measure_e2e(cfg: dict, spec, fastq: str, threads: int, n_kmers: int) -> dict
             tail["process_start_and_exit_s"] = round(wall - tail.get("main_s", 0.0), 3)
         arrays = os.path.join(work, "out", "CRISPR_Arrays.txt")
         n_arr = None
+        recall = None
         if os.path.exists(arrays):
             for line in open(arrays):
                 if line.startswith("Number of Systems:"):
                     n_arr = int(line.split(":")[1])
+            # every planted array of the synthetic community should be in the report
+            from mcaat_amd.truth import parse_crispr_arrays, planted_recall
+
+            rec = planted_recall(parse_crispr_arrays(arrays), M.synth_arrays(spec))
+            recall = {kk: rec[kk] for kk in ("planted", "recalled", "recall", "systems")}
         return {
             "value": n_kmers / span, "unit": "k-mers/s", "T_s": round(span, 3),
             "build_lib_s": round(lib, 3), "sdbg_build_s": round(build, 3), "cycle_finder_s": round(cf, 3),
             "fastq_bytes": os.path.getsize(fastq), "fastq_GBps": round(os.path.getsize(fastq) / lib / 1e9, 2),
-            "cli_wall_s": round(wall, 3), "cli_phases_s": tail, "crispr_systems": n_arr,
+            "cli_wall_s": round(wall, 3), "cli_phases_s": tail, "crispr_systems": n_arr, "planted_recall": recall,
             "note": "fresh CLI process on a GPU no earlier process of this job used, FASTQ in tmpfs (/dev/shm, "
                     "pages settled by one untimed read); the span excludes process start, HIP runtime init (input "
                     "check) and the downstream steps 6-8 (cli_wall_s includes them)",

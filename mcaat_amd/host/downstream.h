@@ -71,6 +71,10 @@ std::vector<std::vector<uint64_t>> get_relevant_reads(const Graph &graph,
                                                       const std::vector<std::vector<uint64_t>> &all_reads);
 std::vector<std::vector<uint64_t>> get_relevant_cycles(const Graph &graph,
                                                        const std::vector<std::vector<uint64_t>> &all_cycles);
+void get_relevant_reads_and_cycles(const std::vector<Graph> &regions, const std::vector<std::vector<uint64_t>> &all_reads,
+                                   const std::vector<std::vector<uint64_t>> &all_cycles,
+                                   std::vector<std::vector<std::vector<uint64_t>>> &reads_out,
+                                   std::vector<std::vector<std::vector<uint64_t>>> &cycles_out);
 void get_minimum_cycles_for_full_coverage(std::vector<std::vector<uint64_t>> &cycles);
 std::vector<size_t> solve_min_cover_problem(const std::unordered_set<uint32_t> &universe,
                                             const std::vector<std::vector<uint32_t>> &sets);

@@ -13,14 +13,36 @@
 // CRISPRAnalyzer only compares spacers of 23..50 symbols, so the short-needle (<= 64)
 // variant is the one restated.
 #include <algorithm>
+#include <cstdint>
 #include <vector>
 
 #include "downstream.h"
 
 namespace {
 
+// bit-parallel LCS (Hyyro's formulation, as rapidfuzz computes it for patterns of <= 64
+// symbols): PM[c] has bit i set where a[i] == c; one add/or per symbol of b
+struct Pattern {
+    uint64_t pm[256] = {};
+    size_t n = 0;
+    Pattern(const char *a, size_t na) : n(na) {
+        for (size_t i = 0; i < na; ++i) pm[(unsigned char)a[i]] |= 1ULL << i;
+    }
+    size_t lcs(const char *b, size_t nb) const {
+        uint64_t S = ~0ULL;
+        for (size_t j = 0; j < nb; ++j) {
+            const uint64_t u = S & pm[(unsigned char)b[j]];
+            S = (S + u) | (S - u);
+        }
+        const uint64_t mask = n >= 64 ? ~0ULL : ((1ULL << n) - 1);
+        return (size_t)__builtin_popcountll(~S & mask);
+    }
+};
+
 size_t lcs_length(const char *a, size_t na, const char *b, size_t nb) {
     if (!na || !nb) return 0;
+    if (na <= 64) return Pattern(a, na).lcs(b, nb);
+    if (nb <= 64) return Pattern(b, nb).lcs(a, na);
     std::vector<uint32_t> row(nb + 1, 0);
     for (size_t i = 0; i < na; ++i) {
         uint32_t diag = 0;
@@ -45,8 +67,16 @@ double partial_short_needle(const std::string &needle, const std::string &hay) {
     bool in_needle[256] = {false};
     for (unsigned char c : needle) in_needle[c] = true;
     double best = 0.0;
+    const Pattern pat(needle.data(), std::min<size_t>(n1, 64));  // used when n1 <= 64 (CRISPRAnalyzer's spacers)
     auto consider = [&](size_t first, size_t len) {
-        const double r = ratio_raw(needle.data(), n1, hay.data() + first, len);
+        double r;
+        if (n1 <= 64) {
+            const size_t sum = n1 + len;
+            r = sum ? (1.0 - static_cast<double>(sum - 2 * pat.lcs(hay.data() + first, len)) / static_cast<double>(sum)) * 100.0
+                    : 100.0;
+        } else {
+            r = ratio_raw(needle.data(), n1, hay.data() + first, len);
+        }
         if (r > best) best = r;
     };
     for (size_t i = 1; i < n1 && best < 100.0; ++i)

@@ -45,9 +45,12 @@ std::vector<FoundSystem> run_and_debug_spacer_ordering(const std::vector<std::ve
         std::vector<std::vector<uint64_t>> reads, cycles;
     };
     std::vector<Sub> subs;
-    for (const auto &g : regions) {
-        auto rr = get_relevant_reads(g, reads);
-        auto rc = get_relevant_cycles(g, cycles);
+    std::vector<std::vector<std::vector<uint64_t>>> region_reads, region_cycles;
+    get_relevant_reads_and_cycles(regions, reads, cycles, region_reads, region_cycles);
+    for (size_t ri = 0; ri < regions.size(); ++ri) {
+        const Graph &g = regions[ri];
+        auto rr = std::move(region_reads[ri]);
+        auto rc = std::move(region_cycles[ri]);
         get_minimum_cycles_for_full_coverage(rc);
         // the reverse-complement twin of a region is expected to carry no relevant reads
         if (rr.empty() || rc.size() < 3) continue;

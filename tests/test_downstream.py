@@ -113,6 +113,12 @@ def test_fuzz_matches_brute_force_on_dna():
             b = a[i:i + rng.randint(10, len(a) - i)] + b[: rng.randint(0, 5)]
         assert DS.fuzz_ratio(a, b) == _ratio(a, b)
         assert DS.fuzz_partial_ratio(a, b) == _partial(a, b)
+    # the bit-parallel LCS takes either string of <= 64 symbols as the pattern; both longer: DP
+    for la, lb in ((64, 100), (65, 64), (100, 130), (1, 64), (64, 64)):
+        a = "".join(rng.choice("ACGT") for _ in range(la))
+        b = "".join(rng.choice("ACGT") for _ in range(lb))
+        assert DS.fuzz_ratio(a, b) == _ratio(a, b)
+        assert DS.fuzz_ratio(b, a) == _ratio(b, a)
 
 
 # ---- CRISPRAnalyzer ----------------------------------------------------------------------
