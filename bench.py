@@ -222,25 +222,30 @@ def measure_e2e(cfg: dict, spec, fastq: str, threads: int, n_kmers: int) -> dict
         shutil.rmtree(work, ignore_errors=True)
 
 
-def step_traffic_from_profiles() -> float | None:
-    """HBM bytes of one profiled step: every kernel's per-launch PMC bytes times its launches
-    (profiles/traffic.json), the synthetic-read generator excluded."""
-    path = os.path.join(ROOT, "profiles", "traffic.json")
+def _traffic_file(config: str) -> str:
+    """The committed PMC summary of this config (tools/traffic_summary.py)."""
+    return os.path.join(ROOT, "profiles", f"traffic_{config}.json")
+
+
+def step_traffic_from_profiles(config: str) -> dict | None:
+    """HBM bytes of one profiled step of this config: every kernel's per-launch PMC bytes times
+    its launches, the synthetic-read generator excluded; FETCH doubled only for the kernels
+    whose reads are wide coalesced streams (corrected), and as counted (raw)."""
     try:
-        with open(path) as f:
+        with open(_traffic_file(config)) as f:
             d = json.load(f)
         # entries without "launches" are the bench's short-name aliases of a k_* entry
-        return float(sum(v["hbm_bytes_per_launch"] * v["launches"] for kk, v in d.items()
-                         if kk != "k_synth" and "launches" in v))
+        rows = [v for kk, v in d.items() if kk != "k_synth" and "launches" in v]
+        return {"corrected": float(sum(v["hbm_bytes_per_launch"] * v["launches"] for v in rows)),
+                "raw": float(sum(v.get("hbm_bytes_raw", v["hbm_bytes_per_launch"]) * v["launches"] for v in rows))}
     except Exception:
         return None
 
 
-def traffic_from_profiles(kernel: str) -> float | None:
-    """HBM bytes per launch of the dominant kernel from the committed PMC summary, if any."""
-    path = os.path.join(ROOT, "profiles", "traffic.json")
+def traffic_from_profiles(config: str, kernel: str) -> float | None:
+    """HBM bytes per launch of the dominant kernel from this config's PMC summary, if any."""
     try:
-        with open(path) as f:
+        with open(_traffic_file(config)) as f:
             d = json.load(f)
         return float(d[kernel]["hbm_bytes_per_launch"])
     except Exception:
@@ -528,7 +533,7 @@ def main() -> int:
         impl = "native shared-memory communicator, CycleFinder over the ranks"
     if rank == 0:
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-        traffic = traffic_from_profiles(kern)
+        traffic = traffic_from_profiles(args.config, kern)
         out = {
             "metric": "k-mers/sec through sdbg_build+cycle_finder, 1B-node graph @ 1/2/4/8 GPUs",
             "value": value,
@@ -590,9 +595,11 @@ def main() -> int:
             out["step_roofline"] = {
                 "B_alg": b_alg, "achieved_GBps": b_alg / dt / 1e9 / world,
                 "frac": b_alg / dt / 1e9 / world / PEAK_HBM_GBS,
-                "pmc_bytes_per_step": step_traffic_from_profiles(),
+                "pmc_bytes_per_step": step_traffic_from_profiles(args.config),
                 "note": "SURVEY.md §8d algorithmic bytes over the step time, per GPU; pmc_bytes_per_step = "
-                        "FETCH+WRITE of every kernel of one profiled step (profiles/traffic.json)",
+                        f"FETCH+WRITE of every kernel of one profiled step of this config "
+                        f"(profiles/traffic_{args.config}.json; FETCH doubled only for wide coalesced "
+                        "stream reads: corrected, and as counted: raw)",
             }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
         try:

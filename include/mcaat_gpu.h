@@ -285,6 +285,9 @@ void mcaat_reset_timing(mcaat_ctx *ctx);
  *   nc.fine_bits       log2 fine partitions (8..19)
  *   nc.edge_cap        distinct edges per LDS partition before the class split / fallback
  *   nc.desc_cap        distinct super-k-mers per LDS partition before the class split / raw path
+ *   nc.big_table       1: pass C always with the 8192-slot edge table (one workgroup per CU),
+ *                      0: never; default: from the group after one that split more than 1 in 8
+ *                      of its partitions into classes
  *   nc.overlap         0: passes B and C of successive groups in turn on one stream (default
  *                      1: the next group's pass B on a second stream while C counts this one)
  *   sort.msd           0: radix sort only, 1: MSD sort whenever k <= 28 (default: D >= 2^16)
@@ -292,6 +295,8 @@ void mcaat_reset_timing(mcaat_ctx *ctx);
  *                      one-wave, 256-thread and 1024-thread LDS sorts (above the last: radix)
  *   sort.l3_counting   0: one-wave level-3 buckets by the bitonic network only (default 1: LDS
  *                      counting sort by the next key bits, bitonic for clustered buckets)
+ *   sort.mid_counting  0: level-3 buckets above the one-wave limit by the 256-thread bitonic
+ *                      network (default 1: the 256-thread LDS counting sort)
  *   cf.dls_stack / cf.dls_visited   initial DepthLevelSearch scratch (grows x8 on overflow)
  *   cf.fc_lock / cf.fc_relax / cf.fc_out   initial FindCycle scratch (grows on overflow)
  *   cf.fc_window       initial FindCycle speculation window

@@ -770,24 +770,32 @@ __device__ __forceinline__ bool ovf_in_class(uint32_t e, uint32_t dw) {  // dw: 
     return ((dw >> (kHShift - 32)) & ((1u << lgn) - 1)) == cls;
 }
 
+// LG = log2 of the edge-table size
+template <int LG>
 __device__ __forceinline__ uint32_t edge_slot(uint64_t c) {
-    return (((uint32_t)c ^ (uint32_t)(c >> 32)) * 0x9E3779B1u) >> (32 - 12);
+    return (((uint32_t)c ^ (uint32_t)(c >> 32)) * 0x9E3779B1u) >> (32 - LG);
 }
-static_assert(kCap == 4096, "edge_slot yields 12 bits");
+// the error-rich variant (C2, C5: most partitions hold more distinct edges than kCapMax): an
+// edge table twice the size, one 1024-thread workgroup per CU (96 KB of LDS)
+constexpr int kCapBig = 8192;
+constexpr int kCapMaxBig = kCapBig * 85 / 100 - kCWaves * 64;
+constexpr int cap_lg(int cap) { return cap == 4096 ? 12 : cap == 8192 ? 13 : -1; }
 __device__ __forceinline__ uint32_t desc_slot(uint64_t w0, uint64_t w1) {
     const uint64_t x = (w0 ^ (w1 * 0x9E3779B97F4A7C15ULL)) * 0xD6E8FEB86659FD93ULL;
     return (uint32_t)(x >> (64 - 11));
 }
 static_assert(kDCap == 2048, "desc_slot yields 11 bits");
 
-template <bool PROF>
-__global__ void __launch_bounds__(kCThreads, kCPerCu * kCThreads / 256) k_lds_count(const uint4 *__restrict__ data, uint64_t gbase,
+template <bool PROF, int kCap, int PERCU>
+__global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_count(const uint4 *__restrict__ data, uint64_t gbase,
                                                          const uint64_t *__restrict__ fine_base, uint64_t p0,
                                                          uint64_t F, int E,
                                                          uint64_t *out_keys, uint32_t *out_cnt, uint64_t out_cap,
                                                          unsigned long long *out_cursor, uint32_t *ovf_list,
                                                          unsigned long long *ovf_n, uint32_t cap_max, uint32_t dmax,
-                                                         unsigned long long *prof) {
+                                                         unsigned long long *split_n, unsigned long long *prof) {
+    constexpr int LG = cap_lg(kCap);
+    static_assert(LG > 0, "edge table of 4096 or 8192 slots");
     // The descriptor table (phase 1) and the edge table (phases 2-3) share one LDS region:
     // between the phases each thread keeps its two descriptor slots in registers. 48 KB per
     // workgroup, so two 1024-thread workgroups share a CU and one's loads overlap the other's
@@ -820,7 +828,7 @@ __global__ void __launch_bounds__(kCThreads, kCPerCu * kCThreads / 256) k_lds_co
 
     // add weight to canonical edge c; false once the table has overflowed
     auto insert = [&](uint64_t c, uint32_t weight) {
-        uint32_t h = edge_slot(c);
+        uint32_t h = edge_slot<LG>(c);
         for (int probe = 0; probe < kCap; ++probe) {
             const unsigned long long cur = keys[h];
             if (cur == c) {
@@ -933,6 +941,7 @@ __global__ void __launch_bounds__(kCThreads, kCPerCu * kCThreads / 256) k_lds_co
         __syncthreads();
         tick(1);
         if (dovf && lgn == 0 && !n_deferred_over(n_deferred)) {
+            if (threadIdx.x == 0) atomicAdd(split_n, 1ull);
             lgn = kSplitLg;
             cls = ~0u;  // -> class 0 of 2^kSplitLg
             __syncthreads();  // every thread has read dovf before the next clear resets it
@@ -1028,6 +1037,7 @@ __global__ void __launch_bounds__(kCThreads, kCPerCu * kCThreads / 256) k_lds_co
             // edge-disjoint classes (shallow or error-rich data); a class that still overflows
             // goes to the global-table fallback
             if (lgn == 0) {
+                if (threadIdx.x == 0) atomicAdd(split_n, 1ull);
                 lgn = kSplitLg;
                 cls = ~0u;
             } else if (threadIdx.x == 0) {
@@ -1421,6 +1431,11 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     const uint64_t group_budget =
         (uint64_t)knob(ctx, "nc.group_budget", (int64_t)std::max<uint64_t>(n_live / 4 + 1, 1ULL << 28));  // descriptors per group
     const uint32_t cap_max = (uint32_t)std::min<int64_t>(kCapMax, std::max<int64_t>(1, knob(ctx, "nc.edge_cap", kCapMax)));
+    const uint32_t cap_max_big = (uint32_t)std::min<int64_t>(kCapMaxBig, std::max<int64_t>(1, knob(ctx, "nc.edge_cap", kCapMaxBig)));
+    // big edge tables: knob nc.big_table 0 never, 1 always, default: from the next group on once
+    // a group split more than 1 in 8 of its partitions into classes (error-rich data)
+    const int64_t big_knob = knob(ctx, "nc.big_table", -1);
+    bool big = big_knob == 1;
     const uint32_t dmax = (uint32_t)std::min<int64_t>(kDMax, std::max<int64_t>(1, knob(ctx, "nc.desc_cap", kDMax)));
     // groups of L1 buckets; with the overlap knob (default on) group g+1's pass B runs on the
     // side stream while group g's pass C counts on the main stream (two groups' fine
@@ -1481,19 +1496,24 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
         DevBuf<uint4> &fine = grp.fine;
         // C; a group whose output overflows the key buffers is counted again after they grow
         for (int attempt = 0;; ++attempt) {
-            HIP_OK(hipMemsetAsync(dcnt.p + 1, 0, 8, st));
+            HIP_OK(hipMemsetAsync(dcnt.p + 1, 0, 16, st));
             {
                 KernelTimer kt(ctx, "lds_count", 16.0 * (double)gn);
-                hipLaunchKernelGGL(prof_c ? k_lds_count<true> : k_lds_count<false>, dim3((unsigned)std::min<uint64_t>(p1 - p0, (uint64_t)kCPerCu * ctx->n_cu)),
-                                   dim3(kCThreads), 0, st, fine.p, gbase, dfine.p, p0, p1, E, out.keys.p, out.counts.p,
-                                   out_cap, dcnt.p, ovf_list.p, dcnt.p + 1, cap_max, dmax, prof_c ? dprof.p : nullptr);
+                const unsigned wg = (unsigned)std::min<uint64_t>(p1 - p0, (uint64_t)(big ? 1 : kCPerCu) * ctx->n_cu);
+                auto kern = big ? (prof_c ? k_lds_count<true, kCapBig, 1> : k_lds_count<false, kCapBig, 1>)
+                                : (prof_c ? k_lds_count<true, kCap, kCPerCu> : k_lds_count<false, kCap, kCPerCu>);
+                hipLaunchKernelGGL(kern, dim3(wg), dim3(kCThreads), 0, st, fine.p, gbase, dfine.p, p0, p1, E, out.keys.p,
+                                   out.counts.p, out_cap, dcnt.p, ovf_list.p, dcnt.p + 1, big ? cap_max_big : cap_max, dmax,
+                                   dcnt.p + 2, prof_c ? dprof.p : nullptr);
                 LAUNCH_OK();
                 kt.stop();
             }
-            unsigned long long hc[2];
-            HIP_OK(hipMemcpyAsync(hc, dcnt.p, 16, hipMemcpyDeviceToHost, st));
+            unsigned long long hc[3];
+            HIP_OK(hipMemcpyAsync(hc, dcnt.p, 24, hipMemcpyDeviceToHost, st));
             HIP_OK(hipStreamSynchronize(st));
             const uint64_t n_ovf = hc[1];
+            ctx->kstats["lds_count_split_partitions"].launches += hc[2];
+            if (big_knob < 0 && !big && hc[2] * 8 > p1 - p0) big = true;
             ctx->kstats["lds_count_overflow_partitions"].launches += n_ovf;
             if (n_ovf) {
                 // global-table fallback for the partitions whose distinct edges overflowed LDS,

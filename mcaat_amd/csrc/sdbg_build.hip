@@ -626,6 +626,131 @@ __global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in,
     }
 }
 
+// k_msd3_wave's counting sort for the listed buckets above the one-wave limit (deep graphs:
+// D / 2^22 above 512 items, C2 ~570, C5 ~935): one THREADS-thread workgroup per bucket of
+// <= CAP items. Items are compacted into LDS (padding dropped; their order does not matter, as
+// each item's final rank is its bin start plus the number of smaller items in its bin), binned
+// by the next lg(P) key bits (LDS histogram atomics give each item a slot in its bin), the bin
+// counts are scanned by the workgroup, items move to their bins and are written straight to
+// HBM at their final ranks. A bucket whose largest bin holds more than kMaxBin items
+// (clustered keys) is sorted by the bitonic network instead. Larger buckets are forwarded.
+template <int THREADS, int CAP>
+__global__ void __launch_bounds__(THREADS) k_msd3_count(const uint64_t *in, const uint64_t *off2, const uint64_t *real2,
+                                                        const uint64_t *base3, int k, const uint32_t *big, uint64_t nbig,
+                                                        uint64_t *key, uint16_t *mult, uint32_t *fwd,
+                                                        unsigned long long *nfwd, uint32_t limit) {
+    static_assert(CAP % THREADS == 0 && CAP >= THREADS && THREADS % 64 == 0, "bins per thread");
+    constexpr int NW = THREADS / 64, NR = CAP / THREADS;
+    __shared__ uint64_t s[CAP];
+    __shared__ uint64_t o[CAP];
+    __shared__ uint32_t cnt[CAP];
+    __shared__ uint32_t wsum[NW];
+    __shared__ uint32_t fillc, mxs;
+    const int E = k + 1;
+    const int rb = 2 * E - 2 * kMB;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (uint64_t q = blockIdx.x; q < nbig; q += gridDim.x) {
+        const uint64_t b = big[q], lo = off2[b], n = off2[b + 1] - lo;
+        const uint32_t nreal = (uint32_t)real2[b];
+        if (n > (uint64_t)CAP || nreal > limit) {
+            if (threadIdx.x == 0) fwd[atomicAdd(nfwd, 1ull)] = (uint32_t)b;
+            continue;
+        }
+        const uint64_t base = base3[b], hi = (b >> kMB) << (2 * E - kMB);
+        if (threadIdx.x == 0) {
+            fillc = 0;
+            mxs = 0;
+        }
+        __syncthreads();
+        // compacted load: one LDS cursor atomic per wave and round
+        for (uint32_t i0 = 0; i0 < (uint32_t)n; i0 += THREADS) {
+            const uint32_t i = i0 + threadIdx.x;
+            const uint64_t x = i < n ? in[lo + i] : kPad;
+            const unsigned long long m = __ballot(x != kPad);
+            uint32_t w0 = 0;
+            if (lane == 0 && m) w0 = atomicAdd(&fillc, (uint32_t)__popcll(m));
+            w0 = __shfl(w0, 0);
+            if (x != kPad) s[w0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = x;
+        }
+        uint32_t lgb = 0;
+        while ((1u << lgb) < (uint32_t)THREADS) ++lgb;  // at least one bin per thread
+        while ((1u << lgb) < nreal) ++lgb;
+        bool done = false;
+        if (lgb <= (uint32_t)rb) {
+            const uint32_t nbins = 1u << lgb, per = nbins / THREADS, sh = 16 + rb - lgb;
+            for (uint32_t i = threadIdx.x; i < nbins; i += THREADS) cnt[i] = 0;
+            __syncthreads();
+            uint32_t rk[NR];
+#pragma unroll
+            for (int t = 0; t < NR; ++t) {
+                const uint32_t i = t * THREADS + threadIdx.x;
+                rk[t] = i < nreal ? atomicAdd(&cnt[(uint32_t)(s[i] >> sh) & (nbins - 1)], 1u) : 0;
+            }
+            __syncthreads();
+            uint32_t loc = 0, mx = 0;
+            for (uint32_t j = 0; j < per; ++j) {
+                const uint32_t c = cnt[threadIdx.x * per + j];
+                loc += c;
+                mx = c > mx ? c : mx;
+            }
+            uint32_t incl = loc;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t u = __shfl_up(incl, d);
+                if (lane >= d) incl += u;
+            }
+            for (int d = 32; d > 0; d >>= 1) {
+                const uint32_t u = __shfl_xor(mx, d);
+                mx = u > mx ? u : mx;
+            }
+            if (lane == 63) wsum[wave] = incl;
+            if (lane == 0) atomicMax(&mxs, mx);
+            __syncthreads();
+            if (mxs <= kMaxBin) {
+                uint32_t run = incl - loc;
+                for (int w = 0; w < wave; ++w) run += wsum[w];
+                for (uint32_t j = 0; j < per; ++j) {
+                    const uint32_t c = cnt[threadIdx.x * per + j];
+                    cnt[threadIdx.x * per + j] = run;
+                    run += c;
+                }
+                __syncthreads();
+#pragma unroll
+                for (int t = 0; t < NR; ++t) {
+                    const uint32_t i = t * THREADS + threadIdx.x;
+                    if (i < nreal) {
+                        const uint64_t x = s[i];
+                        o[cnt[(uint32_t)(x >> sh) & (nbins - 1)] + rk[t]] = x;
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int t = 0; t < NR; ++t) {
+                    const uint32_t p = t * THREADS + threadIdx.x;
+                    if (p < nreal) {
+                        const uint64_t x = o[p];
+                        const uint32_t bi = (uint32_t)(x >> sh) & (nbins - 1);
+                        const uint32_t bs = cnt[bi], be = bi + 1 < nbins ? cnt[bi + 1] : nreal;
+                        uint32_t r = bs;
+                        for (uint32_t z = bs; z < be; ++z) r += o[z] < x;
+                        key[base + r] = hi | (x >> 16);
+                        mult[base + r] = (uint16_t)(x & 0xFFFF);
+                    }
+                }
+                done = true;
+            }
+        }
+        if (!done) {  // clustered keys: the bitonic network over the compacted items
+            uint32_t P = 8;
+            while (P < nreal) P <<= 1;
+            for (uint32_t i = nreal + threadIdx.x; i < P; i += THREADS) s[i] = kPad;
+            __syncthreads();
+            lds_bitonic(s, P, threadIdx.x, THREADS, false);
+            msd_emit(s, nreal, threadIdx.x, THREADS, hi, key, mult, base);
+        }
+        __syncthreads();
+    }
+}
+
 // one workgroup per listed level-3 bucket of <= CAP items; larger ones are forwarded to the
 // next list (or flagged when there is none: the caller falls back to the radix sort)
 template <int THREADS, int CAP>
@@ -740,10 +865,17 @@ bool msd_sort(mcaat_ctx *ctx, const uint64_t *ckeys, const uint32_t *ccnt, uint6
         DevBuf<uint32_t> big2(hb);
         DevBuf<unsigned long long> nbig2(1);
         HIP_OK(hipMemsetAsync(nbig2.p, 0, 8, st));
-        hipLaunchKernelGGL((k_msd3_block<256, kMidSort>), dim3((unsigned)std::min<uint64_t>(hb, (uint64_t)ctx->n_cu * 8)),
-                           dim3(256), 0, st, l2.p, off2.p, (const uint64_t *)real2.p, (const uint64_t *)base3.p, k, big.p,
-                           (uint64_t)hb, key, mult, big2.p, nbig2.p, too.p,
-                           (uint32_t)std::min<int64_t>(kMidSort, knob(ctx, "sort.mid_limit", kMidSort)));
+        const uint32_t mid_limit = (uint32_t)std::min<int64_t>(kMidSort, knob(ctx, "sort.mid_limit", kMidSort));
+        if (knob(ctx, "sort.mid_counting", 1)) {
+            // 40 KB of LDS per workgroup: four per CU
+            hipLaunchKernelGGL((k_msd3_count<256, kMidSort>), dim3((unsigned)std::min<uint64_t>(hb, (uint64_t)ctx->n_cu * 4)),
+                               dim3(256), 0, st, l2.p, off2.p, (const uint64_t *)real2.p, (const uint64_t *)base3.p, k,
+                               big.p, (uint64_t)hb, key, mult, big2.p, nbig2.p, mid_limit);
+        } else {
+            hipLaunchKernelGGL((k_msd3_block<256, kMidSort>), dim3((unsigned)std::min<uint64_t>(hb, (uint64_t)ctx->n_cu * 8)),
+                               dim3(256), 0, st, l2.p, off2.p, (const uint64_t *)real2.p, (const uint64_t *)base3.p, k,
+                               big.p, (uint64_t)hb, key, mult, big2.p, nbig2.p, too.p, mid_limit);
+        }
         LAUNCH_OK();
         unsigned long long hb2 = 0;
         HIP_OK(hipMemcpyAsync(&hb2, nbig2.p, 8, hipMemcpyDeviceToHost, st));

@@ -14,9 +14,11 @@ void mcaat_check(int rc, const char *what) {
     if (rc != MCAAT_OK) throw std::runtime_error(std::string(what) + ": " + mcaat_last_error());
 }
 
+// device < 0: the context already bound (the run's --gpu / rank device), else device 0
 mcaat_ctx *mcaat_host_ctx(int device) {
     static mcaat_ctx *ctx = nullptr;
     static int dev = -1;
+    if (device < 0) device = ctx ? dev : 0;
     if (ctx && dev != device) {
         mcaat_finalize(ctx);
         ctx = nullptr;
@@ -146,7 +148,9 @@ void SDBG::LoadFromDevice(mcaat_graph *g) {
 
 void SDBG::LoadFromFile(const char *path) {
     mcaat_graph *g = nullptr;
-    mcaat_check(mcaat_graph_load(mcaat_host_ctx(0), path, &g), "SDBG::LoadFromFile");
+    // on the GPU this process already works on (settings.gpu / the rank's device): binding
+    // device 0 here would finalize that context
+    mcaat_check(mcaat_graph_load(mcaat_host_ctx(-1), path, &g), "SDBG::LoadFromFile");
     LoadFromDevice(g);
 }
 

@@ -17,7 +17,7 @@
 void mcaat_check(int rc, const char *what);
 
 // One GPU context per process (one process per GPU).
-mcaat_ctx *mcaat_host_ctx(int device);
+mcaat_ctx *mcaat_host_ctx(int device);  // device < 0: the one already bound (else 0)
 // the GPU of this process's rank (settings.gpu on one GPU)
 int mcaat_rank_device(const Settings &s);
 

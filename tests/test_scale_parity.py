@@ -20,6 +20,7 @@ import pytest
 
 import mcaat_amd as M
 import oracle as O
+from mcaat_amd.configs import CONFIGS
 
 pytestmark = pytest.mark.gpu
 
@@ -42,10 +43,14 @@ KNOBS = {
     # every partition overflows the LDS edge table: class split, then the class-filtered global
     # fallback, one (partition, class) per batch
     "fallback": {"nc.edge_cap": 8, "nc.fallback_budget": 1},
+    # pass C with the 8192-slot edge table (error-rich variant), alone and with its class split
+    "big_table": {"nc.big_table": 1},
+    "big_table_split": {"nc.big_table": 1, "nc.edge_cap": 600, "nc.group_budget": 1},
     # every partition overflows the descriptor table: class split, then the raw path
     "desc_raw": {"nc.desc_cap": 2, "nc.fine_bits": 9},
     # level-3 buckets through the 256-thread LDS sort, the 1024-thread one, and the radix fallback
     "sort_mid": {"sort.msd": 1, "sort.wave_limit": 0},
+    "sort_mid_bitonic": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_counting": 0},
     "sort_block": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_limit": 0},
     "sort_radix": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_limit": 0, "sort.block_limit": 0},
     "sort_radix_only": {"sort.msd": 0},
@@ -149,6 +154,9 @@ SAMPLES = {
     "c2_sample": (M.SynthSpec(seed=2, n_genomes=40, genome_len=200_000, arrays_per_genome=2, spacers_per_array=12,
                               repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
                               read_len=150, n_reads=1_000_000, error_rate=5.0e-3, paired=True), 27, 20),
+    # C5 regime (low abundance): threshold_multiplicity 2, 150x coverage, e = 0.17 %
+    # (D / N_occ ~ 0.11 as at C5), k = 27
+    "c5_sample": (CONFIGS["c5"]["sample"], 27, 2),
 }
 
 
@@ -186,6 +194,8 @@ FULL = {
     "c3_full": (M.SynthSpec(seed=3, n_genomes=200, genome_len=1_500_000, arrays_per_genome=2, spacers_per_array=12,
                             repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
                             read_len=150, n_reads=300_000_000, error_rate=2.0e-4), 27, 20),
+    # bench.py "c5": the C3 community at e = 0.17 %, threshold_multiplicity 2 -> D ~ 3.9e9 > 2^31
+    "c5_full": (CONFIGS["c5"]["spec"], 27, 2),
 }
 
 
@@ -202,7 +212,7 @@ def test_full_size_graph_properties(gpu_ctx, name):
     reads.free()
     D = g.size
     n_occ = spec.n_reads * (spec.read_len - k)
-    if name == "c2_full":
+    if name in ("c2_full", "c5_full"):
         assert D > 2 ** 31  # ids above int32 (reference UB region)
     # 1. keys strictly ascending and inside 2E bits; sum of multiplicities = 2 N_occ
     chunk = 1 << 27

@@ -1,7 +1,8 @@
 # PMC counters for the hot-path kernels, one rocprofv3 pass per counter group
 # (never combined with --sys-trace / runtime traces). Usage: bash tools/pmc_c3.sh [reads] [groups]
-R=$PWD; N=${1:-300000000}; G=${2:-"f w"}; mkdir -p gpurun_out/pmc; export TMPDIR=/tmp; cd /tmp
-B="python $R/bench.py --config c3 --reads $N --steps 1 --warmup 0 --no-cpu-baseline --no-post --ingest-reads 0 --no-e2e"
+# CFG=c5 (or c2) profiles that config instead (its full read count unless N is given)
+R=$PWD; CFG=${CFG:-c3}; N=${1:-0}; G=${2:-"f w"}; mkdir -p gpurun_out/pmc; export TMPDIR=/tmp; cd /tmp
+B="python $R/bench.py --config $CFG --reads $N --steps 1 --warmup 0 --no-cpu-baseline --no-post --ingest-reads 0 --no-e2e"
 run() { name=$1; shift; timeout -k 10 400 rocprofv3 --pmc "$@" --output-format csv -d $R/gpurun_out/pmc/$name -o $name -- $B > $R/gpurun_out/pmc/$name.log 2>&1; }
 for g in $G; do
   case $g in
