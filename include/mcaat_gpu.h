@@ -303,6 +303,8 @@ void mcaat_reset_timing(mcaat_ctx *ctx);
  *   cf.walk_budget     > 0: counter-driven peel walks of this many steps before the
  *                      list-ranking peel (default 0: the list-ranking peel alone)
  *   cf.ruler_mask      1 in (mask + 1) unary nodes is a peel ruler besides the chain heads
+ *   cf.fused_init      0: the peel's first pass as its own kernel (default 1: done by the tips /
+ *                      multiplicity-filter pass)
  *   cf.peel_list_div   first ruler-list capacity D / div (default 16; the prep pass runs again
  *                      with the counted size when it overflows)
  *   cf.peel_list_cap / cf.cand_cap   first capacity of the ruler and branch lists / of the

@@ -43,15 +43,22 @@ constexpr int kScanU = 4;
 // were before the filter (every successor window is read from `valid`, which this pass does not
 // write), the filtered bits into `post` (swapped in by the driver); counts[0] tips, counts[1]
 // every mult <= 1 edge (the reference counts valid or not)
+// With nf / nxk (the list-ranking peel's arrays, nf zeroed) the pass also does the peel's
+// first D-wide pass (k_peel_init) from the same loads: an edge's filtered valid out-degree is
+// its successors' unfiltered bits AND their multiplicities > 1 (consecutive ids, one line), so
+// kinds, unary successors and the predecessor flags come out here instead of from a second
+// streaming pass over out_info and the filtered bitmap.
 __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t *tip_bm, uint64_t *post,
-                                                        unsigned long long *counts) {
+                                                        unsigned long long *counts, uint8_t *nf, uint64_t *nxk) {
     const int lane = threadIdx.x & 63;
     const uint64_t nw = (g.D + 63) / 64;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const bool peel = nf != nullptr;
     unsigned long long acc = 0, low_n = 0;
     for (uint64_t wb = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; wb < nw; wb += kScanU * wstride) {
         uint64_t sv[kScanU], oi[kScanU], a0[kScanU], a1[kScanU];
         uint32_t mu[kScanU];
+        uint16_t sm[kScanU][4];
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
             const uint64_t w = wb + u * wstride, e = w * 64 + lane;
@@ -64,12 +71,19 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t *t
             const uint64_t lo = oi[u] & kIdxMask;
             a0[u] = g.valid[this_word(lo, nw)];
             a1[u] = g.valid[next_word(lo, nw)];
+            if (peel) {
+                const uint32_t cnt = __popc((unsigned)(oi[u] >> kIdxBits) & 0xF);
+#pragma unroll
+                for (int i = 0; i < 4; ++i) sm[u][i] = (uint32_t)i < cnt ? g.mult[lo + i] : 0;
+            }
         }
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
-            const uint64_t w = wb + u * wstride;
+            const uint64_t w = wb + u * wstride, e = w * 64 + lane;
+            const uint64_t lo = oi[u] & kIdxMask;
             const uint32_t cnt = __popc((unsigned)(oi[u] >> kIdxBits) & 0xF);
-            const bool t = ((sv[u] >> lane) & 1) && (bits16(a0[u], a1[u], oi[u] & kIdxMask) & ((1u << cnt) - 1)) == 0;
+            const uint32_t pre = bits16(a0[u], a1[u], lo) & ((1u << cnt) - 1);
+            const bool t = ((sv[u] >> lane) & 1) && pre == 0;
             const unsigned long long m = __ballot(t);
             const unsigned long long lowm = __ballot(mu[u] <= 1);
             if (lane == 0 && w < nw) {
@@ -77,6 +91,23 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t *t
                 post[w] = sv[u] & ~lowm;
                 acc += __popcll(m);
                 low_n += __popcll(lowm);
+            }
+            if (peel && e < g.D) {
+                if (!((sv[u] >> lane) & 1) || mu[u] <= 1) {
+                    nf[4 * e] = 0x3F;  // kInvalid
+                } else {
+                    uint64_t out[4];
+                    int od = 0;
+                    for (int i = (int)cnt - 1; i >= 0; --i)  // descending ids, as dev_outgoing
+                        if (((pre >> i) & 1) && sm[u][i] > 1) out[od++] = lo + i;
+                    nf[4 * e] = (uint8_t)od;
+                    if (od == 1) {
+                        nxk[e] = out[0];
+                        nf[4 * out[0] + 1] = 1;  // upred
+                    } else {
+                        for (int j = 0; j < od; ++j) nf[4 * out[j] + 2] = 1;  // bpred
+                    }
+                }
             }
         }
     }
@@ -1235,19 +1266,32 @@ uint64_t select_flagged(mcaat_ctx *ctx, const uint8_t *flags, uint64_t n, uint64
 }  // namespace
 
 // ------------------------------ peel driver -----------------------------------
-static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm) {
+// the peel's per-edge arrays; with `ready` set, k_tips_filter has already filled nf and nxk
+struct PeelState {
+    DevBuf<uint8_t> nf;
+    DevBuf<uint64_t> nxk;
+    bool ready = false;
+};
+
+static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm, PeelState *pre = nullptr) {
     mcaat_ctx *ctx = g->ctx;
     hipStream_t st = ctx->stream;
     const uint64_t D = g->D;
     if (!D) return;
     GraphView v = g->view();
-    DevBuf<uint8_t> nf(4 * D);
-    DevBuf<uint64_t> nxk(D);
+    PeelState local;
+    PeelState &ps = pre ? *pre : local;
     DevBuf<uint32_t> owner(D);
-    HIP_OK(hipMemsetAsync(nf.p, 0, nf.bytes(), st));  // the flag bytes other nodes set
-    PeelArrays pa{nf.p, nxk.p, owner.p, nullptr, nullptr, seed_bm};
-    hipLaunchKernelGGL(k_peel_init, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, v, pa);
-    LAUNCH_OK();
+    if (!ps.ready) {
+        ps.nf.alloc(4 * D);
+        ps.nxk.alloc(D);
+        HIP_OK(hipMemsetAsync(ps.nf.p, 0, ps.nf.bytes(), st));  // the flag bytes other nodes set
+    }
+    PeelArrays pa{ps.nf.p, ps.nxk.p, owner.p, nullptr, nullptr, seed_bm};
+    if (!ps.ready) {
+        hipLaunchKernelGGL(k_peel_init, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, v, pa);
+        LAUNCH_OK();
+    }
     // 1 in (ruler_mask + 1) unary nodes is a ruler besides the chain heads: a walk costs one
     // random read per node whatever the spacing; the rulers are then ranked one level up
     // (1 in 64 of them, plus the heads, are super rulers) before pointer jumping
@@ -1338,7 +1382,7 @@ static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm) {
 // removed) with a per-thread step budget; if chains are longer than that, the pending
 // frontier seeds the parallel ruler/list-ranking peel, whose fixpoint from this state is
 // the same (every pending node is valid, has no valid successor and must be removed).
-static void run_peel(mcaat_graph *g, const uint64_t *seed_bm) {
+static void run_peel(mcaat_graph *g, const uint64_t *seed_bm, PeelState *pre = nullptr) {
     mcaat_ctx *ctx = g->ctx;
     // C3: the reduction walks chains of tens of thousands of edges back from a few hundred
     // seeds (budget 512: 164 walks still pending; 32768: 12, at 0.5 s), so by default the
@@ -1346,7 +1390,7 @@ static void run_peel(mcaat_graph *g, const uint64_t *seed_bm) {
     // counter-driven walks with that step budget first
     const int64_t walk_budget = knob(ctx, "cf.walk_budget", 0);
     if (walk_budget <= 0) {
-        run_peel_rulers(g, seed_bm);
+        run_peel_rulers(g, seed_bm, pre);
         return;
     }
     const uint32_t kBudget = (uint32_t)std::min<int64_t>(walk_budget, 0xFFFFFFFFLL);
@@ -1831,11 +1875,22 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
     // 1-2. CollectTips (before the multiplicity filter) -> seeds of the reduction, and
     // InvalidateMultiplicityOneNodes, in one pass (the filtered bits go to a second bitmap)
     DevBuf<uint64_t> seeds(nw);
+    // the list-ranking peel (the default) gets its first pass from this one (cf.fused_init=0:
+    // its own k_peel_init)
+    PeelState ps;
+    const bool fuse = knob(ctx, "cf.walk_budget", 0) <= 0 && knob(ctx, "cf.fused_init", 1) != 0 && D;
+    if (fuse) {
+        ps.nf.alloc(4 * D);
+        ps.nxk.alloc(D);
+        HIP_OK(hipMemsetAsync(ps.nf.p, 0, ps.nf.bytes(), st));
+        ps.ready = true;
+    }
     {
         DevBuf<uint64_t> post(nw);
         DevBuf<unsigned long long> c2(2);
         HIP_OK(hipMemsetAsync(c2.p, 0, 16, st));
-        hipLaunchKernelGGL(k_tips_filter, dim3(wgrid), dim3(kBlock), 0, st, v, seeds.p, post.p, c2.p);
+        hipLaunchKernelGGL(k_tips_filter, dim3(wgrid), dim3(kBlock), 0, st, v, seeds.p, post.p, c2.p,
+                           fuse ? ps.nf.p : (uint8_t *)nullptr, fuse ? ps.nxk.p : (uint64_t *)nullptr);
         LAUNCH_OK();
         unsigned long long hc[2];
         HIP_OK(hipMemcpyAsync(hc, c2.p, 16, hipMemcpyDeviceToHost, st));
@@ -1848,8 +1903,10 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
     timer.mark("tips_filter");
     verbose_mark(ctx, "cf.tips_filter");
     // 3. RecursiveReduction from every seed
-    run_peel(g, seeds.p);
+    run_peel(g, seeds.p, fuse ? &ps : nullptr);
     seeds.release();
+    ps.nf.release();
+    ps.nxk.release();
     timer.mark("peel");
     verbose_mark(ctx, "cf.peel");
     // 4-5. valid count + tips after pruning, and ChunkStartNodes' candidate filter (its

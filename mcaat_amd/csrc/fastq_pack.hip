@@ -21,6 +21,7 @@
 // the counting view.
 #include <fcntl.h>
 #include <immintrin.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -179,6 +180,17 @@ class PartPacker {
 };
 
 // parse [b, e) of a plain file: 4-line records, each sequence packed; false = declined
+// MCAAT_PACK_MMAP=1: the part is mapped (page-cache pages read in place, no copy) and its page
+// tables are filled a window ahead by madvise(MADV_POPULATE_READ) instead of one fault per page
+bool pack_mmap() {
+    const char *e = getenv("MCAAT_PACK_MMAP");
+    return e && e[0] == '1';
+}
+#ifndef MADV_POPULATE_READ
+#define MADV_POPULATE_READ 22
+#endif
+constexpr size_t kWin = 32u << 20;
+
 bool pack_part(const char *path, uint64_t b, uint64_t e, bool file_end, PartPacker &pk, Shared &sh, PartOut &o) {
     const int fd = open(path, O_RDONLY);
     if (fd < 0) {
@@ -189,12 +201,48 @@ bool pack_part(const char *path, uint64_t b, uint64_t e, bool file_end, PartPack
         int fd;
         ~Fd() { close(fd); }
     } guard{fd};
-    std::vector<uint8_t> buf(kBlk + kMaxRecord + 64);
+    const bool mapped = pack_mmap() && e > b;
+    std::vector<uint8_t> buf(mapped ? 0 : kBlk + kMaxRecord + 64);
     uint8_t *B = buf.data();
     size_t have = 0;  // bytes in B
     uint64_t off = b;
     size_t i = 0;     // parse position in B
     bool eof = b >= e;
+    // mapped: [map_off, e) with B at byte b; the whole part is "read" at once
+    uint8_t *map = nullptr;
+    size_t map_len = 0, populated = 0;
+    struct Unmap {
+        uint8_t *&p;
+        size_t &n;
+        ~Unmap() {
+            if (p) munmap(p, n);
+        }
+    } unmap_guard{map, map_len};
+    if (mapped) {
+        const uint64_t map_off = b & ~(uint64_t)4095;
+        map_len = (size_t)(e - map_off);
+        void *m = mmap(nullptr, map_len, PROT_READ, MAP_SHARED, fd, (off_t)map_off);
+        if (m == MAP_FAILED) {
+            o.error = "mmap failed";
+            return false;
+        }
+        map = (uint8_t *)m;
+        B = map + (b - map_off);
+        have = (size_t)(e - b);
+        off = e;
+        eof = true;
+    }
+    auto populate = [&](size_t upto) {  // page tables of B[0, upto) filled ahead of the parse
+        if (!mapped) return;
+        while (populated < upto && populated < have) {
+            const size_t n = std::min(kWin, have - populated);
+            // page-aligned start inside the mapping
+            const size_t a0 = (size_t)(B - map) + populated, a = a0 & ~(size_t)4095;
+            (void)madvise(map + a, n + (a0 - a), MADV_POPULATE_READ);
+            populated += n;
+        }
+    };
+    std::vector<uint8_t> tail;  // a sequence too close to the end of the mapping for 32-B loads
     auto refill = [&]() -> bool {
         // keep the unparsed tail, read the next block behind it
         if (i) {
@@ -216,13 +264,14 @@ bool pack_part(const char *path, uint64_t b, uint64_t e, bool file_end, PartPack
         memset(B + have, 0, 64);  // the packer reads up to 31 bytes past a line
         return true;
     };
-    if (!refill()) return false;
+    if (!mapped && !refill()) return false;
     auto line_end = [&](size_t from) -> size_t {  // index of the '\n' ending the line at from, or ~0
         const void *p = memchr(B + from, '\n', have - from);
         return p ? (size_t)((const uint8_t *)p - B) : ~(size_t)0;
     };
     for (;;) {
         if (sh.decline.load(std::memory_order_relaxed)) return false;
+        if (mapped && i + kMaxRecord > populated) populate(i + kMaxRecord + kWin);
         if (i == have) {
             if (eof) break;
             if (!refill()) return false;
@@ -250,7 +299,13 @@ bool pack_part(const char *path, uint64_t b, uint64_t e, bool file_end, PartPack
         const size_t n = s - (h + 1);
         if (n == 0 || q - (p + 1) != n) return false;
         if (B[s - 1] == '\r' || B[h - 1] == '\r' || B[q - 1] == '\r' || B[p - 1] == '\r') return false;
-        if (!pk.append(B + h + 1, (uint32_t)n)) return false;
+        if (mapped && h + 1 + n + 32 > have) {  // the 32-B loads would leave the mapping
+            tail.assign(B + h + 1, B + h + 1 + n);
+            tail.resize(n + 64, 0);
+            if (!pk.append(tail.data(), (uint32_t)n)) return false;
+        } else if (!pk.append(B + h + 1, (uint32_t)n)) {
+            return false;
+        }
         i = q < have ? q + 1 : have;
     }
     return true;

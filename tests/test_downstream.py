@@ -255,3 +255,27 @@ def test_cli_crispr_arrays_match_oracle_path(tmp_path, paired, gpus):
     DS.crispr_arrays(23, keys, mult, valid, cycles, reads, str(ref_file))
     assert got == ref_file.read_text()
     assert "Number of Systems: 2" in got
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("comm", ["shm", "rccl"])
+def test_cli_rank_dying_before_it_joins_ends_the_run(tmp_path, comm):
+    """A forked rank that exits before joining the communicator (device selection, OOM, ...)
+    ends the run at once: rank 0 reaps its children from the fork on, so it does not wait in
+    the join (ncclCommInitRank has no timeout; the shared-memory join waits 900 s). With one
+    GPU on the box, rccl with 2 ranks stops at its own GPU-count check, also promptly."""
+    import time
+
+    spec = M.SynthSpec()
+    packed, offs = M.synth_host(spec)
+    p = tmp_path / "r.fq"
+    with open(p, "w") as f:
+        for i in range(len(offs) - 1):
+            s = unpack_read(packed, int(offs[i]), int(offs[i + 1]))
+            f.write(f"@r{i}\n{s}\n+\n{'I' * len(s)}\n")
+    env = dict(os.environ, MCAAT_TEST_RANK_EXIT="1")
+    t0 = time.time()
+    out = subprocess.run([CLI, "-i", str(p), "--output-folder", str(tmp_path / "o"), "--threads", "2", "--gpus", "2",
+                          "--comm", comm], capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode != 0
+    assert time.time() - t0 < 120, "the run waited for a rank that had already died"

@@ -251,14 +251,17 @@ def _packed_by_host(ctx):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("mmap", ["0", "1"])
 @pytest.mark.parametrize("threads,lens,final_nl", [("16", [150], True), ("3", [150], False),
                                                      ("7", [1, 31, 32, 33, 64, 150, 251, 1000], True),
-                                                     ("1", [77], True)])
-def test_host_pack_single_end(gpu_ctx, tmp_path, monkeypatch, threads, lens, final_nl):
+                                                     ("1", [77], True), ("2", [1], False)])
+def test_host_pack_single_end(gpu_ctx, tmp_path, monkeypatch, threads, lens, final_nl, mmap):
     """Fixed and variable read lengths (words shared by reads, 32-base boundaries), parts cut
-    at record starts for 1..16 threads, a final record without its newline: the same library
-    as the text parser's restatement, and the host packer is the path that ran."""
+    at record starts for 1..16 threads, a final record without its newline, the part read with
+    pread() or mapped (MCAAT_PACK_MMAP; short final records near the end of the mapping): the
+    same library as the text parser's restatement, and the host packer is the path that ran."""
     monkeypatch.setenv("MCAAT_PACK_THREADS", threads)
+    monkeypatch.setenv("MCAAT_PACK_MMAP", mmap)
     rng = np.random.default_rng(int(threads) * 7 + len(lens))
     seqs = _acgt_records(rng, 3001, lens)
     text = _fastq_text(seqs, final_newline=final_nl)

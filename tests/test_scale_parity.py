@@ -70,6 +70,8 @@ KNOBS = {
     # the ruler / branch lists and the candidate list start with one entry: the passes that
     # fill them run again with the counted sizes
     "list_regrow": {"cf.peel_list_cap": 1, "cf.cand_cap": 1},
+    # the peel's first pass as its own kernel instead of inside the tips / filter pass
+    "peel_own_init": {"cf.fused_init": 0},
     # passes B and C of successive groups in turn on one stream
     "nc_no_overlap": {"nc.overlap": 0, "nc.group_budget": 1 << 14},
     # adjacency: per-edge global directory searches, and the LDS-range kernel with every range
