@@ -778,6 +778,15 @@ int mcaat_graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, i
     });
 }
 
+int mcaat_graph_gather(const mcaat_graph *g, const uint64_t *ids, size_t n, uint64_t *keys, uint16_t *mult) {
+    return guarded([&] {
+        require(g && (n == 0 || ids), "null argument");
+        for (size_t i = 0; i < n; ++i) require(ids[i] < g->D, "edge id out of range");
+        HIP_OK(hipSetDevice(g->ctx->device));
+        graph_gather(g, ids, n, keys, mult);
+    });
+}
+
 int mcaat_graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n) {
     return guarded([&] {
         require(g && (ids || n == 0), "null argument");

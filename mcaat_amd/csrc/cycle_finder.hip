@@ -2012,6 +2012,29 @@ void graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, int in
     HIP_OK(hipStreamSynchronize(st));
 }
 
+__global__ void k_gather_key_mult(const uint64_t *key, const uint16_t *mult, const uint64_t *ids, uint64_t n,
+                                  uint64_t *ko, uint16_t *mo) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t e = ids[i];
+    if (ko) ko[i] = key[e];
+    if (mo) mo[i] = mult[e];
+}
+
+void graph_gather(const mcaat_graph *g, const uint64_t *ids, size_t n, uint64_t *keys, uint16_t *mult) {
+    if (!n) return;
+    hipStream_t st = g->ctx->stream;
+    DevBuf<uint64_t> di(n), dk(keys ? n : 1);
+    DevBuf<uint16_t> dm(mult ? n : 1);
+    HIP_OK(hipMemcpyAsync(di.p, ids, 8 * n, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(k_gather_key_mult, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, g->key.p, g->mult.p, di.p,
+                       (uint64_t)n, keys ? dk.p : (uint64_t *)nullptr, mult ? dm.p : (uint16_t *)nullptr);
+    LAUNCH_OK();
+    if (keys) HIP_OK(hipMemcpyAsync(keys, dk.p, 8 * n, hipMemcpyDeviceToHost, st));
+    if (mult) HIP_OK(hipMemcpyAsync(mult, dm.p, 2 * n, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+}
+
 void graph_set_valid(mcaat_graph *g, const uint64_t *ids, size_t n, int valid) {
     if (!n) return;
     for (size_t i = 0; i < n; ++i)

@@ -366,6 +366,7 @@ void synth_genome_host(const mcaat_synth_spec &s, std::vector<uint64_t> &genome)
 void graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, int incoming, uint64_t *out,
                      int32_t *counts);
 void graph_set_valid(mcaat_graph *g, const uint64_t *ids, size_t n, int valid);
+void graph_gather(const mcaat_graph *g, const uint64_t *ids, size_t n, uint64_t *keys, uint16_t *mult);
 void graph_download_valid(const mcaat_graph *g, uint8_t *valid);
 void graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n);
 // FASTQ(.gz) inputs parsed on the GPU (fastq_ingest.hip)

@@ -9,6 +9,7 @@
 // over batched (device) neighbour queries, Tarjan's recursion is an explicit stack, and
 // the invalidation of everything outside the regions is one bitmap AND.
 #include <algorithm>
+#include <chrono>
 #include <functional>
 #include <iomanip>
 #include <iostream>
@@ -91,8 +92,8 @@ std::vector<uint32_t> merge_runs(const std::vector<uint32_t> &v) {  // A,A,B,C,C
 
 std::vector<std::vector<uint64_t>> find_strongly_connected_components(const SDBG &sdbg) {
     Tarjan t(sdbg);
-    for (uint64_t v = 0; v < sdbg.size(); ++v)  // valid nodes in ascending id order
-        if (sdbg.IsValidEdge(v) && !t.index.count(v)) t.run(v);
+    for (uint64_t v : sdbg.ValidIds())  // valid nodes in ascending id order
+        if (!t.index.count(v)) t.run(v);
     return std::move(t.components);
 }
 
@@ -122,6 +123,13 @@ void keep_crispr_regions_extended_by_k(SDBG &sdbg, const size_t &k, const std::v
     }
     std::vector<uint64_t> keep(region.begin(), region.end());
     sdbg.KeepOnly(keep);
+    // every node the SCC split and the subgraphs query from here on is one of these: their
+    // out-neighbours (valid-only, after the AND) and labels in two device calls
+    std::vector<uint64_t> live;
+    for (uint64_t e : keep)
+        if (sdbg.IsValidEdge(e)) live.push_back(e);
+    sdbg.PrefetchOutgoing(live);
+    sdbg.PrefetchKeys(live);
 }
 
 // spacer_ordering.cpp:140-173: one Graph per SCC, edges inside the component only
@@ -144,8 +152,14 @@ std::vector<Graph> divide_graph_into_subgraphs(const SDBG &sdbg) {
 
 std::vector<Graph> get_crispr_regions_extended_by_k(SDBG &sdbg, const size_t &k,
                                                     const std::vector<std::vector<uint64_t>> &cycles) {
+    using clk = std::chrono::high_resolution_clock;
+    const auto t0 = clk::now();
     keep_crispr_regions_extended_by_k(sdbg, k, cycles);
-    return divide_graph_into_subgraphs(sdbg);
+    const auto t1 = clk::now();
+    auto out = divide_graph_into_subgraphs(sdbg);
+    std::cout << "TIMING_REGIONS grow_s=" << std::chrono::duration<double>(t1 - t0).count()
+              << " divide_s=" << std::chrono::duration<double>(clk::now() - t1).count() << std::endl;
+    return out;
 }
 
 // spacer_ordering.cpp:184-198: reads starting or ending inside the region

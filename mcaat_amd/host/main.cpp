@@ -6,6 +6,7 @@
 #include <sys/wait.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <chrono>
 #include <csignal>
@@ -249,6 +250,14 @@ static int run(Settings &settings, Ranks &ranks) {
         std::cout << "Number of nodes in results: " << cycles_map.size() << std::endl;
         auto cycles = cycles_map_to_cycles(cycles_map);        // main.cpp:542
         if (rank0) {
+            {  // the cycles' labels in one device call (not a host copy of the whole graph)
+                std::vector<uint64_t> nodes;
+                for (const auto &[start, inner] : cycles_map)
+                    for (const auto &c : inner) nodes.insert(nodes.end(), c.begin(), c.end());
+                std::sort(nodes.begin(), nodes.end());
+                nodes.erase(std::unique(nodes.begin(), nodes.end()), nodes.end());
+                sdbg.PrefetchKeys(nodes);
+            }
             const std::string out = settings.cycles_folder + "/cycles.txt";
             std::ofstream f(out);
             size_t idx = 0;

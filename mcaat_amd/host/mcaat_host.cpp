@@ -2,6 +2,7 @@
 #include "mcaat_host.h"
 
 #include <algorithm>
+#include <cstring>
 #include <chrono>
 #include <filesystem>
 #include <fstream>
@@ -141,6 +142,8 @@ void SDBG::LoadFromDevice(mcaat_graph *g) {
     g_ = g;
     mcaat_check(mcaat_graph_info(g_, &k_, &D_), "mcaat_graph_info");
     have_arrays_ = have_valid_ = false;
+    kcache_.clear();
+    ocache_.clear();
     std::vector<uint64_t>().swap(key_);
     std::vector<uint16_t>().swap(mult_);
     std::vector<uint8_t>().swap(valid_);
@@ -171,6 +174,8 @@ void SDBG::LoadFromArrays(int k, std::vector<uint64_t> keys, std::vector<uint16_
     mult_ = std::move(mult);
     valid_ = std::move(valid);
     have_arrays_ = have_valid_ = true;
+    kcache_.clear();
+    ocache_.clear();
 }
 
 const std::vector<uint64_t> &SDBG::host_key() const {
@@ -199,9 +204,11 @@ const std::vector<uint8_t> &SDBG::host_valid() const {
 
 void SDBG::SyncFromDevice() {
     if (g_) have_valid_ = false;  // re-read on the next host query
+    ocache_.clear();
 }
 
 void SDBG::KeepOnly(const std::vector<uint64_t> &ids) {
+    ocache_.clear();
     if (have_valid_ || !g_) {
         std::vector<uint8_t> keep(valid_.size(), 0);
         for (uint64_t e : ids)
@@ -212,11 +219,13 @@ void SDBG::KeepOnly(const std::vector<uint64_t> &ids) {
 }
 
 void SDBG::SetInvalidEdge(uint64_t e) {
+    ocache_.clear();
     if (have_valid_ || !g_) valid_[e] = 0;
     if (g_) mcaat_check(mcaat_graph_set_valid(g_, &e, 1, 0), "mcaat_graph_set_valid");
 }
 
 void SDBG::SetValidEdge(uint64_t e) {
+    ocache_.clear();
     if (have_valid_ || !g_) valid_[e] = 1;
     if (g_) mcaat_check(mcaat_graph_set_valid(g_, &e, 1, 1), "mcaat_graph_set_valid");
 }
@@ -227,6 +236,14 @@ uint64_t SDBG::lower(uint64_t q) const {
 }
 
 int SDBG::OutgoingEdges(uint64_t e, uint64_t *out) const {
+    if (!ocache_.empty()) {
+        auto it = ocache_.find(e);
+        if (it != ocache_.end()) {
+            const int n = (int)it->second[0];
+            for (int i = 0; i < n; ++i) out[i] = it->second[1 + i];
+            return n;
+        }
+    }
     const auto &key_ = host_key();
     const auto &valid_ = host_valid();
     const uint64_t K = key_[e], W = K & 3, R = K >> 2;
@@ -265,8 +282,50 @@ void SDBG::NeighborsBatch(const std::vector<uint64_t> &ids, bool incoming, std::
         counts[i] = incoming ? IncomingEdges(ids[i], &out[4 * i]) : OutgoingEdges(ids[i], &out[4 * i]);
 }
 
+void SDBG::PrefetchKeys(const std::vector<uint64_t> &ids) {
+    if (!g_ || ids.empty()) return;
+    std::vector<uint64_t> want;
+    for (uint64_t e : ids)
+        if (!kcache_.count(e)) want.push_back(e);
+    if (want.empty()) return;
+    std::vector<uint64_t> kk(want.size());
+    std::vector<uint16_t> mm(want.size());
+    mcaat_check(mcaat_graph_gather(g_, want.data(), want.size(), kk.data(), mm.data()), "mcaat_graph_gather");
+    for (size_t i = 0; i < want.size(); ++i) kcache_[want[i]] = {kk[i], mm[i]};
+}
+
+void SDBG::PrefetchOutgoing(const std::vector<uint64_t> &ids) {
+    if (!g_ || ids.empty()) return;
+    std::vector<uint64_t> nb;
+    std::vector<int32_t> cnt;
+    NeighborsBatch(ids, false, nb, cnt);
+    for (size_t i = 0; i < ids.size(); ++i) {
+        std::array<uint64_t, 5> a{(uint64_t)cnt[i], 0, 0, 0, 0};
+        for (int j = 0; j < cnt[i]; ++j) a[1 + j] = nb[4 * i + j];
+        ocache_[ids[i]] = a;
+    }
+}
+
+std::vector<uint64_t> SDBG::ValidIds() const {
+    const auto &v = host_valid();
+    std::vector<uint64_t> out;
+    const uint64_t n = v.size(), nw = n / 8;
+    const uint8_t *p = v.data();
+    for (uint64_t w = 0; w < nw; ++w) {  // eight bytes at a time, all-zero words skipped
+        uint64_t x;
+        memcpy(&x, p + 8 * w, 8);
+        if (!x) continue;
+        for (int j = 0; j < 8; ++j)
+            if (p[8 * w + j]) out.push_back(8 * w + j);
+    }
+    for (uint64_t e = 8 * nw; e < n; ++e)
+        if (p[e]) out.push_back(e);
+    return out;
+}
+
 uint32_t SDBG::GetLabel(uint64_t e, uint8_t *seq) const {
-    const uint64_t R = host_key()[e] >> 2;
+    auto it = kcache_.find(e);
+    const uint64_t R = (it != kcache_.end() ? it->second.first : host_key()[e]) >> 2;
     for (int i = 0; i < k_; ++i) seq[i] = (uint8_t)(((R >> (2 * i)) & 3) + 1);
     return (uint32_t)k_;
 }

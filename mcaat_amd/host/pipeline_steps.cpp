@@ -38,6 +38,7 @@ std::vector<FoundSystem> run_and_debug_spacer_ordering(const std::vector<std::ve
     std::cout << "  ▸ Splitting into subproblems" << std::endl;
     const size_t read_nodes = reads.at(0).size();  // the region growth radius (reference: reads.at(0).size())
     auto regions = get_crispr_regions_extended_by_k(sdbg, read_nodes, cycles);
+    const auto t_regions = std::chrono::high_resolution_clock::now();
 
     std::cout << "  🔄 Filtering subproblems:" << std::endl;
     struct Sub {
@@ -58,6 +59,7 @@ std::vector<FoundSystem> run_and_debug_spacer_ordering(const std::vector<std::ve
     }
     std::cout << "  ✅ Filtered out " << regions.size() - subs.size() << "/" << regions.size() << " subproblems"
               << std::endl;
+    const auto t_filtered = std::chrono::high_resolution_clock::now();
     std::cout << "  🔄 Solving " << subs.size() << " subproblems..." << std::endl;
 
     std::vector<FoundSystem> found;
@@ -88,6 +90,13 @@ std::vector<FoundSystem> run_and_debug_spacer_ordering(const std::vector<std::ve
         found.emplace_back(sequence, repeat, spacers, conf_resolution, conf_sort);
     }
     std::cout << "  ✅ Completed each subproblem" << std::endl;
+    {
+        using sec = std::chrono::duration<double>;
+        const auto t_end = std::chrono::high_resolution_clock::now();
+        std::cout << "TIMING_STEP7 regions_s=" << sec(t_regions - t0).count()
+                  << " filter_s=" << sec(t_filtered - t_regions).count() << " solve_s=" << sec(t_end - t_filtered).count()
+                  << std::endl;
+    }
     print_elapsed(t0);
     return found;
 }

@@ -107,6 +107,7 @@ SIGNATURES = {
                                           C.POINTER(C.c_void_p)]),
     "mcaat_reads_records_info": (C.c_int, [C.c_void_p, _u64p, C.POINTER(C.c_int)]),
     "mcaat_graph_keep_only": (C.c_int, [C.c_void_p, _u64p, C.c_size_t]),
+    "mcaat_graph_gather": (C.c_int, [C.c_void_p, _u64p, C.c_size_t, _u64p, _u16p]),
     "mcaat_map_reads": (C.c_int, [C.c_void_p, C.c_void_p, _u64p, C.c_size_t, C.c_uint64, C.POINTER(C.c_void_p)]),
     "mcaat_mapped_get": (C.c_int, [C.c_void_p, _u64p, C.POINTER(_u64p), C.POINTER(_u64p), C.POINTER(_u64p)]),
     "mcaat_mapped_free": (None, [C.c_void_p]),
@@ -627,6 +628,14 @@ class Graph:
         _check(self.ctx._lib.mcaat_graph_neighbors(self.h, _ptr(ids, _u64p), ids.size, int(incoming),
                                                    _ptr(out, _u64p), _ptr(cnt, _i32p)))
         return out[: 4 * ids.size].reshape(-1, 4), cnt[: ids.size]
+
+    def gather(self, ids: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        """(keys, mult) of the given edge ids (mcaat_graph_gather)."""
+        ids = np.ascontiguousarray(ids, dtype=np.uint64)
+        kk = np.zeros(max(ids.size, 1), dtype=np.uint64)
+        mm = np.zeros(max(ids.size, 1), dtype=np.uint16)
+        _check(self.ctx._lib.mcaat_graph_gather(self.h, _ptr(ids, _u64p), ids.size, _ptr(kk, _u64p), _ptr(mm, _u16p)))
+        return kk[: ids.size], mm[: ids.size]
 
     def keep_only(self, ids: np.ndarray) -> None:
         """valid &= {ids} (keep_crispr_regions_extended_by_k, spacer_ordering.cpp:129-137)."""

@@ -24,7 +24,7 @@ sys.path.insert(0, ROOT)
 import mcaat_amd as M  # noqa: E402
 
 
-def digest(g, res) -> dict:
+def checksums(g, res) -> dict:
     """Order-sensitive checksums of the graph (keys, multiplicities, valid bits after
     CycleFinder) and the full CycleFinder results; two runs agree iff these agree (up to
     64-bit checksum collisions)."""
@@ -86,7 +86,7 @@ def main() -> int:
             g = M.Graph.build_sharded(ctx, comm, mine, k)
             mine.free()
             res = g.cycle_finder(prm, comm=comm)
-        d = digest(g, res)
+        d = checksums(g, res)
         d["seconds"] = round(time.time() - t0, 1)
         g.free()
         if comm is not None:
