@@ -561,11 +561,155 @@ std::vector<uint32_t> solve_constraints_with_topological_sort(
     return order;
 }
 
+// ---- the same constraints as (distinct pair, multiplicity) in first-occurrence order --------
+// Everything downstream of generate_constraints depends on the constraint list only through
+// (a) each distinct pair's multiplicity (Kruskal's weights, heuristic penalties, affection,
+// topological edge weights, the confidence ratio) and (b) the order in which distinct pairs
+// first occur (the insertion order of the topological sort's unordered_map, whose iteration
+// order decides ties; re-inserting a present key changes nothing). A read's pairs are
+// every_possible_combination of its cycle-index sequence: with the sequence as runs (value a_p,
+// length c_p), pair (a_p, a_q), p < q, a_p != a_q, occurs c_p * c_q times and the pairs first
+// occur in (p, q) order — O(runs^2) per read instead of O(nodes^2) (C3: 800 regions x ~460
+// reads x ~120 nodes; step 7 of the CLI 15.5 s). MCAAT_ORDER_REF=1 runs the list form.
+struct WeightedConstraints {
+    std::vector<std::tuple<uint32_t, uint32_t>> pair;
+    std::vector<int64_t> weight;
+    std::unordered_map<std::tuple<uint32_t, uint32_t>, uint32_t, TupleHash> index;
+    void add(std::tuple<uint32_t, uint32_t> t, int64_t w) {
+        auto it = index.find(t);
+        if (it == index.end()) {
+            index.emplace(t, (uint32_t)pair.size());
+            pair.push_back(t);
+            weight.push_back(w);
+        } else {
+            weight[it->second] += w;
+        }
+    }
+    int64_t total() const {
+        int64_t n = 0;
+        for (int64_t w : weight) n += w;
+        return n;
+    }
+};
+
+static WeightedConstraints generate_constraints_weighted(const std::vector<std::vector<uint64_t>> &reads,
+                                                         const std::unordered_map<uint64_t, uint32_t> &node_to_cycle_map) {
+    WeightedConstraints wc;
+    std::vector<uint32_t> seq;                   // cycle index per node, NOT_IN_ANY_CYCLE_INDEX outside
+    std::vector<std::pair<uint32_t, int64_t>> runs;  // runs of the in-cycle subsequence
+    for (const auto &r : reads) {
+        seq.clear();
+        for (uint64_t x : r) {
+            auto it = node_to_cycle_map.find(x);
+            seq.push_back(it == node_to_cycle_map.end() ? NOT_IN_ANY_CYCLE_INDEX : it->second);
+        }
+        runs.clear();
+        for (uint32_t v : seq) {
+            if (v == NOT_IN_ANY_CYCLE_INDEX) continue;
+            if (!runs.empty() && runs.back().first == v) ++runs.back().second;
+            else runs.push_back({v, 1});
+        }
+        for (size_t p = 0; p < runs.size(); ++p)
+            for (size_t q = p + 1; q < runs.size(); ++q)
+                if (runs[p].first != runs[q].first)
+                    wc.add(std::make_tuple(runs[p].first, runs[q].first), runs[p].second * runs[q].second);
+        // generate_out_of_cycles_constraints_from_read
+        if (!seq.empty() && seq.front() != NOT_IN_ANY_CYCLE_INDEX && seq.back() != NOT_IN_ANY_CYCLE_INDEX) {
+            const std::vector<uint32_t> m = merge_runs(seq);
+            if (m.size() > 1) wc.add(std::make_tuple(m[0], m[1]), 1);
+        }
+    }
+    return wc;
+}
+
+static void resolve_cycles_greedy_weighted(WeightedConstraints &wc, std::unordered_map<uint32_t, int> &heuristic) {
+    // get_maximal_spanning_tree: weights per distinct pair, heaviest first, ties by larger tuple
+    std::vector<std::pair<int64_t, std::tuple<uint32_t, uint32_t>>> order;
+    for (size_t i = 0; i < wc.pair.size(); ++i) order.push_back({wc.weight[i], wc.pair[i]});
+    std::sort(order.begin(), order.end(), std::greater<std::pair<int64_t, std::tuple<uint32_t, uint32_t>>>());
+    std::unordered_map<uint32_t, uint32_t> parent;
+    std::unordered_map<uint32_t, int> rank;
+    std::function<uint32_t(uint32_t)> root = [&](uint32_t x) -> uint32_t {
+        if (!parent.count(x)) {
+            parent[x] = x;
+            rank[x] = 0;
+        }
+        if (parent[x] != x) parent[x] = root(parent[x]);
+        return parent[x];
+    };
+    std::unordered_set<std::tuple<uint32_t, uint32_t>, TupleHash> in_tree;
+    for (const auto &we : order) {
+        const uint32_t a = root(std::get<0>(we.second)), b = root(std::get<1>(we.second));
+        if (a == b) continue;
+        if (rank[a] < rank[b]) parent[a] = b;
+        else if (rank[a] > rank[b]) parent[b] = a;
+        else {
+            parent[b] = a;
+            rank[a]++;
+        }
+        in_tree.insert(we.second);
+    }
+    WeightedConstraints kept;
+    for (size_t i = 0; i < wc.pair.size(); ++i) {
+        const auto &c = wc.pair[i];
+        const uint32_t from = std::get<0>(c), to = std::get<1>(c);
+        if (!in_tree.count(c) && from != NOT_IN_ANY_CYCLE_INDEX && to != NOT_IN_ANY_CYCLE_INDEX)
+            heuristic[to] -= (int)wc.weight[i];
+        else
+            kept.add(c, wc.weight[i]);
+    }
+    wc = std::move(kept);
+}
+
+static std::vector<uint32_t> solve_topological_weighted(const WeightedConstraints &wc,
+                                                        std::unordered_map<uint32_t, int> &heuristic,
+                                                        const std::vector<uint32_t> &nodes, float &confidence) {
+    std::unordered_map<std::tuple<uint32_t, uint32_t>, int, TupleHash> edges;
+    for (size_t i = 0; i < wc.pair.size(); ++i) {  // first-occurrence order, as the list fills it
+        const auto &c = wc.pair[i];
+        if (std::get<0>(c) != NOT_IN_ANY_CYCLE_INDEX && std::get<1>(c) != NOT_IN_ANY_CYCLE_INDEX)
+            edges[c] += (int)wc.weight[i];
+    }
+    std::unordered_set<uint32_t> has_in;
+    for (const auto &c : wc.pair)
+        if (std::get<0>(c) != NOT_IN_ANY_CYCLE_INDEX) has_in.insert(std::get<1>(c));
+    std::vector<uint32_t> starts;
+    for (uint32_t v : nodes)
+        if (!has_in.count(v)) starts.push_back(v);
+    std::unordered_map<uint32_t, int> affection;
+    for (uint32_t v : nodes) affection[v] = 0;
+    for (size_t i = 0; i < wc.pair.size(); ++i) {
+        const uint32_t a = std::get<0>(wc.pair[i]), b = std::get<1>(wc.pair[i]);
+        if (a != NOT_IN_ANY_CYCLE_INDEX && b != NOT_IN_ANY_CYCLE_INDEX) continue;
+        if (a == NOT_IN_ANY_CYCLE_INDEX) affection[b] += (int)wc.weight[i];
+        else affection[a] -= (int)wc.weight[i];
+    }
+    std::vector<uint32_t> order;
+    confidence = 0.0;
+    apply_topological_sort(starts, affection, heuristic, edges, order, confidence);
+    confidence /= order.size();
+    return order;
+}
+
 std::vector<uint32_t> order_cycles(const Graph &graph, const std::vector<std::vector<uint64_t>> &reads,
                                    const std::vector<std::vector<uint64_t>> &cycles, float &confidence_cycle_resolution,
                                    float &confidence_topological_sort) {  // spacer_ordering.cpp:719-754
     const auto node_to_cycle = get_node_to_unique_cycle_map(cycles);
     const auto cycle_ids = get_all_cycle_indices(node_to_cycle);
+    const char *ref = getenv("MCAAT_ORDER_REF");
+    if (!(ref && ref[0] == '1')) {
+        auto wc = generate_constraints_weighted(reads, node_to_cycle);
+        const int64_t before = wc.total();
+        std::cout << "      ▸ " << before << " constraints derived" << std::endl;
+        std::unordered_map<uint32_t, int> heuristic;
+        for (uint32_t c : cycle_ids) heuristic[c] = 0;
+        resolve_cycles_greedy_weighted(wc, heuristic);
+        const int64_t after = wc.total();
+        confidence_cycle_resolution = static_cast<float>(after) / static_cast<float>(before);
+        std::cout << "      ▸ " << after << " constraints remain after resolving cycles (confidence = " << std::fixed
+                  << std::setprecision(2) << (confidence_cycle_resolution * 100) << "%)" << std::endl;
+        return solve_topological_weighted(wc, heuristic, cycle_ids, confidence_topological_sort);
+    }
     auto constraints = generate_constraints(graph, reads, node_to_cycle);
     std::cout << "      ▸ " << constraints.size() << " constraints derived" << std::endl;
     std::unordered_map<uint32_t, int> heuristic;
