@@ -20,61 +20,67 @@
 namespace {
 
 // Tarjan's SCC from `root` (spacer_ordering.cpp:3-51) with an explicit frame stack visiting
-// successors in OutgoingEdges order, exactly as the recursion does.
+// successors in OutgoingEdges order, exactly as the recursion does. The nodes it can reach are
+// the valid ones (ids, ascending), so index / low / on-stack are dense arrays over their
+// positions in that list instead of hash maps keyed by edge id.
 struct Tarjan {
     const SDBG &g;
-    std::unordered_map<uint64_t, int> index, low;
-    std::unordered_set<uint64_t> on_stack;
-    std::vector<uint64_t> stack;
+    const std::vector<uint64_t> &ids;  // valid ids, ascending
+    std::vector<int> index, low;       // -1: not visited
+    std::vector<char> on_stack;
+    std::vector<uint32_t> stack;
     std::vector<std::vector<uint64_t>> components;
     int counter = 0;
-    explicit Tarjan(const SDBG &s) : g(s) {}
+    Tarjan(const SDBG &s, const std::vector<uint64_t> &v)
+        : g(s), ids(v), index(v.size(), -1), low(v.size(), 0), on_stack(v.size(), 0) {}
+    uint32_t pos(uint64_t e) const { return (uint32_t)(std::lower_bound(ids.begin(), ids.end(), e) - ids.begin()); }
 
     struct Frame {
-        uint64_t v;
+        uint32_t v;
         uint64_t nb[4];
         int n, next;
     };
-    void open(std::vector<Frame> &frames, uint64_t v) {
+    void open(std::vector<Frame> &frames, uint32_t v) {
         index[v] = counter;
         low[v] = counter;
         ++counter;
         stack.push_back(v);
-        on_stack.insert(v);
+        on_stack[v] = 1;
         Frame f{v, {0, 0, 0, 0}, 0, 0};
-        if (g.EdgeOutdegree(v) > 0) f.n = std::max(0, g.OutgoingEdges(v, f.nb));
+        if (g.EdgeOutdegree(ids[v]) > 0) f.n = std::max(0, g.OutgoingEdges(ids[v], f.nb));
         frames.push_back(f);
     }
-    void run(uint64_t root) {
+    void run(uint32_t root) {
         std::vector<Frame> frames;
         open(frames, root);
         while (!frames.empty()) {
             Frame &f = frames.back();
             if (f.next < f.n) {
-                const uint64_t w = f.nb[f.next++];
-                if (!g.IsValidEdge(w)) continue;
-                if (!index.count(w)) {
+                const uint64_t we = f.nb[f.next++];
+                if (!g.IsValidEdge(we)) continue;
+                const uint32_t w = pos(we);  // a valid edge is in ids
+                if (index[w] < 0) {
                     open(frames, w);  // invalidates f
-                } else if (on_stack.count(w)) {
+                } else if (on_stack[w]) {
                     low[f.v] = std::min(low[f.v], index[w]);
                 }
                 continue;
             }
-            const uint64_t v = f.v;
+            const uint32_t v = f.v;
             if (low[v] == index[v]) {
                 std::vector<uint64_t> comp;
-                uint64_t w;
+                uint32_t w;
                 do {
                     w = stack.back();
                     stack.pop_back();
-                    on_stack.erase(w);
-                    comp.push_back(w);
+                    on_stack[w] = 0;
+                    comp.push_back(ids[w]);
                 } while (w != v);
                 if (comp.size() > 1) components.push_back(std::move(comp));
             }
             frames.pop_back();
             if (!frames.empty()) {  // back in the caller: low[parent] = min(low[parent], low[v])
-                const uint64_t p = frames.back().v;
+                const uint32_t p = frames.back().v;
                 low[p] = std::min(low[p], low[v]);
             }
         }
@@ -91,9 +97,10 @@ std::vector<uint32_t> merge_runs(const std::vector<uint32_t> &v) {  // A,A,B,C,C
 }  // namespace
 
 std::vector<std::vector<uint64_t>> find_strongly_connected_components(const SDBG &sdbg) {
-    Tarjan t(sdbg);
-    for (uint64_t v : sdbg.ValidIds())  // valid nodes in ascending id order
-        if (!t.index.count(v)) t.run(v);
+    const std::vector<uint64_t> ids = sdbg.ValidIds();
+    Tarjan t(sdbg, ids);
+    for (uint32_t v = 0; v < ids.size(); ++v)  // valid nodes in ascending id order
+        if (t.index[v] < 0) t.run(v);
     return std::move(t.components);
 }
 

@@ -210,10 +210,13 @@ void SDBG::SyncFromDevice() {
 void SDBG::KeepOnly(const std::vector<uint64_t> &ids) {
     ocache_.clear();
     if (have_valid_ || !g_) {
-        std::vector<uint8_t> keep(valid_.size(), 0);
+        // valid &= keep: the kept ids' bits survive, everything else clears (no second D-byte
+        // array)
+        std::vector<uint64_t> live;
         for (uint64_t e : ids)
-            if (e < keep.size()) keep[e] = 1;
-        for (size_t e = 0; e < valid_.size(); ++e) valid_[e] &= keep[e];
+            if (e < valid_.size() && valid_[e]) live.push_back(e);
+        std::fill(valid_.begin(), valid_.end(), 0);
+        for (uint64_t e : live) valid_[e] = 1;
     }
     if (g_) mcaat_check(mcaat_graph_keep_only(g_, ids.data(), ids.size()), "mcaat_graph_keep_only");
 }
