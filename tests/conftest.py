@@ -12,6 +12,9 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libmcaat_gpu.so on the device)")
 
 
+_SESSION_CTX = []
+
+
 @pytest.fixture(scope="session")
 def gpu_ctx():
     import mcaat_amd as M
@@ -19,5 +22,17 @@ def gpu_ctx():
     if M.device_count() < 1:
         pytest.fail("GPU test requested but no HIP device is visible")
     ctx = M.Context(0)
+    _SESSION_CTX.append(ctx)
     yield ctx
+    _SESSION_CTX.clear()
     ctx.close()
+
+
+@pytest.fixture(autouse=True)
+def _release_cached_device_memory():
+    """The session context's arena keeps freed device blocks for reuse; the full-size tests
+    leave up to ~260 GB of them. Released before every test, so tests that start other GPU
+    processes (ranks, the CLI) find the memory free."""
+    for ctx in _SESSION_CTX:
+        ctx.trim()
+    yield
