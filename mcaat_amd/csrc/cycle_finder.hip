@@ -48,23 +48,26 @@ constexpr int kScanU = 4;
 // its successors' unfiltered bits AND their multiplicities > 1 (consecutive ids, one line), so
 // kinds, unary successors and the predecessor flags come out here instead of from a second
 // streaming pass over out_info and the filtered bitmap.
-__global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t *tip_bm, uint64_t *post,
-                                                        unsigned long long *counts, uint8_t *nf, uint64_t *nxk) {
+// words [w_lo, w_hi) of the bitmaps (a rank's share; all of them on one GPU); tip_bm / post
+// are indexed from w_lo
+__global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_lo, uint64_t w_hi, uint64_t *tip_bm,
+                                                        uint64_t *post, unsigned long long *counts, uint8_t *nf,
+                                                        uint64_t *nxk) {
     const int lane = threadIdx.x & 63;
     const uint64_t nw = (g.D + 63) / 64;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const bool peel = nf != nullptr;
     unsigned long long acc = 0, low_n = 0;
-    for (uint64_t wb = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; wb < nw; wb += kScanU * wstride) {
+    for (uint64_t wb = w_lo + (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); wb < w_hi; wb += kScanU * wstride) {
         uint64_t sv[kScanU], oi[kScanU], a0[kScanU], a1[kScanU];
         uint32_t mu[kScanU];
         uint16_t sm[kScanU][4];
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
             const uint64_t w = wb + u * wstride, e = w * 64 + lane;
-            sv[u] = w < nw ? g.valid[w] : 0;
-            oi[u] = e < g.D ? g.out_info[e] : 0;
-            mu[u] = e < g.D ? g.mult[e] : 0xFFFFu;
+            sv[u] = w < w_hi ? g.valid[w] : 0;
+            oi[u] = e < g.D && w < w_hi ? g.out_info[e] : 0;
+            mu[u] = e < g.D && w < w_hi ? g.mult[e] : 0xFFFFu;
         }
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
@@ -86,13 +89,13 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t *t
             const bool t = ((sv[u] >> lane) & 1) && pre == 0;
             const unsigned long long m = __ballot(t);
             const unsigned long long lowm = __ballot(mu[u] <= 1);
-            if (lane == 0 && w < nw) {
-                tip_bm[w] = m;
-                post[w] = sv[u] & ~lowm;
+            if (lane == 0 && w < w_hi) {
+                tip_bm[w - w_lo] = m;
+                post[w - w_lo] = sv[u] & ~lowm;
                 acc += __popcll(m);
                 low_n += __popcll(lowm);
             }
-            if (peel && e < g.D) {
+            if (peel && e < g.D && w < w_hi) {
                 if (!((sv[u] >> lane) & 1) || mu[u] <= 1) {
                     nf[4 * e] = 0x3F;  // kInvalid
                 } else {
@@ -118,22 +121,24 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t *t
 // the recount after the reduction (valid edges, tips) and ChunkStartNodes' candidate filter in
 // one pass: counts[0] valid, counts[1] tips (whole graph), candidates only in [lo, hi) (a rank's
 // share), appended to list while they fit in cap (counts[2] counts them all)
+// the words covering ids [lo, hi) (a rank's share; all of them on one GPU): counts over those
+// words (summed over the ranks), candidates among ids [lo, hi)
 __global__ void __launch_bounds__(kBlock) k_recount_candidates(GraphView g, uint64_t thr, uint64_t lo, uint64_t hi,
-                                                               uint64_t *list, uint64_t cap,
-                                                               unsigned long long *counts) {
+                                                               uint64_t w_lo, uint64_t w_hi, uint64_t *list,
+                                                               uint64_t cap, unsigned long long *counts) {
     const int lane = threadIdx.x & 63;
     const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const uint64_t nw = (g.D + 63) / 64;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     unsigned long long nvalid = 0, ntips = 0;
-    for (uint64_t wb = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; wb < nw; wb += kScanU * wstride) {
+    for (uint64_t wb = w_lo + (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); wb < w_hi; wb += kScanU * wstride) {
         uint64_t sv[kScanU], oi[kScanU], ii[kScanU], a0[kScanU], a1[kScanU], b0[kScanU], b1[kScanU];
         uint32_t mu[kScanU];
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
             const uint64_t w = wb + u * wstride, e = w * 64 + lane;
-            const bool in = e < g.D;
-            sv[u] = w < nw ? g.valid[w] : 0;
+            const bool in = e < g.D && w < w_hi;
+            sv[u] = w < w_hi ? g.valid[w] : 0;
             oi[u] = in ? g.out_info[e] : 0;
             const bool cr = in && e >= lo && e < hi && ((sv[u] >> lane) & 1);
             ii[u] = cr ? g.in_info[e] : 0;
@@ -154,7 +159,7 @@ __global__ void __launch_bounds__(kBlock) k_recount_candidates(GraphView g, uint
             const uint32_t cnt = __popc((unsigned)(oi[u] >> kIdxBits) & 0xF);
             const bool t = v && (bits16(a0[u], a1[u], oi[u] & kIdxMask) & ((1u << cnt) - 1)) == 0;
             const unsigned long long tm = __ballot(t);
-            if (lane == 0 && w < nw) {
+            if (lane == 0 && w < w_hi) {
                 ntips += __popcll(tm);
                 nvalid += __popcll(sv[u]);
             }
@@ -1869,16 +1874,20 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
     // counter's atomics to a few thousand
     const unsigned wgrid = grid_for(nw * 64, kBlock, (unsigned)ctx->n_cu * 16);
 
-    // Steps 1-4 change the valid bits every later step reads, so every rank runs them on its
-    // replica of the graph (the peel is a global fixpoint); the scans of step 5 and the
-    // searches of steps 5-6 are split over the ranks.
+    // The scans are split over the ranks by 64-edge words ([R*nw/N, (R+1)*nw/N): rank R's ids
+    // are whole words): the tips / filter pass's two bitmaps are all-gathered (D/8 bytes each),
+    // the recount's counts summed and the candidates gathered. The peel is a global fixpoint
+    // over the whole graph and runs on every rank's replica (its first pass then runs as its
+    // own kernel: its arrays are 12 B per edge, too much to gather); the searches of steps 5-6
+    // are split over the ranks.
+    const uint64_t w_lo = nw * (uint64_t)R / (uint64_t)N, w_hi = nw * (uint64_t)(R + 1) / (uint64_t)N;
     // 1-2. CollectTips (before the multiplicity filter) -> seeds of the reduction, and
     // InvalidateMultiplicityOneNodes, in one pass (the filtered bits go to a second bitmap)
     DevBuf<uint64_t> seeds(nw);
     // the list-ranking peel (the default) gets its first pass from this one (cf.fused_init=0:
     // its own k_peel_init)
     PeelState ps;
-    const bool fuse = knob(ctx, "cf.walk_budget", 0) <= 0 && knob(ctx, "cf.fused_init", 1) != 0 && D;
+    const bool fuse = !comm && knob(ctx, "cf.walk_budget", 0) <= 0 && knob(ctx, "cf.fused_init", 1) != 0 && D;
     if (fuse) {
         ps.nf.alloc(4 * D);
         ps.nxk.alloc(D);
@@ -1889,12 +1898,29 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
         DevBuf<uint64_t> post(nw);
         DevBuf<unsigned long long> c2(2);
         HIP_OK(hipMemsetAsync(c2.p, 0, 16, st));
-        hipLaunchKernelGGL(k_tips_filter, dim3(wgrid), dim3(kBlock), 0, st, v, seeds.p, post.p, c2.p,
-                           fuse ? ps.nf.p : (uint8_t *)nullptr, fuse ? ps.nxk.p : (uint64_t *)nullptr);
-        LAUNCH_OK();
+        DevBuf<uint64_t> mseeds, mpost;  // this rank's words when the bitmaps are gathered
+        if (comm) {
+            mseeds.alloc(w_hi - w_lo);
+            mpost.alloc(w_hi - w_lo);
+        }
+        if (w_hi > w_lo) {
+            hipLaunchKernelGGL(k_tips_filter, dim3(wgrid), dim3(kBlock), 0, st, v, w_lo, w_hi, comm ? mseeds.p : seeds.p,
+                               comm ? mpost.p : post.p, c2.p, fuse ? ps.nf.p : (uint8_t *)nullptr,
+                               fuse ? ps.nxk.p : (uint64_t *)nullptr);
+            LAUNCH_OK();
+        }
         unsigned long long hc[2];
         HIP_OK(hipMemcpyAsync(hc, c2.p, 16, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
+        if (comm) {
+            std::vector<uint64_t> sz(N);
+            for (int r = 0; r < N; ++r) sz[r] = 8 * (nw * (uint64_t)(r + 1) / N - nw * (uint64_t)r / N);
+            comm->allgatherv_dev(mseeds.p, seeds.p, sz.data());
+            comm->allgatherv_dev(mpost.p, post.p, sz.data());
+            const auto all = comm->allgather_vec(std::vector<unsigned long long>{hc[0], hc[1]});
+            hc[0] = hc[1] = 0;
+            for (int r = 0; r < N; ++r) hc[0] += all[2 * r], hc[1] += all[2 * r + 1];
+        }
         out->stats[0] = hc[0];
         out->stats[1] = hc[1];
         std::swap(g->valid, post);  // the pre-filter bitmap is released here
@@ -1915,17 +1941,19 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
     // print is stats[1], every mult <= 1 edge, valid or not)
     std::vector<uint64_t> cand;
     {
-        // rank R takes the candidates among ids [R*D/N, (R+1)*D/N)
-        const uint64_t lo = (uint64_t)((unsigned __int128)D * R / N), hi = (uint64_t)((unsigned __int128)D * (R + 1) / N);
+        // rank R takes the candidates among its words' ids, and counts over its words
+        const uint64_t lo = std::min<uint64_t>(D, 64 * w_lo), hi = std::min<uint64_t>(D, 64 * w_hi);
         uint64_t cap = std::min<uint64_t>(hi - lo, (hi - lo) / 64 + (1u << 20));
         if (knob_set(ctx, "cf.cand_cap")) cap = (uint64_t)std::max<int64_t>(1, knob(ctx, "cf.cand_cap", 1));  // test knob
         DevBuf<unsigned long long> c3(3);
         for (;;) {
             DevBuf<uint64_t> list(cap ? cap : 1);
             HIP_OK(hipMemsetAsync(c3.p, 0, 24, st));
-            hipLaunchKernelGGL(k_recount_candidates, dim3(wgrid), dim3(kBlock), 0, st, v, (uint64_t)p.threshold_multiplicity,
-                               lo, hi, list.p, cap, c3.p);
-            LAUNCH_OK();
+            if (w_hi > w_lo) {
+                hipLaunchKernelGGL(k_recount_candidates, dim3(wgrid), dim3(kBlock), 0, st, v,
+                                   (uint64_t)p.threshold_multiplicity, lo, hi, w_lo, w_hi, list.p, cap, c3.p);
+                LAUNCH_OK();
+            }
             unsigned long long hc[3];
             HIP_OK(hipMemcpyAsync(hc, c3.p, 24, hipMemcpyDeviceToHost, st));
             HIP_OK(hipStreamSynchronize(st));
@@ -1948,6 +1976,11 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
             }
             break;
         }
+    }
+    if (comm) {  // the ranks' word counts summed
+        const auto all = comm->allgather_vec(std::vector<uint64_t>{out->stats[2], out->stats[3]});
+        out->stats[2] = out->stats[3] = 0;
+        for (int r = 0; r < N; ++r) out->stats[2] += all[2 * r], out->stats[3] += all[2 * r + 1];
     }
     timer.mark("recount");
     if (comm) cand = gather_sorted(comm, cand);
