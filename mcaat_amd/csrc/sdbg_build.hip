@@ -495,7 +495,21 @@ __global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in,
     __shared__ uint64_t sm[kL3Waves][kWaveSort];
     __shared__ uint64_t so[kL3Waves][kWaveSort];
     __shared__ uint32_t sc[kL3Waves][kWaveSort];
+    // buckets above the limit are listed 64 at a time per wave (one cursor atomic per 64: at
+    // C5 ~3M of the 4M buckets are listed, and one atomic each on a single counter took 50 ms)
+    __shared__ uint32_t pend[kL3Waves][64];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t npend = 0;
+    auto flush_pend = [&]() {
+        unsigned long long at = 0;
+        if (lane == 0) at = atomicAdd(nbig, (unsigned long long)npend);
+        at = __shfl(at, 0);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if ((uint32_t)lane < npend) big[at + lane] = pend[wave][lane];
+        npend = 0;
+    };
     uint64_t *s = sm[wave], *o = so[wave];
     uint32_t *cnt = sc[wave];
     const int E = k + 1;
@@ -529,7 +543,8 @@ __global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in,
         }
         if (n == 0) continue;
         if (nr64 > (uint64_t)limit || n > (uint64_t)NL * 64) {
-            if (lane == 0) big[atomicAdd(nbig, 1ull)] = (uint32_t)b;
+            if (lane == 0) pend[wave][npend] = (uint32_t)b;
+            if (++npend == 64) flush_pend();
             continue;
         }
         // load the bucket (all loads in flight together), compacted: line padding dropped, so
@@ -624,6 +639,7 @@ __global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in,
         }
         wave_sync();
     }
+    if (npend) flush_pend();
 }
 
 // k_msd3_wave's counting sort for the listed buckets above the one-wave limit (deep graphs:
