@@ -39,6 +39,49 @@ constexpr uint8_t kUnk = 0, kRem = 1, kSurv = 2;
 // self-loop test of the candidate filter are two bitmap words as well
 constexpr int kScanU = 4;
 
+// A wave's appends to a global id list, staged in LDS and published 64 at a time with one
+// cursor atomic (at C5 the candidates and the peel's branch nodes occur in most waves, and an
+// atomic per wave on one counter serialised tens of millions of them). `buf` is this wave's
+// 128-entry LDS slice; `n` is wave-uniform. Entries past `cap` are counted, not written (the
+// caller re-runs with the counted size).
+struct WaveList {
+    uint64_t *buf;
+    uint64_t *out;
+    unsigned long long *cursor;
+    uint64_t cap;
+    uint32_t n = 0;
+    __device__ __forceinline__ void wave_fence() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    __device__ __forceinline__ void publish(uint32_t count) {  // the first `count` (<= 64)
+        const int lane = threadIdx.x & 63;
+        wave_fence();
+        unsigned long long at = 0;
+        if (lane == 0) at = atomicAdd(cursor, (unsigned long long)count);
+        at = __shfl(at, 0);
+        const uint64_t v = buf[lane], keep = buf[64 + lane];
+        if ((uint32_t)lane < count && at + lane < cap) out[at + lane] = v;
+        wave_fence();
+        if (count == 64) buf[lane] = keep;  // the rest moves to the front
+        n -= count;
+        wave_fence();
+    }
+    __device__ __forceinline__ void push(bool f, uint64_t v) {
+        const unsigned long long m = __ballot(f);
+        if (!m) return;
+        const int lane = threadIdx.x & 63;
+        if (f) buf[n + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = v;
+        n += (uint32_t)__popcll(m);
+        if (n >= 64) publish(64);
+        (void)lane;
+    }
+    __device__ __forceinline__ void finish() {
+        if (n) publish(n);
+    }
+};
+
 // CollectTips and InvalidateMultiplicityOneNodes in one pass: tips from the valid bits as they
 // were before the filter (every successor window is read from `valid`, which this pass does not
 // write), the filtered bits into `post` (swapped in by the driver); counts[0] tips, counts[1]
@@ -127,10 +170,11 @@ __global__ void __launch_bounds__(kBlock) k_recount_candidates(GraphView g, uint
                                                                uint64_t w_lo, uint64_t w_hi, uint64_t *list,
                                                                uint64_t cap, unsigned long long *counts) {
     const int lane = threadIdx.x & 63;
-    const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const uint64_t nw = (g.D + 63) / 64;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     unsigned long long nvalid = 0, ntips = 0;
+    __shared__ uint64_t wbuf[kBlock / 64][128];
+    WaveList wl{wbuf[threadIdx.x >> 6], list, counts + 2, cap};
     for (uint64_t wb = w_lo + (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); wb < w_hi; wb += kScanU * wstride) {
         uint64_t sv[kScanU], oi[kScanU], ii[kScanU], a0[kScanU], a1[kScanU], b0[kScanU], b1[kScanU];
         uint32_t mu[kScanU];
@@ -168,15 +212,10 @@ __global__ void __launch_bounds__(kBlock) k_recount_candidates(GraphView g, uint
             // _IncomingNotEqualToCurrentNode: e must not be one of its own in-edges
             const bool self = e >= l && e - l < 16 && ((in >> (e - l)) & 1);
             const bool c = v && e >= lo && e < hi && (uint64_t)mu[u] > thr && __popc(in) >= 2 && !self;
-            const unsigned long long cm = __ballot(c);
-            if (cm) {
-                unsigned long long off = 0;
-                if (lane == 0) off = atomicAdd(counts + 2, (unsigned long long)__popcll(cm));
-                off = __shfl(off, 0);
-                if (c && off + __popcll(cm & lt) < cap) list[off + __popcll(cm & lt)] = e;
-            }
+            wl.push(c, e);
         }
     }
+    wl.finish();
     block_add(counts, nvalid);
     block_add(counts + 1, ntips);
 }
@@ -258,7 +297,9 @@ __global__ void __launch_bounds__(kBlock) k_peel_prep(uint64_t D, PeelArrays pa,
                                                       uint64_t bcap, unsigned long long *bcursor) {
     __shared__ uint32_t wcnt[kBlock / 64];
     __shared__ unsigned long long tbase;
+    __shared__ uint64_t bbuf[kBlock / 64][128];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    WaveList bl{bbuf[wave], blist, bcursor, bcap};
     const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const uint64_t tile = (uint64_t)kBlock * kTileJ;
     for (uint64_t t0 = (uint64_t)blockIdx.x * tile; t0 < D; t0 += (uint64_t)gridDim.x * tile) {
@@ -324,13 +365,7 @@ __global__ void __launch_bounds__(kBlock) k_peel_prep(uint64_t D, PeelArrays pa,
                 }
                 m[j] = __ballot(r);
                 c += __popcll(m[j]);
-                const unsigned long long mb = __ballot(br);
-                if (mb) {  // branch nodes are rare: one atomic per wave that has any
-                    unsigned long long off = 0;
-                    if (lane == 0) off = atomicAdd(bcursor, (unsigned long long)__popcll(mb));
-                    off = __shfl(off, 0);
-                    if (br && off + __popcll(mb & lt) < bcap) blist[off + __popcll(mb & lt)] = e;
-                }
+                bl.push(br, e);
             }
         }
         if (lane == 0) wcnt[wave] = c;
@@ -359,6 +394,7 @@ __global__ void __launch_bounds__(kBlock) k_peel_prep(uint64_t D, PeelArrays pa,
         }
         __syncthreads();
     }
+    bl.finish();
 }
 
 // each ruler walks its chain to the next ruler or non-unary node (Brent cycle check) and
