@@ -650,6 +650,9 @@ __global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in,
 // counts are scanned by the workgroup, items move to their bins and are written straight to
 // HBM at their final ranks. A bucket whose largest bin holds more than kMaxBin items
 // (clustered keys) is sorted by the bitonic network instead. Larger buckets are forwarded.
+// Round 3: a bucket's metadata and items are loaded into registers while the previous bucket
+// is sorted (all CAP / THREADS loads of a thread in flight together, LDS-only barriers so the
+// sort does not drain them); round 2 loaded each 256-item round after the last had landed.
 template <int THREADS, int CAP>
 __global__ void __launch_bounds__(THREADS) k_msd3_count(const uint64_t *in, const uint64_t *off2, const uint64_t *real2,
                                                         const uint64_t *base3, int k, const uint32_t *big, uint64_t nbig,
@@ -660,49 +663,76 @@ __global__ void __launch_bounds__(THREADS) k_msd3_count(const uint64_t *in, cons
     __shared__ uint64_t s[CAP];
     __shared__ uint64_t o[CAP];
     __shared__ uint32_t cnt[CAP];
-    __shared__ uint32_t wsum[NW];
-    __shared__ uint32_t fillc, mxs;
+    __shared__ uint32_t wsum[NW], wfill[NW], wmax[NW];
     const int E = k + 1;
     const int rb = 2 * E - 2 * kMB;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint64_t v[NR];
+    uint64_t f_b = 0, f_lo = 0, f_n = 0;
+    uint32_t f_real = 0;
+    bool f_ok = false;
+    auto fetch = [&](uint64_t q) {
+        f_ok = false;
+        f_n = 0;
+        if (q < nbig) {
+            f_b = big[q];
+            f_lo = off2[f_b];
+            f_n = off2[f_b + 1] - f_lo;
+            f_real = (uint32_t)real2[f_b];
+            f_ok = f_n <= (uint64_t)CAP && f_real <= limit;
+        }
+#pragma unroll
+        for (int t = 0; t < NR; ++t) {
+            const uint32_t i = t * THREADS + threadIdx.x;
+            v[t] = f_ok && i < f_n ? in[f_lo + i] : kPad;
+        }
+    };
+    fetch(blockIdx.x);
     for (uint64_t q = blockIdx.x; q < nbig; q += gridDim.x) {
-        const uint64_t b = big[q], lo = off2[b], n = off2[b + 1] - lo;
-        const uint32_t nreal = (uint32_t)real2[b];
-        if (n > (uint64_t)CAP || nreal > limit) {
+        const uint64_t b = f_b;
+        const uint32_t nreal = f_real;
+        if (!f_ok) {
             if (threadIdx.x == 0) fwd[atomicAdd(nfwd, 1ull)] = (uint32_t)b;
+            fetch(q + gridDim.x);
             continue;
         }
         const uint64_t base = base3[b], hi = (b >> kMB) << (2 * E - kMB);
-        if (threadIdx.x == 0) {
-            fillc = 0;
-            mxs = 0;
+        // compaction: each wave's item count, then its items at the wave's prefix
+        unsigned long long m[NR];
+        uint32_t wc = 0;
+#pragma unroll
+        for (int t = 0; t < NR; ++t) {
+            m[t] = __ballot(v[t] != kPad);
+            wc += (uint32_t)__popcll(m[t]);
         }
-        __syncthreads();
-        // compacted load: one LDS cursor atomic per wave and round
-        for (uint32_t i0 = 0; i0 < (uint32_t)n; i0 += THREADS) {
-            const uint32_t i = i0 + threadIdx.x;
-            const uint64_t x = i < n ? in[lo + i] : kPad;
-            const unsigned long long m = __ballot(x != kPad);
-            uint32_t w0 = 0;
-            if (lane == 0 && m) w0 = atomicAdd(&fillc, (uint32_t)__popcll(m));
-            w0 = __shfl(w0, 0);
-            if (x != kPad) s[w0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = x;
+        if (lane == 0) wfill[wave] = wc;
+        lds_barrier();  // B1: every thread is past the previous bucket; wfill complete
+        uint32_t at = 0;
+        for (int w = 0; w < wave; ++w) at += wfill[w];
+#pragma unroll
+        for (int t = 0; t < NR; ++t) {
+            if (v[t] != kPad)
+                s[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(m[t] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[t], 0))] = v[t];
+            at += (uint32_t)__popcll(m[t]);
         }
         uint32_t lgb = 0;
         while ((1u << lgb) < (uint32_t)THREADS) ++lgb;  // at least one bin per thread
         while ((1u << lgb) < nreal) ++lgb;
-        bool done = false;
-        if (lgb <= (uint32_t)rb) {
-            const uint32_t nbins = 1u << lgb, per = nbins / THREADS, sh = 16 + rb - lgb;
+        const bool counting = lgb <= (uint32_t)rb;
+        const uint32_t nbins = 1u << lgb, per = nbins / THREADS, sh = counting ? 16 + rb - lgb : 0;
+        if (counting)
             for (uint32_t i = threadIdx.x; i < nbins; i += THREADS) cnt[i] = 0;
-            __syncthreads();
+        fetch(q + gridDim.x);  // the next bucket's loads overlap this one's sort
+        lds_barrier();  // B2: items compacted, bins cleared
+        bool done = false;
+        if (counting) {
             uint32_t rk[NR];
 #pragma unroll
             for (int t = 0; t < NR; ++t) {
                 const uint32_t i = t * THREADS + threadIdx.x;
                 rk[t] = i < nreal ? atomicAdd(&cnt[(uint32_t)(s[i] >> sh) & (nbins - 1)], 1u) : 0;
             }
-            __syncthreads();
+            lds_barrier();  // B3: histogram complete
             uint32_t loc = 0, mx = 0;
             for (uint32_t j = 0; j < per; ++j) {
                 const uint32_t c = cnt[threadIdx.x * per + j];
@@ -719,9 +749,11 @@ __global__ void __launch_bounds__(THREADS) k_msd3_count(const uint64_t *in, cons
                 mx = u > mx ? u : mx;
             }
             if (lane == 63) wsum[wave] = incl;
-            if (lane == 0) atomicMax(&mxs, mx);
-            __syncthreads();
-            if (mxs <= kMaxBin) {
+            if (lane == 0) wmax[wave] = mx;
+            lds_barrier();  // B4: per-wave sums and maxima
+            uint32_t gmx = 0;
+            for (int w = 0; w < NW; ++w) gmx = wmax[w] > gmx ? wmax[w] : gmx;
+            if (gmx <= kMaxBin) {
                 uint32_t run = incl - loc;
                 for (int w = 0; w < wave; ++w) run += wsum[w];
                 for (uint32_t j = 0; j < per; ++j) {
@@ -729,7 +761,7 @@ __global__ void __launch_bounds__(THREADS) k_msd3_count(const uint64_t *in, cons
                     cnt[threadIdx.x * per + j] = run;
                     run += c;
                 }
-                __syncthreads();
+                lds_barrier();  // B5: bin starts
 #pragma unroll
                 for (int t = 0; t < NR; ++t) {
                     const uint32_t i = t * THREADS + threadIdx.x;
@@ -738,7 +770,7 @@ __global__ void __launch_bounds__(THREADS) k_msd3_count(const uint64_t *in, cons
                         o[cnt[(uint32_t)(x >> sh) & (nbins - 1)] + rk[t]] = x;
                     }
                 }
-                __syncthreads();
+                lds_barrier();  // B6: items in their bins
 #pragma unroll
                 for (int t = 0; t < NR; ++t) {
                     const uint32_t p = t * THREADS + threadIdx.x;
@@ -759,11 +791,11 @@ __global__ void __launch_bounds__(THREADS) k_msd3_count(const uint64_t *in, cons
             uint32_t P = 8;
             while (P < nreal) P <<= 1;
             for (uint32_t i = nreal + threadIdx.x; i < P; i += THREADS) s[i] = kPad;
-            __syncthreads();
+            lds_barrier();
             lds_bitonic(s, P, threadIdx.x, THREADS, false);
             msd_emit(s, nreal, threadIdx.x, THREADS, hi, key, mult, base);
         }
-        __syncthreads();
+        // no trailing barrier: the next bucket writes LDS only after its B1
     }
 }
 
