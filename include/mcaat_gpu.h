@@ -300,6 +300,7 @@ void mcaat_reset_timing(mcaat_ctx *ctx);
  *                      counting sort by the next key bits, bitonic for clustered buckets)
  *   sort.mid_counting  0: level-3 buckets above the one-wave limit by the 256-thread bitonic
  *                      network (default 1: the 256-thread LDS counting sort)
+ *   sort.mid_occ       5: that counting sort at five workgroups per CU (default 4)
  *   cf.dls_stack / cf.dls_visited   initial DepthLevelSearch scratch (grows x8 on overflow)
  *   cf.fc_lock / cf.fc_relax / cf.fc_out   initial FindCycle scratch (grows on overflow)
  *   cf.fc_window       initial FindCycle speculation window

@@ -53,22 +53,17 @@ __global__ void __launch_bounds__(kBlock) k_count_pal(const uint64_t *ckeys, uin
     block_add(n_pal, c);
 }
 
-// dir[p] = first index whose key prefix (top B of 2E bits) >= p, p in [0, 2^B]
+// dir[p] = first index whose key prefix (top B of 2E bits) >= p, p in [0, 2^B]: one streaming
+// pass over the sorted keys, edge e writing the prefixes (prefix(e-1), prefix(e)] (every prefix
+// is written by exactly one edge: the first at or above it, or e = D for those above the last
+// key). Round 2 ran one binary search over all D keys per prefix (C2: 2^28 searches, 9.9 ms).
 __global__ void __launch_bounds__(kBlock) k_dir(const uint64_t *key, uint64_t D, int shift, uint64_t nprefix,
                                                 uint64_t *dir) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p <= nprefix; p += stride) {
-        const uint64_t q = p << shift;
-        uint64_t lo = 0, hi = D;
-        if (p == nprefix) {
-            lo = D;
-        } else {
-            while (lo < hi) {
-                const uint64_t mid = (lo + hi) >> 1;
-                if (key[mid] < q) lo = mid + 1; else hi = mid;
-            }
-        }
-        dir[p] = lo;
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e <= D; e += stride) {
+        const uint64_t p = e < D ? key[e] >> shift : nprefix;
+        const uint64_t first = e ? (key[e - 1] >> shift) + 1 : 0;
+        for (uint64_t q = first; q <= p; ++q) dir[q] = e;
     }
 }
 
@@ -121,30 +116,51 @@ __global__ void __launch_bounds__(kBlock) k_adjacency(const uint64_t *key, uint6
 // range, bounded by the run's first and last source; the four ranges (~kAdjB/4 keys each)
 // and the run's own keys (with a group-sized halo on each side, for the in-group scans) are
 // loaded once, coalesced. A range larger than cap (skewed key spaces) falls back to the
-// directory search in global memory.
+// directory search in global memory. The ranges come from k_adj_bounds (one thread per
+// (run, W)), so a run's range and own-key loads go out together: round 2 searched the
+// directory inside the run's workgroup first, a chain of dependent loads per run (C2 30 ms).
 constexpr int kAdjB = 2048;
 constexpr int kAdjT = 1024;   // threads per run: two edges each
 constexpr int kAdjCap = 1024;
 constexpr int kAdjHalo = 16;  // an in-group holds at most 16 edges
-__global__ void __launch_bounds__(kAdjT) k_adjacency_lds(const uint64_t *key, uint64_t D, int k, const uint64_t *dir,
-                                                         int shift, uint32_t cap, uint64_t *out_info,
-                                                         uint64_t *in_info) {
-    __shared__ uint64_t rng[4][kAdjCap];
-    __shared__ uint64_t own[kAdjB + 2 * kAdjHalo];
-    __shared__ uint64_t rlo[4];
-    __shared__ uint32_t rn[4];
-    const uint64_t e0 = (uint64_t)blockIdx.x * kAdjB;
-    if (e0 >= D) return;
-    const uint64_t e1 = e0 + kAdjB < D ? e0 + kAdjB : D;
+__global__ void __launch_bounds__(kBlock) k_adj_bounds(const uint64_t *key, uint64_t D, int k, const uint64_t *dir,
+                                                       int shift, uint64_t nruns, uint64_t *bounds) {
     const uint64_t top = (uint64_t)1 << (2 * (k - 1));
-    if (threadIdx.x < 4) {
-        const uint64_t W = threadIdx.x;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < 4 * nruns; t += stride) {
+        const uint64_t r = t >> 2, W = t & 3;
+        const uint64_t e0 = r * kAdjB, e1 = e0 + kAdjB < D ? e0 + kAdjB : D;
         const uint64_t a = (W * top) | (key[e0] >> 4), b = (W * top) | (key[e1 - 1] >> 4);
         const uint64_t lo = lower_bound_dir(key, dir, shift, a << 2);
         const uint64_t qb = (b + 1) << 2;  // past the key space when b is the last label
         const uint64_t hi = qb >> (2 * (k + 1)) ? D : lower_bound_dir(key, dir, shift, qb);
-        rlo[W] = lo;
-        rn[W] = hi - lo <= (uint64_t)cap ? (uint32_t)(hi - lo) : 0xFFFFFFFFu;
+        bounds[8 * r + W] = lo;
+        bounds[8 * r + 4 + W] = hi;
+    }
+}
+
+__global__ void __launch_bounds__(kAdjT) k_adjacency_lds(const uint64_t *key, uint64_t D, int k, const uint64_t *dir,
+                                                         int shift, uint32_t cap, const uint64_t *bounds,
+                                                         uint64_t *out_info, uint64_t *in_info) {
+    __shared__ uint64_t rng[4][kAdjCap];
+    __shared__ uint64_t own[kAdjB + 2 * kAdjHalo];
+    __shared__ uint64_t srlo[4];
+    __shared__ uint32_t srn[4];
+    const uint64_t e0 = (uint64_t)blockIdx.x * kAdjB;
+    if (e0 >= D) return;
+    const uint64_t e1 = e0 + kAdjB < D ? e0 + kAdjB : D;
+    // the run's four ranges (uniform loads), also kept in LDS for the per-edge lookups
+    uint64_t rlo[4];
+    uint32_t rn[4];
+#pragma unroll
+    for (int W = 0; W < 4; ++W) {
+        rlo[W] = bounds[8 * blockIdx.x + W];
+        const uint64_t hi = bounds[8 * blockIdx.x + 4 + W];
+        rn[W] = hi - rlo[W] <= (uint64_t)cap ? (uint32_t)(hi - rlo[W]) : 0xFFFFFFFFu;
+    }
+    if (threadIdx.x < 4) {
+        srlo[threadIdx.x] = rlo[threadIdx.x];
+        srn[threadIdx.x] = rn[threadIdx.x];
     }
     // own[j] = key[e0 - kAdjHalo + j]; outside [0, D): a value no group matches
     const uint64_t olo = e0 >= (uint64_t)kAdjHalo ? e0 - kAdjHalo : 0;
@@ -153,7 +169,6 @@ __global__ void __launch_bounds__(kAdjT) k_adjacency_lds(const uint64_t *key, ui
         const uint64_t x = e0 + j - kAdjHalo;  // wraps below 0 for the first run
         own[j] = (j >= (uint32_t)kAdjHalo - opad && x < D) ? key[x] : ~0ULL;
     }
-    __syncthreads();
 #pragma unroll
     for (int W = 0; W < 4; ++W) {
         const uint32_t n = rn[W];
@@ -168,7 +183,7 @@ __global__ void __launch_bounds__(kAdjT) k_adjacency_lds(const uint64_t *key, ui
         const uint64_t Rt = (W << (2 * (k - 1))) | (R >> 2);
         uint64_t lo;
         unsigned m = 0;
-        const uint32_t n = rn[W];
+        const uint32_t n = srn[W];
         if (n != 0xFFFFFFFFu) {
             const uint64_t *r = rng[W];
             const uint64_t q = Rt << 2;
@@ -177,7 +192,7 @@ __global__ void __launch_bounds__(kAdjT) k_adjacency_lds(const uint64_t *key, ui
                 const uint32_t mid = (a + b) >> 1;
                 if (r[mid] < q) a = mid + 1; else b = mid;
             }
-            lo = rlo[W] + a;
+            lo = srlo[W] + a;
             // the range holds every key below (last target + 1) << 2: all of Rt's edges
             for (uint32_t i = a; i < n && (r[i] >> 2) == Rt; ++i) m |= 1u << (r[i] & 3);
         } else {
@@ -482,42 +497,41 @@ __device__ __forceinline__ void msd_emit(const uint64_t *s, uint32_t nreal, uint
 // one wave per level-2 bucket of <= kWaveSort items; larger ones are listed. A bucket is
 // counting-sorted by the next lg(P) key bits (P = its size rounded up to a power of two, so
 // about one item per bin): each item's rank inside its bin comes from the LDS histogram atomic,
-// a wave scan turns counts into bin starts, items go to their bins in LDS, and each then finds
-// its final rank among the few items of its own bin and is written straight to HBM (ranks
-// are nearly the LDS order, so the writes stay coalesced). A bucket whose largest bin holds
-// more than kMaxBin items (clustered keys) takes the bitonic network instead.
+// a wave scan turns counts into bin starts, items go from registers to their bins in LDS, and
+// each then finds its final rank among the few items of its own bin and is written straight to
+// HBM (ranks are nearly the LDS order, so the writes stay coalesced). A bucket whose largest
+// bin holds more than kMaxBin items (clustered keys) takes the bitonic network instead.
+// The items stay in the registers they were loaded into until they are placed (padding is
+// skipped, never compacted), so a wave holds 6 KB of LDS and five workgroups share a CU (the
+// register limit at 96).
 constexpr int kL3Waves = 4;
 constexpr uint32_t kMaxBin = 16;
-__global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in, const uint64_t *off2,
+__global__ void __launch_bounds__(kL3Waves * 64) __attribute__((amdgpu_waves_per_eu(5))) k_msd3_wave(const uint64_t *in, const uint64_t *off2,
                                                              const uint64_t *real2, const uint64_t *base3, int k,
                                                              uint64_t *key, uint16_t *mult, uint32_t *big,
                                                              unsigned long long *nbig, uint32_t limit, int counting) {
-    __shared__ uint64_t sm[kL3Waves][kWaveSort];
     __shared__ uint64_t so[kL3Waves][kWaveSort];
     __shared__ uint32_t sc[kL3Waves][kWaveSort];
     // buckets above the limit are listed 64 at a time per wave (one cursor atomic per 64: at
-    // C5 ~3M of the 4M buckets are listed, and one atomic each on a single counter took 50 ms)
-    __shared__ uint32_t pend[kL3Waves][64];
+    // C5 ~3M of the 4M buckets are listed, and one atomic each on a single counter took 50 ms);
+    // lane j holds the j-th pending bucket in a register
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    uint32_t npend = 0;
+    uint32_t npend = 0, mypend = 0;
     auto flush_pend = [&]() {
         unsigned long long at = 0;
         if (lane == 0) at = atomicAdd(nbig, (unsigned long long)npend);
         at = __shfl(at, 0);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if ((uint32_t)lane < npend) big[at + lane] = pend[wave][lane];
+        if ((uint32_t)lane < npend) big[at + lane] = mypend;
         npend = 0;
     };
-    uint64_t *s = sm[wave], *o = so[wave];
+    uint64_t *o = so[wave];
     uint32_t *cnt = sc[wave];
     const int E = k + 1;
     const int rb = 2 * E - 2 * kMB;  // key bits below the two MSD levels (item bits 16 .. 16 + rb)
     const uint64_t nb = (uint64_t)kMS * kMS;
     const uint64_t bstride = (uint64_t)gridDim.x * kL3Waves;
     constexpr int NL = 10;  // loads per lane: buckets of up to 640 padded items
-    constexpr int NR = kWaveSort / 64;  // items per lane once compacted
+    constexpr int NR = kWaveSort / 64;  // sorted items per lane
     auto wave_sync = [] {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -543,26 +557,17 @@ __global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in,
         }
         if (n == 0) continue;
         if (nr64 > (uint64_t)limit || n > (uint64_t)NL * 64) {
-            if (lane == 0) pend[wave][npend] = (uint32_t)b;
+            if ((uint32_t)lane == npend) mypend = (uint32_t)b;
             if (++npend == 64) flush_pend();
             continue;
         }
-        // load the bucket (all loads in flight together), compacted: line padding dropped, so
-        // the sort is sized by the real items
+        // load the bucket (all loads in flight together); line padding is kPad
         const uint32_t nreal = (uint32_t)nr64;
         uint64_t v[NL];
 #pragma unroll
         for (int t = 0; t < NL; ++t) {
             const uint32_t i = t * 64 + lane;
             v[t] = i < n ? in[lo + i] : kPad;
-        }
-        uint32_t fill = 0;
-#pragma unroll
-        for (int t = 0; t < NL; ++t) {
-            const unsigned long long m = __ballot(v[t] != kPad);
-            if (v[t] != kPad)
-                s[fill + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = v[t];
-            fill += (uint32_t)__popcll(m);
         }
         const uint64_t hi = (b >> kMB) << (2 * E - kMB);
         // bins: P >= nreal, at least 64 (one per lane), at most 2^rb
@@ -573,12 +578,10 @@ __global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in,
             const uint32_t nbins = 1u << lgb, per = nbins / 64, sh = 16 + rb - lgb;
             for (uint32_t i = lane; i < nbins; i += 64) cnt[i] = 0;
             wave_sync();
-            uint32_t rk[NR];
+            uint32_t rk[NL];
 #pragma unroll
-            for (int t = 0; t < NR; ++t) {
-                const uint32_t i = t * 64 + lane;
-                rk[t] = i < nreal ? atomicAdd(&cnt[(uint32_t)(s[i] >> sh) & (nbins - 1)], 1u) : 0;
-            }
+            for (int t = 0; t < NL; ++t)
+                rk[t] = v[t] != kPad ? atomicAdd(&cnt[(uint32_t)(v[t] >> sh) & (nbins - 1)], 1u) : 0;
             wave_sync();
             // bin counts -> bin starts (each lane owns `per` consecutive bins)
             uint32_t loc = 0, mx = 0;
@@ -605,13 +608,8 @@ __global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in,
                 }
                 wave_sync();
 #pragma unroll
-                for (int t = 0; t < NR; ++t) {
-                    const uint32_t i = t * 64 + lane;
-                    if (i < nreal) {
-                        const uint64_t x = s[i];
-                        o[cnt[(uint32_t)(x >> sh) & (nbins - 1)] + rk[t]] = x;
-                    }
-                }
+                for (int t = 0; t < NL; ++t)
+                    if (v[t] != kPad) o[cnt[(uint32_t)(v[t] >> sh) & (nbins - 1)] + rk[t]] = v[t];
                 wave_sync();
 #pragma unroll
                 for (int t = 0; t < NR; ++t) {
@@ -629,13 +627,21 @@ __global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in,
                 sorted = true;
             }
         }
-        if (!sorted) {
+        if (!sorted) {  // the items compacted into LDS, padded to a power of two, bitonic network
+            uint32_t fill = 0;
+#pragma unroll
+            for (int t = 0; t < NL; ++t) {
+                const unsigned long long m = __ballot(v[t] != kPad);
+                if (v[t] != kPad)
+                    o[fill + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0))] = v[t];
+                fill += (uint32_t)__popcll(m);
+            }
             uint32_t P = 8;
             while (P < nreal) P <<= 1;
-            for (uint32_t i = nreal + lane; i < P; i += 64) s[i] = kPad;
+            for (uint32_t i = nreal + lane; i < P; i += 64) o[i] = kPad;
             wave_sync();
-            lds_bitonic(s, P, lane, 64, true);
-            msd_emit(s, nreal, lane, 64, hi, key, mult, base);
+            lds_bitonic(o, P, lane, 64, true);
+            msd_emit(o, nreal, lane, 64, hi, key, mult, base);
         }
         wave_sync();
     }
@@ -644,23 +650,23 @@ __global__ void __launch_bounds__(kL3Waves * 64) k_msd3_wave(const uint64_t *in,
 
 // k_msd3_wave's counting sort for the listed buckets above the one-wave limit (deep graphs:
 // D / 2^22 above 512 items, C2 ~570, C5 ~935): one THREADS-thread workgroup per bucket of
-// <= CAP items. Items are compacted into LDS (padding dropped; their order does not matter, as
-// each item's final rank is its bin start plus the number of smaller items in its bin), binned
-// by the next lg(P) key bits (LDS histogram atomics give each item a slot in its bin), the bin
-// counts are scanned by the workgroup, items move to their bins and are written straight to
-// HBM at their final ranks. A bucket whose largest bin holds more than kMaxBin items
+// <= CAP items. Items are binned by the next lg(P) key bits (LDS histogram atomics give each
+// item a slot in its bin; their order does not matter, as each item's final rank is its bin
+// start plus the number of smaller items in its bin), the bin counts are scanned by the
+// workgroup, items move to their bins and are written straight to HBM at their final ranks. A bucket whose largest bin holds more than kMaxBin items
 // (clustered keys) is sorted by the bitonic network instead. Larger buckets are forwarded.
 // Round 3: a bucket's metadata and items are loaded into registers while the previous bucket
 // is sorted (all CAP / THREADS loads of a thread in flight together, LDS-only barriers so the
-// sort does not drain them); round 2 loaded each 256-item round after the last had landed.
-template <int THREADS, int CAP>
-__global__ void __launch_bounds__(THREADS) k_msd3_count(const uint64_t *in, const uint64_t *off2, const uint64_t *real2,
+// sort does not drain them; round 2 loaded each 256-item round after the last had landed), and
+// the items go from those registers straight to their bins (padding skipped, no compaction
+// buffer): 24 KB of LDS, four workgroups per CU (the registers).
+template <int THREADS, int CAP, int OCC>
+__global__ void __launch_bounds__(THREADS) __attribute__((amdgpu_waves_per_eu(OCC))) k_msd3_count(const uint64_t *in, const uint64_t *off2, const uint64_t *real2,
                                                         const uint64_t *base3, int k, const uint32_t *big, uint64_t nbig,
                                                         uint64_t *key, uint16_t *mult, uint32_t *fwd,
                                                         unsigned long long *nfwd, uint32_t limit) {
     static_assert(CAP % THREADS == 0 && CAP >= THREADS && THREADS % 64 == 0, "bins per thread");
     constexpr int NW = THREADS / 64, NR = CAP / THREADS;
-    __shared__ uint64_t s[CAP];
     __shared__ uint64_t o[CAP];
     __shared__ uint32_t cnt[CAP];
     __shared__ uint32_t wsum[NW], wfill[NW], wmax[NW];
@@ -697,41 +703,25 @@ __global__ void __launch_bounds__(THREADS) k_msd3_count(const uint64_t *in, cons
             continue;
         }
         const uint64_t base = base3[b], hi = (b >> kMB) << (2 * E - kMB);
-        // compaction: each wave's item count, then its items at the wave's prefix
-        unsigned long long m[NR];
-        uint32_t wc = 0;
+        uint64_t x[NR];
 #pragma unroll
-        for (int t = 0; t < NR; ++t) {
-            m[t] = __ballot(v[t] != kPad);
-            wc += (uint32_t)__popcll(m[t]);
-        }
-        if (lane == 0) wfill[wave] = wc;
-        lds_barrier();  // B1: every thread is past the previous bucket; wfill complete
-        uint32_t at = 0;
-        for (int w = 0; w < wave; ++w) at += wfill[w];
-#pragma unroll
-        for (int t = 0; t < NR; ++t) {
-            if (v[t] != kPad)
-                s[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(m[t] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[t], 0))] = v[t];
-            at += (uint32_t)__popcll(m[t]);
-        }
+        for (int t = 0; t < NR; ++t) x[t] = v[t];
         uint32_t lgb = 0;
         while ((1u << lgb) < (uint32_t)THREADS) ++lgb;  // at least one bin per thread
         while ((1u << lgb) < nreal) ++lgb;
         const bool counting = lgb <= (uint32_t)rb;
         const uint32_t nbins = 1u << lgb, per = nbins / THREADS, sh = counting ? 16 + rb - lgb : 0;
+        lds_barrier();  // B1: every thread is past the previous bucket (o and cnt free)
         if (counting)
             for (uint32_t i = threadIdx.x; i < nbins; i += THREADS) cnt[i] = 0;
         fetch(q + gridDim.x);  // the next bucket's loads overlap this one's sort
-        lds_barrier();  // B2: items compacted, bins cleared
+        lds_barrier();  // B2: bins cleared
         bool done = false;
         if (counting) {
             uint32_t rk[NR];
 #pragma unroll
-            for (int t = 0; t < NR; ++t) {
-                const uint32_t i = t * THREADS + threadIdx.x;
-                rk[t] = i < nreal ? atomicAdd(&cnt[(uint32_t)(s[i] >> sh) & (nbins - 1)], 1u) : 0;
-            }
+            for (int t = 0; t < NR; ++t)
+                rk[t] = x[t] != kPad ? atomicAdd(&cnt[(uint32_t)(x[t] >> sh) & (nbins - 1)], 1u) : 0;
             lds_barrier();  // B3: histogram complete
             uint32_t loc = 0, mx = 0;
             for (uint32_t j = 0; j < per; ++j) {
@@ -763,37 +753,49 @@ __global__ void __launch_bounds__(THREADS) k_msd3_count(const uint64_t *in, cons
                 }
                 lds_barrier();  // B5: bin starts
 #pragma unroll
-                for (int t = 0; t < NR; ++t) {
-                    const uint32_t i = t * THREADS + threadIdx.x;
-                    if (i < nreal) {
-                        const uint64_t x = s[i];
-                        o[cnt[(uint32_t)(x >> sh) & (nbins - 1)] + rk[t]] = x;
-                    }
-                }
+                for (int t = 0; t < NR; ++t)
+                    if (x[t] != kPad) o[cnt[(uint32_t)(x[t] >> sh) & (nbins - 1)] + rk[t]] = x[t];
                 lds_barrier();  // B6: items in their bins
 #pragma unroll
                 for (int t = 0; t < NR; ++t) {
                     const uint32_t p = t * THREADS + threadIdx.x;
                     if (p < nreal) {
-                        const uint64_t x = o[p];
-                        const uint32_t bi = (uint32_t)(x >> sh) & (nbins - 1);
+                        const uint64_t y = o[p];
+                        const uint32_t bi = (uint32_t)(y >> sh) & (nbins - 1);
                         const uint32_t bs = cnt[bi], be = bi + 1 < nbins ? cnt[bi + 1] : nreal;
                         uint32_t r = bs;
-                        for (uint32_t z = bs; z < be; ++z) r += o[z] < x;
-                        key[base + r] = hi | (x >> 16);
-                        mult[base + r] = (uint16_t)(x & 0xFFFF);
+                        for (uint32_t z = bs; z < be; ++z) r += o[z] < y;
+                        key[base + r] = hi | (y >> 16);
+                        mult[base + r] = (uint16_t)(y & 0xFFFF);
                     }
                 }
                 done = true;
             }
         }
-        if (!done) {  // clustered keys: the bitonic network over the compacted items
+        if (!done) {  // clustered keys: the items compacted into LDS, then the bitonic network
+            unsigned long long m[NR];
+            uint32_t wc = 0;
+#pragma unroll
+            for (int t = 0; t < NR; ++t) {
+                m[t] = __ballot(x[t] != kPad);
+                wc += (uint32_t)__popcll(m[t]);
+            }
+            if (lane == 0) wfill[wave] = wc;
+            lds_barrier();
+            uint32_t at = 0;
+            for (int w = 0; w < wave; ++w) at += wfill[w];
+#pragma unroll
+            for (int t = 0; t < NR; ++t) {
+                if (x[t] != kPad)
+                    o[at + __builtin_amdgcn_mbcnt_hi((uint32_t)(m[t] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m[t], 0))] = x[t];
+                at += (uint32_t)__popcll(m[t]);
+            }
             uint32_t P = 8;
             while (P < nreal) P <<= 1;
-            for (uint32_t i = nreal + threadIdx.x; i < P; i += THREADS) s[i] = kPad;
+            for (uint32_t i = nreal + threadIdx.x; i < P; i += THREADS) o[i] = kPad;
             lds_barrier();
-            lds_bitonic(s, P, threadIdx.x, THREADS, false);
-            msd_emit(s, nreal, threadIdx.x, THREADS, hi, key, mult, base);
+            lds_bitonic(o, P, threadIdx.x, THREADS, false);
+            msd_emit(o, nreal, threadIdx.x, THREADS, hi, key, mult, base);
         }
         // no trailing barrier: the next bucket writes LDS only after its B1
     }
@@ -898,8 +900,8 @@ bool msd_sort(mcaat_ctx *ctx, const uint64_t *ckeys, const uint32_t *ccnt, uint6
     DevBuf<int> too(1);
     HIP_OK(hipMemsetAsync(nbig.p, 0, 8, st));
     HIP_OK(hipMemsetAsync(too.p, 0, 4, st));
-    // 40 KB of LDS per workgroup: four resident per CU
-    hipLaunchKernelGGL(k_msd3_wave, dim3((unsigned)ctx->n_cu * 4), dim3(kL3Waves * 64), 0, st, l2.p, off2.p,
+    // 24 KB of LDS per workgroup, 96 registers: five resident per CU
+    hipLaunchKernelGGL(k_msd3_wave, dim3((unsigned)ctx->n_cu * 5), dim3(kL3Waves * 64), 0, st, l2.p, off2.p,
                        (const uint64_t *)real2.p, (const uint64_t *)base3.p, k, key, mult, big.p, nbig.p,
                        (uint32_t)std::min<int64_t>(kWaveSort, knob(ctx, "sort.wave_limit", kWaveSort)),
                        (int)knob(ctx, "sort.l3_counting", 1));
@@ -915,10 +917,15 @@ bool msd_sort(mcaat_ctx *ctx, const uint64_t *ckeys, const uint32_t *ccnt, uint6
         HIP_OK(hipMemsetAsync(nbig2.p, 0, 8, st));
         const uint32_t mid_limit = (uint32_t)std::min<int64_t>(kMidSort, knob(ctx, "sort.mid_limit", kMidSort));
         if (knob(ctx, "sort.mid_counting", 1)) {
-            // 40 KB of LDS per workgroup: four per CU
-            hipLaunchKernelGGL((k_msd3_count<256, kMidSort>), dim3((unsigned)std::min<uint64_t>(hb, (uint64_t)ctx->n_cu * 4)),
-                               dim3(256), 0, st, l2.p, off2.p, (const uint64_t *)real2.p, (const uint64_t *)base3.p, k,
-                               big.p, (uint64_t)hb, key, mult, big2.p, nbig2.p, mid_limit);
+            // 24 KB of LDS per workgroup; the registers (125) allow four per CU (`sort.mid_occ=5`: five, at 96 registers with spills; C2 2 ms slower)
+            if (knob(ctx, "sort.mid_occ", 4) >= 5)
+                hipLaunchKernelGGL((k_msd3_count<256, kMidSort, 5>), dim3((unsigned)std::min<uint64_t>(hb, (uint64_t)ctx->n_cu * 5)),
+                                   dim3(256), 0, st, l2.p, off2.p, (const uint64_t *)real2.p, (const uint64_t *)base3.p, k,
+                                   big.p, (uint64_t)hb, key, mult, big2.p, nbig2.p, mid_limit);
+            else
+                hipLaunchKernelGGL((k_msd3_count<256, kMidSort, 4>), dim3((unsigned)std::min<uint64_t>(hb, (uint64_t)ctx->n_cu * 4)),
+                                   dim3(256), 0, st, l2.p, off2.p, (const uint64_t *)real2.p, (const uint64_t *)base3.p, k,
+                                   big.p, (uint64_t)hb, key, mult, big2.p, nbig2.p, mid_limit);
         } else {
             hipLaunchKernelGGL((k_msd3_block<256, kMidSort>), dim3((unsigned)std::min<uint64_t>(hb, (uint64_t)ctx->n_cu * 8)),
                                dim3(256), 0, st, l2.p, off2.p, (const uint64_t *)real2.p, (const uint64_t *)base3.p, k,
@@ -1018,8 +1025,8 @@ void sdbg_finish(mcaat_ctx *ctx, mcaat_graph *g) {
     DevBuf<uint64_t> &dir = g->dir;
     dir.alloc(nprefix + 1);
     g->dir_shift = shift;
-    hipLaunchKernelGGL(k_dir, dim3(grid_for(nprefix + 1, kBlock)), dim3(kBlock), 0, st, g->key.p, D, shift, nprefix,
-                       dir.p);
+    hipLaunchKernelGGL(k_dir, dim3(grid_for(D + 1, kBlock, (unsigned)ctx->n_cu * 16)), dim3(kBlock), 0, st, g->key.p, D,
+                       shift, nprefix, dir.p);
     LAUNCH_OK();
     g->out_info.alloc(D);
     g->in_info.alloc(D);
@@ -1031,8 +1038,13 @@ void sdbg_finish(mcaat_ctx *ctx, mcaat_graph *g) {
         HIP_OK(hipMemsetAsync(g->in_info.p, 0, 8 * D, st));
         if (knob(ctx, "sdbg.adj_lds", 1)) {
             const uint32_t cap = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(kAdjCap, knob(ctx, "sdbg.adj_cap", kAdjCap)));
-            hipLaunchKernelGGL(k_adjacency_lds, dim3((unsigned)((D + kAdjB - 1) / kAdjB)), dim3(kAdjT), 0, st, g->key.p,
-                               D, k, dir.p, shift, cap, g->out_info.p, g->in_info.p);
+            const uint64_t nruns = (D + kAdjB - 1) / kAdjB;
+            DevBuf<uint64_t> bounds(8 * nruns);
+            hipLaunchKernelGGL(k_adj_bounds, dim3(grid_for(4 * nruns, kBlock, (unsigned)ctx->n_cu * 16)), dim3(kBlock), 0,
+                               st, g->key.p, D, k, dir.p, shift, nruns, bounds.p);
+            LAUNCH_OK();
+            hipLaunchKernelGGL(k_adjacency_lds, dim3((unsigned)nruns), dim3(kAdjT), 0, st, g->key.p, D, k, dir.p, shift,
+                               cap, (const uint64_t *)bounds.p, g->out_info.p, g->in_info.p);
         } else {
             hipLaunchKernelGGL(k_adjacency, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, g->key.p, D, k, dir.p,
                                shift, g->out_info.p, g->in_info.p);

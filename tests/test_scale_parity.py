@@ -51,6 +51,7 @@ KNOBS = {
     # level-3 buckets through the 256-thread LDS sort, the 1024-thread one, and the radix fallback
     "sort_mid": {"sort.msd": 1, "sort.wave_limit": 0},
     "sort_mid_bitonic": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_counting": 0},
+    "sort_mid_occ5": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_occ": 5},
     "sort_block": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_limit": 0},
     "sort_radix": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_limit": 0, "sort.block_limit": 0},
     "sort_radix_only": {"sort.msd": 0},
