@@ -56,14 +56,32 @@ __global__ void __launch_bounds__(kBlock) k_count_pal(const uint64_t *ckeys, uin
 // dir[p] = first index whose key prefix (top B of 2E bits) >= p, p in [0, 2^B]: one streaming
 // pass over the sorted keys, edge e writing the prefixes (prefix(e-1), prefix(e)] (every prefix
 // is written by exactly one edge: the first at or above it, or e = D for those above the last
-// key). Round 2 ran one binary search over all D keys per prefix (C2: 2^28 searches, 9.9 ms).
+// key). A wave takes 256 consecutive edges (four coalesced loads in flight); each edge's
+// predecessor prefix comes from the neighbouring lane. Round 2 ran one binary search over all
+// D keys per prefix (C2: 2^28 searches, 9.9 ms).
+constexpr int kDirU = 4;
 __global__ void __launch_bounds__(kBlock) k_dir(const uint64_t *key, uint64_t D, int shift, uint64_t nprefix,
                                                 uint64_t *dir) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e <= D; e += stride) {
-        const uint64_t p = e < D ? key[e] >> shift : nprefix;
-        const uint64_t first = e ? (key[e - 1] >> shift) + 1 : 0;
-        for (uint64_t q = first; q <= p; ++q) dir[q] = e;
+    const int lane = threadIdx.x & 63;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c * 64 * kDirU <= D; c += nwaves) {
+        const uint64_t base = c * 64 * kDirU;
+        uint64_t p[kDirU];
+#pragma unroll
+        for (int j = 0; j < kDirU; ++j) {
+            const uint64_t e = base + 64 * j + lane;
+            p[j] = e < D ? key[e] >> shift : nprefix;
+        }
+        const uint64_t before = base ? (key[base - 1] >> shift) + 1 : 0;  // first prefix of this chunk
+#pragma unroll
+        for (int j = 0; j < kDirU; ++j) {
+            const uint64_t e = base + 64 * j + lane;
+            const uint64_t up = __shfl_up(p[j], 1);
+            const uint64_t last = j ? __shfl(p[j - 1], 63) + 1 : before;
+            const uint64_t first = lane ? up + 1 : last;
+            if (e <= D)
+                for (uint64_t q = first; q <= p[j]; ++q) dir[q] = e;
+        }
     }
 }
 
@@ -1025,8 +1043,8 @@ void sdbg_finish(mcaat_ctx *ctx, mcaat_graph *g) {
     DevBuf<uint64_t> &dir = g->dir;
     dir.alloc(nprefix + 1);
     g->dir_shift = shift;
-    hipLaunchKernelGGL(k_dir, dim3(grid_for(D + 1, kBlock, (unsigned)ctx->n_cu * 16)), dim3(kBlock), 0, st, g->key.p, D,
-                       shift, nprefix, dir.p);
+    hipLaunchKernelGGL(k_dir, dim3(grid_for((D + kDirU) / kDirU, kBlock, (unsigned)ctx->n_cu * 16)), dim3(kBlock), 0, st,
+                       g->key.p, D, shift, nprefix, dir.p);
     LAUNCH_OK();
     g->out_info.alloc(D);
     g->in_info.alloc(D);
