@@ -37,7 +37,9 @@ constexpr uint8_t kUnk = 0, kRem = 1, kSurv = 2;
 // is a popcount of at most two bitmap words (no per-successor loads); the in-edges of e are the
 // positions of a 16-bit mask inside the group starting at in_lo, so the valid in-degree and the
 // self-loop test of the candidate filter are two bitmap words as well
-constexpr int kScanU = 4;
+// (knob cf.scan_u). More words per wave means fewer waves: C3 recount with 1 / 2 / 4 / 8 words
+// 5.5 / 5.7 / 8.3 / 18.0 ms (79 VGPRs at 2, 141 at 4, 256 at 8), the occupancy matters more
+constexpr int kScanUDefault = 2;
 
 // A wave's appends to a global id list, staged in LDS and published 64 at a time with one
 // cursor atomic (at C5 the candidates and the peel's branch nodes occur in most waves, and an
@@ -93,6 +95,7 @@ struct WaveList {
 // streaming pass over out_info and the filtered bitmap.
 // words [w_lo, w_hi) of the bitmaps (a rank's share; all of them on one GPU); tip_bm / post
 // are indexed from w_lo
+template <int kScanU>
 __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_lo, uint64_t w_hi, uint64_t *tip_bm,
                                                         uint64_t *post, unsigned long long *counts, uint8_t *nf,
                                                         uint64_t *nxk) {
@@ -166,6 +169,7 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_
 // share), appended to list while they fit in cap (counts[2] counts them all)
 // the words covering ids [lo, hi) (a rank's share; all of them on one GPU): counts over those
 // words (summed over the ranks), candidates among ids [lo, hi)
+template <int kScanU>
 __global__ void __launch_bounds__(kBlock) k_recount_candidates(GraphView g, uint64_t thr, uint64_t lo, uint64_t hi,
                                                                uint64_t w_lo, uint64_t w_hi, uint64_t *list,
                                                                uint64_t cap, unsigned long long *counts) {
@@ -292,6 +296,7 @@ __global__ void __launch_bounds__(kBlock) k_peel_init(GraphView g, PeelArrays pa
 constexpr int kTileJ = 16;  // 64-edge words per wave per tile
 // (list / blist hold cap / bcap entries; the cursors count past them, and the driver then
 // runs the pass again with larger lists: it is idempotent)
+template <int kPB>
 __global__ void __launch_bounds__(kBlock) k_peel_prep(uint64_t D, PeelArrays pa, uint64_t ruler_mask, uint64_t *list,
                                                       uint64_t cap, unsigned long long *cursor, uint64_t *blist,
                                                       uint64_t bcap, unsigned long long *bcursor) {
@@ -307,7 +312,6 @@ __global__ void __launch_bounds__(kBlock) k_peel_prep(uint64_t D, PeelArrays pa,
         uint32_t c = 0;
         // kPB edges per thread at a time: their own bytes and successors are loaded first (all
         // in flight together), then their successors' flags, then everything is written
-        constexpr int kPB = 8;
         static_assert(kTileJ % kPB == 0, "whole batches per tile");
 #pragma unroll
         for (int h = 0; h < kTileJ; h += kPB) {
@@ -1350,8 +1354,10 @@ static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm, PeelState *
         list.alloc(cap);
         blist.alloc(bcap);
         HIP_OK(hipMemsetAsync(cur.p, 0, cur.bytes(), st));
-        hipLaunchKernelGGL(k_peel_prep, dim3(grid_for(D, kBlock * kTileJ)), dim3(kBlock), 0, st, D, pa, ruler_mask,
-                           list.p, cap, cur.p, blist.p, bcap, cur.p + 1);
+        const int64_t pb = knob(ctx, "cf.prep_batch", 2);  // edges per thread in flight: C3 2 / 4 / 8 / 16 -> peel 22.8 / 23.3 / 24.3 / 26.0 ms
+        auto prep = pb == 4 ? k_peel_prep<4> : pb == 8 ? k_peel_prep<8> : pb == 16 ? k_peel_prep<16> : k_peel_prep<2>;
+        hipLaunchKernelGGL(prep, dim3(grid_for(D, kBlock * kTileJ)), dim3(kBlock), 0, st, D, pa, ruler_mask, list.p,
+                           cap, cur.p, blist.p, bcap, cur.p + 1);
         LAUNCH_OK();
         unsigned long long hc[2];
         HIP_OK(hipMemcpyAsync(hc, cur.p, 16, hipMemcpyDeviceToHost, st));
@@ -1909,6 +1915,7 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
     // grid-stride scans whose per-block totals meet in one counter: a capped grid keeps that
     // counter's atomics to a few thousand
     const unsigned wgrid = grid_for(nw * 64, kBlock, (unsigned)ctx->n_cu * 16);
+    const int64_t scan_u = knob(ctx, "cf.scan_u", kScanUDefault);  // words in flight per wave (1, 2, 4)
 
     // The scans are split over the ranks by 64-edge words ([R*nw/N, (R+1)*nw/N): rank R's ids
     // are whole words): the tips / filter pass's two bitmaps are all-gathered (D/8 bytes each),
@@ -1940,7 +1947,8 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
             mpost.alloc(w_hi - w_lo);
         }
         if (w_hi > w_lo) {
-            hipLaunchKernelGGL(k_tips_filter, dim3(wgrid), dim3(kBlock), 0, st, v, w_lo, w_hi, comm ? mseeds.p : seeds.p,
+            auto kern = scan_u == 1 ? k_tips_filter<1> : scan_u == 4 ? k_tips_filter<4> : k_tips_filter<kScanUDefault>;
+            hipLaunchKernelGGL(kern, dim3(wgrid), dim3(kBlock), 0, st, v, w_lo, w_hi, comm ? mseeds.p : seeds.p,
                                comm ? mpost.p : post.p, c2.p, fuse ? ps.nf.p : (uint8_t *)nullptr,
                                fuse ? ps.nxk.p : (uint64_t *)nullptr);
             LAUNCH_OK();
@@ -1986,7 +1994,9 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
             DevBuf<uint64_t> list(cap ? cap : 1);
             HIP_OK(hipMemsetAsync(c3.p, 0, 24, st));
             if (w_hi > w_lo) {
-                hipLaunchKernelGGL(k_recount_candidates, dim3(wgrid), dim3(kBlock), 0, st, v,
+                auto kern = scan_u == 1 ? k_recount_candidates<1> : scan_u == 4 ? k_recount_candidates<4>
+                                                                                : k_recount_candidates<kScanUDefault>;
+                hipLaunchKernelGGL(kern, dim3(wgrid), dim3(kBlock), 0, st, v,
                                    (uint64_t)p.threshold_multiplicity, lo, hi, w_lo, w_hi, list.p, cap, c3.p);
                 LAUNCH_OK();
             }

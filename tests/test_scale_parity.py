@@ -52,6 +52,9 @@ KNOBS = {
     "sort_mid": {"sort.msd": 1, "sort.wave_limit": 0},
     "sort_mid_bitonic": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_counting": 0},
     "sort_mid_occ5": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_occ": 5},
+    # the scans with four 64-edge words in flight per wave, the peel prep with eight edges
+    "scan_u4_prep8": {"cf.scan_u": 4, "cf.prep_batch": 8},
+    "scan_u1_prep16": {"cf.scan_u": 1, "cf.prep_batch": 16},
     "sort_block": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_limit": 0},
     "sort_radix": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_limit": 0, "sort.block_limit": 0},
     "sort_radix_only": {"sort.msd": 0},
