@@ -304,6 +304,7 @@ void mcaat_reset_timing(mcaat_ctx *ctx);
  *   cf.scan_u          64-edge words in flight per wave in the tips/filter and recount scans
  *                      (1, 2 default, 4)
  *   cf.prep_batch      edges per thread in flight in the peel's prep pass (2 default, 4, 8, 16)
+ *   cf.dls_lanes       DepthLevelSearch searches per wave (1..64, default 16)
  *   cf.dls_stack / cf.dls_visited   initial DepthLevelSearch scratch (grows x8 on overflow)
  *   cf.fc_lock / cf.fc_relax / cf.fc_out   initial FindCycle scratch (grows on overflow)
  *   cf.fc_window       initial FindCycle speculation window

@@ -1500,9 +1500,12 @@ static std::vector<uint64_t> run_dls(mcaat_graph *g, const std::vector<uint64_t>
             DevBuf<uint64_t> dids(n), dstk(n * cs), dvis(n * cv);
             DevBuf<int8_t> dres(n);
             h2d(g->ctx, dids.p, ids.data(), 8 * n);
-            constexpr int kDlsLanes = 4;
-            hipLaunchKernelGGL(k_dls, dim3(grid_for(n, kDlsLanes)), dim3(64), 0, st, g->view(), dids.p, n, limit, dstk.p,
-                               cs, dvis.p, cv, dres.p, kDlsLanes);
+            // searches per wave: a wave runs as long as its longest search, but more searches
+            // per wave keep more loads in flight (C5, 3.8M candidates: 4 / 16 / 64 lanes ->
+            // DLS 91 / 60 / 69 ms; C3 2.7-3.0 ms for any)
+            const int lanes = (int)std::max<int64_t>(1, std::min<int64_t>(64, knob(ctx, "cf.dls_lanes", 16)));
+            hipLaunchKernelGGL(k_dls, dim3(grid_for(n, (unsigned)lanes)), dim3(64), 0, st, g->view(), dids.p, n, limit,
+                               dstk.p, cs, dvis.p, cv, dres.p, lanes);
             LAUNCH_OK();
             std::vector<int8_t> h(n);
             HIP_OK(hipMemcpyAsync(h.data(), dres.p, n, hipMemcpyDeviceToHost, st));

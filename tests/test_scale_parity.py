@@ -55,6 +55,9 @@ KNOBS = {
     # the scans with four 64-edge words in flight per wave, the peel prep with eight edges
     "scan_u4_prep8": {"cf.scan_u": 4, "cf.prep_batch": 8},
     "scan_u1_prep16": {"cf.scan_u": 1, "cf.prep_batch": 16},
+    # DepthLevelSearch with one search per wave and with a full wave of them
+    "dls_lanes1": {"cf.dls_lanes": 1},
+    "dls_lanes64": {"cf.dls_lanes": 64, "cf.dls_stack": 1, "cf.dls_visited": 2},
     "sort_block": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_limit": 0},
     "sort_radix": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_limit": 0, "sort.block_limit": 0},
     "sort_radix_only": {"sort.msd": 0},
