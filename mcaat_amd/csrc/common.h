@@ -80,19 +80,7 @@ struct GraphView {
 
 __device__ __forceinline__ bool bit_get(const uint64_t *bm, uint64_t i) { return (bm[i >> 6] >> (i & 63)) & 1; }
 
-// valid out-edges of e in DESCENDING id order (DESIGN.md convention); returns count
-__device__ __forceinline__ int dev_outgoing(const GraphView &g, uint64_t e, uint64_t *out) {
-    const uint64_t oi = g.out_info[e];
-    const uint64_t lo = oi & kIdxMask;
-    const unsigned m = (unsigned)(oi >> kIdxBits) & 0xF;
-    const int cnt = __popc(m);
-    int n = 0;
-    for (int i = cnt - 1; i >= 0; --i) {
-        const uint64_t id = lo + i;
-        if (bit_get(g.valid, id)) out[n++] = id;
-    }
-    return n;
-}
+
 // valid in-edges of e in ASCENDING id order; returns count
 __device__ __forceinline__ int dev_incoming(const GraphView &g, uint64_t e, uint64_t *in) {
     const uint64_t ii = g.in_info[e];
@@ -121,6 +109,46 @@ __device__ __forceinline__ uint64_t this_word(uint64_t lo, uint64_t nw) {
 __device__ __forceinline__ uint64_t next_word(uint64_t lo, uint64_t nw) {
     const uint64_t w = (lo >> 6) + 1;
     return w < nw ? w : nw - 1;
+}
+// the two bitmap words at lo/64 (clamped like this_word) in one 16-B load: bitmaps are
+// allocated with a padding word after the last (mcaat_graph::bitmap_words), so the pair always
+// lies inside the allocation. Scans are bound by how many distinct addresses their gathers
+// issue, not by bytes: one load instead of two.
+struct __attribute__((aligned(8))) WordPair {
+    uint64_t a, b;
+};
+__device__ __forceinline__ WordPair word_pair(const uint64_t *bm, uint64_t lo, uint64_t nw) {
+    return *(const WordPair *)(bm + this_word(lo, nw));
+}
+// multiplicities of edges lo .. lo+3 from the three dwords holding them (one 12-B load; mult is
+// allocated 8 entries past D, mcaat_graph::mult_entries); entries past D are garbage the
+// caller masks
+struct __attribute__((aligned(4))) Dword3 {
+    uint32_t x, y, z;
+};
+__device__ __forceinline__ void mult4(const uint16_t *mult, uint64_t lo, uint32_t *m) {
+    const Dword3 d = *(const Dword3 *)(mult + (lo & ~1ull));
+    const uint64_t w = (uint64_t)d.x | ((uint64_t)d.y << 32);
+    if (lo & 1) {
+        const uint64_t v = (w >> 16) | ((uint64_t)d.z << 48);
+        m[0] = (uint32_t)v & 0xFFFF, m[1] = (uint32_t)(v >> 16) & 0xFFFF, m[2] = (uint32_t)(v >> 32) & 0xFFFF, m[3] = (uint32_t)(v >> 48);
+    } else {
+        m[0] = (uint32_t)w & 0xFFFF, m[1] = (uint32_t)(w >> 16) & 0xFFFF, m[2] = (uint32_t)(w >> 32) & 0xFFFF, m[3] = (uint32_t)(w >> 48);
+    }
+}
+// valid out-edges of e in DESCENDING id order (DESIGN.md convention); returns count. The
+// out-edges are the consecutive ids [lo, lo + cnt): their valid bits are one bitmap window.
+__device__ __forceinline__ int dev_outgoing(const GraphView &g, uint64_t e, uint64_t *out) {
+    const uint64_t oi = g.out_info[e];
+    const uint64_t lo = oi & kIdxMask;
+    const unsigned m = (unsigned)(oi >> kIdxBits) & 0xF;
+    const int cnt = __popc(m);
+    const WordPair w = word_pair(g.valid, lo, (g.D + 63) / 64);
+    const uint32_t vb = bits16(w.a, w.b, lo);
+    int n = 0;
+    for (int i = cnt - 1; i >= 0; --i)
+        if ((vb >> i) & 1) out[n++] = lo + i;
+    return n;
 }
 __device__ __forceinline__ int dev_outdeg(const GraphView &g, uint64_t e) {
     uint64_t t[4];

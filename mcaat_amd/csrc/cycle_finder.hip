@@ -105,9 +105,10 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_
     const bool peel = nf != nullptr;
     unsigned long long acc = 0, low_n = 0;
     for (uint64_t wb = w_lo + (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); wb < w_hi; wb += kScanU * wstride) {
-        uint64_t sv[kScanU], oi[kScanU], a0[kScanU], a1[kScanU];
+        uint64_t sv[kScanU], oi[kScanU];
+        WordPair a[kScanU];
         uint32_t mu[kScanU];
-        uint16_t sm[kScanU][4];
+        uint32_t sm[kScanU][4];
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
             const uint64_t w = wb + u * wstride, e = w * 64 + lane;
@@ -118,20 +119,15 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
             const uint64_t lo = oi[u] & kIdxMask;
-            a0[u] = g.valid[this_word(lo, nw)];
-            a1[u] = g.valid[next_word(lo, nw)];
-            if (peel) {
-                const uint32_t cnt = __popc((unsigned)(oi[u] >> kIdxBits) & 0xF);
-#pragma unroll
-                for (int i = 0; i < 4; ++i) sm[u][i] = (uint32_t)i < cnt ? g.mult[lo + i] : 0;
-            }
+            a[u] = word_pair(g.valid, lo, nw);
+            if (peel) mult4(g.mult, lo, sm[u]);  // entries past cnt are masked by pre below
         }
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
             const uint64_t w = wb + u * wstride, e = w * 64 + lane;
             const uint64_t lo = oi[u] & kIdxMask;
             const uint32_t cnt = __popc((unsigned)(oi[u] >> kIdxBits) & 0xF);
-            const uint32_t pre = bits16(a0[u], a1[u], lo) & ((1u << cnt) - 1);
+            const uint32_t pre = bits16(a[u].a, a[u].b, lo) & ((1u << cnt) - 1);
             const bool t = ((sv[u] >> lane) & 1) && pre == 0;
             const unsigned long long m = __ballot(t);
             const unsigned long long lowm = __ballot(mu[u] <= 1);
@@ -180,7 +176,8 @@ __global__ void __launch_bounds__(kBlock) k_recount_candidates(GraphView g, uint
     __shared__ uint64_t wbuf[kBlock / 64][128];
     WaveList wl{wbuf[threadIdx.x >> 6], list, counts + 2, cap};
     for (uint64_t wb = w_lo + (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); wb < w_hi; wb += kScanU * wstride) {
-        uint64_t sv[kScanU], oi[kScanU], ii[kScanU], a0[kScanU], a1[kScanU], b0[kScanU], b1[kScanU];
+        uint64_t sv[kScanU], oi[kScanU], ii[kScanU];
+        WordPair a[kScanU], b[kScanU];
         uint32_t mu[kScanU];
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
@@ -194,25 +191,22 @@ __global__ void __launch_bounds__(kBlock) k_recount_candidates(GraphView g, uint
         }
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
-            const uint64_t l = oi[u] & kIdxMask, m = ii[u] & kIdxMask;
-            a0[u] = g.valid[this_word(l, nw)];
-            a1[u] = g.valid[next_word(l, nw)];
-            b0[u] = g.valid[this_word(m, nw)];
-            b1[u] = g.valid[next_word(m, nw)];
+            a[u] = word_pair(g.valid, oi[u] & kIdxMask, nw);
+            b[u] = word_pair(g.valid, ii[u] & kIdxMask, nw);
         }
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
             const uint64_t w = wb + u * wstride, e = w * 64 + lane;
             const bool v = (sv[u] >> lane) & 1;
             const uint32_t cnt = __popc((unsigned)(oi[u] >> kIdxBits) & 0xF);
-            const bool t = v && (bits16(a0[u], a1[u], oi[u] & kIdxMask) & ((1u << cnt) - 1)) == 0;
+            const bool t = v && (bits16(a[u].a, a[u].b, oi[u] & kIdxMask) & ((1u << cnt) - 1)) == 0;
             const unsigned long long tm = __ballot(t);
             if (lane == 0 && w < w_hi) {
                 ntips += __popcll(tm);
                 nvalid += __popcll(sv[u]);
             }
             const uint64_t l = ii[u] & kIdxMask;
-            const uint32_t in = bits16(b0[u], b1[u], l) & (uint32_t)((ii[u] >> kIdxBits) & 0xFFFF);  // valid in-edges
+            const uint32_t in = bits16(b[u].a, b[u].b, l) & (uint32_t)((ii[u] >> kIdxBits) & 0xFFFF);  // valid in-edges
             // _IncomingNotEqualToCurrentNode: e must not be one of its own in-edges
             const bool self = e >= l && e - l < 16 && ((in >> (e - l)) & 1);
             const bool c = v && e >= lo && e < hi && (uint64_t)mu[u] > thr && __popc(in) >= 2 && !self;
@@ -826,8 +820,7 @@ struct FcThread {
         const uint64_t lo = oi & kIdxMask;
         const int cnt = __popc((unsigned)(oi >> kIdxBits) & 0xF);
         if (cnt == 0) return 0;
-        const uint64_t v0 = g.valid[this_word(lo, nw)], v1 = g.valid[next_word(lo, nw)];
-        const uint64_t q0 = visited[this_word(lo, nw)], q1 = visited[next_word(lo, nw)];
+        const WordPair vw = word_pair(g.valid, lo, nw), qw = word_pair(visited, lo, nw);
         uint32_t mu[4];
         uint64_t no[4], k0[4];
         uint32_t h0[4];
@@ -845,8 +838,8 @@ struct FcThread {
                 k0[i] = s.lk[h0[i]].key;
             }
         }
-        const uint32_t vb = bits16(v0, v1, lo) & ((1u << cnt) - 1);
-        const uint32_t qb = bits16(q0, q1, lo);
+        const uint32_t vb = bits16(vw.a, vw.b, lo) & ((1u << cnt) - 1);
+        const uint32_t qb = bits16(qw.a, qw.b, lo);
         uint64_t fx[4] = {0, 0, 0, 0}, fo[4] = {0, 0, 0, 0};
         int32_t fs[4] = {0, 0, 0, 0};
         uint32_t fm[4] = {0, 0, 0, 0};
@@ -905,8 +898,7 @@ struct FcThread {
                 m = q + 1;
             }
         }
-        const uint64_t v0 = g.valid[this_word(lo, nw)], v1 = g.valid[next_word(lo, nw)];
-        const uint64_t q0 = visited[this_word(lo, nw)], q1 = visited[next_word(lo, nw)];
+        const WordPair vw = word_pair(g.valid, lo, nw), qw = word_pair(visited, lo, nw);
         uint32_t mu[4];
         uint64_t ni[4], k0[4];
         uint32_t h0[4];
@@ -924,8 +916,8 @@ struct FcThread {
                 k0[q] = s.lk[h0[q]].key;
             }
         }
-        const uint32_t vb = bits16(v0, v1, lo);
-        const uint32_t qb = bits16(q0, q1, lo);
+        const uint32_t vb = bits16(vw.a, vw.b, lo);
+        const uint32_t qb = bits16(qw.a, qw.b, lo);
         uint32_t wr[4];
         int nwr = 0, n = 0;
 #pragma unroll
@@ -1563,7 +1555,7 @@ struct FcRunner {
         caps.CC = (uint32_t)std::max(1, p.cluster_bound);
         caps.CO = (uint32_t)std::max<uint64_t>(caps.P, (uint64_t)caps.CC * (caps.P - 1));
         if (const int64_t co = knob(ctx, "cf.fc_out", 0)) caps.CO = (uint32_t)co;
-        dvis.alloc(gr->n_words());
+        dvis.alloc(mcaat_graph::bitmap_words(gr->D));
         HIP_OK(hipMemsetAsync(dvis.p, 0, dvis.bytes(), gr->ctx->stream));
     }
     uint64_t per_al() const { return fc_per_search(caps); }
@@ -1941,7 +1933,8 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
         ps.ready = true;
     }
     {
-        DevBuf<uint64_t> post(nw);
+        DevBuf<uint64_t> post(mcaat_graph::bitmap_words(D));
+        HIP_OK(hipMemsetAsync(post.p + nw, 0, 8, st));  // the padding word
         DevBuf<unsigned long long> c2(2);
         HIP_OK(hipMemsetAsync(c2.p, 0, 16, st));
         DevBuf<uint64_t> mseeds, mpost;  // this rank's words when the bitmaps are gathered

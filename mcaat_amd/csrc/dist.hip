@@ -99,7 +99,7 @@ void build_graph_sharded(mcaat_ctx *ctx, Comm &comm, const mcaat_reads *r, int k
     g->k = k;
     g->D = D;
     g->key.alloc(D ? D : 1);
-    g->mult.alloc(D ? D : 1);
+    g->mult.alloc(mcaat_graph::mult_entries(D));
     std::vector<uint64_t> b8(N), b2(N);
     for (int p = 0; p < N; ++p) b8[p] = 8 * ns[p], b2[p] = 2 * ns[p];
     HIP_OK(hipStreamSynchronize(st));

@@ -116,7 +116,7 @@ void graph_load(mcaat_ctx *ctx, const char *path, mcaat_graph *g) {
     g->k = k;
     g->D = D;
     g->key.alloc(D ? D : 1);
-    g->mult.alloc(D ? D : 1);
+    g->mult.alloc(mcaat_graph::mult_entries(D));
     file_to_dev(in, g->key.p, 8 * D, sum, stage);
     file_to_dev(in, g->mult.p, 2 * D, sum, stage);
     DevBuf<uint64_t> valid(nw ? nw : 1);

@@ -187,6 +187,11 @@ struct mcaat_graph {
         return mcaat::GraphView{k, D, key.p, mult.p, out_info.p, in_info.p, valid.p};
     }
     uint64_t n_words() const { return (D + 63) / 64; }
+    // allocation sizes: a valid/visited bitmap keeps one word past its last, and mult 8
+    // entries past its last, so a neighbour window is one 16-B / 12-B load (common.h win16,
+    // mult4) even at the end of the graph
+    static uint64_t bitmap_words(uint64_t d) { return (d + 63) / 64 + 1; }
+    static uint64_t mult_entries(uint64_t d) { return d + 8; }
 };
 
 struct mcaat_cycles {

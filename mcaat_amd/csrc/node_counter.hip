@@ -735,7 +735,10 @@ __global__ void __launch_bounds__(kBThreads) k_l2_scatter(const uint4 *__restric
 // partition with too many distinct descriptors (shallow data) is expanded from the raw
 // descriptor stream instead; one with too many distinct edges for LDS goes to the
 // global-table fallback.
-constexpr int kCThreads = 1024;
+#ifndef MCAAT_CTHREADS
+#define MCAAT_CTHREADS 1024
+#endif
+constexpr int kCThreads = MCAAT_CTHREADS;
 constexpr int kCWaves = kCThreads / 64;
 constexpr int kCap = 4096;                                 // edge slots
 constexpr int kCapMax = kCap * 85 / 100 - kCWaves * 64;    // distinct edges before giving up
@@ -985,13 +988,14 @@ __global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_coun
         };
         // the distinct descriptors move to registers (slots threadIdx.x + j * kCThreads), then
         // the region becomes the edge table
-        static_assert(kDCap == 2 * kCThreads, "two descriptor slots per thread");
+        constexpr int kSlots = kDCap / kCThreads;
+        static_assert(kDCap % kCThreads == 0, "whole descriptor slots per thread");
         const bool raw = dovf;
-        uint64_t r0[2] = {0, 0}, r1[2] = {0, 0};
-        uint32_t rc[2] = {0, 0};
+        uint64_t r0[kSlots] = {}, r1[kSlots] = {};
+        uint32_t rc[kSlots] = {};
         if (!raw) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) {
+            for (int j = 0; j < kSlots; ++j) {
                 const int i = threadIdx.x + j * kCThreads;
                 rc[j] = dcnt[i];
                 if (rc[j]) {
@@ -1008,7 +1012,7 @@ __global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_coun
         __syncthreads();
         if (!raw) {
 #pragma unroll
-            for (int j = 0; j < 2; ++j) spread(r0[j], r1[j], (int)((r1[j] >> kNShift) & 63), rc[j]);
+            for (int j = 0; j < kSlots; ++j) spread(r0[j], r1[j], (int)((r1[j] >> kNShift) & 63), rc[j]);
             if (wave == 0) {
                 // n_deferred <= kDefer here (more sends the partition raw)
                 const bool live = (uint32_t)lane < n_deferred;

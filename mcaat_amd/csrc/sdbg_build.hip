@@ -990,7 +990,7 @@ void sdbg_build(mcaat_ctx *ctx, CountResult &c, int k, mcaat_graph *g) {
     const uint64_t D = n2 - n_pal;
     g->D = D;
     g->key.alloc(D ? D : 1);
-    g->mult.alloc(D ? D : 1);
+    g->mult.alloc(mcaat_graph::mult_entries(D));
     // MSD sort with LDS bucket sorts (k <= 28: key remainder and mult share one word);
     // the radix sort otherwise, or when a bucket is too skewed for LDS
     bool done = false;
@@ -1070,7 +1070,8 @@ void sdbg_finish(mcaat_ctx *ctx, mcaat_graph *g) {
         LAUNCH_OK();
         kt.stop();
     }
-    g->valid.alloc((D + 63) / 64);
+    g->valid.alloc(mcaat_graph::bitmap_words(D));
+    HIP_OK(hipMemsetAsync(g->valid.p + (D + 63) / 64, 0, 8, st));  // the padding word
     hipLaunchKernelGGL(k_valid_init, dim3(grid_for((D + 63) / 64, kBlock)), dim3(kBlock), 0, st, g->valid.p, D);
     LAUNCH_OK();
     HIP_OK(hipStreamSynchronize(st));

@@ -192,7 +192,7 @@ void graph_from_sorted(mcaat_ctx *ctx, int k, const uint64_t *keys, const uint16
     g->k = k;
     g->D = D;
     g->key.alloc(D ? D : 1);
-    g->mult.alloc(D ? D : 1);
+    g->mult.alloc(mcaat_graph::mult_entries(D));
     if (D) {
         HIP_OK(hipMemcpyAsync(g->key.p, keys, 8 * D, hipMemcpyDeviceToDevice, st));
         HIP_OK(hipMemcpyAsync(g->mult.p, mult, 2 * D, hipMemcpyDeviceToDevice, st));
