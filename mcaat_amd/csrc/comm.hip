@@ -292,16 +292,35 @@ struct ShmComm final : Comm {
 
     uint8_t *slot_of(int r) const { return slots + slot * (uint64_t)r; }
 
+    // a device-to-device copy that has landed when this returns: ordered on the context's
+    // stream (the caller's kernels run there) and waited for. A plain hipMemcpy between two
+    // device buffers returns before the copy completes and runs on the null stream, which the
+    // context's non-blocking stream does not wait for: with one rank (nothing but this copy in
+    // an exchange) the next kernels read the buffer while it was still being written.
+    void d2d(void *dst, const void *src, uint64_t n) {
+        HIP_OK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToDevice, ctx->stream));
+        HIP_OK(hipStreamSynchronize(ctx->stream));
+    }
     // copies between host or device memory and a slot (ctx null: host memory only)
+    // (device sides on the context's stream and waited for: a host-to-device hipMemcpy from
+    // pageable memory may return before its DMA has landed)
     void put(uint8_t *dst, const void *src, uint64_t n, bool dev) {
         if (!n) return;
-        if (dev) HIP_OK(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost));
-        else memcpy(dst, src, n);
+        if (dev) {
+            HIP_OK(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, ctx->stream));
+            HIP_OK(hipStreamSynchronize(ctx->stream));
+        } else {
+            memcpy(dst, src, n);
+        }
     }
     void get(void *dst, const uint8_t *src, uint64_t n, bool dev) {
         if (!n) return;
-        if (dev) HIP_OK(hipMemcpy(dst, src, n, hipMemcpyHostToDevice));
-        else memcpy(dst, src, n);
+        if (dev) {
+            HIP_OK(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, ctx->stream));
+            HIP_OK(hipStreamSynchronize(ctx->stream));
+        } else {
+            memcpy(dst, src, n);
+        }
     }
 
     // all-gather of sizes[r] bytes per rank (known to all) through the slots, in rounds
@@ -317,7 +336,7 @@ struct ShmComm final : Comm {
                 const uint64_t n = std::min(slot, sizes[r] - c0);
                 uint8_t *dst = (uint8_t *)recv + off[r] + c0;
                 if (r == rank) {
-                    if (dev) HIP_OK(hipMemcpy(dst, (const uint8_t *)send + c0, n, hipMemcpyDeviceToDevice));
+                    if (dev) d2d(dst, (const uint8_t *)send + c0, n);
                     else memcpy(dst, (const uint8_t *)send + c0, n);
                 } else {
                     get(dst, slot_of(r), n, dev);
@@ -352,7 +371,7 @@ struct ShmComm final : Comm {
             uint8_t *dst = (uint8_t *)recv + ro[from];
             if (s == 0) {
                 if (send_bytes[rank] != recv_bytes[rank]) throw Error(MCAAT_E_INVALID, "alltoallv: self sizes differ");
-                if (send_bytes[rank]) HIP_OK(hipMemcpy(dst, src, send_bytes[rank], hipMemcpyDeviceToDevice));
+                if (send_bytes[rank]) d2d(dst, src, send_bytes[rank]);
                 continue;
             }
             const auto out_n = exchange(send_bytes[to]);

@@ -4,11 +4,17 @@
 //   1. every rank counts its own reads (node_counter; the LDS collapse pre-aggregates);
 //   2. the ranks sum a histogram of the top BOSS-key bits and cut it into `world` owner
 //      ranges of equal weight, contiguous in BOSS order;
-//   3. each rank writes its oriented (BOSS key, partial count) pairs owner-major and the ranks
-//      exchange them in one all-to-all (keys and counts);
-//   4. each owner sorts its pairs and sums equal keys (saturating at 65535 after the sum);
+//   3. each rank sends every canonical edge once, with its partial count saturated to 16 bits,
+//      to the owner of the smaller of its two BOSS keys (one all-to-all of keys and counts);
+//   4. that owner sorts and sums them, expands each to its oriented edges (multiplicity
+//      saturated at 65535) and routes each to the owner of its BOSS range (a second, small
+//      all-to-all); each owner sorts what it holds — its range, every key exactly once;
 //   5. an exact-size all-gather in rank order concatenates the owners' ranges into the
 //      single-GPU edge array (edge ids bit-identical), and every rank builds the adjacency.
+// Round 3: at high coverage every rank's reads hold nearly every edge, so the round-2 exchange
+// of both orientations with 32-bit counts (knob dist.oriented=1, kept for comparison) sent
+// 2 x D_local x 12 B per rank and each owner sorted ~2 x D_local pairs whatever N; steps 3-4
+// send D_local x 10 B and sort D_local, then D / N.
 // Replaces: Read2SdbgS2::Run driven from sdbg_build.cpp:171-187, for reads split over ranks.
 #include <algorithm>
 #include <vector>
@@ -62,35 +68,89 @@ void build_graph_sharded(mcaat_ctx *ctx, Comm &comm, const mcaat_reads *r, int k
         for (size_t i = 0; i < all.size(); ++i) hist[i % hist.size()] += all[i];
     }
     const std::vector<uint64_t> splits = choose_splits(hist, N, 2 * (k + 1));
-    const uint64_t cap = std::max<uint64_t>(1, 2 * c.n);
-    DevBuf<uint64_t> okeys(cap);
-    DevBuf<uint32_t> ocnt(cap);
-    std::vector<uint64_t> sizes(N);
-    counts_partition(ctx, c, k, N, splits.data(), sizes.data(), okeys.p, ocnt.p, cap);
-    c = CountResult{};
-    timer.mark("shard_partition");
+    DevBuf<uint64_t> uk;
+    DevBuf<uint16_t> um;
+    uint64_t u = 0;
+    if (knob(ctx, "dist.oriented", 0)) {
+        const uint64_t cap = std::max<uint64_t>(1, 2 * c.n);
+        DevBuf<uint64_t> okeys(cap);
+        DevBuf<uint32_t> ocnt(cap);
+        std::vector<uint64_t> sizes(N);
+        counts_partition(ctx, c, k, N, splits.data(), sizes.data(), okeys.p, ocnt.p, cap);
+        c = CountResult{};
+        timer.mark("shard_partition");
 
-    // sizes[s][d] of every rank s -> what this rank receives
-    const std::vector<uint64_t> mat = comm.allgather_vec(sizes);
-    std::vector<uint64_t> in(N), sb(N), rb(N);
-    uint64_t n_in = 0;
-    for (int s = 0; s < N; ++s) n_in += in[s] = mat[(uint64_t)s * N + R];
-    DevBuf<uint64_t> rk(n_in);
-    DevBuf<uint32_t> rc(n_in);
-    for (int p = 0; p < N; ++p) sb[p] = 8 * sizes[p], rb[p] = 8 * in[p];
-    comm.alltoallv_dev(okeys.p, sb.data(), rk.p, rb.data());
-    for (int p = 0; p < N; ++p) sb[p] = 4 * sizes[p], rb[p] = 4 * in[p];
-    comm.alltoallv_dev(ocnt.p, sb.data(), rc.p, rb.data());
-    okeys.release();
-    ocnt.release();
-    timer.mark("shard_all_to_all");
+        // sizes[s][d] of every rank s -> what this rank receives
+        const std::vector<uint64_t> mat = comm.allgather_vec(sizes);
+        std::vector<uint64_t> in(N), sb(N), rb(N);
+        uint64_t n_in = 0;
+        for (int s = 0; s < N; ++s) n_in += in[s] = mat[(uint64_t)s * N + R];
+        DevBuf<uint64_t> rk(n_in);
+        DevBuf<uint32_t> rc(n_in);
+        for (int p = 0; p < N; ++p) sb[p] = 8 * sizes[p], rb[p] = 8 * in[p];
+        comm.alltoallv_dev(okeys.p, sb.data(), rk.p, rb.data());
+        for (int p = 0; p < N; ++p) sb[p] = 4 * sizes[p], rb[p] = 4 * in[p];
+        comm.alltoallv_dev(ocnt.p, sb.data(), rc.p, rb.data());
+        okeys.release();
+        ocnt.release();
+        timer.mark("shard_all_to_all");
 
-    DevBuf<uint64_t> uk(n_in);
-    DevBuf<uint16_t> um(n_in);
-    const uint64_t u = edges_reduce(ctx, k, rk.p, rc.p, n_in, uk.p, um.p);
-    rk.release();
-    rc.release();
-    timer.mark("shard_reduce");
+        uk.alloc(n_in ? n_in : 1);
+        um.alloc(n_in ? n_in : 1);
+        u = edges_reduce(ctx, k, rk.p, rc.p, n_in, uk.p, um.p);
+        timer.mark("shard_reduce");
+    } else {
+        // step 3: canonical edges to the owner of their smaller BOSS key
+        const uint64_t cap = std::max<uint64_t>(1, c.n);
+        DevBuf<uint64_t> okeys(cap);
+        DevBuf<uint16_t> ocnt(cap);
+        std::vector<uint64_t> sizes(N);
+        counts_partition_canon(ctx, c, k, N, splits.data(), sizes.data(), okeys.p, ocnt.p, cap);
+        c = CountResult{};
+        timer.mark("shard_partition");
+        auto exchange = [&](const std::vector<uint64_t> &out_sizes, const uint64_t *skeys, const uint16_t *svals,
+                            DevBuf<uint64_t> &rkeys, DevBuf<uint16_t> &rvals) {
+            const std::vector<uint64_t> mat = comm.allgather_vec(out_sizes);
+            std::vector<uint64_t> in(N), sb(N), rb(N);
+            uint64_t n_in = 0;
+            for (int s = 0; s < N; ++s) n_in += in[s] = mat[(uint64_t)s * N + R];
+            rkeys.alloc(n_in ? n_in : 1);
+            rvals.alloc(n_in ? n_in : 1);
+            for (int p = 0; p < N; ++p) sb[p] = 8 * out_sizes[p], rb[p] = 8 * in[p];
+            comm.alltoallv_dev(skeys, sb.data(), rkeys.p, rb.data());
+            for (int p = 0; p < N; ++p) sb[p] = 2 * out_sizes[p], rb[p] = 2 * in[p];
+            comm.alltoallv_dev(svals, sb.data(), rvals.p, rb.data());
+            return n_in;
+        };
+        DevBuf<uint64_t> rk;
+        DevBuf<uint16_t> rc;
+        const uint64_t n_in = exchange(sizes, okeys.p, ocnt.p, rk, rc);
+        okeys.release();
+        ocnt.release();
+        timer.mark("shard_all_to_all");
+        // step 4: sum, expand, route the oriented edges to their range owners, sort
+        DevBuf<uint64_t> ck(n_in ? n_in : 1);
+        DevBuf<uint32_t> ct(n_in ? n_in : 1);
+        const uint64_t nc = canon_reduce(ctx, k, rk.p, rc.p, n_in, ck.p, ct.p);
+        rk.release();
+        rc.release();
+        const uint64_t cap2 = std::max<uint64_t>(1, 2 * nc);
+        DevBuf<uint64_t> qk(cap2);
+        DevBuf<uint16_t> qm(cap2);
+        std::vector<uint64_t> sizes2(N);
+        route_oriented(ctx, k, ck.p, ct.p, nc, N, splits.data(), sizes2.data(), qk.p, qm.p, cap2);
+        ck.release();
+        ct.release();
+        DevBuf<uint64_t> sk2;
+        DevBuf<uint16_t> sm2;
+        u = exchange(sizes2, qk.p, qm.p, sk2, sm2);
+        qk.release();
+        qm.release();
+        uk.alloc(u ? u : 1);
+        um.alloc(u ? u : 1);
+        sort_oriented(ctx, k, sk2.p, sm2.p, u, uk.p, um.p);
+        timer.mark("shard_reduce");
+    }
 
     const std::vector<uint64_t> ns = comm.allgather_one(u);
     uint64_t D = 0;

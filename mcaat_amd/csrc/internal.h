@@ -362,6 +362,18 @@ void counts_partition(mcaat_ctx *ctx, const CountResult &c, int k, int n_owners,
 uint64_t edges_reduce(mcaat_ctx *ctx, int k, const uint64_t *keys, const uint32_t *cnt, uint64_t n, uint64_t *keys_out,
                       uint16_t *mult_out);
 void graph_from_sorted(mcaat_ctx *ctx, int k, const uint64_t *keys, const uint16_t *mult, uint64_t D, mcaat_graph *g);
+// the native multi-GPU build's canonical-pair exchange (shard.hip): canonical edges routed to the
+// owner of their smaller BOSS key with 16-bit partial counts; the owner sums them
+// (canon_reduce), routes the oriented edges to their range owners (route_oriented), and each
+// owner sorts what it received (sort_oriented)
+uint64_t counts_partition_canon(mcaat_ctx *ctx, const CountResult &c, int k, int n_owners, const uint64_t *splits_host,
+                                uint64_t *sizes_host, uint64_t *okeys, uint16_t *ocnt, uint64_t cap);
+uint64_t canon_reduce(mcaat_ctx *ctx, int k, const uint64_t *keys, const uint16_t *cnt16, uint64_t n, uint64_t *keys_out,
+                      uint32_t *tot_out);
+uint64_t route_oriented(mcaat_ctx *ctx, int k, const uint64_t *keys, const uint32_t *tot, uint64_t n, int n_owners,
+                        const uint64_t *splits_host, uint64_t *sizes_host, uint64_t *okeys, uint16_t *omult, uint64_t cap);
+void sort_oriented(mcaat_ctx *ctx, int k, const uint64_t *keys, const uint16_t *mult, uint64_t n, uint64_t *keys_out,
+                   uint16_t *mult_out);
 struct Comm;  // comm.h
 // comm: the ranks of a multi-GPU run that each hold this graph (null: one GPU); every rank
 // gets the same results

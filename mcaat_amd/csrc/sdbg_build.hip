@@ -70,9 +70,11 @@ __global__ void __launch_bounds__(kBlock) k_dir(const uint64_t *key, uint64_t D,
 #pragma unroll
         for (int j = 0; j < kDirU; ++j) {
             const uint64_t e = base + 64 * j + lane;
-            p[j] = e < D ? key[e] >> shift : nprefix;
+            const uint64_t x = e < D ? key[e] >> shift : nprefix;
+            p[j] = x < nprefix ? x : nprefix;  // keys are < 2^2E; clamped so a bad key cannot write past dir
         }
-        const uint64_t before = base ? (key[base - 1] >> shift) + 1 : 0;  // first prefix of this chunk
+        uint64_t before = base ? (key[base - 1] >> shift) + 1 : 0;  // first prefix of this chunk
+        before = before < nprefix + 1 ? before : nprefix + 1;
 #pragma unroll
         for (int j = 0; j < kDirU; ++j) {
             const uint64_t e = base + 64 * j + lane;

@@ -60,6 +60,7 @@ def main() -> int:
     ap.add_argument("--config", default="", help="a bench config (mcaat_amd/configs.py) at full size")
     ap.add_argument("--digest", default="", help="write checksums here (JSON) instead of comparing")
     ap.add_argument("--single", action="store_true", help="the one-GPU path alone (with --digest)")
+    ap.add_argument("--knob", action="append", default=[], help="name=value knob on every rank's context")
     a = ap.parse_args()
 
     if a.config:
@@ -70,6 +71,9 @@ def main() -> int:
         cfg = CONFIGS[a.config]
         spec, k, prm = cfg["spec"], cfg["k"], M.CfParams(threshold_multiplicity=cfg["thr"])
         ctx = M.Context(a.rank % max(1, M.device_count()) if a.comm == "rccl" else 0)
+        for kv in a.knob:
+            kn, kval = kv.split("=")
+            ctx.set_knob(kn, int(kval))
         t0 = time.time()
         if a.single:
             reads = M.Reads.synth(ctx, spec)
@@ -84,10 +88,13 @@ def main() -> int:
             count = (a.rank + 1) * spec.n_reads // a.world - first
             mine = M.Reads.synth_range(ctx, spec, first, count)
             g = M.Graph.build_sharded(ctx, comm, mine, k)
+            build_stages = {kk: round(vv, 2) for kk, vv in ctx.stage_times().items()}
             mine.free()
             res = g.cycle_finder(prm, comm=comm)
         d = checksums(g, res)
         d["seconds"] = round(time.time() - t0, 1)
+        if not a.single:
+            d["build_stages_ms"] = build_stages
         g.free()
         if comm is not None:
             comm.barrier()
@@ -107,6 +114,9 @@ def main() -> int:
     ctx = M.Context(dev)
     if a.window:
         ctx.set_knob("cf.fc_window", a.window)
+    for kv in a.knob:
+        kn, kval = kv.split("=")
+        ctx.set_knob(kn, int(kval))
     if a.comm == "shm":
         comm = M.Comm.shm(ctx, a.world, a.rank, a.name, a.slot)
     else:
