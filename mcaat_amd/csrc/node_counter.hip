@@ -214,7 +214,10 @@ constexpr uint32_t kMini = 1024;  // descriptors reserved per (workgroup, L1 buc
 constexpr uint16_t kDeadSub = 0xffff;  // sub-partition mark of an inert (n = 0) slot
 
 
-constexpr int kWB = 4;  // write batch (entries per thread per round: 12 loads in flight)
+#ifndef MCAAT_WB
+#define MCAAT_WB 4
+#endif
+constexpr int kWB = MCAAT_WB;  // write batch (entries per thread per round: 3 loads each in flight)
 
 // 8-byte pre-entry of a closed super-k-mer: minimizer hash (low 32 bits); above it the
 // close position (7 bits), the first position (7), batch parity (1) and lane (6), all in
@@ -592,7 +595,12 @@ constexpr uint32_t kChunk = 65536;
 
 // Every (chunk, sub) run is rounded up to a multiple of 4 descriptors (64 B) and padded
 // with inert ones, so each 64-B line of the fine partitions is written by one workgroup.
-__device__ __forceinline__ uint32_t round4(uint32_t x) { return (x + 3) & ~3u; }
+#ifndef MCAAT_BLG
+#define MCAAT_BLG 4
+#endif
+constexpr int kLG = MCAAT_BLG;  // descriptors per buffered line (4: 64 B)
+static_assert(kLG == 2 || kLG == 4, "32-B or 64-B lines");
+__device__ __forceinline__ uint32_t round4(uint32_t x) { return (x + kLG - 1) & ~(uint32_t)(kLG - 1); }
 
 // LDS histogram of one chunk's sub rows (16-B aligned: 8 rows per load, all loads of a
 // thread in flight together)
@@ -640,7 +648,6 @@ __global__ void __launch_bounds__(kBThreads) k_l2_hist(const uint16_t *__restric
 // more descriptors in one round than its buffered line holds writes the excess directly
 // (rare), and copies the ones that belong to its new partial line into the buffer once the
 // old line has been written.
-constexpr int kLG = 4;          // descriptors per line
 constexpr int kMaxSub = 2048;   // l2_bits <= 11: 128 KB of line buffers
 #ifndef MCAAT_BPF
 #define MCAAT_BPF 2
@@ -763,6 +770,25 @@ constexpr int kCPerCu = MCAAT_CPERCU;                      // resident workgroup
 #endif
 constexpr uint32_t kSplitLg = MCAAT_CSPLIT;                // log2 classes of an overflowing partition (<= 3 spare hash bits)
 static_assert(kSplitLg <= 3, "the sub-partition takes the top 11 of the 14 stored hash bits");
+#ifndef MCAAT_CRING
+#define MCAAT_CRING 0
+#endif
+// collapse rounds in flight in an LDS-DMA ring (0: the register prefetch below). Measured and
+// rejected (round 3, C3): a 2-round ring, 74.8 KB of LDS per workgroup, took pass C 56.4 -> 62.6 ms
+constexpr int kCRing = MCAAT_CRING;
+// one 16-B LDS-DMA per lane: lds is the wave-uniform base, lane i lands at lds + 16 i
+// (inline asm: the compiler's own wait bookkeeping would otherwise drain every DMA before the
+// next LDS access, vmcnt(0); the callers count their DMAs with wait_vm0 / wait_vm1)
+__device__ __forceinline__ void dma16(const uint4 *src, uint4 *lds) {
+    const uint32_t dst = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) void *)lds);
+    uint32_t keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(src), "s"(dst) : "memory");
+}
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void wait_vm1() { asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); }
+__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 // the deferred list only overflows on pathological T runs: those partitions go raw at once
 __device__ __forceinline__ bool n_deferred_over(uint32_t n) { return n > (uint32_t)kDefer; }
 
@@ -803,8 +829,12 @@ __global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_coun
     // between the phases each thread keeps its two descriptor slots in registers. 48 KB per
     // workgroup, so two 1024-thread workgroups share a CU and one's loads overlap the other's
     // LDS work.
-    constexpr int kEdgeBytes = kCap * 12, kDescBytes = kDCap * 20;
-    __shared__ __attribute__((aligned(16))) unsigned char region[kEdgeBytes > kDescBytes ? kEdgeBytes : kDescBytes];
+    // With kCRing > 0 the collapse streams the partition through a ring of kCRing rounds of
+    // descriptors placed after the descriptor table, filled by LDS-DMA (global_load_lds): the
+    // loads of the next kCRing rounds are in flight without holding registers.
+    constexpr int kEdgeBytes = kCap * 12, kDescBytes = kDCap * 20, kRingBytes = kCRing * kCThreads * 16;
+    constexpr int kCollBytes = kDescBytes + kRingBytes;
+    __shared__ __attribute__((aligned(16))) unsigned char region[kEdgeBytes > kCollBytes ? kEdgeBytes : kCollBytes];
     unsigned long long *const keys = (unsigned long long *)region;
     uint32_t *const cnt = (uint32_t *)(keys + kCap);
     unsigned long long *const dk0 = (unsigned long long *)region, *const dk1 = dk0 + kDCap;
@@ -912,6 +942,37 @@ __global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_coun
             dovf = 1;
             if (PROF) atomicAdd(&prof[5], 1ull);
         };
+        if constexpr (kCRing > 0) {
+            // LDS-DMA ring: wave w's 64 lanes land round r's descriptors d0 + 64w .. in slot
+            // r % kCRing (one 1-KB global_load_lds per wave); a lane reads back only its own
+            // entry, so no barrier orders the waves, and each wave counts its own DMAs (vmcnt)
+            uint4 *const ring = (uint4 *)(region + kDescBytes);
+            auto issue = [&](uint64_t d0, int slot) {
+                const uint64_t d = d0 + threadIdx.x;
+                const uint4 *src = data + (d < end ? d : beg);  // in bounds; masked when read
+                dma16(src, ring + slot * kCThreads + wave * 64);
+            };
+#pragma unroll
+            for (int r = 0; r < kCRing; ++r)
+                if (beg + (uint64_t)r * kCThreads < end) issue(beg + (uint64_t)r * kCThreads, r);
+            int slot = 0;
+            for (uint64_t d0 = beg; d0 < end; d0 += kCThreads) {
+                if (__hip_atomic_load(&dovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+                // DMAs issued after this round's (uniform): rounds d0+1 .. min(d0+kCRing-1, last)
+                const uint64_t left = (end - d0 - 1) / kCThreads;  // rounds after this one
+                if (left >= 1 && kCRing >= 2) wait_vm1(); else wait_vm0();
+                const uint4 cq = ring[slot * kCThreads + threadIdx.x];
+                const uint64_t d = d0 + threadIdx.x;
+                if (left >= (uint64_t)kCRing) {
+                    wait_lgkm0();  // the read has landed before the DMA may overwrite the slot
+                    issue(d0 + (uint64_t)kCRing * kCThreads, slot);
+                }
+                if (d < end)
+                    collapse((uint64_t)cq.x | ((uint64_t)cq.y << 32), (uint64_t)cq.z | ((uint64_t)cq.w << 32));
+                slot = slot + 1 == kCRing ? 0 : slot + 1;
+            }
+            wait_vm0();  // no DMA may land in the region once it becomes the edge table
+        } else {
         // kCB descriptors per thread per round: their loads are all in flight together, and
         // with kCPF the next round's are issued before this round's probes
         uint4 q[kCB];
@@ -940,6 +1001,7 @@ __global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_coun
             for (int k = 0; k < kCB; ++k)
                 if (d0 + (uint64_t)k * kCThreads < end)
                     collapse((uint64_t)cq[k].x | ((uint64_t)cq[k].y << 32), (uint64_t)cq[k].z | ((uint64_t)cq[k].w << 32));
+        }
         }
         __syncthreads();
         tick(1);
