@@ -238,6 +238,130 @@ __global__ void __launch_bounds__(kAdjT) k_adjacency_lds(const uint64_t *key, ui
     }
 }
 
+// Round 3: in_info written from the owning side, coalesced. Runs start at group boundaries
+// (edges sharing key >> 4; at most 16), so every in-edge of a node sits in one run: the run of
+// the node's writer (the first in-edge of the group with the node's W, as above). Run r owns,
+// for each W, the in_info slots of the targets between its first source and the next run's
+// first source: [O_W(r), O_W(r + 1)) with O_W(r) = lower_bound((W, key[s_r] >> 4) << 2), run 0
+// from the start of the W quarter and the last run to its end, so the owned ranges tile
+// [0, D) and a run's targets (the old per-W search ranges) lie inside its owned ranges. A run
+// stages the keys of its four owned ranges and their in_info words (zero: no predecessor) in
+// LDS, searches and fills them there, and writes every owned slot once: no clearing pass and
+// no scattered 8-B stores (C2: those cost 7.5 ms of 23 plus the 19-GB clear). A run whose owned
+// ranges exceed the LDS cap clears them in global memory and writes directly (directory search).
+constexpr int kOwnT = 1024;               // threads per run
+constexpr int kOwnB = 2048;               // nominal edges per run (its start moves to a group start)
+constexpr int kOwnMax = kOwnB + 16;       // a run holds at most this many edges
+constexpr int kOwnCap = 3072;             // staged owned slots (~kOwnB on average)
+// bounds[5 r] = s_r (run start, group aligned), bounds[5 r + 1 + W] = O_W(r); r = nruns: D, quarter ends
+__global__ void __launch_bounds__(kBlock) k_own_bounds(const uint64_t *key, uint64_t D, int k, const uint64_t *dir,
+                                                       int shift, uint64_t nruns, uint64_t *bounds) {
+    const uint64_t top = (uint64_t)1 << (2 * (k - 1));
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r <= nruns; r += stride) {
+        uint64_t s = r * kOwnB;
+        if (r == nruns || s >= D) s = D;
+        else if (s > 0) {
+            const uint64_t g0 = key[s - 1] >> 4;
+            while (s < D && (key[s] >> 4) == g0) ++s;  // the next group start (<= 15 steps)
+        }
+        bounds[5 * r] = s;
+        for (uint64_t W = 0; W < 4; ++W) {
+            // target key prefix (W, label s[1..k-1]) of the run's first source; run 0 and the
+            // end sentinel take the W quarter's ends
+            uint64_t t;
+            if (r == 0) t = W * top;
+            else if (s >= D) t = (W + 1) * top;
+            else t = (W * top) | (key[s] >> 4);
+            const uint64_t q = t << 2;
+            bounds[5 * r + 1 + W] = q >> (2 * (k + 1)) ? D : lower_bound_dir(key, dir, shift, q);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kOwnT) k_adjacency_own(const uint64_t *key, uint64_t D, int k, const uint64_t *dir,
+                                                         int shift, uint32_t cap, const uint64_t *bounds,
+                                                         uint64_t *out_info, uint64_t *in_info) {
+    __shared__ uint64_t own[kOwnMax];
+    __shared__ uint64_t okey[kOwnCap];   // keys of the owned ranges, W after W
+    __shared__ uint64_t ist[kOwnCap];    // their in_info words
+    const uint64_t r = blockIdx.x;
+    const uint64_t s0 = bounds[5 * r], s1 = bounds[5 * (r + 1)];
+    if (s0 >= s1) return;
+    const uint32_t n = (uint32_t)(s1 - s0);
+    uint64_t a[4];
+    uint32_t len[4], off[4];
+    uint32_t tot = 0;
+#pragma unroll
+    for (int W = 0; W < 4; ++W) {
+        a[W] = bounds[5 * r + 1 + W];
+        len[W] = (uint32_t)(bounds[5 * (r + 1) + 1 + W] - a[W]);
+        off[W] = tot;
+        tot += len[W];
+    }
+    const bool staged = tot <= cap;
+    for (uint32_t j = threadIdx.x; j < n; j += kOwnT) own[j] = key[s0 + j];
+    if (staged) {
+#pragma unroll
+        for (int W = 0; W < 4; ++W)
+            for (uint32_t i = threadIdx.x; i < len[W]; i += kOwnT) {
+                okey[off[W] + i] = key[a[W] + i];
+                ist[off[W] + i] = 0;
+            }
+    } else {
+#pragma unroll
+        for (int W = 0; W < 4; ++W)
+            for (uint32_t i = threadIdx.x; i < len[W]; i += kOwnT) in_info[a[W] + i] = 0;
+    }
+    __syncthreads();  // (also drains the clearing stores of an unstaged run before its direct writes)
+    for (uint32_t j = threadIdx.x; j < n; j += kOwnT) {
+        const uint64_t e = s0 + j;
+        const uint64_t K = own[j];
+        const uint32_t W = (uint32_t)(K & 3);
+        const uint64_t Rt = ((uint64_t)W << (2 * (k - 1))) | (K >> 4);
+        uint64_t lo;
+        unsigned m = 0;
+        if (staged) {
+            const uint64_t *rk = okey + off[W];
+            const uint32_t nn = len[W], q = 0;
+            (void)q;
+            const uint64_t qk = Rt << 2;
+            uint32_t x = 0, y = nn;
+            while (x < y) {
+                const uint32_t mid = (x + y) >> 1;
+                if (rk[mid] < qk) x = mid + 1; else y = mid;
+            }
+            lo = a[W] + x;
+            for (uint32_t i = x; i < nn && (rk[i] >> 2) == Rt; ++i) m |= 1u << (rk[i] & 3);
+        } else {
+            lo = lower_bound_dir(key, dir, shift, Rt << 2);
+            for (uint64_t i = lo; i < D && (key[i] >> 2) == Rt; ++i) m |= 1u << (key[i] & 3);
+        }
+        out_info[e] = lo | ((uint64_t)m << kIdxBits);
+        if (!m) continue;
+        // e's group lies inside the run (runs start at group starts)
+        const uint64_t gk = K >> 4;
+        uint32_t gs = j;
+        while (gs > 0 && (own[gs - 1] >> 4) == gk) --gs;
+        unsigned pm = 0;
+        int t = 0;
+        for (uint32_t q = gs; q < n && (own[q] >> 4) == gk && t < 16; ++q, ++t)
+            if ((own[q] & 3) == W) pm |= 1u << t;
+        if ((uint32_t)(__ffs(pm) - 1) != j - gs) continue;  // another in-edge of the node writes
+        const uint64_t v = (s0 + gs) | ((uint64_t)pm << kIdxBits);
+        const int deg = __popc(m);
+        if (staged)
+            for (int q = 0; q < deg; ++q) ist[off[W] + (uint32_t)(lo - a[W]) + q] = v;
+        else
+            for (int q = 0; q < deg; ++q) in_info[lo + q] = v;
+    }
+    if (!staged) return;
+    __syncthreads();
+#pragma unroll
+    for (int W = 0; W < 4; ++W)
+        for (uint32_t i = threadIdx.x; i < len[W]; i += kOwnT) in_info[a[W] + i] = ist[off[W] + i];
+}
+
 __global__ void __launch_bounds__(kBlock) k_valid_init(uint64_t *valid, uint64_t D) {
     const uint64_t nw = (D + 63) / 64;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -1055,8 +1179,18 @@ void sdbg_finish(mcaat_ctx *ctx, mcaat_graph *g) {
         // one edge per lane: neighbouring lanes search neighbouring key ranges, so the
         // searches' loads share lines across the wave (a thread-per-run merge walk that
         // loses this was 5x slower)
-        HIP_OK(hipMemsetAsync(g->in_info.p, 0, 8 * D, st));
-        if (knob(ctx, "sdbg.adj_lds", 1)) {
+        const int64_t adj = knob(ctx, "sdbg.adj_lds", 1);  // 1: owner-side runs, 2: round-2 LDS runs, 0: global search
+        if (adj == 1) {
+            const uint32_t cap = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(kOwnCap, knob(ctx, "sdbg.adj_cap", kOwnCap)));
+            const uint64_t nruns = (D + kOwnB - 1) / kOwnB;
+            DevBuf<uint64_t> bounds(5 * (nruns + 1));
+            hipLaunchKernelGGL(k_own_bounds, dim3(grid_for(nruns + 1, kBlock)), dim3(kBlock), 0, st, g->key.p, D, k,
+                               dir.p, shift, nruns, bounds.p);
+            LAUNCH_OK();
+            hipLaunchKernelGGL(k_adjacency_own, dim3((unsigned)nruns), dim3(kOwnT), 0, st, g->key.p, D, k, dir.p, shift,
+                               cap, (const uint64_t *)bounds.p, g->out_info.p, g->in_info.p);
+        } else if (adj == 2) {
+            HIP_OK(hipMemsetAsync(g->in_info.p, 0, 8 * D, st));
             const uint32_t cap = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(kAdjCap, knob(ctx, "sdbg.adj_cap", kAdjCap)));
             const uint64_t nruns = (D + kAdjB - 1) / kAdjB;
             DevBuf<uint64_t> bounds(8 * nruns);
@@ -1066,6 +1200,7 @@ void sdbg_finish(mcaat_ctx *ctx, mcaat_graph *g) {
             hipLaunchKernelGGL(k_adjacency_lds, dim3((unsigned)nruns), dim3(kAdjT), 0, st, g->key.p, D, k, dir.p, shift,
                                cap, (const uint64_t *)bounds.p, g->out_info.p, g->in_info.p);
         } else {
+            HIP_OK(hipMemsetAsync(g->in_info.p, 0, 8 * D, st));
             hipLaunchKernelGGL(k_adjacency, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, g->key.p, D, k, dir.p,
                                shift, g->out_info.p, g->in_info.p);
         }

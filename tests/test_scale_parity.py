@@ -81,11 +81,14 @@ KNOBS = {
     "peel_own_init": {"cf.fused_init": 0},
     # passes B and C of successive groups in turn on one stream
     "nc_no_overlap": {"nc.overlap": 0, "nc.group_budget": 1 << 14},
-    # adjacency: per-edge global directory searches, and the LDS-range kernel with every range
-    # (cap 0) or the larger ones (cap 200) sent to its global fallback
+    # adjacency: per-edge global directory searches; the owner-side runs (default) with every
+    # run (cap 0) or the runs whose owned ranges exceed 1500 slots sent to their global
+    # fallback; the round-2 LDS-range kernel, alone and with its ranges over 200 keys in global
     "adj_global": {"sdbg.adj_lds": 0},
     "adj_cap0": {"sdbg.adj_cap": 0},
-    "adj_cap200": {"sdbg.adj_cap": 200},
+    "adj_cap1500": {"sdbg.adj_cap": 1500},
+    "adj_lds2": {"sdbg.adj_lds": 2},
+    "adj_lds2_cap200": {"sdbg.adj_lds": 2, "sdbg.adj_cap": 200},
 }
 
 _oracle_cache = {}
@@ -281,3 +284,31 @@ def test_full_size_graph_properties(gpu_ctx, name):
         if n_checked >= 300:
             break
     g.free()
+
+
+@pytest.mark.parametrize("spec_k", [("c1_k27", None), ("pe_err", None), ("pe_err", 15), ("low_thr", 29)])
+def test_adjacency_modes_agree_on_every_edge(gpu_ctx, spec_k):
+    """The owner-side adjacency (runs starting at group starts, in_info written once per owned
+    slot) answers every edge's in- and out-neighbour query exactly like the per-edge global
+    search and the round-2 LDS-range kernel, with and without its LDS staging, including
+    k = 15 (short keys: the directory covers the whole key space) and k = 29."""
+    name, k_over = spec_k
+    spec, k, _ = CASES[name]
+    k = k_over or k
+    reads = M.Reads.synth(gpu_ctx, spec)
+    ref = None
+    for knobs in ({"sdbg.adj_lds": 0}, {"sdbg.adj_lds": 2}, {}, {"sdbg.adj_cap": 0}, {"sdbg.adj_cap": 700}):
+        with gpu_ctx.knobs(**{n.replace(".", "__"): v for n, v in knobs.items()}):
+            g = M.Graph.build(gpu_ctx, reads, k)
+            ids = np.arange(g.size, dtype=np.uint64)
+            out, oc = g.neighbors(ids, incoming=False)
+            inn, ic = g.neighbors(ids, incoming=True)
+            g.free()
+        got = (out, oc, inn, ic)
+        if ref is None:
+            ref = got
+            assert ic.sum() == oc.sum() > 0  # every edge is some edge's successor exactly once
+        else:
+            for a, b in zip(got, ref):
+                assert np.array_equal(a, b), (name, k, knobs)
+    reads.free()
