@@ -405,9 +405,13 @@ __device__ __forceinline__ int msd_items(uint64_t a, uint32_t c, int k, uint32_t
     return 2;
 }
 
-// level-1 per-chunk bucket counts, rounded to lines, summed per bucket
+// level-1 per-chunk bucket counts: written per chunk (cc[c][b]), and their line counts summed
+// per block of kBlkCh chunks (blk[j][b]); k_blk_scan / k_chunk_off turn them into each chunk's
+// line-aligned run start per bucket, so the scatter needs no counting pass of its own and no
+// cursor atomics (round 2: every chunk counted its items twice and reserved by atomics)
+constexpr int kBlkCh = 64;
 __global__ void __launch_bounds__(kBlock) k_msd1_hist(const uint64_t *ckeys, const uint32_t *ccnt, uint64_t n, int k,
-                                                      unsigned long long *tot) {
+                                                      uint32_t *cc, unsigned long long *blk) {
     __shared__ uint32_t lc[kMS];
     const uint64_t c0 = (uint64_t)blockIdx.x * kCh1, c1 = c0 + kCh1 < n ? c0 + kCh1 : n;
     for (int i = threadIdx.x; i < kMS; i += kBlock) lc[i] = 0;
@@ -419,8 +423,55 @@ __global__ void __launch_bounds__(kBlock) k_msd1_hist(const uint64_t *ckeys, con
         for (int j = 0; j < no; ++j) atomicAdd(&lc[bk[j]], 1u);
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < kMS; i += kBlock)
-        if (lc[i]) atomicAdd(&tot[i], (unsigned long long)round8(lc[i]));
+    const uint64_t c = blockIdx.x;
+    for (int i = threadIdx.x; i < kMS; i += kBlock) {
+        const uint32_t x = lc[i];
+        cc[c * kMS + i] = x;
+        if (x) atomicAdd(&blk[(c / kBlkCh) * kMS + i], (unsigned long long)(round8(x) / kIL));
+    }
+}
+
+// per bucket b: exclusive scan of the block line totals over the blocks (in place), total in tot[b]
+__global__ void __launch_bounds__(kBlock) k_blk_scan(unsigned long long *blk, uint64_t nblk, uint64_t nb,
+                                                     unsigned long long *tot) {
+    const uint64_t b = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    unsigned long long run = 0;
+    for (uint64_t j = 0; j < nblk; ++j) {
+        const unsigned long long v = blk[j * nb + b];
+        blk[j * nb + b] = run;
+        run += v;
+    }
+    tot[b] = run;
+}
+
+// chunk run starts (in lines), in place of the chunk counts: chunk c of segment g (a run of
+// chunks sharing one set of nb buckets) starts bucket b at base[g * nb + b] + the earlier
+// blocks' lines (blk, when given) + the lines of the segment's earlier chunks in its block
+__global__ void __launch_bounds__(kBlock) k_chunk_off(uint32_t *cc, uint64_t nch, uint64_t nb,
+                                                      const unsigned long long *blk, const unsigned long long *base,
+                                                      const uint64_t *seg_first, uint64_t nseg, int base_in_items) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t b = t % nb, q = t / nb;  // q: block (level 1) or segment (level 2)
+    uint64_t c0, c1;
+    unsigned long long run;
+    if (seg_first) {  // level 2: segment q = the chunks of L1 bucket q
+        if (q >= nseg) return;
+        c0 = seg_first[q];
+        c1 = seg_first[q + 1];
+        run = base[q * nb + b];
+    } else {           // level 1: block q of kBlkCh chunks, one segment
+        c0 = q * kBlkCh;
+        if (c0 >= nch) return;
+        c1 = c0 + kBlkCh < nch ? c0 + kBlkCh : nch;
+        run = base[b] + blk[q * nb + b];
+    }
+    if (base_in_items) run /= kIL;
+    for (uint64_t c = c0; c < c1; ++c) {
+        const uint32_t x = cc[c * nb + b];
+        cc[c * nb + b] = (uint32_t)run;
+        run += round8(x) / kIL;
+    }
 }
 
 // line-buffered placement of one item (see k_l2_scatter in node_counter.hip): the lane that
@@ -464,36 +515,12 @@ struct LinePlace {
 constexpr int kSBlock = 1024;
 
 __global__ void __launch_bounds__(kSBlock) k_msd1_scatter(const uint64_t *ckeys, const uint32_t *ccnt, uint64_t n,
-                                                          int k, unsigned long long *cursor, uint64_t *out) {
+                                                          int k, const uint32_t *off, uint64_t *out) {
     __shared__ uint64_t buf[kMS * kIL];
     __shared__ uint32_t lb[kMS], lc[kMS], bl[kMS];
     const uint64_t c0 = (uint64_t)blockIdx.x * kCh1, c1 = c0 + kCh1 < n ? c0 + kCh1 : n;
-    for (int i = threadIdx.x; i < kMS; i += kSBlock) lc[i] = 0;
-    __syncthreads();
-    // counting: kCL entries per thread have their loads in flight together
-    constexpr int kCL = 4;
-    for (uint64_t i0 = c0 + threadIdx.x; i0 < c1; i0 += (uint64_t)kSBlock * kCL) {
-        uint64_t a[kCL];
-        uint32_t cc[kCL];
-#pragma unroll
-        for (int q = 0; q < kCL; ++q) {
-            const uint64_t i = i0 + (uint64_t)q * kSBlock;
-            a[q] = i < c1 ? ckeys[i] : 0;
-            cc[q] = i < c1 ? ccnt[i] : 0;
-        }
-#pragma unroll
-        for (int q = 0; q < kCL; ++q) {
-            if (i0 + (uint64_t)q * kSBlock >= c1) break;
-            uint32_t bk[2];
-            uint64_t it[2];
-            const int no = msd_items(a[q], cc[q], k, bk, it);
-            for (int j = 0; j < no; ++j) atomicAdd(&lc[bk[j]], 1u);
-        }
-    }
-    __syncthreads();
     for (int i = threadIdx.x; i < kMS; i += kSBlock) {
-        const uint32_t c = lc[i];
-        lb[i] = c ? (uint32_t)(atomicAdd(&cursor[i], (unsigned long long)round8(c)) / kIL) : 0;
+        lb[i] = off[(uint64_t)blockIdx.x * kMS + i];
         lc[i] = 0;
         bl[i] = 0;
     }
@@ -537,7 +564,7 @@ __device__ __forceinline__ uint32_t msd_sub(uint64_t it, int k) {
 
 __global__ void __launch_bounds__(kBlock) k_msd2_hist(const uint64_t *in, const uint64_t *cstart, const uint32_t *clen,
                                                       const uint32_t *cbucket, int k, unsigned long long *tot,
-                                                      unsigned long long *real) {
+                                                      unsigned long long *real, uint32_t *cc) {
     __shared__ uint32_t lc[kMS];
     const uint64_t c = blockIdx.x;
     for (int i = threadIdx.x; i < kMS; i += kBlock) lc[i] = 0;
@@ -550,41 +577,29 @@ __global__ void __launch_bounds__(kBlock) k_msd2_hist(const uint64_t *in, const 
     }
     __syncthreads();
     const uint64_t fb = (uint64_t)cbucket[c] * kMS;
-    for (int i = threadIdx.x; i < kMS; i += kBlock)
+    for (int i = threadIdx.x; i < kMS; i += kBlock) {
+        cc[c * kMS + i] = lc[i];
         if (lc[i]) {
             atomicAdd(&tot[fb + i], (unsigned long long)round8(lc[i]));
             atomicAdd(&real[fb + i], (unsigned long long)lc[i]);
         }
+    }
 }
 
 __global__ void __launch_bounds__(kSBlock) k_msd2_scatter(const uint64_t *in, const uint64_t *cstart,
-                                                          const uint32_t *clen, const uint32_t *cbucket, int k,
-                                                          unsigned long long *cursor, uint64_t *out) {
+                                                          const uint32_t *clen, const uint32_t *off, int k,
+                                                          uint64_t *out) {
     __shared__ uint64_t buf[kMS * kIL];
     __shared__ uint32_t lb[kMS], lc[kMS], bl[kMS];
     const uint64_t c = blockIdx.x;
-    for (int i = threadIdx.x; i < kMS; i += kSBlock) lc[i] = 0;
-    __syncthreads();
-    const uint64_t s0 = cstart[c];
-    const uint32_t n = clen[c];
-    constexpr int kCL = 4;  // counting loads in flight per thread
-    for (uint32_t i0 = threadIdx.x; i0 < n; i0 += kSBlock * kCL) {
-        uint64_t v[kCL];
-#pragma unroll
-        for (int q = 0; q < kCL; ++q) v[q] = i0 + q * kSBlock < n ? in[s0 + i0 + q * kSBlock] : kPad;
-#pragma unroll
-        for (int q = 0; q < kCL; ++q)
-            if (v[q] != kPad) atomicAdd(&lc[msd_sub(v[q], k)], 1u);
-    }
-    __syncthreads();
-    const uint64_t fb = (uint64_t)cbucket[c] * kMS;
     for (int i = threadIdx.x; i < kMS; i += kSBlock) {
-        const uint32_t x = lc[i];
-        lb[i] = x ? (uint32_t)(atomicAdd(&cursor[fb + i], (unsigned long long)round8(x)) / kIL) : 0;
+        lb[i] = off[c * kMS + i];
         lc[i] = 0;
         bl[i] = 0;
     }
     __syncthreads();
+    const uint64_t s0 = cstart[c];
+    const uint32_t n = clen[c];
     LinePlace lp{buf, lb, lc, bl, out, 0};
     uint64_t nxt = threadIdx.x < n ? in[s0 + threadIdx.x] : kPad;
     for (uint32_t i0 = 0; i0 < n; i0 += kSBlock) {
@@ -987,39 +1002,56 @@ bool msd_sort(mcaat_ctx *ctx, const uint64_t *ckeys, const uint32_t *ccnt, uint6
               uint64_t *key, uint16_t *mult) {
     hipStream_t st = ctx->stream;
     const uint64_t nch1 = (n + kCh1 - 1) / kCh1;
-    // level 1
-    DevBuf<unsigned long long> tot1(kMS + 1), cur1(kMS + 1);
+    // level 1: per-chunk counts -> per-block line totals -> bucket bases -> chunk run starts
+    const uint64_t nblk1 = (nch1 + kBlkCh - 1) / kBlkCh;
+    DevBuf<uint32_t> cc1(nch1 * kMS ? nch1 * kMS : 1);
+    DevBuf<unsigned long long> blk1(nblk1 * kMS ? nblk1 * kMS : 1), tot1(kMS + 1), base1(kMS + 1);
+    HIP_OK(hipMemsetAsync(blk1.p, 0, blk1.bytes(), st));
     HIP_OK(hipMemsetAsync(tot1.p, 0, tot1.bytes(), st));
-    hipLaunchKernelGGL(k_msd1_hist, dim3((unsigned)nch1), dim3(kBlock), 0, st, ckeys, ccnt, n, k, tot1.p);
+    hipLaunchKernelGGL(k_msd1_hist, dim3((unsigned)nch1), dim3(kBlock), 0, st, ckeys, ccnt, n, k, cc1.p, blk1.p);
     LAUNCH_OK();
-    excl_scan(st, (const uint64_t *)tot1.p, (uint64_t *)cur1.p, kMS + 1);
+    hipLaunchKernelGGL(k_blk_scan, dim3(grid_for(kMS, kBlock)), dim3(kBlock), 0, st, blk1.p, nblk1, (uint64_t)kMS,
+                       tot1.p);
+    LAUNCH_OK();
+    excl_scan(st, (const uint64_t *)tot1.p, (uint64_t *)base1.p, kMS + 1);  // in lines
+    hipLaunchKernelGGL(k_chunk_off, dim3(grid_for(nblk1 * kMS, kBlock)), dim3(kBlock), 0, st, cc1.p, nch1,
+                       (uint64_t)kMS, (const unsigned long long *)blk1.p, (const unsigned long long *)base1.p,
+                       (const uint64_t *)nullptr, (uint64_t)0, 0);
+    LAUNCH_OK();
     std::vector<uint64_t> off1(kMS + 1);
-    HIP_OK(hipMemcpyAsync(off1.data(), cur1.p, 8 * (kMS + 1), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(off1.data(), base1.p, 8 * (kMS + 1), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
+    for (auto &x : off1) x *= kIL;  // lines -> items
     DevBuf<uint64_t> l1(off1[kMS] ? off1[kMS] : 1);
-    hipLaunchKernelGGL(k_msd1_scatter, dim3((unsigned)nch1), dim3(kSBlock), 0, st, ckeys, ccnt, n, k, cur1.p, l1.p);
+    hipLaunchKernelGGL(k_msd1_scatter, dim3((unsigned)nch1), dim3(kSBlock), 0, st, ckeys, ccnt, n, k,
+                       (const uint32_t *)cc1.p, l1.p);
     LAUNCH_OK();
-    // level 2
-    std::vector<uint64_t> cstart;
+    blk1.release();
+    // level 2: chunks of each level-1 bucket (consecutive), per-chunk sub counts
+    std::vector<uint64_t> cstart, seg_first(kMS + 1);
     std::vector<uint32_t> clen, cbk;
-    for (int b = 0; b < kMS; ++b)
+    for (int b = 0; b < kMS; ++b) {
+        seg_first[b] = cstart.size();
         for (uint64_t o = off1[b]; o < off1[b + 1]; o += kCh2) {
             cstart.push_back(o);
             clen.push_back((uint32_t)std::min<uint64_t>(kCh2, off1[b + 1] - o));
             cbk.push_back((uint32_t)b);
         }
+    }
+    seg_first[kMS] = cstart.size();
     const uint64_t nch2 = cstart.size(), NB = (uint64_t)kMS * kMS;
-    DevBuf<uint64_t> dcs(nch2 ? nch2 : 1);
-    DevBuf<uint32_t> dcl(nch2 ? nch2 : 1), dcb(nch2 ? nch2 : 1);
+    DevBuf<uint64_t> dcs(nch2 ? nch2 : 1), dseg(kMS + 1);
+    DevBuf<uint32_t> dcl(nch2 ? nch2 : 1), dcb(nch2 ? nch2 : 1), cc2(nch2 * kMS ? nch2 * kMS : 1);
     DevBuf<unsigned long long> tot2(NB + 1), real2(NB + 1), cur2(NB + 1), base3(NB + 1);
     HIP_OK(hipMemcpyAsync(dcs.p, cstart.data(), 8 * nch2, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(dcl.p, clen.data(), 4 * nch2, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(dcb.p, cbk.data(), 4 * nch2, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(dseg.p, seg_first.data(), 8 * (kMS + 1), hipMemcpyHostToDevice, st));
     HIP_OK(hipMemsetAsync(tot2.p, 0, tot2.bytes(), st));
     HIP_OK(hipMemsetAsync(real2.p, 0, real2.bytes(), st));
     if (nch2) {
         hipLaunchKernelGGL(k_msd2_hist, dim3((unsigned)nch2), dim3(kBlock), 0, st, l1.p, dcs.p, dcl.p, dcb.p, k,
-                           tot2.p, real2.p);
+                           tot2.p, real2.p, cc2.p);
         LAUNCH_OK();
     }
     excl_scan(st, (const uint64_t *)tot2.p, (uint64_t *)cur2.p, NB + 1);
@@ -1029,12 +1061,17 @@ bool msd_sort(mcaat_ctx *ctx, const uint64_t *ckeys, const uint32_t *ccnt, uint6
     HIP_OK(hipMemcpyAsync(&nreal, base3.p + NB, 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
     if (nreal != D) throw Error(MCAAT_E_CAPACITY, "msd_sort: item count mismatch");
+    if (n2 / kIL >= (1ull << 32)) throw Error(MCAAT_E_CAPACITY, "msd_sort: 2^32 or more lines");
     DevBuf<uint64_t> off2(NB + 1);
     HIP_OK(hipMemcpyAsync(off2.p, cur2.p, 8 * (NB + 1), hipMemcpyDeviceToDevice, st));
     DevBuf<uint64_t> l2(n2 ? n2 : 1);
     if (nch2) {
-        hipLaunchKernelGGL(k_msd2_scatter, dim3((unsigned)nch2), dim3(kSBlock), 0, st, l1.p, dcs.p, dcl.p, dcb.p, k,
-                           cur2.p, l2.p);
+        hipLaunchKernelGGL(k_chunk_off, dim3(grid_for(NB, kBlock)), dim3(kBlock), 0, st, cc2.p, nch2, (uint64_t)kMS,
+                           (const unsigned long long *)nullptr, (const unsigned long long *)cur2.p,
+                           (const uint64_t *)dseg.p, (uint64_t)kMS, 1);
+        LAUNCH_OK();
+        hipLaunchKernelGGL(k_msd2_scatter, dim3((unsigned)nch2), dim3(kSBlock), 0, st, l1.p, dcs.p, dcl.p,
+                           (const uint32_t *)cc2.p, k, l2.p);
         LAUNCH_OK();
     }
     l1.release();
