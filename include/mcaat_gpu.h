@@ -301,6 +301,10 @@ void mcaat_reset_timing(mcaat_ctx *ctx);
  *   sort.mid_counting  0: level-3 buckets above the one-wave limit by the 256-thread bitonic
  *                      network (default 1: the 256-thread LDS counting sort)
  *   sort.mid_occ       5: that counting sort at five workgroups per CU (default 4)
+ *   sort.small_mid     1: a 128-thread counting-sort stage for level-3 buckets of up to 1024
+ *                      items before the 256-thread one, 0: none (default: when D / 2^22 <= 768)
+ *   sort.small_limit   largest bucket that stage sorts (default and maximum 1024; larger ones
+ *                      are forwarded)
  *   cf.scan_u          64-edge words in flight per wave in the tips/filter and recount scans
  *                      (1, 2 default, 4)
  *   cf.prep_batch      edges per thread in flight in the peel's prep pass (2 default, 4, 8, 16)
@@ -319,10 +323,13 @@ void mcaat_reset_timing(mcaat_ctx *ctx);
  *                      start-candidate list (regrowth test knobs)
  *   fq.hostpack        0: FASTQ always through the GPU text parser (default 1: plain files of
  *                      upper-case ACGT 4-line records packed to 2 bits by host threads first)
- *   sdbg.adj_lds       0: adjacency by per-edge directory searches in global memory
- *                      (default 1: per-run target key ranges staged in LDS)
- *   sdbg.adj_cap       largest target key range staged in LDS (default and maximum 1024;
- *                      larger ranges take the global search) */
+ *   sdbg.adj_lds       0: adjacency by per-edge directory searches in global memory;
+ *                      1 (default): group-aligned runs that own disjoint in_info slot ranges,
+ *                      staged in LDS and written once; 2: per-run target key ranges in LDS with
+ *                      in_info stored from the predecessor side (round 2)
+ *   sdbg.adj_cap       mode 1: most owned slots a run stages in LDS (default and maximum 3072;
+ *                      a larger run clears its slots and writes them directly); mode 2: largest
+ *                      target key range staged (maximum 1024) */
 int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value);
 
 #ifdef __cplusplus

@@ -385,6 +385,7 @@ constexpr uint32_t kCh1 = 32768;      // canonical entries per level-1 chunk (<=
 constexpr uint32_t kCh2 = 65536;      // items per level-2 chunk
 constexpr int kWaveSort = 512;        // largest level-3 bucket sorted by one wave
 constexpr int kMidSort = 2048;        // largest sorted by a 256-thread workgroup (16 KB)
+constexpr int kSmallMid = 1024;       // largest sorted by a 128-thread workgroup (8 KB)
 constexpr int kBlockSort = 16384;     // largest sorted by a 1024-thread workgroup (128 KB)
 
 __device__ __forceinline__ uint32_t round8(uint32_t x) { return (x + kIL - 1) & ~(uint32_t)(kIL - 1); }
@@ -1097,7 +1098,28 @@ bool msd_sort(mcaat_ctx *ctx, const uint64_t *ckeys, const uint32_t *ccnt, uint6
         DevBuf<unsigned long long> nbig2(1);
         HIP_OK(hipMemsetAsync(nbig2.p, 0, 8, st));
         const uint32_t mid_limit = (uint32_t)std::min<int64_t>(kMidSort, knob(ctx, "sort.mid_limit", kMidSort));
-        if (knob(ctx, "sort.mid_counting", 1)) {
+        // buckets of <= 1024 items by 128-thread workgroups first (12 KB of LDS, two-wave
+        // barriers, eight resident per CU), the larger ones forwarded; by default only where the
+        // average level-3 bucket is small enough for that stage to take most of them (C2: D / 2^22
+        // ~ 570, sdbg_build 97.4 -> 92.8 ms; C5 ~ 935: 152.8 -> 179.6, so not there)
+        const int64_t small_knob = knob(ctx, "sort.small_mid", -1);
+        const bool small = small_knob >= 0 ? small_knob != 0 : D / NB <= 768;
+        if (small && knob(ctx, "sort.mid_counting", 1) && mid_limit >= kSmallMid) {
+            DevBuf<uint32_t> big1(hb);
+            DevBuf<unsigned long long> nbig1(1);
+            HIP_OK(hipMemsetAsync(nbig1.p, 0, 8, st));
+            hipLaunchKernelGGL((k_msd3_count<128, kSmallMid, 4>), dim3((unsigned)std::min<uint64_t>(hb, (uint64_t)ctx->n_cu * 8)),
+                               dim3(128), 0, st, l2.p, off2.p, (const uint64_t *)real2.p, (const uint64_t *)base3.p, k,
+                               big.p, (uint64_t)hb, key, mult, big1.p, nbig1.p,
+                               (uint32_t)std::min<int64_t>(kSmallMid, knob(ctx, "sort.small_limit", kSmallMid)));
+            LAUNCH_OK();
+            HIP_OK(hipMemcpyAsync(&hb, nbig1.p, 8, hipMemcpyDeviceToHost, st));
+            HIP_OK(hipStreamSynchronize(st));
+            HIP_OK(hipMemcpyAsync(big.p, big1.p, 4 * hb, hipMemcpyDeviceToDevice, st));
+        }
+        if (!hb) {
+            // every listed bucket was sorted above
+        } else if (knob(ctx, "sort.mid_counting", 1)) {
             // 24 KB of LDS per workgroup; the registers (125) allow four per CU (`sort.mid_occ=5`: five, at 96 registers with spills; C2 2 ms slower)
             if (knob(ctx, "sort.mid_occ", 4) >= 5)
                 hipLaunchKernelGGL((k_msd3_count<256, kMidSort, 5>), dim3((unsigned)std::min<uint64_t>(hb, (uint64_t)ctx->n_cu * 5)),

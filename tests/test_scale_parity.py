@@ -52,6 +52,10 @@ KNOBS = {
     "sort_mid": {"sort.msd": 1, "sort.wave_limit": 0},
     "sort_mid_bitonic": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_counting": 0},
     "sort_mid_occ5": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_occ": 5},
+    # the 128-thread level-3 stage forwarding everything to the 256-thread one, and skipped
+    "sort_small_fwd": {"sort.msd": 1, "sort.wave_limit": 0, "sort.small_mid": 1, "sort.small_limit": 0},
+    "sort_small_on": {"sort.msd": 1, "sort.wave_limit": 0, "sort.small_mid": 1},
+    "sort_small_off": {"sort.msd": 1, "sort.wave_limit": 0, "sort.small_mid": 0},
     # the scans with four 64-edge words in flight per wave, the peel prep with eight edges
     "scan_u4_prep8": {"cf.scan_u": 4, "cf.prep_batch": 8},
     "scan_u1_prep16": {"cf.scan_u": 1, "cf.prep_batch": 16},
