@@ -317,6 +317,11 @@ void mcaat_reset_timing(mcaat_ctx *ctx);
  *   cf.ruler_mask      1 in (mask + 1) unary nodes is a peel ruler besides the chain heads
  *   cf.fused_init      0: the peel's first pass as its own kernel (default 1: done by the tips /
  *                      multiplicity-filter pass)
+ *   cf.recount         1: the valid / tips recount and ChunkStartNodes' candidate filter as
+ *                      their own pass after the peel (default 0: the tips / filter pass lists the
+ *                      post-filter candidates and counts the post-filter tips that are not
+ *                      seeds; after the peel the candidates still valid are kept and the valid
+ *                      bits are popcounted)
  *   cf.peel_list_div   first ruler-list capacity D / div (default 16; the prep pass runs again
  *                      with the counted size when it overflows)
  *   cf.peel_list_cap / cf.cand_cap   first capacity of the ruler and branch lists / of the

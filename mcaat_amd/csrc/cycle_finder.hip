@@ -95,15 +95,24 @@ struct WaveList {
 // streaming pass over out_info and the filtered bitmap.
 // words [w_lo, w_hi) of the bitmaps (a rank's share; all of them on one GPU); tip_bm / post
 // are indexed from w_lo
+// With a candidate list (cand != nullptr) the pass also does the recount's work on the
+// post-filter graph (round 3): counts[2] post-filter tips that are not seeds (every one of them
+// survives the peel, and no surviving edge becomes a tip: the reduction removes every valid edge
+// whose successors it all removed), and ChunkStartNodes' filter on post-filter validity
+// (valid, mult > thr, at least two valid in-edges, not its own in-edge) into cand (counts[3]
+// counts them all). A removed edge had no valid successor, so the peel changes no surviving
+// edge's valid in-edges: the final candidates are these, still valid after the peel.
 template <int kScanU>
 __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_lo, uint64_t w_hi, uint64_t *tip_bm,
                                                         uint64_t *post, unsigned long long *counts, uint8_t *nf,
-                                                        uint64_t *nxk) {
+                                                        uint64_t *nxk, uint64_t thr, uint64_t *cand, uint64_t cap) {
     const int lane = threadIdx.x & 63;
     const uint64_t nw = (g.D + 63) / 64;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    const bool peel = nf != nullptr;
-    unsigned long long acc = 0, low_n = 0;
+    const bool peel = nf != nullptr, fold = cand != nullptr;
+    __shared__ uint64_t cbuf[kBlock / 64][128];
+    WaveList cl{cbuf[threadIdx.x >> 6], cand, counts + 3, cap};
+    unsigned long long acc = 0, low_n = 0, tips_pf = 0;
     for (uint64_t wb = w_lo + (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); wb < w_hi; wb += kScanU * wstride) {
         uint64_t sv[kScanU], oi[kScanU];
         WordPair a[kScanU];
@@ -116,11 +125,21 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_
             oi[u] = e < g.D && w < w_hi ? g.out_info[e] : 0;
             mu[u] = e < g.D && w < w_hi ? g.mult[e] : 0xFFFFu;
         }
+        uint64_t ii[kScanU];
+        WordPair b[kScanU];
+#pragma unroll
+        for (int u = 0; u < kScanU; ++u) {
+            const uint64_t w = wb + u * wstride, e = w * 64 + lane;
+            // the candidate filter's in-edge window, for post-filter valid edges above thr
+            const bool cv = fold && e < g.D && w < w_hi && ((sv[u] >> lane) & 1) && mu[u] > 1 && (uint64_t)mu[u] > thr;
+            ii[u] = cv ? g.in_info[e] : 0;
+        }
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
             const uint64_t lo = oi[u] & kIdxMask;
             a[u] = word_pair(g.valid, lo, nw);
-            if (peel) mult4(g.mult, lo, sm[u]);  // entries past cnt are masked by pre below
+            if (peel || fold) mult4(g.mult, lo, sm[u]);  // entries past cnt are masked by pre below
+            if (fold) b[u] = word_pair(g.valid, ii[u] & kIdxMask, nw);
         }
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
@@ -136,6 +155,29 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_
                 post[w - w_lo] = sv[u] & ~lowm;
                 acc += __popcll(m);
                 low_n += __popcll(lowm);
+            }
+            if (fold) {
+                const bool vpf = e < g.D && w < w_hi && ((sv[u] >> lane) & 1) && mu[u] > 1;  // valid after the filter
+                unsigned pfo = 0;  // successors valid after the filter
+                for (int i = 0; i < (int)cnt; ++i)
+                    if (((pre >> i) & 1) && sm[u][i] > 1) pfo |= 1u << i;
+                // a post-filter tip that is not a seed (t: a pre-filter tip, i.e. a seed)
+                const unsigned long long tpm = __ballot(vpf && pfo == 0 && !t);
+                if (lane == 0) tips_pf += __popcll(tpm);
+                bool c = false;
+                if (vpf && (uint64_t)mu[u] > thr) {
+                    const uint64_t l = ii[u] & kIdxMask;
+                    unsigned in = bits16(b[u].a, b[u].b, l) & (uint32_t)((ii[u] >> kIdxBits) & 0xFFFF);  // pre-filter valid in-edges
+                    unsigned im = in;
+                    while (im) {  // at most four: drop the ones the filter invalidates
+                        const int j = __ffs(im) - 1;
+                        im &= im - 1;
+                        if (g.mult[l + j] <= 1) in &= ~(1u << j);
+                    }
+                    const bool self = e >= l && e - l < 16 && ((in >> (e - l)) & 1);
+                    c = __popc(in) >= 2 && !self;
+                }
+                cl.push(c, e);
             }
             if (peel && e < g.D && w < w_hi) {
                 if (!((sv[u] >> lane) & 1) || mu[u] <= 1) {
@@ -156,8 +198,25 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_
             }
         }
     }
+    if (fold) cl.finish();
     block_add(counts, acc);
     block_add(counts + 1, low_n);
+    block_add(counts + 2, tips_pf);
+}
+
+// popcount of bitmap words [w_lo, w_hi)
+__global__ void __launch_bounds__(kBlock) k_popcount(const uint64_t *bm, uint64_t w_lo, uint64_t w_hi,
+                                                     unsigned long long *out) {
+    unsigned long long c = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t w = w_lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < w_hi; w += stride) c += __popcll(bm[w]);
+    block_add(out, c);
+}
+
+// the candidates still valid (flags for select_flagged)
+__global__ void __launch_bounds__(kBlock) k_still_valid(const uint64_t *bm, const uint64_t *ids, uint64_t n, uint8_t *f) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) f[i] = bit_get(bm, ids[i]);
 }
 
 // the recount after the reduction (valid edges, tips) and ChunkStartNodes' candidate filter in
@@ -1932,11 +1991,21 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
         HIP_OK(hipMemsetAsync(ps.nf.p, 0, ps.nf.bytes(), st));
         ps.ready = true;
     }
+    // the recount's counts and ChunkStartNodes' filter come from the tips / filter pass
+    // (cf.recount = 1: the separate post-peel pass of round 2)
+    const bool fold = knob(ctx, "cf.recount", 0) == 0;
+    const uint64_t c_lo = std::min<uint64_t>(D, 64 * w_lo), c_hi = std::min<uint64_t>(D, 64 * w_hi);
+    uint64_t ccap = std::min<uint64_t>(c_hi - c_lo, (c_hi - c_lo) / 64 + (1u << 20));
+    if (knob_set(ctx, "cf.cand_cap")) ccap = (uint64_t)std::max<int64_t>(1, knob(ctx, "cf.cand_cap", 1));  // test knob
+    DevBuf<uint64_t> clist;
+    uint64_t n_cand = 0, tips_after = 0;
     {
         DevBuf<uint64_t> post(mcaat_graph::bitmap_words(D));
         HIP_OK(hipMemsetAsync(post.p + nw, 0, 8, st));  // the padding word
-        DevBuf<unsigned long long> c2(2);
-        HIP_OK(hipMemsetAsync(c2.p, 0, 16, st));
+        DevBuf<unsigned long long> c2(4);
+      for (;;) {
+        if (fold) clist.alloc(ccap ? ccap : 1);
+        HIP_OK(hipMemsetAsync(c2.p, 0, 32, st));
         DevBuf<uint64_t> mseeds, mpost;  // this rank's words when the bitmaps are gathered
         if (comm) {
             mseeds.alloc(w_hi - w_lo);
@@ -1946,12 +2015,19 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
             auto kern = scan_u == 1 ? k_tips_filter<1> : scan_u == 4 ? k_tips_filter<4> : k_tips_filter<kScanUDefault>;
             hipLaunchKernelGGL(kern, dim3(wgrid), dim3(kBlock), 0, st, v, w_lo, w_hi, comm ? mseeds.p : seeds.p,
                                comm ? mpost.p : post.p, c2.p, fuse ? ps.nf.p : (uint8_t *)nullptr,
-                               fuse ? ps.nxk.p : (uint64_t *)nullptr);
+                               fuse ? ps.nxk.p : (uint64_t *)nullptr, (uint64_t)p.threshold_multiplicity,
+                               fold ? clist.p : (uint64_t *)nullptr, ccap);
             LAUNCH_OK();
         }
-        unsigned long long hc[2];
-        HIP_OK(hipMemcpyAsync(hc, c2.p, 16, hipMemcpyDeviceToHost, st));
+        unsigned long long hc[4];
+        HIP_OK(hipMemcpyAsync(hc, c2.p, 32, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
+        if (fold && hc[3] > ccap) {  // more candidates than the list held: the pass again (idempotent), sized
+            ccap = hc[3];
+            continue;
+        }
+        n_cand = fold ? hc[3] : 0;
+        tips_after = hc[2];
         if (comm) {
             std::vector<uint64_t> sz(N);
             for (int r = 0; r < N; ++r) sz[r] = 8 * (nw * (uint64_t)(r + 1) / N - nw * (uint64_t)r / N);
@@ -1965,6 +2041,8 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
         out->stats[1] = hc[1];
         std::swap(g->valid, post);  // the pre-filter bitmap is released here
         v = g->view();
+        break;
+      }
     }
     timer.mark("tips_filter");
     verbose_mark(ctx, "cf.tips_filter");
@@ -1980,7 +2058,42 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
     // cleared every mult <= 1 edge and nothing since sets a valid bit, and the count it would
     // print is stats[1], every mult <= 1 edge, valid or not)
     std::vector<uint64_t> cand;
-    {
+    if (fold) {
+        // valid count: a popcount of this rank's words; tips: the post-filter tips that were
+        // not seeds (tips pass); candidates: the listed ones still valid, in ascending id order
+        DevBuf<unsigned long long> c1(1);
+        HIP_OK(hipMemsetAsync(c1.p, 0, 8, st));
+        if (w_hi > w_lo) {
+            hipLaunchKernelGGL(k_popcount, dim3(wgrid), dim3(kBlock), 0, st, (const uint64_t *)g->valid.p, w_lo, w_hi, c1.p);
+            LAUNCH_OK();
+        }
+        out->stats[2] = read_counter(ctx, c1.p);
+        out->stats[3] = tips_after;  // this rank's words (summed over the ranks below)
+        if (n_cand) {
+            DevBuf<uint8_t> fl(n_cand);
+            DevBuf<uint64_t> kept(n_cand), sorted(n_cand);
+            DevBuf<unsigned long long> nk(1);
+            hipLaunchKernelGGL(k_still_valid, dim3(grid_for(n_cand, kBlock)), dim3(kBlock), 0, st, (const uint64_t *)g->valid.p,
+                               (const uint64_t *)clist.p, n_cand, fl.p);
+            LAUNCH_OK();
+            size_t tmp = 0;
+            HIP_OK(hipcub::DeviceSelect::Flagged(nullptr, tmp, clist.p, fl.p, kept.p, nk.p, (size_t)n_cand, st));
+            {
+                DevBuf<uint8_t> t(tmp);
+                HIP_OK(hipcub::DeviceSelect::Flagged(t.p, tmp, clist.p, fl.p, kept.p, nk.p, (size_t)n_cand, st));
+            }
+            const uint64_t nkept = read_counter(ctx, nk.p);
+            cand.resize(nkept);
+            if (nkept) {
+                tmp = 0;
+                HIP_OK(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, kept.p, sorted.p, (size_t)nkept, 0, 40, st));
+                DevBuf<uint8_t> t(tmp);
+                HIP_OK(hipcub::DeviceRadixSort::SortKeys(t.p, tmp, kept.p, sorted.p, (size_t)nkept, 0, 40, st));
+                d2h(ctx, cand.data(), sorted.p, 8 * nkept);
+            }
+        }
+        clist.release();
+    } else {
         // rank R takes the candidates among its words' ids, and counts over its words
         const uint64_t lo = std::min<uint64_t>(D, 64 * w_lo), hi = std::min<uint64_t>(D, 64 * w_hi);
         uint64_t cap = std::min<uint64_t>(hi - lo, (hi - lo) / 64 + (1u << 20));

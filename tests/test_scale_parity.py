@@ -81,6 +81,9 @@ KNOBS = {
     # the ruler / branch lists and the candidate list start with one entry: the passes that
     # fill them run again with the counted sizes
     "list_regrow": {"cf.peel_list_cap": 1, "cf.cand_cap": 1},
+    # the round-2 recount pass after the peel instead of the tips-pass fold, and with regrowth
+    "recount_pass": {"cf.recount": 1},
+    "recount_pass_regrow": {"cf.recount": 1, "cf.cand_cap": 1},
     # the peel's first pass as its own kernel instead of inside the tips / filter pass
     "peel_own_init": {"cf.fused_init": 0},
     # passes B and C of successive groups in turn on one stream
