@@ -627,9 +627,12 @@ __device__ __forceinline__ void chunk_hist(const uint16_t *__restrict__ sub, uin
     }
 }
 
+// (round 3) each chunk's sub counts are also kept (cc[c][i]); k_chunk_runs turns them into the
+// chunk's run start per sub, so k_l2_scatter needs neither a counting pass over the chunk's sub
+// rows nor one cursor atomic per (chunk, sub)
 __global__ void __launch_bounds__(kBThreads) k_l2_hist(const uint16_t *__restrict__ sub, const uint64_t *chunk_start,
                                                        const uint32_t *chunk_len, const uint32_t *chunk_bucket,
-                                                       int l2_bits, unsigned long long *tot) {
+                                                       int l2_bits, unsigned long long *tot, uint32_t *cc) {
     extern __shared__ uint32_t lh[];
     const uint32_t S = 1u << l2_bits;
     const uint64_t c = blockIdx.x;
@@ -638,8 +641,25 @@ __global__ void __launch_bounds__(kBThreads) k_l2_hist(const uint16_t *__restric
     chunk_hist(sub, chunk_start[c], chunk_len[c], lh);
     __syncthreads();
     const uint64_t fb = (uint64_t)chunk_bucket[c] * S;
-    for (uint32_t i = threadIdx.x; i < S; i += kBThreads)
+    for (uint32_t i = threadIdx.x; i < S; i += kBThreads) {
+        cc[c * S + i] = lh[i];
         if (lh[i]) atomicAdd(&tot[fb + i], (unsigned long long)round4(lh[i]));
+    }
+}
+
+// chunk run starts in lines, in place of the chunk counts: one thread per (L1 bucket, sub) walks
+// the bucket's chunks from the sub's fine-partition base
+__global__ void __launch_bounds__(256) k_chunk_runs(uint32_t *cc, const uint64_t *bchunk, const uint64_t *fine,
+                                                    uint32_t S) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= 256ull * S) return;
+    const uint64_t b = t / S, i = t % S;
+    uint64_t run = fine[t] / kLG;
+    for (uint64_t c = bchunk[b]; c < bchunk[b + 1]; ++c) {
+        const uint32_t x = cc[c * S + i];
+        cc[c * S + i] = (uint32_t)run;
+        run += round4(x) / kLG;
+    }
 }
 
 // Each sub keeps one 64-B line (4 descriptors) of its run in LDS; the lane that completes
@@ -657,29 +677,22 @@ constexpr int kBPF = MCAAT_BPF;  // rounds of descriptor loads in flight
 __global__ void __launch_bounds__(kBThreads) k_l2_scatter(const uint4 *__restrict__ data,
                                                           const uint16_t *__restrict__ sub,
                                                           const uint64_t *chunk_start, const uint32_t *chunk_len,
-                                                          const uint32_t *chunk_bucket, int l2_bits,
-                                                          unsigned long long *cursor, uint4 *__restrict__ out,
-                                                          uint64_t gbase) {
+                                                          const uint32_t *runs, int l2_bits,
+                                                          uint4 *__restrict__ out, uint64_t gbase) {
     __shared__ uint4 buf[kMaxSub * kLG];
     __shared__ uint32_t lb[kMaxSub];  // this workgroup's run of each sub, in lines
-    __shared__ uint32_t lc[kMaxSub];  // descriptors per sub: counted, then placed
+    __shared__ uint32_t lc[kMaxSub];  // descriptors per sub placed so far
     __shared__ uint32_t bl[kMaxSub];  // line of the run held in buf
     const uint32_t S = 1u << l2_bits;
-    const uint64_t c = blockIdx.x;
-    for (uint32_t i = threadIdx.x; i < S; i += kBThreads) lc[i] = 0;
-    __syncthreads();
-    const uint64_t s0 = chunk_start[c];
-    const uint32_t n = chunk_len[c];
-    chunk_hist(sub, s0, n, lc);
-    __syncthreads();
-    const uint64_t fb = (uint64_t)chunk_bucket[c] * S;
+    const uint64_t c = blockIdx.x;  // (chunk index relative to the launch's first chunk: runs is offset to match)
     for (uint32_t i = threadIdx.x; i < S; i += kBThreads) {
-        const uint32_t k = lc[i];
-        lb[i] = k ? (uint32_t)(atomicAdd(&cursor[fb + i], (unsigned long long)round4(k)) / kLG) : 0;
+        lb[i] = runs[c * S + i];
         lc[i] = 0;
         bl[i] = 0;
     }
     __syncthreads();
+    const uint64_t s0 = chunk_start[c];
+    const uint32_t n = chunk_len[c];
     // one descriptor per thread per round, the next kBPF rounds' already in flight
     uint32_t v[kBPF];
     uint4 d[kBPF];
@@ -1463,23 +1476,32 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     bchunk[256] = cstart.size();
     const uint64_t nch = cstart.size();
     DevBuf<uint64_t> dcs(nch ? nch : 1), dfine(F + 1);
-    DevBuf<unsigned long long> dtot(F + 1), dcursor(F + 1);
+    DevBuf<unsigned long long> dtot(F + 1);
     DevBuf<uint32_t> dcl(nch ? nch : 1), dcb(nch ? nch : 1);
     HIP_OK(hipMemcpyAsync(dcs.p, cstart.data(), 8 * nch, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(dcl.p, clen.data(), 4 * nch, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(dcb.p, cbucket.data(), 4 * nch, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemsetAsync(dtot.p, 0, dtot.bytes(), st));
     std::vector<uint64_t> hfine(F + 1);
+    DevBuf<uint32_t> druns(nch * S ? nch * S : 1);  // per chunk and sub: count, then run start (lines)
     {
         KernelTimer kt(ctx, "l2_hist", 2.0 * (double)n_desc);
         if (nch) {
             hipLaunchKernelGGL(k_l2_hist, dim3((unsigned)nch), dim3(kBThreads), 4 * S, st, l1s.p, dcs.p, dcl.p, dcb.p,
-                               P.l2_bits, dtot.p);
+                               P.l2_bits, dtot.p, druns.p);
             LAUNCH_OK();
         }
         exclusive_scan(ctx, (const uint64_t *)dtot.p, dfine.p, F + 1);
-        HIP_OK(hipMemcpyAsync(dcursor.p, dfine.p, 8 * (F + 1), hipMemcpyDeviceToDevice, st));
         d2h(ctx, hfine.data(), dfine.p, 8 * (F + 1));
+        if (hfine[F] / kLG >= (1ull << 32)) throw Error(MCAAT_E_CAPACITY, "node_counter: 2^32 or more fine-partition lines");
+        if (nch) {
+            DevBuf<uint64_t> dbch(257);
+            HIP_OK(hipMemcpyAsync(dbch.p, bchunk.data(), 8 * 257, hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(k_chunk_runs, dim3(grid_for(256ull * S, 256)), dim3(256), 0, st, druns.p,
+                               (const uint64_t *)dbch.p, (const uint64_t *)dfine.p, S);
+            LAUNCH_OK();
+            HIP_OK(hipStreamSynchronize(st));  // dbch is freed on scope exit
+        }
         kt.stop();
     }
     const uint64_t n_live = hfine[F];
@@ -1537,7 +1559,7 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
         auto *kt = new KernelTimer(ctx, "l2_partition", 34.0 * (double)gn, sb);  // sub rows + descriptors read, descriptors written
         if (c1 > c0) {
             hipLaunchKernelGGL(k_l2_scatter, dim3((unsigned)(c1 - c0)), dim3(kBThreads), 0, sb, l1.p, l1s.p,
-                               dcs.p + c0, dcl.p + c0, dcb.p + c0, P.l2_bits, dcursor.p, g.fine.p, gbase);
+                               dcs.p + c0, dcl.p + c0, (const uint32_t *)druns.p + c0 * S, P.l2_bits, g.fine.p, gbase);
             LAUNCH_OK();
         }
         kt->mark();
