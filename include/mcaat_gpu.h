@@ -322,6 +322,8 @@ void mcaat_reset_timing(mcaat_ctx *ctx);
  *                      post-filter candidates and counts the post-filter tips that are not
  *                      seeds; after the peel the candidates still valid are kept and the valid
  *                      bits are popcounted)
+ *   cf.dls_host        1: DepthLevelSearch candidates and results through the host (default 0:
+ *                      on one GPU they stay on the device and only the passing ids come back)
  *   cf.peel_list_div   first ruler-list capacity D / div (default 16; the prep pass runs again
  *                      with the counted size when it overflows)
  *   cf.peel_list_cap / cf.cand_cap   first capacity of the ruler and branch lists / of the

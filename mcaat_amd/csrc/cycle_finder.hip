@@ -1586,6 +1586,95 @@ static std::vector<uint64_t> run_dls(mcaat_graph *g, const std::vector<uint64_t>
     return pass;
 }
 
+__global__ void __launch_bounds__(kBlock) k_iota(uint64_t *x, uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] = i;
+}
+__global__ void __launch_bounds__(kBlock) k_gather_ids(const uint64_t *cand, const uint64_t *idx, uint64_t n, uint64_t *out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) out[i] = cand[idx[i]];
+}
+__global__ void __launch_bounds__(kBlock) k_scatter_res(const int8_t *r, const uint64_t *idx, uint64_t n, int8_t *res,
+                                                        uint8_t *ovf) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        res[idx[i]] = r[i];
+        ovf[i] = r[i] < 0;
+    }
+}
+__global__ void __launch_bounds__(kBlock) k_res_pass(const int8_t *res, uint64_t n, uint8_t *f) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) f[i] = res[i] == 1;
+}
+
+template <class T>
+static uint64_t select_dev(mcaat_ctx *ctx, const T *in, const uint8_t *flags, uint64_t n, T *out) {
+    hipStream_t st = ctx->stream;
+    DevBuf<unsigned long long> num(1);
+    size_t tmp = 0;
+    HIP_OK(hipcub::DeviceSelect::Flagged(nullptr, tmp, in, flags, out, num.p, (size_t)n, st));
+    DevBuf<uint8_t> t(tmp);
+    HIP_OK(hipcub::DeviceSelect::Flagged(t.p, tmp, in, flags, out, num.p, (size_t)n, st));
+    return read_counter(ctx, num.p);
+}
+
+// DepthLevelSearch over candidates already on the device (ascending ids; one GPU): the same
+// searches, batches and x8 scratch regrowth as run_dls, with the overflowed candidates and the
+// passing ids selected on the device, so only the passing ids cross to the host (C5: 3.8M
+// candidate ids went to the host and back, and their results were looped over there)
+static std::vector<uint64_t> run_dls_dev(mcaat_graph *g, const uint64_t *dcand, uint64_t n, int limit) {
+    mcaat_ctx *ctx = g->ctx;
+    hipStream_t st = ctx->stream;
+    std::vector<uint64_t> pass;
+    if (!n) return pass;
+    const bool many = n * 8ULL * (1024 + 2048) > (8ULL << 30);
+    uint32_t cs = (uint32_t)std::max<int64_t>(1, knob(ctx, "cf.dls_stack", many ? 128 : 1024));
+    uint32_t cv = (uint32_t)next_pow2((uint64_t)std::max<int64_t>(2, knob(ctx, "cf.dls_visited", many ? 256 : 2048)));
+    const int lanes = (int)std::max<int64_t>(1, std::min<int64_t>(64, knob(ctx, "cf.dls_lanes", 16)));
+    DevBuf<int8_t> res(n);
+    DevBuf<uint64_t> idx(n), idx2(n), ids(n);
+    DevBuf<uint8_t> flags(n);
+    hipLaunchKernelGGL(k_iota, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, idx.p, n);
+    LAUNCH_OK();
+    uint64_t nt = n;
+    for (bool first = true; nt; first = false) {
+        const uint64_t batch_cap = std::max<uint64_t>(64, (8ULL << 30) / (8ULL * (cs + cv)));
+        const uint64_t *src = dcand;
+        if (!first) {  // the candidates to search again, in candidate order
+            hipLaunchKernelGGL(k_gather_ids, dim3(grid_for(nt, kBlock)), dim3(kBlock), 0, st, dcand,
+                               (const uint64_t *)idx.p, nt, ids.p);
+            LAUNCH_OK();
+            src = ids.p;
+        }
+        DevBuf<int8_t> r(nt);
+        for (uint64_t b0 = 0; b0 < nt; b0 += batch_cap) {
+            const uint64_t m = std::min<uint64_t>(batch_cap, nt - b0);
+            DevBuf<uint64_t> dstk(m * cs), dvis(m * cv);
+            hipLaunchKernelGGL(k_dls, dim3(grid_for(m, (unsigned)lanes)), dim3(64), 0, st, g->view(), src + b0, m, limit,
+                               dstk.p, cs, dvis.p, cv, r.p + b0, lanes);
+            LAUNCH_OK();
+            HIP_OK(hipStreamSynchronize(st));  // the batch's scratch is freed on scope exit
+        }
+        hipLaunchKernelGGL(k_scatter_res, dim3(grid_for(nt, kBlock)), dim3(kBlock), 0, st, (const int8_t *)r.p,
+                           (const uint64_t *)idx.p, nt, res.p, flags.p);
+        LAUNCH_OK();
+        const uint64_t again = select_dev(ctx, (const uint64_t *)idx.p, flags.p, nt, idx2.p);
+        std::swap(idx, idx2);
+        nt = again;
+        if (nt) {
+            if (cs >= (1u << 26)) throw Error(MCAAT_E_CAPACITY, "DepthLevelSearch scratch exceeded 2^26 entries");
+            cs *= 8;
+            cv *= 8;
+        }
+    }
+    hipLaunchKernelGGL(k_res_pass, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, (const int8_t *)res.p, n, flags.p);
+    LAUNCH_OK();
+    const uint64_t np = select_dev(ctx, dcand, flags.p, n, ids.p);
+    pass.resize(np);
+    if (np) d2h(ctx, pass.data(), ids.p, 8 * np);
+    return pass;
+}
+
 // ---------------------------- FindCycle driver -----------------------------------
 struct FcRunner {
     mcaat_graph *g;
@@ -2058,6 +2147,9 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
     // cleared every mult <= 1 edge and nothing since sets a valid bit, and the count it would
     // print is stats[1], every mult <= 1 edge, valid or not)
     std::vector<uint64_t> cand;
+    DevBuf<uint64_t> dcand;  // one GPU, fold path: the sorted candidates stay on the device
+    uint64_t n_dcand = 0;
+    const bool dev_dls = knob(ctx, "cf.dls_host", 0) == 0;
     if (fold) {
         // valid count: a popcount of this rank's words; tips: the post-filter tips that were
         // not seeds (tips pass); candidates: the listed ones still valid, in ascending id order
@@ -2083,13 +2175,18 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
                 HIP_OK(hipcub::DeviceSelect::Flagged(t.p, tmp, clist.p, fl.p, kept.p, nk.p, (size_t)n_cand, st));
             }
             const uint64_t nkept = read_counter(ctx, nk.p);
-            cand.resize(nkept);
             if (nkept) {
                 tmp = 0;
                 HIP_OK(hipcub::DeviceRadixSort::SortKeys(nullptr, tmp, kept.p, sorted.p, (size_t)nkept, 0, 40, st));
                 DevBuf<uint8_t> t(tmp);
                 HIP_OK(hipcub::DeviceRadixSort::SortKeys(t.p, tmp, kept.p, sorted.p, (size_t)nkept, 0, 40, st));
-                d2h(ctx, cand.data(), sorted.p, 8 * nkept);
+            }
+            if (comm || !dev_dls) {
+                cand.resize(nkept);
+                if (nkept) d2h(ctx, cand.data(), sorted.p, 8 * nkept);
+            } else {  // one GPU: DepthLevelSearch straight from the device list
+                dcand = std::move(sorted);
+                n_dcand = nkept;
             }
         }
         clist.release();
@@ -2147,6 +2244,9 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
         std::vector<uint64_t> mine;
         for (size_t i = R; i < cand.size(); i += N) mine.push_back(cand[i]);
         pass = gather_sorted(comm, run_dls(g, mine, p.cycle_max_length));
+    } else if (fold && dev_dls) {
+        pass = run_dls_dev(g, dcand.p, n_dcand, p.cycle_max_length);
+        dcand.release();
     } else {
         pass = run_dls(g, cand, p.cycle_max_length);
     }

@@ -84,6 +84,9 @@ KNOBS = {
     # the round-2 recount pass after the peel instead of the tips-pass fold, and with regrowth
     "recount_pass": {"cf.recount": 1},
     "recount_pass_regrow": {"cf.recount": 1, "cf.cand_cap": 1},
+    # DepthLevelSearch through the host lists, and the device driver's scratch regrowth
+    "dls_host": {"cf.dls_host": 1},
+    "dls_dev_regrow": {"cf.dls_stack": 1, "cf.dls_visited": 2},
     # the peel's first pass as its own kernel instead of inside the tips / filter pass
     "peel_own_init": {"cf.fused_init": 0},
     # passes B and C of successive groups in turn on one stream
