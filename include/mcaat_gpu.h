@@ -136,11 +136,11 @@ int mcaat_graph_set_valid(mcaat_graph *g, const uint64_t *ids, size_t n, int val
  * counts[i] for each id; order DESCENDING for outgoing, ASCENDING for incoming. */
 int mcaat_graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, int incoming,
                           uint64_t *out, int32_t *counts);
-/* valid &= {ids}: keep_crispr_regions_extended_by_k (spacer_ordering.cpp:129-137) invalidates
- * every valid edge outside the extended cycle set; here one bitmap AND on the device. */
 /* BOSS keys and multiplicities of n edges (either output may be null): the host SDBG mirror's
  * label queries for a set of nodes (GetLabel, sdbg.h) without downloading the whole graph */
 int mcaat_graph_gather(const mcaat_graph *g, const uint64_t *ids, size_t n, uint64_t *keys, uint16_t *mult);
+/* valid &= {ids}: keep_crispr_regions_extended_by_k (spacer_ordering.cpp:129-137) invalidates
+ * every valid edge outside the extended cycle set; here one bitmap AND on the device. */
 int mcaat_graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n);
 /* Checkpoint / resume. Replaces: the on-disk graph between SDBGBuild and CycleFinder
  * (MEGAHIT graph.sdbg* + SDBG::LoadFromFile, main.cpp:386-393, 522-530). The library's own

@@ -34,11 +34,12 @@ int mcaat_host_min_cover(const uint32_t *universe, size_t n_universe, const uint
  * valid bytes after CycleFinder), the cycles (cycles_map_to_cycles order) and the relevant
  * reads (get_reads order): run_and_debug_spacer_ordering (main_run_and_debug.cpp:32-143), then
  * CRISPRAnalyzer(all_systems, output_file).run_analysis(). *n_found = found systems before the
- * analyzer's filters. The graph's valid bytes are updated in place (the reference mutates them). */
+ * analyzer's filters. The graph's valid bytes are updated in place (the reference mutates them).
+ * threads (<= 1: one) solves the independent subproblems in parallel; the output is the same. */
 int mcaat_host_crispr_arrays(int k, const uint64_t *keys, const uint16_t *mult, uint8_t *valid, uint64_t D,
                              const uint64_t *cycles_flat, const uint64_t *cycle_offsets, size_t n_cycles,
                              const uint64_t *reads_flat, const uint64_t *read_offsets, size_t n_reads,
-                             const char *output_file, size_t *n_found);
+                             const char *output_file, size_t *n_found, int threads);
 
 /* CRISPRAnalyzer alone (post_processing.h): systems given as repeats[i] with spacers
  * joined by ',' in spacers[i], inserted into the unordered_map in index order. */

@@ -458,6 +458,9 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
     std::vector<std::string> err(P);
     auto job = [&](int t) {
         try {
+            // the HIP current device is per thread: a worker's events must belong to the
+            // context's device, as its stream does
+            HIP_OK(hipSetDevice(ctx->device));
             uint64_t *s0 = (uint64_t *)ctx->pack_pinned + (size_t)t * 2 * kStageWords;
             PartPacker pk(regions.p + outs[t].region, s0, s0 + kStageWords, streams[t], outs[t]);
             const bool good = pack_part(files[parts[t].file], parts[t].b, parts[t].e, parts[t].file_end, pk, sh, outs[t]);

@@ -59,21 +59,37 @@ __global__ void __launch_bounds__(kBlock) k_count_pal(const uint64_t *ckeys, uin
 // key). A wave takes 256 consecutive edges (four coalesced loads in flight); each edge's
 // predecessor prefix comes from the neighbouring lane. Round 2 ran one binary search over all
 // D keys per prefix (C2: 2^28 searches, 9.9 ms).
+// The keys must be strictly ascending and below 2^2E (sorted unique BOSS keys): an edge that
+// breaks either sets *bad and writes nothing past dir (its prefix is clamped), and the host
+// turns the flag into MCAAT_E_INVALID.
 constexpr int kDirU = 4;
 __global__ void __launch_bounds__(kBlock) k_dir(const uint64_t *key, uint64_t D, int shift, uint64_t nprefix,
-                                                uint64_t *dir) {
+                                                uint64_t key_lim, uint64_t *dir, int *bad) {
     const int lane = threadIdx.x & 63;
     const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     for (uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c * 64 * kDirU <= D; c += nwaves) {
         const uint64_t base = c * 64 * kDirU;
+        const uint64_t kprev = base ? key[base - 1] : 0;
         uint64_t p[kDirU];
+        bool wrong = false;
 #pragma unroll
         for (int j = 0; j < kDirU; ++j) {
             const uint64_t e = base + 64 * j + lane;
-            const uint64_t x = e < D ? key[e] >> shift : nprefix;
-            p[j] = x < nprefix ? x : nprefix;  // keys are < 2^2E; clamped so a bad key cannot write past dir
+            const uint64_t kv = e < D ? key[e] : 0;
+            const uint64_t kl = __shfl_up(kv, 1);  // the predecessor's key (lanes > 0)
+            p[j] = e < D ? kv >> shift : nprefix;
+            if (e < D) wrong |= kv >= key_lim;
+            if (e < D && lane) wrong |= kv <= kl;
+            p[j] = p[j] < nprefix ? p[j] : nprefix;
         }
-        uint64_t before = base ? (key[base - 1] >> shift) + 1 : 0;  // first prefix of this chunk
+        // the first key of each 64-edge row against the last of the row before it
+#pragma unroll
+        for (int j = 0; j < kDirU; ++j) {
+            const uint64_t e = base + 64 * j;
+            if (lane == 0 && e < D && e > 0) wrong |= key[e] <= (j ? key[e - 1] : kprev);
+        }
+        if (wrong) *bad = 1;
+        uint64_t before = base ? (kprev >> shift) + 1 : 0;  // first prefix of this chunk
         before = before < nprefix + 1 ? before : nprefix + 1;
 #pragma unroll
         for (int j = 0; j < kDirU; ++j) {
@@ -1228,9 +1244,17 @@ void sdbg_finish(mcaat_ctx *ctx, mcaat_graph *g) {
     DevBuf<uint64_t> &dir = g->dir;
     dir.alloc(nprefix + 1);
     g->dir_shift = shift;
-    hipLaunchKernelGGL(k_dir, dim3(grid_for((D + kDirU) / kDirU, kBlock, (unsigned)ctx->n_cu * 16)), dim3(kBlock), 0, st,
-                       g->key.p, D, shift, nprefix, dir.p);
-    LAUNCH_OK();
+    {
+        DevBuf<int> bad(1);
+        HIP_OK(hipMemsetAsync(bad.p, 0, sizeof(int), st));
+        const uint64_t key_lim = E >= 32 ? ~0ULL : 1ULL << (2 * E);
+        hipLaunchKernelGGL(k_dir, dim3(grid_for((D + kDirU) / kDirU, kBlock, (unsigned)ctx->n_cu * 16)), dim3(kBlock), 0,
+                           st, g->key.p, D, shift, nprefix, key_lim, dir.p, bad.p);
+        LAUNCH_OK();
+        int hb = 0;
+        d2h(ctx, &hb, bad.p, sizeof(int));
+        if (hb) throw Error(MCAAT_E_INVALID, "sdbg: edge keys are not strictly ascending below 4^(k+1)");
+    }
     g->out_info.alloc(D);
     g->in_info.alloc(D);
     if (D) {

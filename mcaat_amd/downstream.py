@@ -25,7 +25,7 @@ HOST_SIGNATURES = {
     "mcaat_host_fuzz_partial_ratio": (C.c_double, [C.c_char_p, C.c_char_p]),
     "mcaat_host_min_cover": (C.c_int, [_u32p, C.c_size_t, _u32p, _u64p, C.c_size_t, _u64p, C.POINTER(C.c_size_t)]),
     "mcaat_host_crispr_arrays": (C.c_int, [C.c_int, _u64p, _u16p, _u8p, C.c_uint64, _u64p, _u64p, C.c_size_t, _u64p,
-                                           _u64p, C.c_size_t, C.c_char_p, C.POINTER(C.c_size_t)]),
+                                           _u64p, C.c_size_t, C.c_char_p, C.POINTER(C.c_size_t), C.c_int]),
     "mcaat_host_crispr_analyzer": (C.c_int, [C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), C.c_size_t, C.c_char_p]),
 }
 
@@ -85,9 +85,10 @@ def min_cover(universe: Sequence[int], sets: Sequence[Sequence[int]]) -> List[in
 
 
 def crispr_arrays(k: int, keys: np.ndarray, mult: np.ndarray, valid: np.ndarray, cycles: Sequence[Sequence[int]],
-                  reads: Sequence[Sequence[int]], output_file: str) -> int:
+                  reads: Sequence[Sequence[int]], output_file: str, threads: int = 1) -> int:
     """Steps 7-8 + CRISPRAnalyzer on a host copy of the graph; writes output_file. `valid`
-    (uint8, one per edge) is updated in place as the reference mutates the SDBG."""
+    (uint8, one per edge) is updated in place as the reference mutates the SDBG. threads > 1 solves
+    the subproblems on that many host threads (the output is the serial loop's)."""
     keys = np.ascontiguousarray(keys, dtype=np.uint64)
     mult = np.ascontiguousarray(mult, dtype=np.uint16)
     assert valid.dtype == np.uint8 and valid.flags["C_CONTIGUOUS"] and valid.size == keys.size
@@ -97,7 +98,7 @@ def crispr_arrays(k: int, keys: np.ndarray, mult: np.ndarray, valid: np.ndarray,
     _check(load_host_library().mcaat_host_crispr_arrays(
         k, keys.ctypes.data_as(_u64p), mult.ctypes.data_as(_u16p), valid.ctypes.data_as(_u8p), keys.size,
         cf.ctypes.data_as(_u64p), co.ctypes.data_as(_u64p), len(cycles), rf.ctypes.data_as(_u64p),
-        ro.ctypes.data_as(_u64p), len(reads), output_file.encode(), C.byref(n)))
+        ro.ctypes.data_as(_u64p), len(reads), output_file.encode(), C.byref(n), threads))
     return n.value
 
 

@@ -700,31 +700,31 @@ static std::vector<uint32_t> solve_topological_weighted(const WeightedConstraint
 
 std::vector<uint32_t> order_cycles(const Graph &graph, const std::vector<std::vector<uint64_t>> &reads,
                                    const std::vector<std::vector<uint64_t>> &cycles, float &confidence_cycle_resolution,
-                                   float &confidence_topological_sort) {  // spacer_ordering.cpp:719-754
+                                   float &confidence_topological_sort, std::ostream &log) {  // spacer_ordering.cpp:719-754
     const auto node_to_cycle = get_node_to_unique_cycle_map(cycles);
     const auto cycle_ids = get_all_cycle_indices(node_to_cycle);
     const char *ref = getenv("MCAAT_ORDER_REF");
     if (!(ref && ref[0] == '1')) {
         auto wc = generate_constraints_weighted(reads, node_to_cycle);
         const int64_t before = wc.total();
-        std::cout << "      ▸ " << before << " constraints derived" << std::endl;
+        log << "      ▸ " << before << " constraints derived" << std::endl;
         std::unordered_map<uint32_t, int> heuristic;
         for (uint32_t c : cycle_ids) heuristic[c] = 0;
         resolve_cycles_greedy_weighted(wc, heuristic);
         const int64_t after = wc.total();
         confidence_cycle_resolution = static_cast<float>(after) / static_cast<float>(before);
-        std::cout << "      ▸ " << after << " constraints remain after resolving cycles (confidence = " << std::fixed
+        log << "      ▸ " << after << " constraints remain after resolving cycles (confidence = " << std::fixed
                   << std::setprecision(2) << (confidence_cycle_resolution * 100) << "%)" << std::endl;
         return solve_topological_weighted(wc, heuristic, cycle_ids, confidence_topological_sort);
     }
     auto constraints = generate_constraints(graph, reads, node_to_cycle);
-    std::cout << "      ▸ " << constraints.size() << " constraints derived" << std::endl;
+    log << "      ▸ " << constraints.size() << " constraints derived" << std::endl;
     std::unordered_map<uint32_t, int> heuristic;
     for (uint32_t c : cycle_ids) heuristic[c] = 0;
     const int before = constraints.size();
     resolve_cycles_greedy(constraints, heuristic);
     confidence_cycle_resolution = static_cast<float>(constraints.size()) / static_cast<float>(before);
-    std::cout << "      ▸ " << constraints.size() << " constraints remain after resolving cycles (confidence = "
+    log << "      ▸ " << constraints.size() << " constraints remain after resolving cycles (confidence = "
               << std::fixed << std::setprecision(2) << (confidence_cycle_resolution * 100) << "%)" << std::endl;
     return solve_constraints_with_topological_sort(constraints, heuristic, cycle_ids, confidence_topological_sort);
 }

@@ -1,4 +1,5 @@
 // capi_host.cpp — extern "C" entry points of libmcaat_host.so (include/mcaat_host.h).
+#include <algorithm>
 #include <cstring>
 #include <sstream>
 
@@ -55,7 +56,7 @@ int mcaat_host_min_cover(const uint32_t *universe, size_t n_universe, const uint
 int mcaat_host_crispr_arrays(int k, const uint64_t *keys, const uint16_t *mult, uint8_t *valid, uint64_t D,
                              const uint64_t *cycles_flat, const uint64_t *cycle_offsets, size_t n_cycles,
                              const uint64_t *reads_flat, const uint64_t *read_offsets, size_t n_reads,
-                             const char *output_file, size_t *n_found) {
+                             const char *output_file, size_t *n_found, int threads) {
     return guarded([&] {
         if (!keys || !mult || !valid || !cycle_offsets || !read_offsets || !output_file)
             throw std::invalid_argument("null argument");
@@ -64,7 +65,7 @@ int mcaat_host_crispr_arrays(int k, const uint64_t *keys, const uint16_t *mult, 
                             std::vector<uint8_t>(valid, valid + D));
         const auto cycles = unflatten(cycles_flat, cycle_offsets, n_cycles);
         const auto reads = unflatten(reads_flat, read_offsets, n_reads);
-        const auto found = run_and_debug_spacer_ordering(reads, sdbg, cycles);
+        const auto found = run_and_debug_spacer_ordering(reads, sdbg, cycles, (unsigned)std::max(1, threads));
         std::unordered_map<std::string, std::vector<std::string>> all_systems;
         for (const auto &[_s, repeat, spacers, _a, _b] : found) all_systems[repeat] = spacers;
         CRISPRAnalyzer analyzer(all_systems, output_file);

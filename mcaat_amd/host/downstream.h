@@ -12,6 +12,7 @@
 //   * rapidfuzz fuzz::ratio / partial_ratio are restated from rapidfuzz-cpp (absent).
 #pragma once
 #include <cstdint>
+#include <iostream>
 #include <limits>
 #include <optional>
 #include <string>
@@ -95,9 +96,11 @@ void resolve_cycles_greedy(std::vector<std::tuple<uint32_t, uint32_t>> &constrai
 std::vector<uint32_t> solve_constraints_with_topological_sort(
     const std::vector<std::tuple<uint32_t, uint32_t>> &constraints, std::unordered_map<uint32_t, int> &heuristic_node_values,
     const std::vector<uint32_t> &nodes, float &confidence);
+// log: where the per-subproblem constraint lines go (the step-7 driver solves subproblems on
+// several threads and prints each one's lines in subproblem order)
 std::vector<uint32_t> order_cycles(const Graph &graph, const std::vector<std::vector<uint64_t>> &reads,
                                    const std::vector<std::vector<uint64_t>> &cycles, float &confidence_cycle_resolution,
-                                   float &confidence_topological_sort);
+                                   float &confidence_topological_sort, std::ostream &log = std::cout);
 std::vector<std::vector<uint64_t>> get_ordered_cycles(const std::vector<uint32_t> &cycle_order,
                                                       const std::vector<std::vector<uint64_t>> &cycles);
 
@@ -126,8 +129,10 @@ using FoundSystem = std::tuple<std::string, std::string, std::vector<std::string
 std::vector<std::vector<uint64_t>> run_and_debug_finding_of_relevant_reads(
     const std::vector<std::vector<uint64_t>> &cycles, const mcaat_reads *reads, const SDBG &sdbg,
     mcaat_comm *comm = nullptr, int n_files = 1);
+// threads: host threads for the independent subproblems (output order is the serial loop's)
 std::vector<FoundSystem> run_and_debug_spacer_ordering(const std::vector<std::vector<uint64_t>> &reads, SDBG &sdbg,
-                                                       const std::vector<std::vector<uint64_t>> &cycles);
+                                                       const std::vector<std::vector<uint64_t>> &cycles,
+                                                       unsigned threads = 1);
 void run_and_debug_benchmark_results(const Settings &settings, const std::vector<FoundSystem> &found_systems);
 void run_and_debug_results(const std::vector<FoundSystem> &found_systems);
 

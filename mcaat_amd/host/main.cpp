@@ -139,24 +139,28 @@ struct Ranks {
     void watch() {
         std::vector<pid_t> kids = children;
         watcher = std::thread([kids]() {
-            // whichever rank ends first is reaped first: a failure of rank 3 is seen while
-            // rank 1 is still running
+            // whichever rank ends first is reaped first (a failure of rank 3 is seen while rank
+            // 1 is still running); only the rank pids are waited on, so another child of rank 0
+            // (a popen, a system()) keeps its own exit status
+            std::vector<bool> done(kids.size(), false);
             for (size_t left = kids.size(); left > 0;) {
-                int st = 0;
-                const pid_t p = waitpid(-1, &st, 0);
-                if (p < 0) {
-                    if (errno == EINTR) continue;
-                    break;
+                bool reaped = false;
+                for (size_t r = 0; r < kids.size(); ++r) {
+                    if (done[r]) continue;
+                    int st = 0;
+                    const pid_t p = waitpid(kids[r], &st, WNOHANG);
+                    if (p == 0 || (p < 0 && errno == EINTR)) continue;
+                    done[r] = true;
+                    --left;
+                    reaped = true;
+                    if (p < 0) continue;  // not ours any more (ECHILD)
+                    if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) {
+                        std::cerr << "rank " << r + 1 << " failed; ending the run" << std::endl;
+                        for (pid_t q : kids) kill(q, SIGTERM);
+                        _exit(1);
+                    }
                 }
-                size_t r = 0;
-                while (r < kids.size() && kids[r] != p) ++r;
-                if (r == kids.size()) continue;
-                --left;
-                if (!WIFEXITED(st) || WEXITSTATUS(st) != 0) {
-                    std::cerr << "rank " << r + 1 << " failed; ending the run" << std::endl;
-                    for (pid_t q : kids) kill(q, SIGTERM);
-                    _exit(1);
-                }
+                if (!reaped) std::this_thread::sleep_for(std::chrono::milliseconds(20));
             }
         });
     }
@@ -287,7 +291,7 @@ static int run(Settings &settings, Ranks &ranks) {
         const double t_step6 = since(g_main_start);
 
         banner("🔸STEP 7: Order the spacers");                  // main.cpp:553-556
-        const auto found_systems = run_and_debug_spacer_ordering(reads, sdbg, cycles);
+        const auto found_systems = run_and_debug_spacer_ordering(reads, sdbg, cycles, (unsigned)std::max<size_t>(1, settings.threads));
 
         const double t_step7 = since(g_main_start);
         if (settings.benchmark_file != "") {                   // main.cpp:559-569

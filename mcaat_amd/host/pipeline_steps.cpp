@@ -1,9 +1,12 @@
 // pipeline_steps.cpp — the reference's steps 6-8 drivers (src/main_run_and_debug.cpp):
 // relevant reads, spacer ordering per CRISPR region, and the result / benchmark reports.
+#include <atomic>
 #include <chrono>
 #include <fstream>
 #include <iomanip>
 #include <iostream>
+#include <sstream>
+#include <thread>
 
 #include "downstream.h"
 
@@ -31,9 +34,14 @@ std::vector<std::vector<uint64_t>> run_and_debug_finding_of_relevant_reads(
     return relevant;
 }
 
-// main_run_and_debug.cpp:32-143
+// main_run_and_debug.cpp:32-143. The regions are disjoint SCCs, so their subproblems (cover
+// filter, constraints, topological order) are independent: they are solved on `threads` host
+// threads (a shared counter deals regions out), each region's lines captured, and everything
+// is then printed and get_systems run in region order, so stdout, `found` and therefore
+// all_systems' insertion order (CRISPR_Arrays.txt) are those of the reference's serial loop.
 std::vector<FoundSystem> run_and_debug_spacer_ordering(const std::vector<std::vector<uint64_t>> &reads, SDBG &sdbg,
-                                                       const std::vector<std::vector<uint64_t>> &cycles) {
+                                                       const std::vector<std::vector<uint64_t>> &cycles,
+                                                       unsigned threads) {
     const auto t0 = std::chrono::high_resolution_clock::now();
     std::cout << "  ▸ Splitting into subproblems" << std::endl;
     const size_t read_nodes = reads.at(0).size();  // the region growth radius (reference: reads.at(0).size())
@@ -41,45 +49,77 @@ std::vector<FoundSystem> run_and_debug_spacer_ordering(const std::vector<std::ve
     const auto t_regions = std::chrono::high_resolution_clock::now();
 
     std::cout << "  🔄 Filtering subproblems:" << std::endl;
-    struct Sub {
-        const Graph *g;
-        std::vector<std::vector<uint64_t>> reads, cycles;
-    };
-    std::vector<Sub> subs;
     std::vector<std::vector<std::vector<uint64_t>>> region_reads, region_cycles;
     get_relevant_reads_and_cycles(regions, reads, cycles, region_reads, region_cycles);
-    for (size_t ri = 0; ri < regions.size(); ++ri) {
-        const Graph &g = regions[ri];
+    struct Sub {
+        bool kept = false;
+        size_t n_reads = 0;
+        std::vector<std::vector<uint64_t>> cycles;  // after the cover filter
+        std::vector<uint32_t> order;
+        float conf_resolution = 1.0, conf_sort = 1.0;
+        std::string log;  // order_cycles' lines
+    };
+    std::vector<Sub> subs(regions.size());
+    const auto t_split = std::chrono::high_resolution_clock::now();
+    auto solve = [&](size_t ri) {
+        Sub &s = subs[ri];
         auto rr = std::move(region_reads[ri]);
-        auto rc = std::move(region_cycles[ri]);
-        get_minimum_cycles_for_full_coverage(rc);
+        s.cycles = std::move(region_cycles[ri]);
+        get_minimum_cycles_for_full_coverage(s.cycles);
         // the reverse-complement twin of a region is expected to carry no relevant reads
-        if (rr.empty() || rc.size() < 3) continue;
-        subs.push_back({&g, std::move(rr), std::move(rc)});
+        if (rr.empty() || s.cycles.size() < 3) return;
+        s.kept = true;
+        s.n_reads = rr.size();
+        std::ostringstream log;
+        s.order = order_cycles(regions[ri], rr, s.cycles, s.conf_resolution, s.conf_sort, log);
+        s.log = log.str();
+    };
+    if (threads == 0) threads = 1;
+    threads = (unsigned)std::min<size_t>(threads, std::max<size_t>(1, regions.size()));
+    {
+        std::atomic<size_t> next{0};
+        std::vector<std::string> err(threads);
+        auto worker = [&](unsigned t) {
+            try {
+                for (size_t ri; (ri = next.fetch_add(1)) < regions.size();) solve(ri);
+            } catch (const std::exception &e) {
+                err[t] = e.what();
+                next.store(regions.size());
+            }
+        };
+        std::vector<std::thread> pool;
+        for (unsigned t = 1; t < threads; ++t) pool.emplace_back(worker, t);
+        worker(0);
+        for (auto &th : pool) th.join();
+        for (const auto &e : err)
+            if (!e.empty()) throw std::runtime_error(e);
     }
-    std::cout << "  ✅ Filtered out " << regions.size() - subs.size() << "/" << regions.size() << " subproblems"
-              << std::endl;
-    const auto t_filtered = std::chrono::high_resolution_clock::now();
-    std::cout << "  🔄 Solving " << subs.size() << " subproblems..." << std::endl;
+    size_t n_kept = 0;
+    for (const Sub &s : subs) n_kept += s.kept;
+    std::cout << "  ✅ Filtered out " << regions.size() - n_kept << "/" << regions.size() << " subproblems" << std::endl;
+    const auto t_solved = std::chrono::high_resolution_clock::now();
+    std::cout << "  🔄 Solving " << n_kept << " subproblems..." << std::endl;
 
     std::vector<FoundSystem> found;
-    for (size_t i = 0; i < subs.size(); ++i) {
-        const Sub &s = subs[i];
-        std::cout << "    Subproblem " << i + 1 << "/" << subs.size() << ":" << std::endl;
-        std::cout << "      🛈 Graph with " << s.g->nodes.size() << " nodes and " << s.g->edge_count() << " edges"
-                  << std::endl;
-        std::cout << "      🛈 Reads with " << s.reads.size() << "/" << reads.size() << " used" << std::endl;
+    size_t i = 0;
+    for (size_t ri = 0; ri < regions.size(); ++ri) {
+        Sub &s = subs[ri];
+        if (!s.kept) continue;
+        ++i;
+        std::cout << "    Subproblem " << i << "/" << n_kept << ":" << std::endl;
+        std::cout << "      🛈 Graph with " << regions[ri].nodes.size() << " nodes and " << regions[ri].edge_count()
+                  << " edges" << std::endl;
+        std::cout << "      🛈 Reads with " << s.n_reads << "/" << reads.size() << " used" << std::endl;
         std::cout << "      🛈 Cycles with " << s.cycles.size() << "/" << get_cycle_count(cycles) << " used" << std::endl;
-        float conf_resolution = 1.0, conf_sort = 1.0;
-        const auto order = order_cycles(*s.g, s.reads, s.cycles, conf_resolution, conf_sort);
+        std::cout << s.log;
         std::cout << "      ▸ The order is ";
-        for (uint32_t c : order) std::cout << c << " ";
+        for (uint32_t c : s.order) std::cout << c << " ";
         std::cout << std::endl;
         std::cout << "      ▸ Cycles were resolved with a confidence of " << std::fixed << std::setprecision(2)
-                  << (conf_resolution * 100) << "%" << std::endl;
-        std::cout << "      ▸ Topological sort has a confidence of " << (conf_sort * 100) << "%" << std::endl;
+                  << (s.conf_resolution * 100) << "%" << std::endl;
+        std::cout << "      ▸ Topological sort has a confidence of " << (s.conf_sort * 100) << "%" << std::endl;
         std::cout << "      ▸ Turning the cycle order into a node order" << std::endl;
-        auto ordered = get_ordered_cycles(order, s.cycles);
+        auto ordered = get_ordered_cycles(s.order, s.cycles);
         if (ordered.size() < 2) {
             std::cout << "      ▸ Node order is to short and is not processed further" << std::endl;
             continue;
@@ -87,15 +127,15 @@ std::vector<FoundSystem> run_and_debug_spacer_ordering(const std::vector<std::ve
         std::cout << "      ▸ Starting the filter process:" << std::endl;
         auto [repeat, spacers, sequence] = get_systems(sdbg, ordered);
         std::cout << "        ▸ Number of spacers: " << spacers.size() << std::endl;
-        found.emplace_back(sequence, repeat, spacers, conf_resolution, conf_sort);
+        found.emplace_back(sequence, repeat, spacers, s.conf_resolution, s.conf_sort);
     }
     std::cout << "  ✅ Completed each subproblem" << std::endl;
     {
         using sec = std::chrono::duration<double>;
         const auto t_end = std::chrono::high_resolution_clock::now();
         std::cout << "TIMING_STEP7 regions_s=" << sec(t_regions - t0).count()
-                  << " filter_s=" << sec(t_filtered - t_regions).count() << " solve_s=" << sec(t_end - t_filtered).count()
-                  << std::endl;
+                  << " split_s=" << sec(t_split - t_regions).count() << " solve_s=" << sec(t_solved - t_split).count()
+                  << " emit_s=" << sec(t_end - t_solved).count() << " threads=" << threads << std::endl;
     }
     print_elapsed(t0);
     return found;

@@ -84,7 +84,7 @@ int main(int argc, char **argv) {
     oracle_graph_valid(g, valid.data());
     size_t n_found = 0;
     const int rc = mcaat_host_crispr_arrays(k, keys.data(), mult.data(), valid.data(), D, cflat.data(), coff.data(),
-                                            coff.size() - 1, rflat, roff, n_rel, argv[4], &n_found);
+                                            coff.size() - 1, rflat, roff, n_rel, argv[4], &n_found, 4);
     if (rc != 0) {
         fprintf(stderr, "mcaat_host_crispr_arrays: %s\n", mcaat_host_last_error());
         return 1;

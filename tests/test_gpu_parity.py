@@ -264,3 +264,44 @@ def test_cycle_results_as_arrays(gpu_ctx):
         assert s1 == s2
         assert cyc == [flat[offs[j]:offs[j + 1]].tolist() for j in range(len(offs) - 1)]
     assert list(b.candidates) == a.candidates and list(b.buckets) == a.buckets
+
+
+def test_graph_from_sorted_rejects_bad_keys(gpu_ctx):
+    """mcaat_graph_from_sorted takes sorted unique BOSS keys below 4^(k+1). The directory pass
+    checks both and a violation is MCAAT_E_INVALID, not a silently wrong directory (the round-3
+    clamp in k_dir kept out-of-range prefixes from writing past it, but built a wrong graph)."""
+    import torch
+
+    spec = M.SynthSpec()
+    k = 23
+    reads = M.Reads.synth(gpu_ctx, spec)
+    keys, mult, _ = M.Graph.build(gpu_ctx, reads, k).download()
+    dev = torch.device("cuda", 0)
+
+    def build(kk):
+        tk = torch.from_numpy(kk.view(np.int64).copy()).to(dev)
+        tm = torch.from_numpy(mult.view(np.int16).copy()).to(dev)
+        torch.cuda.synchronize()
+        return M.Graph.from_sorted(gpu_ctx, k, tk.data_ptr(), tm.data_ptr(), int(kk.size))
+
+    g = build(keys)  # the good keys build the same graph
+    k2, m2, _ = g.download()
+    assert np.array_equal(k2, keys) and np.array_equal(m2, mult)
+    bad = keys.copy()
+    bad[bad.size // 2] = np.uint64(1) << np.uint64(2 * (k + 1))  # past 4^(k+1) (then also unsorted)
+    bad[-1] = np.uint64((1 << (2 * (k + 1))) + 5)
+    with pytest.raises(M.McaatError) as ei:
+        build(bad)
+    assert ei.value.code == -1
+    # in range, out of order / repeated: inside a 64-edge row, across rows, across 256-edge chunks
+    for a in (100, 63, 255):
+        swapped = keys.copy()
+        swapped[[a, a + 1]] = swapped[[a + 1, a]]
+        with pytest.raises(M.McaatError) as ei:
+            build(swapped)
+        assert ei.value.code == -1
+        dup = keys.copy()
+        dup[a + 1] = dup[a]
+        with pytest.raises(M.McaatError) as ei:
+            build(dup)
+        assert ei.value.code == -1

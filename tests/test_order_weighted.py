@@ -54,3 +54,31 @@ def test_weighted_constraints_equal_list_form(tmp_path, capfd, ci):
             os.environ.pop("MCAAT_ORDER_REF", None)
     assert outs["0"] == outs["1"]
     assert outs["0"][2], "no subproblem was solved"
+
+
+@pytest.mark.parametrize("ci", range(len(CASES)))
+def test_step7_threads_equal_serial(tmp_path, capfd, ci):
+    """Step 7 solves its independent subproblems on host threads; everything it prints and the
+    CRISPR_Arrays.txt it leads to (all_systems' insertion order) equal the serial loop's."""
+    spec = CASES[ci]
+    k, thr = 23, 5
+    packed, offs = M.synth_host(spec)
+    og = O.OGraph.build(packed, offs, k, threads=4)
+    res = og.cycle_finder(threshold_multiplicity=thr, threads=1)
+    ent = res["entries"]
+    cycles = [c for i in res["map_order"] for c in ent[i][1]]
+    nodes = sorted({x for c in cycles for x in c})
+    seqs = [unpack_read(packed, int(offs[i]), int(offs[i + 1])) for i in range(len(offs) - 1)]
+    reads = og.get_reads(seqs, len(seqs), nodes)
+    keys, mult = og.arrays()
+    outs = {}
+    for threads in (1, 3, 8):
+        valid = og.valid().astype(np.uint8).copy()
+        path = tmp_path / f"arrays_{threads}.txt"
+        capfd.readouterr()
+        n = DS.crispr_arrays(k, keys, mult, valid, cycles, reads, str(path), threads=threads)
+        printed = [ln for ln in capfd.readouterr().out.splitlines()
+                   if not ln.startswith("TIMING") and "Time elapsed" not in ln]
+        outs[threads] = (n, path.read_text(), printed, valid.tobytes())
+    assert outs[1] == outs[3] == outs[8]
+    assert sum("Subproblem" in ln for ln in outs[1][2]) >= 2, "the fixture must hold several subproblems"
