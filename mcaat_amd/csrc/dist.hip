@@ -15,6 +15,9 @@
 // of both orientations with 32-bit counts (knob dist.oriented=1, kept for comparison) sent
 // 2 x D_local x 12 B per rank and each owner sorted ~2 x D_local pairs whatever N; steps 3-4
 // send D_local x 10 B and sort D_local, then D / N.
+// Round 4 (default): steps 1 and 3-4 become pass A on every rank, the descriptors routed to the
+// owners of their L1 buckets (hash ranges of the minimizer), passes B and C there (final counts),
+// and the oriented edges routed to their BOSS-range owners (exchange_descriptors).
 // Replaces: Read2SdbgS2::Run driven from sdbg_build.cpp:171-187, for reads split over ranks.
 #include <algorithm>
 #include <vector>
@@ -52,13 +55,112 @@ std::vector<uint64_t> choose_splits(const std::vector<uint64_t> &hist, int world
 
 }  // namespace
 
+// Round 4 (default; knob dist.desc=0 keeps the count exchange below): pass A's super-k-mer
+// descriptors go to the owner of their L1 bucket. Every occurrence of a canonical edge has
+// the same minimizer and so the same L1 bucket, so each owner's passes B and C over all ranks'
+// descriptors of its buckets give final counts, each canonical edge on exactly one rank: no
+// partial sums, no owner-side sort of ~D_c pairs whatever N (the count exchange's canon_reduce).
+// The owners are contiguous bucket ranges of equal descriptor weight; a rank sends bucket b's
+// reservations (whole 1024-slot runs, inert padding included) to b's owner, which keeps one
+// region per (bucket, source rank) for pass B.
+// Replaces: the S2 counting of Read2SdbgS2::Run (sdbg_build.cpp:171-187) over reads split by rank.
+static void exchange_descriptors(mcaat_ctx *ctx, Comm &comm, NcBuckets &bk, NcBuckets &own, uint64_t occ_total) {
+    hipStream_t st = ctx->stream;
+    const int N = comm.world, R = comm.rank;
+    std::vector<uint64_t> mine(256, 0);
+    for (int b = 0; b < 256; ++b) {
+        if (bk.regions[b].size() > 1) throw Error(MCAAT_E_INVALID, "descriptor exchange: one region per bucket expected");
+        for (const auto &rg : bk.regions[b]) mine[b] += rg.second;
+    }
+    const std::vector<uint64_t> all = comm.allgather_vec(mine);  // [rank][bucket]
+    std::vector<double> cum(256);
+    double acc = 0;
+    for (int b = 0; b < 256; ++b) {
+        for (int q = 0; q < N; ++q) acc += (double)all[(uint64_t)q * 256 + b];
+        cum[b] = acc;
+    }
+    // owner o takes buckets [lo[o], lo[o+1])
+    std::vector<int> lo(N + 1, 0);
+    lo[N] = 256;
+    for (int o = 1; o < N; ++o) {
+        int b = acc > 0 ? (int)(std::lower_bound(cum.begin(), cum.end(), acc * o / N) - cum.begin()) + 1 : 256;
+        lo[o] = std::min(std::max(b, lo[o - 1]), 256);
+    }
+    // send buffer: each owner's buckets, ascending, back to back
+    uint64_t n_send = 0;
+    for (int b = 0; b < 256; ++b) n_send += mine[b];
+    DevBuf<uint4> sd(n_send ? n_send : 1);
+    DevBuf<uint16_t> ss(n_send ? n_send : 8);
+    std::vector<uint64_t> sb16(N, 0), sb2(N, 0);
+    {
+        uint64_t o = 0;
+        for (int q = 0; q < N; ++q)
+            for (int b = lo[q]; b < lo[q + 1]; ++b) {
+                for (const auto &rg : bk.regions[b]) {
+                    HIP_OK(hipMemcpyAsync(sd.p + o, bk.data.p + rg.first, 16 * rg.second, hipMemcpyDeviceToDevice, st));
+                    HIP_OK(hipMemcpyAsync(ss.p + o, bk.sub.p + rg.first, 2 * rg.second, hipMemcpyDeviceToDevice, st));
+                    o += rg.second;
+                }
+                sb16[q] += 16 * mine[b];
+                sb2[q] += 2 * mine[b];
+            }
+    }
+    bk.data.release();
+    bk.sub.release();
+    // what this rank receives: from each source, its slots of buckets [lo[R], lo[R+1])
+    std::vector<uint64_t> rb16(N, 0), rb2(N, 0);
+    uint64_t n_recv = 0;
+    for (int q = 0; q < N; ++q) {
+        uint64_t n = 0;
+        for (int b = lo[R]; b < lo[R + 1]; ++b) n += all[(uint64_t)q * 256 + b];
+        rb16[q] = 16 * n;
+        rb2[q] = 2 * n;
+        n_recv += n;
+    }
+    own.data.alloc(n_recv ? n_recv : 1);
+    own.sub.alloc(n_recv ? n_recv : 8);
+    HIP_OK(hipStreamSynchronize(st));
+    comm.alltoallv_dev(sd.p, sb16.data(), own.data.p, rb16.data());
+    comm.alltoallv_dev(ss.p, sb2.data(), own.sub.p, rb2.data());
+    own.regions.assign(256, {});
+    {
+        uint64_t o = 0;
+        for (int q = 0; q < N; ++q)
+            for (int b = lo[R]; b < lo[R + 1]; ++b) {
+                const uint64_t n = all[(uint64_t)q * 256 + b];
+                if (n) own.regions[b].push_back({o, n});
+                o += n;
+            }
+    }
+    own.l2_bits = bk.l2_bits;
+    // occurrences behind this owner's descriptors (sizes its output buffer), by its share
+    own.n_occ = acc > 0 ? (uint64_t)((double)occ_total * (double)n_recv / acc) + 1 : 0;
+}
+
 void build_graph_sharded(mcaat_ctx *ctx, Comm &comm, const mcaat_reads *r, int k, mcaat_graph *g) {
     hipStream_t st = ctx->stream;
     const int N = comm.world, R = comm.rank;
     StageTimer timer(ctx);
     CountResult c;
-    node_counter(ctx, r, k, c);
-    timer.mark("node_counter");
+    const bool desc_route = knob(ctx, "dist.desc", 1) != 0 && !knob(ctx, "dist.oriented", 0);
+    if (desc_route) {
+        NcBuckets bk, own;
+        uint64_t occ_total = 0;
+        node_counter_a(ctx, r, k,
+                       [&](uint64_t occ) {
+                           for (uint64_t x : comm.allgather_one(occ)) occ_total += x;
+                           return nc_fine_bits(ctx, occ_total);
+                       },
+                       bk);
+        timer.mark("node_counter_a");
+        exchange_descriptors(ctx, comm, bk, own, occ_total);
+        timer.mark("shard_desc_all_to_all");
+        node_counter_bc(ctx, own, k, c);
+        timer.mark("node_counter_bc");
+    } else {
+        node_counter(ctx, r, k, c);
+        timer.mark("node_counter");
+    }
 
     std::vector<uint64_t> hist(1u << kHistBits);
     counts_histogram(ctx, c, k, kHistBits, hist.data());
@@ -71,7 +173,41 @@ void build_graph_sharded(mcaat_ctx *ctx, Comm &comm, const mcaat_reads *r, int k
     DevBuf<uint64_t> uk;
     DevBuf<uint16_t> um;
     uint64_t u = 0;
-    if (knob(ctx, "dist.oriented", 0)) {
+    auto exchange = [&](const std::vector<uint64_t> &out_sizes, const uint64_t *skeys, const uint16_t *svals,
+                        DevBuf<uint64_t> &rkeys, DevBuf<uint16_t> &rvals) {
+        const std::vector<uint64_t> mat = comm.allgather_vec(out_sizes);
+        std::vector<uint64_t> in(N), sb(N), rb(N);
+        uint64_t n_in = 0;
+        for (int s = 0; s < N; ++s) n_in += in[s] = mat[(uint64_t)s * N + R];
+        rkeys.alloc(n_in ? n_in : 1);
+        rvals.alloc(n_in ? n_in : 1);
+        for (int p = 0; p < N; ++p) sb[p] = 8 * out_sizes[p], rb[p] = 8 * in[p];
+        comm.alltoallv_dev(skeys, sb.data(), rkeys.p, rb.data());
+        for (int p = 0; p < N; ++p) sb[p] = 2 * out_sizes[p], rb[p] = 2 * in[p];
+        comm.alltoallv_dev(svals, sb.data(), rvals.p, rb.data());
+        return n_in;
+    };
+    if (desc_route) {
+        // final counts: expand each canonical edge to its oriented edges and route them to their
+        // BOSS-range owners, which sort their ranges
+        const uint64_t cap2 = std::max<uint64_t>(1, 2 * c.n);
+        DevBuf<uint64_t> qk(cap2);
+        DevBuf<uint16_t> qm(cap2);
+        std::vector<uint64_t> sizes2(N);
+        route_oriented(ctx, k, c.keys.p, c.counts.p, c.n, N, splits.data(), sizes2.data(), qk.p, qm.p, cap2);
+        c = CountResult{};
+        timer.mark("shard_partition");
+        DevBuf<uint64_t> sk2;
+        DevBuf<uint16_t> sm2;
+        u = exchange(sizes2, qk.p, qm.p, sk2, sm2);
+        qk.release();
+        qm.release();
+        timer.mark("shard_all_to_all");
+        uk.alloc(u ? u : 1);
+        um.alloc(u ? u : 1);
+        sort_oriented(ctx, k, sk2.p, sm2.p, u, uk.p, um.p);
+        timer.mark("shard_reduce");
+    } else if (knob(ctx, "dist.oriented", 0)) {
         const uint64_t cap = std::max<uint64_t>(1, 2 * c.n);
         DevBuf<uint64_t> okeys(cap);
         DevBuf<uint32_t> ocnt(cap);
@@ -108,20 +244,6 @@ void build_graph_sharded(mcaat_ctx *ctx, Comm &comm, const mcaat_reads *r, int k
         counts_partition_canon(ctx, c, k, N, splits.data(), sizes.data(), okeys.p, ocnt.p, cap);
         c = CountResult{};
         timer.mark("shard_partition");
-        auto exchange = [&](const std::vector<uint64_t> &out_sizes, const uint64_t *skeys, const uint16_t *svals,
-                            DevBuf<uint64_t> &rkeys, DevBuf<uint16_t> &rvals) {
-            const std::vector<uint64_t> mat = comm.allgather_vec(out_sizes);
-            std::vector<uint64_t> in(N), sb(N), rb(N);
-            uint64_t n_in = 0;
-            for (int s = 0; s < N; ++s) n_in += in[s] = mat[(uint64_t)s * N + R];
-            rkeys.alloc(n_in ? n_in : 1);
-            rvals.alloc(n_in ? n_in : 1);
-            for (int p = 0; p < N; ++p) sb[p] = 8 * out_sizes[p], rb[p] = 8 * in[p];
-            comm.alltoallv_dev(skeys, sb.data(), rkeys.p, rb.data());
-            for (int p = 0; p < N; ++p) sb[p] = 2 * out_sizes[p], rb[p] = 2 * in[p];
-            comm.alltoallv_dev(svals, sb.data(), rvals.p, rb.data());
-            return n_in;
-        };
         DevBuf<uint64_t> rk;
         DevBuf<uint16_t> rc;
         const uint64_t n_in = exchange(sizes, okeys.p, ocnt.p, rk, rc);

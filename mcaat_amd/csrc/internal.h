@@ -8,6 +8,7 @@
 #include <stdexcept>
 #include <string>
 #include <utility>
+#include <functional>
 #include <vector>
 #include <sys/mman.h>
 #include <cstring>
@@ -351,6 +352,19 @@ struct CountResult {
     uint64_t n = 0;
 };
 void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out);
+// node_counter in its two halves (a sharded build exchanges the L1 buckets between them)
+struct NcBuckets {
+    DevBuf<uint4> data;     // 16-B super-k-mer descriptors
+    DevBuf<uint16_t> sub;   // each one's fine sub-partition row (same slots)
+    // per L1 bucket: its regions (first slot, slots) in data/sub, each a whole number of
+    // 1024-slot reservations (so every region starts 16-B aligned in sub)
+    std::vector<std::vector<std::pair<uint64_t, uint64_t>>> regions;
+    int l2_bits = 0;        // fine partitions = 256 << l2_bits
+    uint64_t n_occ = 0;     // edge occurrences behind the descriptors (sizes the output)
+};
+int nc_fine_bits(mcaat_ctx *ctx, uint64_t n_occ);
+void node_counter_a(mcaat_ctx *ctx, const mcaat_reads *r, int k, const std::function<int(uint64_t)> &pick, NcBuckets &b);
+void node_counter_bc(mcaat_ctx *ctx, NcBuckets &b, int k, CountResult &out);
 void verbose_mark(mcaat_ctx *ctx, const char *what);
 void sort_counts(mcaat_ctx *ctx, CountResult &c, int k);
 void sdbg_build(mcaat_ctx *ctx, CountResult &c, int k, mcaat_graph *g);

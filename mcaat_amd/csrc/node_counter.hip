@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <ctime>
+#include <functional>
 #include <type_traits>
 
 #include "internal.h"
@@ -1313,7 +1314,29 @@ void verbose_mark(mcaat_ctx *ctx, const char *what) {
     last = now;
 }
 
+// fine partitions: ~8K edge occurrences each (8 L1 bits + l2_bits), so that even at ~5x
+// coverage (a rank's share of a sharded dataset) a partition's distinct edges fit the LDS
+// table; deep data reaches the 2^19 cap long before (C3: 70K occurrences each, ~1K distinct
+// descriptors after the collapse)
+int nc_fine_bits(mcaat_ctx *ctx, uint64_t n_occ) {
+    int fine_bits = 0;
+    while ((1ULL << (fine_bits + 1)) * 8192ULL <= n_occ) ++fine_bits;
+    fine_bits = (int)knob(ctx, "nc.fine_bits", fine_bits);
+    return std::max(8, std::min(19, fine_bits));  // l2_bits <= 11: k_l2_scatter's line buffers
+}
+
 void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out) {
+    NcBuckets b;
+    node_counter_a(ctx, r, k, nullptr, b);
+    node_counter_bc(ctx, b, k, out);
+}
+
+// pass A: the reads' super-k-mer descriptors in 256 L1 buckets. The fine-partition bits come
+// from the reads' edge occurrences (nc_fine_bits), or from pick(occurrences) when given: a
+// sharded build derives them from the sum over its ranks (pick is collective, called once on
+// every rank), because the sub rows written here depend on them.
+void node_counter_a(mcaat_ctx *ctx, const mcaat_reads *r, int k, const std::function<int(uint64_t)> &pick,
+                    NcBuckets &bk) {
     verbose_mark(ctx, "node_counter.begin");
     const int E = k + 1;
     hipStream_t st = ctx->stream;
@@ -1383,24 +1406,16 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
         src.item_np = item_np.p;
         src.n_items = n_items;
     }
-    out.n = 0;
+    const int fine_bits = pick ? pick(n_occ) : nc_fine_bits(ctx, n_occ);
+    P.l2_bits = fine_bits - 8;
+    bk.l2_bits = P.l2_bits;
+    bk.n_occ = n_occ;
+    bk.regions.assign(256, {});
     if (n_occ == 0) {
-        out.keys.alloc(1);
-        out.counts.alloc(1);
+        bk.data.alloc(1);
+        bk.sub.alloc(8);
         return;
     }
-
-    // fine partitions: ~8K edge occurrences each (8 L1 bits + l2_bits), so that even at
-    // ~5x coverage (a rank's share of a sharded dataset) a partition's distinct edges fit
-    // the LDS table; deep data reaches the 2^19 cap long before (C3: 70K occurrences each,
-    // ~1K distinct descriptors after the collapse)
-    int fine_bits = 0;
-    while ((1ULL << (fine_bits + 1)) * 8192ULL <= n_occ) ++fine_bits;
-    fine_bits = (int)knob(ctx, "nc.fine_bits", fine_bits);
-    fine_bits = std::max(8, std::min(19, fine_bits));  // l2_bits <= 11: k_l2_scatter's line buffers
-    P.l2_bits = fine_bits - 8;
-    const uint32_t S = 1u << P.l2_bits;
-    const uint64_t F = 256ull * S;
 
     // ---- A ----
     // expected descriptors: density 2/(w+1) per edge + one per item, with headroom
@@ -1414,8 +1429,8 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
         for (int b = 0; b < 256; ++b) cap[b] = ((uint64_t)fixed + 7) & ~7ull;
     DevBuf<uint64_t> dcap(256), dbase(257);
     DevBuf<unsigned long long> dcur(256);
-    DevBuf<uint4> l1;
-    DevBuf<uint16_t> l1s;
+    DevBuf<uint4> &l1 = bk.data;
+    DevBuf<uint16_t> &l1s = bk.sub;
     std::vector<unsigned long long> tot(256);
     static const bool prof_a = getenv("MCAAT_PROF_A") && getenv("MCAAT_PROF_A")[0] == '1';
     DevBuf<unsigned long long> dprof(8);
@@ -1445,7 +1460,10 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
         for (int b = 0; b < 256; ++b) cap[b] = (tot[b] + 8) & ~7ull;  // exact on the second run (cursors count every grab)
     }
     uint64_t n_desc = 0;
-    for (int b = 0; b < 256; ++b) n_desc += tot[b];
+    for (int b = 0; b < 256; ++b) {
+        n_desc += tot[b];
+        if (tot[b]) bk.regions[b].push_back({base[b], tot[b]});  // tot: whole 1024-slot reservations
+    }
     // algorithmic bytes of the launch: the 2-bit stream read once, a 16-B descriptor and its
     // 2-B sub row written per reserved slot (the tail slots of a reservation are written inert)
     ctx->kstats["sk_scatter"].total_bytes += 0.25 * (double)r->n_bases + 18.0 * (double)n_desc;
@@ -1457,6 +1475,30 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
                 hp[0] / waves / 1e5, hp[1] / waves / 1e5, hp[2] / waves / 1e5, hp[3] / waves / 1e5, hp[4] / waves / 1e5);
     }
     verbose_mark(ctx, "node_counter.A");
+}
+
+// passes B and C over the L1 buckets' regions (a bucket may hold several, e.g. one per rank
+// after a sharded build's descriptor exchange): final canonical counts of their edges
+void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
+    const int E = k + 1;
+    hipStream_t st = ctx->stream;
+    out.n = 0;
+    uint64_t n_desc = 0;
+    for (const auto &v : bk.regions)
+        for (const auto &rg : v) n_desc += rg.second;
+    if (n_desc == 0) {
+        out.keys.alloc(1);
+        out.counts.alloc(1);
+        return;
+    }
+    const uint64_t n_occ = bk.n_occ;
+    DevBuf<uint4> &l1 = bk.data;
+    DevBuf<uint16_t> &l1s = bk.sub;
+    SkParams P;
+    P.l2_bits = bk.l2_bits;
+    const uint32_t S = 1u << P.l2_bits;
+    const uint64_t F = 256ull * S;
+    DevBuf<unsigned long long> dprof(8);
 
     // ---- B + C, over groups of L1 buckets whose fine partitions fit a memory budget ----
     // The sub histogram of every chunk gives all fine-partition offsets at once; each group
@@ -1467,11 +1509,12 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     std::vector<uint64_t> bchunk(257, 0);  // first chunk of each bucket
     for (int b = 0; b < 256; ++b) {
         bchunk[b] = cstart.size();
-        for (uint64_t o = 0; o < tot[b]; o += kChunk) {
-            cstart.push_back(base[b] + o);
-            clen.push_back((uint32_t)std::min<uint64_t>(kChunk, tot[b] - o));
-            cbucket.push_back((uint32_t)b);
-        }
+        for (const auto &rg : bk.regions[b])
+            for (uint64_t o = 0; o < rg.second; o += kChunk) {
+                cstart.push_back(rg.first + o);
+                clen.push_back((uint32_t)std::min<uint64_t>(kChunk, rg.second - o));
+                cbucket.push_back((uint32_t)b);
+            }
     }
     bchunk[256] = cstart.size();
     const uint64_t nch = cstart.size();
@@ -1685,6 +1728,7 @@ void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out)
     }
     l1.release();
     l1s.release();
+    bk.regions.assign(256, {});
     out.n = n_out;
     verbose_mark(ctx, "node_counter.C");
 }

@@ -92,8 +92,8 @@ def _ranks(world, comm, extra=(), timeout=600):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,extra", [(1, ()), (2, ()), (3, ("--window", "16", "--slot", "65536")),
-                                         (3, ("--knob", "dist.oriented=1"))])
+@pytest.mark.parametrize("world,extra", [(1, ()), (2, ()), (3, ("--window", "16", "--slot", "65536")), (4, ()),
+                                         (3, ("--knob", "dist.oriented=1")), (3, ("--knob", "dist.desc=0"))])
 def test_sharded_build_and_cycle_finder_ranks_share_one_gpu(world, extra):
     outs = _ranks(world, "shm", extra)
     for rc, o, e in outs:
