@@ -296,3 +296,100 @@ def test_oracle_c_fastq_reader_matches_fastx_restatement(tmp_path):
     bad.write_text("@r\nACGT\n+\n")
     with pytest.raises(ValueError):
         O.read_fastq(str(bad))
+
+
+def test_id_convention_relabelling(tmp_path):
+    """edge ids here leave out MEGAHIT's `$` dummy edges, so a real mcaat run
+    numbers the same edges id' = f(id) for an increasing f (dummies interleaved). Two outputs
+    depend on the id VALUES, not only on their order:
+      (1) results' libstdc++ iteration order, i.e. the order cycles_map_to_cycles
+          (tmp_utils.cpp:26-38) hands the cycles to steps 7-8;
+      (2) FindCycle's <= 4-element neighbour sets (unordered_set, identity hash mod 13,
+          cycle_finder.cpp:58-88): the out-sets are invariant (consecutive ids), the in-sets
+          used by the lock relaxation are not.
+    (1) is checked invariant where it should be: on multi-array fixtures CRISPR_Arrays.txt is
+    the same when the cycles come in the relabelled map's order (a compiled libstdc++ probe,
+    pinned against the oracle's own map order). (2) out-sets are shown invariant and in-sets NOT:
+    the relaxation visits in-edges in another order, which changes nothing in the lock values it
+    reaches (a fixpoint) but is where the numbering could show. Everything ordered by
+    id (candidate lists, buckets' ascending order, DESCENDING out / ASCENDING in neighbours) is
+    invariant under any increasing f."""
+    import mcaat_amd as M
+    import mcaat_amd.downstream as DS
+    from tests.helpers import unpack_read
+
+    src = tmp_path / "mapprobe.cpp"
+    src.write_text(r'''
+#include <unordered_map>
+#include <cstdio>
+#include <cstdint>
+#include <vector>
+int main(){ int n; while (scanf("%d", &n) == 1) { std::unordered_map<uint64_t, int> m; uint64_t v;
+  for (int i = 0; i < n; ++i) { scanf("%lu", &v); m[v] = i; }
+  for (auto &kv : m) printf("%d ", kv.second); printf("\n"); } }''')
+    exe = tmp_path / "mapprobe"
+    subprocess.run(["g++", "-O1", "-std=c++17", str(src), "-o", str(exe)], check=True)
+
+    def map_order(keys):
+        inp = f"{len(keys)} " + " ".join(map(str, keys)) + "\n"
+        out = subprocess.run([str(exe)], input=inp, capture_output=True, text=True, check=True).stdout
+        return [int(x) for x in out.split()]
+
+    specs = [M.SynthSpec(seed=21, n_genomes=3, genome_len=20_000, arrays_per_genome=1, spacers_per_array=9,
+                         repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36, n_reads=15_000,
+                         error_rate=0.001),
+             M.SynthSpec(seed=5, n_genomes=4, genome_len=30_000, arrays_per_genome=2, spacers_per_array=12,
+                         repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36, n_reads=30_000,
+                         error_rate=0.002)]
+    rng = np.random.default_rng(3)
+    changed_order = 0
+    for si, spec in enumerate(specs):
+        k = 23
+        packed, offs = M.synth_host(spec)
+        og = O.OGraph.build(packed, offs, k, threads=4)
+        res = og.cycle_finder(threshold_multiplicity=5, threads=1)
+        ent = res["entries"]
+        starts = [int(s) for s, _ in ent]
+        assert map_order(starts) == res["map_order"], "the probe must reproduce the oracle's map order"
+        # an increasing relabelling: 0..3 dummies before every edge
+        f = np.cumsum(rng.integers(0, 4, size=og.size + 1)).astype(np.int64) + np.arange(og.size + 1)
+        relab = map_order([int(f[s]) for s in starts])
+        changed_order += relab != res["map_order"]
+        seqs = [unpack_read(packed, int(offs[i]), int(offs[i + 1])) for i in range(len(offs) - 1)]
+        keys, mult = og.arrays()
+        texts = []
+        for order in (res["map_order"], relab):
+            cycles = [c for i in order for c in ent[i][1]]
+            nodes = sorted({x for c in cycles for x in c})
+            reads = og.get_reads(seqs, len(seqs), nodes)
+            valid = og.valid().astype(np.uint8).copy()
+            path = tmp_path / f"arrays_{si}_{len(texts)}.txt"
+            DS.crispr_arrays(k, keys, mult, valid, cycles, reads, str(path))
+            texts.append(path.read_text())
+        assert texts[0] == texts[1], f"spec {si}: CRISPR_Arrays.txt depends on results' iteration order"
+        assert "Number of Systems: 0" not in texts[0]
+    assert changed_order, "the relabelling should move results' iteration order on these fixtures"
+
+    # (2) neighbour-set order is NOT invariant: a shift by dummies reorders some <= 4-element sets
+    def set_order(ins):
+        L = []
+        for x in ins:
+            if x not in L:
+                L.insert(next((i for i, y in enumerate(L) if y % 13 == x % 13), 0), x)
+        return L
+
+    # Out-neighbour sets are a node's out-edges: consecutive ids (siblings differ only in W, so
+    # no dummy falls between them), a span below 13, distinct buckets: the order is the reverse
+    # insertion order whatever the values, and stays. In-neighbour sets are up to 4 positions of
+    # a 16-edge (k-1)-suffix group, which a dummy `$`-edge with that suffix can join: the span
+    # and the residues mod 13 change unevenly (a uniform shift would keep every collision).
+    f = np.cumsum(rng.integers(0, 2, size=1 << 16)) + np.arange(1 << 16)
+    inv = {int(y): x for x, y in enumerate(f)}
+    out_moved = in_moved = 0
+    for _ in range(2000):
+        lo = int(rng.integers(0, (1 << 16) - 20))
+        outs = list(range(lo, lo + int(rng.integers(2, 5))))[::-1]  # OutgoingEdges: descending
+        out_moved += set_order(outs) != [inv[y] for y in set_order([int(f[x]) for x in outs])]
+        ins = sorted(lo + int(x) for x in rng.choice(16, size=int(rng.integers(2, 5)), replace=False))
+        in_moved += set_order(ins) != [inv[y] for y in set_order([int(f[x]) for x in ins])]
+    assert out_moved == 0 and in_moved > 0
