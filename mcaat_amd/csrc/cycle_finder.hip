@@ -31,6 +31,71 @@ constexpr int kBlock = 256;
 constexpr uint64_t kNone = ~0ULL;
 constexpr uint8_t kUnk = 0, kRem = 1, kSurv = 2;
 
+// ------------------------------- peel --------------------------------------
+// kind[e]: low 6 bits the valid out-degree (0..4; 0x3F invalid edge), 0x80 when e is a
+// ruler, 0x40 when e is a successor of a branch node (only those nodes' owners are ever
+// read, so a walk stores no other owner: the walk is one random read per step).
+// nxk[e] (unary e): its sole successor in bits 0..55 and the successor's kind in 56..63, so a
+// ruler walk pays one dependent load per step.
+constexpr uint8_t kInvalid = 0x3F, kRulerBit = 0x80, kBranchSucc = 0x40;
+constexpr uint64_t kNodeMask = (1ULL << 56) - 1;
+__device__ __forceinline__ int kind_od(uint8_t k) { return k & 0x3F; }
+__device__ __forceinline__ bool kind_chain(uint8_t k) { return (k & 0xBF) == 1; }  // unary, not a ruler
+
+// Per-ruler words live in arrays indexed by the ruler's position in the ruler list, so the
+// only D-sized arrays are the flag words (4 B), nxk (8 B) and owner (4 B): 16 B per edge
+// (the graph itself is 26 B per edge; C5's ~4e9-edge graph must fit beside it).
+// jump[i]: kRRef | index of the next ruler (kRSuper when that ruler is a super ruler), or the
+// terminal node id (a non-unary node), or kNone (a ruler-less unary cycle)
+constexpr uint64_t kRRef = 1ULL << 62, kRSuper = 1ULL << 61, kRIdx = (1ULL << 40) - 1;
+constexpr uint32_t kNoOwner = 0xFFFFFFFFu;
+
+// a node's four flag bytes share one word (nf[4e + field]), so a walk or a successor check
+// touches one line per node instead of one per byte array
+enum : int { kFKind = 0, kFUpred = 1, kFBpred = 2, kFSt = 3 };
+struct PeelArrays {
+    uint8_t *nf;      // per node: kind; upred (1: some unary node points here); bpred (1: some
+                      // branch node, out-degree >= 2, points here); st (kUnk / kRem / kSurv,
+                      // non-unary nodes)
+    __device__ __forceinline__ uint8_t &kind(uint64_t e) const { return nf[4 * e + kFKind]; }
+    __device__ __forceinline__ uint8_t &upred(uint64_t e) const { return nf[4 * e + kFUpred]; }
+    __device__ __forceinline__ uint8_t &bpred(uint64_t e) const { return nf[4 * e + kFBpred]; }
+    __device__ __forceinline__ uint8_t &st(uint64_t e) const { return nf[4 * e + kFSt]; }
+    __device__ __forceinline__ uchar4 flags(uint64_t e) const { return *(const uchar4 *)(nf + 4 * e); }
+    uint64_t *nxk;    // successor | successor kind << 56 (unary nodes)
+    uint32_t *owner;  // rulers: their own list index; non-ruler branch successors: the list index
+                      // of the ruler whose walk passed them (kNoOwner: none); others unused
+    uint64_t *jump;   // per ruler (list index), see kRRef; after k_peel_final: terminal or kNone
+    uint32_t *sowner; // per ruler: the super ruler whose walk over rulers passed it (itself for a
+                      // super ruler, kNoOwner: none)
+    const uint64_t *seed;  // tips bitmap collected before the multiplicity filter
+    // Round 4: the per-edge arrays above hold only the edges valid after the multiplicity filter,
+    // at their rank among them (cidx): post is that filter's bitmap as the peel starts (the peel
+    // clears bits in the graph's own copy, never in this one), wpre[w] the set bits of its words
+    // before w. Null wpre: the arrays are indexed by edge id (every edge has a slot).
+    const uint64_t *post;
+    const uint32_t *wpre;
+    uint64_t nw;
+    __device__ __forceinline__ uint64_t cidx(uint64_t e) const {
+        if (!wpre) return e;
+        const uint64_t w = e >> 6;
+        return (uint64_t)wpre[w] + (uint64_t)__popcll(post[w] & ((1ull << (e & 63)) - 1));
+    }
+    // the edge id of slot c (wpre non-null; only on the removal path: the removed edges)
+    __device__ __forceinline__ uint64_t gid(uint64_t c) const {
+        if (!wpre) return c;
+        uint64_t lo = 0, hi = nw;  // last word w with wpre[w] <= c holds slot c
+        while (hi - lo > 1) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if ((uint64_t)wpre[mid] <= c) lo = mid;
+            else hi = mid;
+        }
+        uint64_t x = post[lo];
+        for (uint32_t r = (uint32_t)(c - wpre[lo]); r; --r) x &= x - 1;
+        return lo * 64 + (uint64_t)__builtin_ctzll(x);
+    }
+};
+
 // ------------------------------- scans -------------------------------------
 // one wave per 64-edge bitmap word, kScanU words per iteration with all their loads in flight
 // together: the out-edges of e are the consecutive ids [lo, lo + cnt), so its valid out-degree
@@ -84,17 +149,54 @@ struct WaveList {
     }
 };
 
-// CollectTips and InvalidateMultiplicityOneNodes in one pass: tips from the valid bits as they
-// were before the filter (every successor window is read from `valid`, which this pass does not
-// write), the filtered bits into `post` (swapped in by the driver); counts[0] tips, counts[1]
-// every mult <= 1 edge (the reference counts valid or not)
-// With nf / nxk (the list-ranking peel's arrays, nf zeroed) the pass also does the peel's
-// first D-wide pass (k_peel_init) from the same loads: an edge's filtered valid out-degree is
-// its successors' unfiltered bits AND their multiplicities > 1 (consecutive ids, one line), so
-// kinds, unary successors and the predecessor flags come out here instead of from a second
-// streaming pass over out_info and the filtered bitmap.
-// words [w_lo, w_hi) of the bitmaps (a rank's share; all of them on one GPU); tip_bm / post
-// are indexed from w_lo
+// InvalidateMultiplicityOneNodes (round 4: a pass of its own, ahead of CollectTips): post[w]
+// (indexed from w_lo) = the valid bits of word w whose edge has multiplicity > 1, and counts[1]
+// += every mult <= 1 edge (the reference counts valid or not). The tips pass then reads the
+// filtered bitmap where it needs post-filter validity (one window per neighbour set instead of
+// the neighbours' multiplicities), and its popcounts give the peel's compact slots.
+template <int kScanU>
+__global__ void __launch_bounds__(kBlock) k_post_filter(GraphView g, uint64_t w_lo, uint64_t w_hi, uint64_t *post,
+                                                        unsigned long long *counts) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    unsigned long long low_n = 0;
+    for (uint64_t wb = w_lo + (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); wb < w_hi; wb += kScanU * wstride) {
+        uint64_t sv[kScanU];
+        uint32_t mu[kScanU];
+#pragma unroll
+        for (int u = 0; u < kScanU; ++u) {
+            const uint64_t w = wb + u * wstride, e = w * 64 + lane;
+            sv[u] = w < w_hi ? g.valid[w] : 0;
+            mu[u] = e < g.D && w < w_hi ? g.mult[e] : 0xFFFFu;
+        }
+#pragma unroll
+        for (int u = 0; u < kScanU; ++u) {
+            const uint64_t w = wb + u * wstride;
+            const unsigned long long lowm = __ballot(mu[u] <= 1);
+            if (lane == 0 && w < w_hi) {
+                post[w - w_lo] = sv[u] & ~lowm;
+                low_n += __popcll(lowm);
+            }
+        }
+    }
+    block_add(counts + 1, low_n);
+}
+
+// set bits per word (the exclusive scan of these is PeelArrays::wpre)
+__global__ void __launch_bounds__(kBlock) k_word_pop(const uint64_t *bm, uint64_t nw, uint32_t *cnt) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) cnt[w] = __popcll(bm[w]);
+}
+
+// CollectTips from the valid bits before the filter (every successor window is read from
+// `valid`, which this pass does not write), counts[0] tips, into tip_bm (indexed from w_lo).
+// `post` is the whole filtered bitmap (k_post_filter; all ranks' words).
+// With pa.nf (the list-ranking peel's arrays, nf zeroed) the pass also does the peel's first
+// D-wide pass (k_peel_init) from the same loads: an edge's filtered valid out-degree is one
+// window of post over its successors (consecutive ids), so kinds, unary successors and the
+// predecessor flags come out here instead of from a second streaming pass over out_info and
+// the filtered bitmap; with pa.wpre they go to the edges' compact slots (PeelArrays::cidx).
+// words [w_lo, w_hi) (a rank's share; all of them on one GPU)
 // With a candidate list (cand != nullptr) the pass also does the recount's work on the
 // post-filter graph (round 3): counts[2] post-filter tips that are not seeds (every one of them
 // survives the peel, and no surviving edge becomes a tip: the reduction removes every valid edge
@@ -104,26 +206,27 @@ struct WaveList {
 // edge's valid in-edges: the final candidates are these, still valid after the peel.
 template <int kScanU>
 __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_lo, uint64_t w_hi, uint64_t *tip_bm,
-                                                        uint64_t *post, unsigned long long *counts, uint8_t *nf,
-                                                        uint64_t *nxk, uint64_t thr, uint64_t *cand, uint64_t cap) {
+                                                        const uint64_t *post, unsigned long long *counts, PeelArrays pa,
+                                                        uint64_t thr, uint64_t *cand, uint64_t cap) {
     const int lane = threadIdx.x & 63;
     const uint64_t nw = (g.D + 63) / 64;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    const bool peel = nf != nullptr, fold = cand != nullptr;
+    const bool peel = pa.nf != nullptr, fold = cand != nullptr;
+    const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     __shared__ uint64_t cbuf[kBlock / 64][128];
     WaveList cl{cbuf[threadIdx.x >> 6], cand, counts + 3, cap};
-    unsigned long long acc = 0, low_n = 0, tips_pf = 0;
+    unsigned long long acc = 0, tips_pf = 0;
     for (uint64_t wb = w_lo + (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); wb < w_hi; wb += kScanU * wstride) {
-        uint64_t sv[kScanU], oi[kScanU];
-        WordPair a[kScanU];
+        uint64_t sv[kScanU], pv[kScanU], oi[kScanU];
+        WordPair a[kScanU], a2[kScanU];
         uint32_t mu[kScanU];
-        uint32_t sm[kScanU][4];
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
             const uint64_t w = wb + u * wstride, e = w * 64 + lane;
             sv[u] = w < w_hi ? g.valid[w] : 0;
+            pv[u] = w < w_hi ? post[w] : 0;
             oi[u] = e < g.D && w < w_hi ? g.out_info[e] : 0;
-            mu[u] = e < g.D && w < w_hi ? g.mult[e] : 0xFFFFu;
+            mu[u] = e < g.D && w < w_hi && fold ? g.mult[e] : 0;
         }
         uint64_t ii[kScanU];
         WordPair b[kScanU];
@@ -131,15 +234,15 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_
         for (int u = 0; u < kScanU; ++u) {
             const uint64_t w = wb + u * wstride, e = w * 64 + lane;
             // the candidate filter's in-edge window, for post-filter valid edges above thr
-            const bool cv = fold && e < g.D && w < w_hi && ((sv[u] >> lane) & 1) && mu[u] > 1 && (uint64_t)mu[u] > thr;
+            const bool cv = fold && e < g.D && w < w_hi && ((pv[u] >> lane) & 1) && (uint64_t)mu[u] > thr;
             ii[u] = cv ? g.in_info[e] : 0;
         }
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
             const uint64_t lo = oi[u] & kIdxMask;
             a[u] = word_pair(g.valid, lo, nw);
-            if (peel || fold) mult4(g.mult, lo, sm[u]);  // entries past cnt are masked by pre below
-            if (fold) b[u] = word_pair(g.valid, ii[u] & kIdxMask, nw);
+            if (peel || fold) a2[u] = word_pair(post, lo, nw);
+            if (fold) b[u] = word_pair(post, ii[u] & kIdxMask, nw);
         }
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
@@ -149,50 +252,52 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_
             const uint32_t pre = bits16(a[u].a, a[u].b, lo) & ((1u << cnt) - 1);
             const bool t = ((sv[u] >> lane) & 1) && pre == 0;
             const unsigned long long m = __ballot(t);
-            const unsigned long long lowm = __ballot(mu[u] <= 1);
             if (lane == 0 && w < w_hi) {
                 tip_bm[w - w_lo] = m;
-                post[w - w_lo] = sv[u] & ~lowm;
                 acc += __popcll(m);
-                low_n += __popcll(lowm);
             }
+            const bool vpf = e < g.D && w < w_hi && ((pv[u] >> lane) & 1);  // valid after the filter
+            const unsigned pfo = (peel || fold) ? bits16(a2[u].a, a2[u].b, lo) & ((1u << cnt) - 1) : 0;  // successors valid after it
             if (fold) {
-                const bool vpf = e < g.D && w < w_hi && ((sv[u] >> lane) & 1) && mu[u] > 1;  // valid after the filter
-                unsigned pfo = 0;  // successors valid after the filter
-                for (int i = 0; i < (int)cnt; ++i)
-                    if (((pre >> i) & 1) && sm[u][i] > 1) pfo |= 1u << i;
                 // a post-filter tip that is not a seed (t: a pre-filter tip, i.e. a seed)
                 const unsigned long long tpm = __ballot(vpf && pfo == 0 && !t);
                 if (lane == 0) tips_pf += __popcll(tpm);
                 bool c = false;
                 if (vpf && (uint64_t)mu[u] > thr) {
                     const uint64_t l = ii[u] & kIdxMask;
-                    unsigned in = bits16(b[u].a, b[u].b, l) & (uint32_t)((ii[u] >> kIdxBits) & 0xFFFF);  // pre-filter valid in-edges
-                    unsigned im = in;
-                    while (im) {  // at most four: drop the ones the filter invalidates
-                        const int j = __ffs(im) - 1;
-                        im &= im - 1;
-                        if (g.mult[l + j] <= 1) in &= ~(1u << j);
-                    }
+                    const unsigned in = bits16(b[u].a, b[u].b, l) & (uint32_t)((ii[u] >> kIdxBits) & 0xFFFF);  // post-filter valid in-edges
                     const bool self = e >= l && e - l < 16 && ((in >> (e - l)) & 1);
                     c = __popc(in) >= 2 && !self;
                 }
                 cl.push(c, e);
             }
             if (peel && e < g.D && w < w_hi) {
-                if (!((sv[u] >> lane) & 1) || mu[u] <= 1) {
-                    nf[4 * e] = 0x3F;  // kInvalid
+                if (!vpf) {
+                    if (!pa.wpre) pa.kind(e) = kInvalid;  // (compact slots exist for valid edges only)
                 } else {
-                    uint64_t out[4];
-                    int od = 0;
+                    const uint64_t ce = pa.wpre ? (uint64_t)pa.wpre[w] + __popcll(pv[u] & lt) : e;
+                    // compact slot of successor lo + i: its word is lo's or the next one
+                    auto cs = [&](int i) -> uint64_t {
+                        const uint64_t y = lo + i;
+                        if (!pa.wpre) return y;
+                        const uint64_t wy = y >> 6;
+                        const uint64_t pw = wy == this_word(lo, nw) ? a2[u].a : a2[u].b;
+                        return (uint64_t)pa.wpre[wy] + __popcll(pw & ((1ull << (y & 63)) - 1));
+                    };
+                    int od = 0, i1 = -1;
                     for (int i = (int)cnt - 1; i >= 0; --i)  // descending ids, as dev_outgoing
-                        if (((pre >> i) & 1) && sm[u][i] > 1) out[od++] = lo + i;
-                    nf[4 * e] = (uint8_t)od;
+                        if ((pfo >> i) & 1) {
+                            ++od;
+                            i1 = i;
+                        }
+                    pa.kind(ce) = (uint8_t)od;
                     if (od == 1) {
-                        nxk[e] = out[0];
-                        nf[4 * out[0] + 1] = 1;  // upred
+                        const uint64_t cy = cs(i1);
+                        pa.nxk[ce] = cy;
+                        pa.upred(cy) = 1;
                     } else {
-                        for (int j = 0; j < od; ++j) nf[4 * out[j] + 2] = 1;  // bpred
+                        for (int i = (int)cnt - 1; i >= 0; --i)
+                            if ((pfo >> i) & 1) pa.bpred(cs(i)) = 1;
                     }
                 }
             }
@@ -200,7 +305,6 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_
     }
     if (fold) cl.finish();
     block_add(counts, acc);
-    block_add(counts + 1, low_n);
     block_add(counts + 2, tips_pf);
 }
 
@@ -279,64 +383,30 @@ __global__ void __launch_bounds__(kBlock) k_recount_candidates(GraphView g, uint
 
 
 
-// ------------------------------- peel --------------------------------------
-// kind[e]: low 6 bits the valid out-degree (0..4; 0x3F invalid edge), 0x80 when e is a
-// ruler, 0x40 when e is a successor of a branch node (only those nodes' owners are ever
-// read, so a walk stores no other owner: the walk is one random read per step).
-// nxk[e] (unary e): its sole successor in bits 0..55 and the successor's kind in 56..63, so a
-// ruler walk pays one dependent load per step.
-constexpr uint8_t kInvalid = 0x3F, kRulerBit = 0x80, kBranchSucc = 0x40;
-constexpr uint64_t kNodeMask = (1ULL << 56) - 1;
-__device__ __forceinline__ int kind_od(uint8_t k) { return k & 0x3F; }
-__device__ __forceinline__ bool kind_chain(uint8_t k) { return (k & 0xBF) == 1; }  // unary, not a ruler
-
-// Per-ruler words live in arrays indexed by the ruler's position in the ruler list, so the
-// only D-sized arrays are the flag words (4 B), nxk (8 B) and owner (4 B): 16 B per edge
-// (the graph itself is 26 B per edge; C5's ~4e9-edge graph must fit beside it).
-// jump[i]: kRRef | index of the next ruler (kRSuper when that ruler is a super ruler), or the
-// terminal node id (a non-unary node), or kNone (a ruler-less unary cycle)
-constexpr uint64_t kRRef = 1ULL << 62, kRSuper = 1ULL << 61, kRIdx = (1ULL << 40) - 1;
-constexpr uint32_t kNoOwner = 0xFFFFFFFFu;
-
-// a node's four flag bytes share one word (nf[4e + field]), so a walk or a successor check
-// touches one line per node instead of one per byte array
-enum : int { kFKind = 0, kFUpred = 1, kFBpred = 2, kFSt = 3 };
-struct PeelArrays {
-    uint8_t *nf;      // per node: kind; upred (1: some unary node points here); bpred (1: some
-                      // branch node, out-degree >= 2, points here); st (kUnk / kRem / kSurv,
-                      // non-unary nodes)
-    __device__ __forceinline__ uint8_t &kind(uint64_t e) const { return nf[4 * e + kFKind]; }
-    __device__ __forceinline__ uint8_t &upred(uint64_t e) const { return nf[4 * e + kFUpred]; }
-    __device__ __forceinline__ uint8_t &bpred(uint64_t e) const { return nf[4 * e + kFBpred]; }
-    __device__ __forceinline__ uint8_t &st(uint64_t e) const { return nf[4 * e + kFSt]; }
-    __device__ __forceinline__ uchar4 flags(uint64_t e) const { return *(const uchar4 *)(nf + 4 * e); }
-    uint64_t *nxk;    // successor | successor kind << 56 (unary nodes)
-    uint32_t *owner;  // rulers: their own list index; non-ruler branch successors: the list index
-                      // of the ruler whose walk passed them (kNoOwner: none); others unused
-    uint64_t *jump;   // per ruler (list index), see kRRef; after k_peel_final: terminal or kNone
-    uint32_t *sowner; // per ruler: the super ruler whose walk over rulers passed it (itself for a
-                      // super ruler, kNoOwner: none)
-    const uint64_t *seed;  // tips bitmap collected before the multiplicity filter
-};
-
 // super rulers: chain heads and 1 in 64 of the other rulers (a ruler reached from another
 // ruler has a unary predecessor, so for it the hash alone decides)
 constexpr uint64_t kSuperMask = 63;
 __device__ __forceinline__ bool peel_super_hash(uint64_t r) { return (mix64(r ^ 0xbeefULL) & kSuperMask) == 0; }
 
 // pass 1 (D-wide): out-degree, the unary successor, unary- and branch-predecessor flags
+// (g.valid: the filtered bitmap, equal to pa.post when the arrays are compact)
 __global__ void __launch_bounds__(kBlock) k_peel_init(GraphView g, PeelArrays pa) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < g.D; e += stride) {
-        if (!bit_get(g.valid, e)) { pa.kind(e) = kInvalid; continue; }
+        if (!bit_get(g.valid, e)) {
+            if (!pa.wpre) pa.kind(e) = kInvalid;
+            continue;
+        }
         uint64_t out[4];
         const int n = dev_outgoing(g, e, out);
-        pa.kind(e) = (uint8_t)n;
+        const uint64_t ce = pa.cidx(e);
+        pa.kind(ce) = (uint8_t)n;
         if (n == 1) {
-            pa.nxk[e] = out[0];
-            pa.upred(out[0]) = 1;
+            const uint64_t cy = pa.cidx(out[0]);
+            pa.nxk[ce] = cy;
+            pa.upred(cy) = 1;
         } else {
-            for (int j = 0; j < n; ++j) pa.bpred(out[j]) = 1;
+            for (int j = 0; j < n; ++j) pa.bpred(pa.cidx(out[j])) = 1;
         }
     }
 }
@@ -370,20 +440,24 @@ __global__ void __launch_bounds__(kBlock) k_peel_prep(uint64_t D, PeelArrays pa,
         for (int h = 0; h < kTileJ; h += kPB) {
             uint8_t od[kPB], bp[kPB], up[kPB], oy[kPB], by[kPB], uy[kPB];
             uint64_t y[kPB];
+            uint64_t ce[kPB];
 #pragma unroll
             for (int q = 0; q < kPB; ++q) {
                 const uint64_t e = t0 + (uint64_t)(h + q) * kBlock + threadIdx.x;
+                // a wave's 64 edges are one word of the filtered bitmap: edges without a valid
+                // bit have no slot (compact arrays) or an invalid kind
+                const uint64_t pw = e < D ? pa.post[e >> 6] : 0;
+                const bool valid = (pw >> (e & 63)) & 1;
+                ce[q] = pa.wpre && valid ? (uint64_t)pa.wpre[e >> 6] + __popcll(pw & lt) : e;
                 // other lanes may already have set their own kind bits: the low 6 are the degree
-                const uchar4 f = e < D ? pa.flags(e) : make_uchar4(kInvalid, 0, 0, 0);
+                const uchar4 f = valid ? pa.flags(ce[q]) : make_uchar4(kInvalid, 0, 0, 0);
                 od[q] = (uint8_t)(f.x & 0x3F);
                 up[q] = f.y;
                 bp[q] = f.z;
             }
 #pragma unroll
-            for (int q = 0; q < kPB; ++q) {
-                const uint64_t e = t0 + (uint64_t)(h + q) * kBlock + threadIdx.x;
-                y[q] = od[q] == 1 ? (pa.nxk[e] & kNodeMask) : 0;  // masked: prep may run again
-            }
+            for (int q = 0; q < kPB; ++q)
+                y[q] = od[q] == 1 ? (pa.nxk[ce[q]] & kNodeMask) : 0;  // masked: prep may run again
 #pragma unroll
             for (int q = 0; q < kPB; ++q) {
                 oy[q] = by[q] = uy[q] = 0;
@@ -398,27 +472,29 @@ __global__ void __launch_bounds__(kBlock) k_peel_prep(uint64_t D, PeelArrays pa,
             for (int q = 0; q < kPB; ++q) {
                 const int j = h + q;
                 const uint64_t e = t0 + (uint64_t)j * kBlock + threadIdx.x;
+                const uint64_t cq = ce[q];
                 bool r = false, br = false;
                 if (od[q] != kInvalid) {
                     uint8_t k = od[q] | (bp[q] ? kBranchSucc : 0);
                     if (od[q] == 1) {
-                        r = up[q] == 0 || (mix64(e ^ 0x5eed) & ruler_mask) == 0;
+                        // the ruler hash is of the slot (compact or id): the same on every rank
+                        r = up[q] == 0 || (mix64(cq ^ 0x5eed) & ruler_mask) == 0;
                         if (r) k |= kRulerBit;
                         // owners: rulers get their list index below; of the others only branch
                         // successors' are ever read (peel_res)
-                        if (!r && bp[q]) pa.owner[e] = kNoOwner;
+                        if (!r && bp[q]) pa.owner[cq] = kNoOwner;
                         uint8_t ky = oy[q] | (by[q] ? kBranchSucc : 0);
                         if (oy[q] == 1 && (uy[q] == 0 || (mix64(y[q] ^ 0x5eed) & ruler_mask) == 0)) ky |= kRulerBit;
-                        pa.nxk[e] = y[q] | ((uint64_t)ky << 56);
+                        pa.nxk[cq] = y[q] | ((uint64_t)ky << 56);
                     } else if (od[q] == 0) {
                         const bool rm = bit_get(pa.seed, e);
-                        pa.st(e) = rm ? kRem : kSurv;
+                        pa.st(cq) = rm ? kRem : kSurv;
                         br = rm;
                     } else {
-                        pa.st(e) = kUnk;
+                        pa.st(cq) = kUnk;
                         br = true;
                     }
-                    pa.kind(e) = k;
+                    pa.kind(cq) = k;
                 }
                 m[j] = __ballot(r);
                 c += __popcll(m[j]);
@@ -443,8 +519,9 @@ __global__ void __launch_bounds__(kBlock) k_peel_prep(uint64_t D, PeelArrays pa,
             if ((m[j] >> lane) & 1) {
                 const uint64_t i = off + __popcll(m[j] & lt), e = t0 + (uint64_t)j * kBlock + threadIdx.x;
                 if (i < cap) {
-                    list[i] = e;
-                    pa.owner[e] = (uint32_t)i;
+                    const uint64_t c = pa.cidx(e);  // rulers are listed by slot
+                    list[i] = c;
+                    pa.owner[c] = (uint32_t)i;
                 }
             }
             off += __popcll(m[j]);
@@ -568,18 +645,18 @@ __global__ void __launch_bounds__(kBlock) k_peel_branch(GraphView g, PeelArrays 
                                                         uint64_t nb, int *changed) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += stride) {
-        const uint64_t b = blist[i];
-        if (pa.st(b) != kUnk) continue;
+        const uint64_t b = blist[i], cb = pa.cidx(b);  // blist: edge ids
+        if (pa.st(cb) != kUnk) continue;
         uint64_t out[4];
         const int n = dev_outgoing(g, b, out);
         bool all_rem = true, any_surv = false;
         for (int j = 0; j < n; ++j) {
-            const uint8_t r = peel_res(pa, out[j]);
+            const uint8_t r = peel_res(pa, pa.cidx(out[j]));
             if (r == kSurv) any_surv = true;
             if (r != kRem) all_rem = false;
         }
-        if (any_surv) { pa.st(b) = kSurv; *changed = 1; }
-        else if (all_rem) { pa.st(b) = kRem; *changed = 1; }
+        if (any_surv) { pa.st(cb) = kSurv; *changed = 1; }
+        else if (all_rem) { pa.st(cb) = kRem; *changed = 1; }
     }
 }
 
@@ -593,18 +670,18 @@ __global__ void __launch_bounds__(kBlock) k_peel_apply_list(GraphView g, PeelArr
                                                             uint64_t nb) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += stride)
-        if (pa.st(blist[i]) == kRem) clear_valid(g, blist[i]);
+        if (pa.st(pa.cidx(blist[i])) == kRem) clear_valid(g, blist[i]);
 }
 
 __global__ void __launch_bounds__(kBlock) k_peel_apply_rulers(GraphView g, PeelArrays pa, const uint64_t *list,
                                                               uint64_t nr) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nr; i += stride) {
-        const uint64_t r = list[i];
+        const uint64_t r = list[i];  // slots; their edge ids by pa.gid (removed edges only)
         if (peel_res(pa, r) != kRem) continue;  // a removed chain ends at a non-unary node: no cycle
-        clear_valid(g, r);
+        clear_valid(g, pa.gid(r));
         for (uint64_t w = pa.nxk[r]; kind_chain((uint8_t)(w >> 56)); w = pa.nxk[w & kNodeMask])
-            clear_valid(g, w & kNodeMask);
+            clear_valid(g, pa.gid(w & kNodeMask));
     }
 }
 
@@ -1363,10 +1440,15 @@ uint64_t select_flagged(mcaat_ctx *ctx, const uint8_t *flags, uint64_t n, uint64
 
 // ------------------------------ peel driver -----------------------------------
 // the peel's per-edge arrays; with `ready` set, k_tips_filter has already filled nf and nxk
+// (round 4) with post / wpre the arrays hold `slots` compact slots, one per edge valid after the
+// filter (PeelArrays::cidx); otherwise one per edge
 struct PeelState {
     DevBuf<uint8_t> nf;
     DevBuf<uint64_t> nxk;
     bool ready = false;
+    const uint64_t *post = nullptr;
+    const uint32_t *wpre = nullptr;
+    uint64_t slots = 0;
 };
 
 static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm, PeelState *pre = nullptr) {
@@ -1377,13 +1459,17 @@ static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm, PeelState *
     GraphView v = g->view();
     PeelState local;
     PeelState &ps = pre ? *pre : local;
-    DevBuf<uint32_t> owner(D);
+    if (!ps.wpre) ps.slots = D;
+    const uint64_t S = std::max<uint64_t>(ps.slots, 1);
+    DevBuf<uint32_t> owner(S);
     if (!ps.ready) {
-        ps.nf.alloc(4 * D);
-        ps.nxk.alloc(D);
+        ps.nf.alloc(4 * S);
+        ps.nxk.alloc(S);
         HIP_OK(hipMemsetAsync(ps.nf.p, 0, ps.nf.bytes(), st));  // the flag bytes other nodes set
     }
-    PeelArrays pa{ps.nf.p, ps.nxk.p, owner.p, nullptr, nullptr, seed_bm};
+    // identity slots: the graph's filtered bitmap tells prep which edges are valid
+    PeelArrays pa{ps.nf.p, ps.nxk.p, owner.p, nullptr, nullptr, seed_bm,
+                  ps.wpre ? ps.post : (const uint64_t *)g->valid.p, ps.wpre, g->n_words()};
     if (!ps.ready) {
         hipLaunchKernelGGL(k_peel_init, dim3(grid_for(D, kBlock)), dim3(kBlock), 0, st, v, pa);
         LAUNCH_OK();
@@ -1395,7 +1481,7 @@ static void run_peel_rulers(mcaat_graph *g, const uint64_t *seed_bm, PeelState *
     // the ruler and branch lists start at a fraction of D (rulers: the chain heads plus 1 in 64
     // unary nodes; branch nodes are rarer still) and the pass runs again if either overflowed
     const int64_t div = std::max<int64_t>(1, knob(ctx, "cf.peel_list_div", 16));
-    uint64_t cap = std::min<uint64_t>(D, D / (uint64_t)div + (1u << 16)), bcap = std::min<uint64_t>(D, D / 64 + (1u << 16));
+    uint64_t cap = std::min<uint64_t>(S, S / (uint64_t)div + (1u << 16)), bcap = std::min<uint64_t>(S, S / 64 + (1u << 16));
     if (knob_set(ctx, "cf.peel_list_cap"))  // test knob: both lists start this small
         cap = bcap = (uint64_t)std::max<int64_t>(1, knob(ctx, "cf.peel_list_cap", 1));
     DevBuf<unsigned long long> cur(4);
@@ -2074,12 +2160,9 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
     // its own k_peel_init)
     PeelState ps;
     const bool fuse = !comm && knob(ctx, "cf.walk_budget", 0) <= 0 && knob(ctx, "cf.fused_init", 1) != 0 && D;
-    if (fuse) {
-        ps.nf.alloc(4 * D);
-        ps.nxk.alloc(D);
-        HIP_OK(hipMemsetAsync(ps.nf.p, 0, ps.nf.bytes(), st));
-        ps.ready = true;
-    }
+    // (round 4) peel arrays over compact slots of the filtered edges (cf.compact=0: one per edge;
+    // the slots are 32-bit prefix counts, so graphs of 2^32 or more edges use one per edge)
+    const bool compact = knob(ctx, "cf.compact", 1) != 0 && D && D < (1ULL << 32) && knob(ctx, "cf.walk_budget", 0) <= 0;
     // the recount's counts and ChunkStartNodes' filter come from the tips / filter pass
     // (cf.recount = 1: the separate post-peel pass of round 2)
     const bool fold = knob(ctx, "cf.recount", 0) == 0;
@@ -2088,23 +2171,69 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
     if (knob_set(ctx, "cf.cand_cap")) ccap = (uint64_t)std::max<int64_t>(1, knob(ctx, "cf.cand_cap", 1));  // test knob
     DevBuf<uint64_t> clist;
     uint64_t n_cand = 0, tips_after = 0;
+    // the filtered bitmap (whole graph); the peel's compact slots index it, so it stays unchanged
+    // until the peel is done (the graph's own copy is the one the peel clears)
+    DevBuf<uint64_t> post(mcaat_graph::bitmap_words(D));
+    DevBuf<uint32_t> wpre;
     {
-        DevBuf<uint64_t> post(mcaat_graph::bitmap_words(D));
         HIP_OK(hipMemsetAsync(post.p + nw, 0, 8, st));  // the padding word
         DevBuf<unsigned long long> c2(4);
+        HIP_OK(hipMemsetAsync(c2.p, 0, 32, st));
+        std::vector<uint64_t> sz(N);
+        for (int r = 0; r < N; ++r) sz[r] = 8 * (nw * (uint64_t)(r + 1) / N - nw * (uint64_t)r / N);
+        // 2. InvalidateMultiplicityOneNodes: this rank's words of the filtered bitmap, gathered
+        {
+            DevBuf<uint64_t> mpost;
+            if (comm) mpost.alloc(std::max<uint64_t>(w_hi - w_lo, 1));
+            if (w_hi > w_lo) {
+                auto kern = scan_u == 1 ? k_post_filter<1> : scan_u == 4 ? k_post_filter<4> : k_post_filter<kScanUDefault>;
+                hipLaunchKernelGGL(kern, dim3(wgrid), dim3(kBlock), 0, st, v, w_lo, w_hi, comm ? mpost.p : post.p + w_lo,
+                                   c2.p);
+                LAUNCH_OK();
+            }
+            if (comm) {
+                HIP_OK(hipStreamSynchronize(st));
+                comm->allgatherv_dev(mpost.p, post.p, sz.data());
+            }
+        }
+        if (compact) {  // compact slots: exclusive prefix of the filtered words' popcounts
+            DevBuf<uint32_t> pc(nw + 1);
+            wpre.alloc(nw + 1);
+            HIP_OK(hipMemsetAsync(pc.p + nw, 0, 4, st));
+            hipLaunchKernelGGL(k_word_pop, dim3(grid_for(nw, kBlock, (unsigned)ctx->n_cu * 16)), dim3(kBlock), 0, st,
+                               (const uint64_t *)post.p, nw, pc.p);
+            LAUNCH_OK();
+            size_t tmp = 0;
+            HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, pc.p, wpre.p, (size_t)(nw + 1), st));
+            DevBuf<uint8_t> t(tmp);
+            HIP_OK(hipcub::DeviceScan::ExclusiveSum(t.p, tmp, pc.p, wpre.p, (size_t)(nw + 1), st));
+            uint32_t slots = 0;
+            d2h(ctx, &slots, wpre.p + nw, 4);
+            ps.post = post.p;
+            ps.wpre = wpre.p;
+            ps.slots = slots;
+        }
+        if (fuse) {
+            const uint64_t S = std::max<uint64_t>(compact ? ps.slots : D, 1);
+            ps.nf.alloc(4 * S);
+            ps.nxk.alloc(S);
+            HIP_OK(hipMemsetAsync(ps.nf.p, 0, ps.nf.bytes(), st));
+            ps.ready = true;
+        }
+        // 1. CollectTips (before the filter: the seeds of the reduction), with the peel's first
+        // pass and the candidate filter
+        PeelArrays fa{fuse ? ps.nf.p : nullptr, fuse ? ps.nxk.p : nullptr, nullptr, nullptr, nullptr, nullptr,
+                      post.p, compact ? wpre.p : nullptr, nw};
       for (;;) {
         if (fold) clist.alloc(ccap ? ccap : 1);
-        HIP_OK(hipMemsetAsync(c2.p, 0, 32, st));
-        DevBuf<uint64_t> mseeds, mpost;  // this rank's words when the bitmaps are gathered
-        if (comm) {
-            mseeds.alloc(w_hi - w_lo);
-            mpost.alloc(w_hi - w_lo);
-        }
+        HIP_OK(hipMemsetAsync(c2.p, 0, 8, st));
+        HIP_OK(hipMemsetAsync(c2.p + 2, 0, 16, st));
+        DevBuf<uint64_t> mseeds;  // this rank's words when the bitmap is gathered
+        if (comm) mseeds.alloc(std::max<uint64_t>(w_hi - w_lo, 1));
         if (w_hi > w_lo) {
             auto kern = scan_u == 1 ? k_tips_filter<1> : scan_u == 4 ? k_tips_filter<4> : k_tips_filter<kScanUDefault>;
-            hipLaunchKernelGGL(kern, dim3(wgrid), dim3(kBlock), 0, st, v, w_lo, w_hi, comm ? mseeds.p : seeds.p,
-                               comm ? mpost.p : post.p, c2.p, fuse ? ps.nf.p : (uint8_t *)nullptr,
-                               fuse ? ps.nxk.p : (uint64_t *)nullptr, (uint64_t)p.threshold_multiplicity,
+            hipLaunchKernelGGL(kern, dim3(wgrid), dim3(kBlock), 0, st, v, w_lo, w_hi, comm ? mseeds.p : seeds.p + w_lo,
+                               (const uint64_t *)post.p, c2.p, fa, (uint64_t)p.threshold_multiplicity,
                                fold ? clist.p : (uint64_t *)nullptr, ccap);
             LAUNCH_OK();
         }
@@ -2113,22 +2242,21 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
         HIP_OK(hipStreamSynchronize(st));
         if (fold && hc[3] > ccap) {  // more candidates than the list held: the pass again (idempotent), sized
             ccap = hc[3];
+            if (fuse) HIP_OK(hipMemsetAsync(ps.nf.p, 0, ps.nf.bytes(), st));  // its flag bytes are set again
             continue;
         }
         n_cand = fold ? hc[3] : 0;
         tips_after = hc[2];
         if (comm) {
-            std::vector<uint64_t> sz(N);
-            for (int r = 0; r < N; ++r) sz[r] = 8 * (nw * (uint64_t)(r + 1) / N - nw * (uint64_t)r / N);
             comm->allgatherv_dev(mseeds.p, seeds.p, sz.data());
-            comm->allgatherv_dev(mpost.p, post.p, sz.data());
             const auto all = comm->allgather_vec(std::vector<unsigned long long>{hc[0], hc[1]});
             hc[0] = hc[1] = 0;
             for (int r = 0; r < N; ++r) hc[0] += all[2 * r], hc[1] += all[2 * r + 1];
         }
         out->stats[0] = hc[0];
         out->stats[1] = hc[1];
-        std::swap(g->valid, post);  // the pre-filter bitmap is released here
+        // the graph's bitmap becomes the filtered one (its pre-filter bits are no longer read)
+        HIP_OK(hipMemcpyAsync(g->valid.p, post.p, 8 * nw, hipMemcpyDeviceToDevice, st));
         v = g->view();
         break;
       }
@@ -2136,10 +2264,13 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
     timer.mark("tips_filter");
     verbose_mark(ctx, "cf.tips_filter");
     // 3. RecursiveReduction from every seed
-    run_peel(g, seeds.p, fuse ? &ps : nullptr);
+    if (!fuse) ps.ready = false;
+    run_peel(g, seeds.p, (fuse || compact) ? &ps : nullptr);
     seeds.release();
     ps.nf.release();
     ps.nxk.release();
+    post.release();
+    wpre.release();
     timer.mark("peel");
     verbose_mark(ctx, "cf.peel");
     // 4-5. valid count + tips after pruning, and ChunkStartNodes' candidate filter (its

@@ -674,6 +674,10 @@ constexpr int kMaxSub = 2048;   // l2_bits <= 11: 128 KB of line buffers
 #define MCAAT_BPF 2
 #endif
 constexpr int kBPF = MCAAT_BPF;  // rounds of descriptor loads in flight
+#ifndef MCAAT_BCOOP
+#define MCAAT_BCOOP 1
+#endif
+constexpr bool kCoopFlush = MCAAT_BCOOP != 0;  // completed lines written by the whole wave
 
 __global__ void __launch_bounds__(kBThreads) k_l2_scatter(const uint4 *__restrict__ data,
                                                           const uint16_t *__restrict__ sub,
@@ -725,7 +729,36 @@ __global__ void __launch_bounds__(kBThreads) k_l2_scatter(const uint4 *__restric
         }
         lds_barrier();
         uint32_t nline = 0;
-        if (live) {
+        if (kCoopFlush) {
+            // the lines completed this round leave the wave kLG lanes per line, each lane one
+            // 16-B piece: one store instruction writes 64/kLG whole lines (one lane per line
+            // with kLG stores before), and the LDS reads are kLG-lane contiguous runs
+            const bool done = live && buffered && (r & (kLG - 1)) == kLG - 1;
+            const unsigned long long dm = __ballot(done);
+            const uint32_t lane = threadIdx.x & 63;
+            const uint64_t dst = done ? ((uint64_t)lb[cv] + line) * kLG - gbase : 0;
+            const uint32_t src = done ? cv * kLG : 0;
+            const int nd = __popcll(dm);
+            for (int b0 = 0; b0 < nd; b0 += 64 / kLG) {
+                const int j = b0 + (int)(lane / kLG);  // the line this lane helps write
+                // lane holding the j-th set bit of dm (binary search on prefix popcounts)
+                int pos = 0;
+                if (j < nd) {
+#pragma unroll
+                    for (int step = 32; step; step >>= 1) {
+                        const unsigned long long below = dm & ((pos + step >= 64) ? ~0ull : ((1ull << (pos + step)) - 1));
+                        if (__popcll(below) <= j) pos += step;
+                    }
+                }
+                const uint64_t d = __shfl(dst, pos);
+                const uint32_t sidx = __shfl(src, pos);
+                if (j < nd) out[d + (lane & (kLG - 1))] = buf[sidx + (lane & (kLG - 1))];
+            }
+            if (live) {
+                nline = lc[cv] / kLG;
+                bl[cv] = nline;  // every writer stores the same value
+            }
+        } else if (live) {
             if (buffered && (r & (kLG - 1)) == kLG - 1) {
                 uint4 *o = out + (((uint64_t)lb[cv] + line) * kLG - gbase);
 #pragma unroll
