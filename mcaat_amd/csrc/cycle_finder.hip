@@ -822,6 +822,87 @@ __global__ void __launch_bounds__(kBlock) k_dls(GraphView g, const uint64_t *can
     res[i] = over ? -1 : found;
 }
 
+// (round 4) The same search with scratch per lane instead of per candidate: lane q of the
+// launch takes candidates q, q + L, q + 2L, ... (L lanes in all), so a wave's time is the sum of
+// its lanes' searches, not the longest search of one batch, and every candidate gets the large
+// scratch. The visited table is not cleared between searches: an entry carries its search's
+// generation in bits 56..63 (node ids are below 2^56), and entries of other generations read
+// as empty; the table is cleared when the 8-bit generation wraps.
+__device__ __forceinline__ bool gset_insert(uint64_t *tab, uint32_t cap, uint64_t x, uint64_t gen, uint32_t &size,
+                                            bool &over) {
+    const uint64_t tx = (gen << 56) | x;
+    uint32_t s = (uint32_t)(mix64(x) & (cap - 1));
+    for (;;) {
+        const uint64_t c = tab[s];
+        if (c == tx) return false;
+        if ((c >> 56) != gen) {
+            if (size + 1 > cap / 4 * 3) { over = true; return false; }
+            tab[s] = tx;
+            ++size;
+            return true;
+        }
+        s = (s + 1) & (cap - 1);
+    }
+}
+__device__ __forceinline__ bool gset_contains(const uint64_t *tab, uint32_t cap, uint64_t x, uint64_t gen) {
+    const uint64_t tx = (gen << 56) | x;
+    uint32_t s = (uint32_t)(mix64(x) & (cap - 1));
+    for (;;) {
+        const uint64_t c = tab[s];
+        if (c == tx) return true;
+        if ((c >> 56) != gen) return false;
+        s = (s + 1) & (cap - 1);
+    }
+}
+
+// vis_all zeroed by the caller (generation 0 = empty); lpw active lanes per wave
+__global__ void __launch_bounds__(kBlock) k_dls_lanes(GraphView g, const uint64_t *cand, uint64_t n, int limit,
+                                                      uint64_t *stack_all, uint32_t cs, uint64_t *vis_all, uint32_t cv,
+                                                      int8_t *res, int lpw, uint64_t n_lanes) {
+    const int lane = threadIdx.x & 63;
+    if (lane >= lpw) return;
+    const uint64_t q = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / 64 * lpw + lane;
+    if (q >= n_lanes) return;
+    uint64_t *stk = stack_all + q * cs;
+    uint64_t *vis = vis_all + q * cv;
+    uint64_t gen = 0;
+    for (uint64_t i = q; i < n; i += n_lanes) {
+        if (++gen == 256) {
+            for (uint32_t j = 0; j < cv; ++j) vis[j] = 0;
+            gen = 1;
+        }
+        const uint64_t start = cand[i];
+        uint32_t sp = 0, vsize = 0;
+        bool over = false;
+        stk[sp++] = start << 8;  // (node << 8) | depth
+        int8_t found = 0;
+        while (sp > 0) {
+            const uint64_t top = stk[--sp];
+            const uint64_t v = top >> 8;
+            const int depth = (int)(top & 0xFF);
+            if (!bit_get(g.valid, v)) continue;
+            uint64_t nb[4];
+            const int od = dev_outgoing(g, v, nb);
+            if (od == 0) continue;  // EdgeOutdegreeZero
+            if (depth >= limit) continue;
+            for (int j = 0; j < od; ++j) {
+                const uint64_t x = nb[j];
+                const bool nv = !gset_contains(vis, cv, x, gen);
+                const bool sr = (x == start && depth > 0);
+                if (nv || sr) {
+                    gset_insert(vis, cv, x, gen, vsize, over);
+                    if (sp >= cs) over = true;
+                    if (over) break;
+                    stk[sp++] = (x << 8) | (uint64_t)(depth + 1);
+                }
+            }
+            if (over) break;
+            if (v == start && depth > 1) { found = 1; break; }
+        }
+        res[i] = over ? -1 : found;
+    }
+}
+
 // ---------------------------- FindCycle ----------------------------------------
 struct FcCaps {
     uint32_t P;    // path/frames capacity (max_len + 2)
@@ -1713,7 +1794,10 @@ static std::vector<uint64_t> run_dls_dev(mcaat_graph *g, const uint64_t *dcand, 
     hipStream_t st = ctx->stream;
     std::vector<uint64_t> pass;
     if (!n) return pass;
-    const bool many = n * 8ULL * (1024 + 2048) > (8ULL << 30);
+    // (round 4) cf.dls_persist: per-lane scratch, candidates strided over the lanes (default);
+    // 0: one scratch slot per candidate in batches
+    const bool persist = knob(ctx, "cf.dls_persist", 1) != 0;
+    const bool many = !persist && n * 8ULL * (1024 + 2048) > (8ULL << 30);
     uint32_t cs = (uint32_t)std::max<int64_t>(1, knob(ctx, "cf.dls_stack", many ? 128 : 1024));
     uint32_t cv = (uint32_t)next_pow2((uint64_t)std::max<int64_t>(2, knob(ctx, "cf.dls_visited", many ? 256 : 2048)));
     const int lanes = (int)std::max<int64_t>(1, std::min<int64_t>(64, knob(ctx, "cf.dls_lanes", 16)));
@@ -1733,13 +1817,26 @@ static std::vector<uint64_t> run_dls_dev(mcaat_graph *g, const uint64_t *dcand, 
             src = ids.p;
         }
         DevBuf<int8_t> r(nt);
-        for (uint64_t b0 = 0; b0 < nt; b0 += batch_cap) {
-            const uint64_t m = std::min<uint64_t>(batch_cap, nt - b0);
-            DevBuf<uint64_t> dstk(m * cs), dvis(m * cv);
-            hipLaunchKernelGGL(k_dls, dim3(grid_for(m, (unsigned)lanes)), dim3(64), 0, st, g->view(), src + b0, m, limit,
-                               dstk.p, cs, dvis.p, cv, r.p + b0, lanes);
+        if (persist) {
+            // scratch per lane: as many lanes as the GPU holds at once (or fewer candidates),
+            // within the same 8-GB scratch budget
+            const uint64_t nl = std::max<uint64_t>(
+                1, std::min<uint64_t>({nt, (uint64_t)ctx->n_cu * 32 * (uint64_t)lanes, batch_cap}));
+            DevBuf<uint64_t> dstk(nl * cs), dvis(nl * cv);
+            HIP_OK(hipMemsetAsync(dvis.p, 0, dvis.bytes(), st));
+            hipLaunchKernelGGL(k_dls_lanes, dim3(grid_for(nl, (unsigned)lanes)), dim3(64), 0, st, g->view(), src, nt,
+                               limit, dstk.p, cs, dvis.p, cv, r.p, lanes, nl);
             LAUNCH_OK();
-            HIP_OK(hipStreamSynchronize(st));  // the batch's scratch is freed on scope exit
+            HIP_OK(hipStreamSynchronize(st));  // the scratch is freed on scope exit
+        } else {
+            for (uint64_t b0 = 0; b0 < nt; b0 += batch_cap) {
+                const uint64_t m = std::min<uint64_t>(batch_cap, nt - b0);
+                DevBuf<uint64_t> dstk(m * cs), dvis(m * cv);
+                hipLaunchKernelGGL(k_dls, dim3(grid_for(m, (unsigned)lanes)), dim3(64), 0, st, g->view(), src + b0, m,
+                                   limit, dstk.p, cs, dvis.p, cv, r.p + b0, lanes);
+                LAUNCH_OK();
+                HIP_OK(hipStreamSynchronize(st));  // the batch's scratch is freed on scope exit
+            }
         }
         hipLaunchKernelGGL(k_scatter_res, dim3(grid_for(nt, kBlock)), dim3(kBlock), 0, st, (const int8_t *)r.p,
                            (const uint64_t *)idx.p, nt, res.p, flags.p);
