@@ -154,9 +154,15 @@ struct WaveList {
 // += every mult <= 1 edge (the reference counts valid or not). The tips pass then reads the
 // filtered bitmap where it needs post-filter validity (one window per neighbour set instead of
 // the neighbours' multiplicities), and its popcounts give the peel's compact slots.
+// the valid bits of word w of a graph whose every edge is valid (mcaat_graph::all_valid)
+__device__ __forceinline__ uint64_t word_ones(uint64_t w, uint64_t D) {
+    const uint64_t e0 = w * 64;
+    return e0 + 64 <= D ? ~0ull : e0 < D ? (~0ull >> (64 - (D - e0))) : 0ull;
+}
+
 template <int kScanU>
 __global__ void __launch_bounds__(kBlock) k_post_filter(GraphView g, uint64_t w_lo, uint64_t w_hi, uint64_t *post,
-                                                        unsigned long long *counts) {
+                                                        unsigned long long *counts, bool fresh) {
     const int lane = threadIdx.x & 63;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     unsigned long long low_n = 0;
@@ -166,7 +172,7 @@ __global__ void __launch_bounds__(kBlock) k_post_filter(GraphView g, uint64_t w_
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
             const uint64_t w = wb + u * wstride, e = w * 64 + lane;
-            sv[u] = w < w_hi ? g.valid[w] : 0;
+            sv[u] = w < w_hi ? (fresh ? word_ones(w, g.D) : g.valid[w]) : 0;
             mu[u] = e < g.D && w < w_hi ? g.mult[e] : 0xFFFFu;
         }
 #pragma unroll
@@ -205,9 +211,11 @@ __global__ void __launch_bounds__(kBlock) k_word_pop(const uint64_t *bm, uint64_
 // counts them all). A removed edge had no valid successor, so the peel changes no surviving
 // edge's valid in-edges: the final candidates are these, still valid after the peel.
 template <int kScanU>
+// fresh: every edge is valid before the filter (mcaat_graph::all_valid), so an edge is a tip
+// iff it has no out-edges at all, and no window of the unfiltered bitmap is read
 __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_lo, uint64_t w_hi, uint64_t *tip_bm,
                                                         const uint64_t *post, unsigned long long *counts, PeelArrays pa,
-                                                        uint64_t thr, uint64_t *cand, uint64_t cap) {
+                                                        uint64_t thr, uint64_t *cand, uint64_t cap, bool fresh) {
     const int lane = threadIdx.x & 63;
     const uint64_t nw = (g.D + 63) / 64;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
@@ -223,7 +231,7 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
             const uint64_t w = wb + u * wstride, e = w * 64 + lane;
-            sv[u] = w < w_hi ? g.valid[w] : 0;
+            sv[u] = w < w_hi ? (fresh ? word_ones(w, g.D) : g.valid[w]) : 0;
             pv[u] = w < w_hi ? post[w] : 0;
             oi[u] = e < g.D && w < w_hi ? g.out_info[e] : 0;
             mu[u] = e < g.D && w < w_hi && fold ? g.mult[e] : 0;
@@ -240,7 +248,7 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
             const uint64_t lo = oi[u] & kIdxMask;
-            a[u] = word_pair(g.valid, lo, nw);
+            if (!fresh) a[u] = word_pair(g.valid, lo, nw);
             if (peel || fold) a2[u] = word_pair(post, lo, nw);
             if (fold) b[u] = word_pair(post, ii[u] & kIdxMask, nw);
         }
@@ -249,7 +257,7 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_
             const uint64_t w = wb + u * wstride, e = w * 64 + lane;
             const uint64_t lo = oi[u] & kIdxMask;
             const uint32_t cnt = __popc((unsigned)(oi[u] >> kIdxBits) & 0xF);
-            const uint32_t pre = bits16(a[u].a, a[u].b, lo) & ((1u << cnt) - 1);
+            const uint32_t pre = fresh ? ((1u << cnt) - 1) : bits16(a[u].a, a[u].b, lo) & ((1u << cnt) - 1);
             const bool t = ((sv[u] >> lane) & 1) && pre == 0;
             const unsigned long long m = __ballot(t);
             if (lane == 0 && w < w_hi) {
@@ -2268,6 +2276,9 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
     if (knob_set(ctx, "cf.cand_cap")) ccap = (uint64_t)std::max<int64_t>(1, knob(ctx, "cf.cand_cap", 1));  // test knob
     DevBuf<uint64_t> clist;
     uint64_t n_cand = 0, tips_after = 0;
+    // every edge valid (as built): the passes before the filter read no unfiltered bitmap
+    const bool fresh = g->all_valid && knob(ctx, "cf.fresh", 1) != 0;
+    g->all_valid = false;  // the filter and the peel clear bits from here on
     // the filtered bitmap (whole graph); the peel's compact slots index it, so it stays unchanged
     // until the peel is done (the graph's own copy is the one the peel clears)
     DevBuf<uint64_t> post(mcaat_graph::bitmap_words(D));
@@ -2285,7 +2296,7 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
             if (w_hi > w_lo) {
                 auto kern = scan_u == 1 ? k_post_filter<1> : scan_u == 4 ? k_post_filter<4> : k_post_filter<kScanUDefault>;
                 hipLaunchKernelGGL(kern, dim3(wgrid), dim3(kBlock), 0, st, v, w_lo, w_hi, comm ? mpost.p : post.p + w_lo,
-                                   c2.p);
+                                   c2.p, fresh);
                 LAUNCH_OK();
             }
             if (comm) {
@@ -2331,7 +2342,7 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
             auto kern = scan_u == 1 ? k_tips_filter<1> : scan_u == 4 ? k_tips_filter<4> : k_tips_filter<kScanUDefault>;
             hipLaunchKernelGGL(kern, dim3(wgrid), dim3(kBlock), 0, st, v, w_lo, w_hi, comm ? mseeds.p : seeds.p + w_lo,
                                (const uint64_t *)post.p, c2.p, fa, (uint64_t)p.threshold_multiplicity,
-                               fold ? clist.p : (uint64_t *)nullptr, ccap);
+                               fold ? clist.p : (uint64_t *)nullptr, ccap, fresh);
             LAUNCH_OK();
         }
         unsigned long long hc[4];
@@ -2558,6 +2569,7 @@ void graph_set_valid(mcaat_graph *g, const uint64_t *ids, size_t n, int valid) {
     hipStream_t st = g->ctx->stream;
     DevBuf<uint64_t> di(n);
     HIP_OK(hipMemcpyAsync(di.p, ids, 8 * n, hipMemcpyHostToDevice, st));
+    if (!valid) g->all_valid = false;
     hipLaunchKernelGGL(k_set_bits, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, g->valid.p, di.p, (uint64_t)n,
                        valid);
     LAUNCH_OK();

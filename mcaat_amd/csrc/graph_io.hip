@@ -126,6 +126,7 @@ void graph_load(mcaat_ctx *ctx, const char *path, mcaat_graph *g) {
     if (want != sum.h) throw Error(MCAAT_E_IO, std::string("graph file checksum mismatch: ") + path);
     sdbg_finish(ctx, g);  // directory, adjacency words, all-valid bitmap
     if (nw) HIP_OK(hipMemcpyAsync(g->valid.p, valid.p, 8 * nw, hipMemcpyDeviceToDevice, ctx->stream));
+    g->all_valid = false;  // the saved bits (e.g. after a CycleFinder run)
     HIP_OK(hipStreamSynchronize(ctx->stream));
 }
 

@@ -181,6 +181,9 @@ struct mcaat_graph {
     mcaat::DevBuf<uint64_t> out_info;
     mcaat::DevBuf<uint64_t> in_info;
     mcaat::DevBuf<uint64_t> valid;
+    // every edge still valid, as the build leaves the graph (round 4): CycleFinder's tips pass
+    // then reads no bitmap windows before the filter; cleared by anything that clears a bit
+    bool all_valid = false;
     // radix directory over the top bits of the BOSS key (label lookups after the build)
     mcaat::DevBuf<uint64_t> dir;
     int dir_shift = 0;

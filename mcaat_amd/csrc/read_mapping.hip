@@ -228,6 +228,7 @@ void graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n) {
         HIP_OK(hipStreamSynchronize(st));
     }
     hipLaunchKernelGGL(k_and_bits, dim3(grid_for(nw, kBlock)), dim3(kBlock), 0, st, g->valid.p, keep.p, nw);
+    g->all_valid = false;
     LAUNCH_OK();
     HIP_OK(hipStreamSynchronize(st));
 }

@@ -1293,6 +1293,7 @@ void sdbg_finish(mcaat_ctx *ctx, mcaat_graph *g) {
     g->valid.alloc(mcaat_graph::bitmap_words(D));
     HIP_OK(hipMemsetAsync(g->valid.p + (D + 63) / 64, 0, 8, st));  // the padding word
     hipLaunchKernelGGL(k_valid_init, dim3(grid_for((D + 63) / 64, kBlock)), dim3(kBlock), 0, st, g->valid.p, D);
+    g->all_valid = true;
     LAUNCH_OK();
     HIP_OK(hipStreamSynchronize(st));
 }

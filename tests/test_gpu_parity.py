@@ -305,3 +305,30 @@ def test_graph_from_sorted_rejects_bad_keys(gpu_ctx):
         with pytest.raises(M.McaatError) as ei:
             build(dup)
         assert ei.value.code == -1
+
+
+@pytest.mark.parametrize("frac", [0.02, 0.3])
+def test_cycle_finder_on_a_graph_with_invalid_edges(gpu_ctx, frac):
+    """CycleFinder on a graph whose valid bits were cleared before it runs (the host's
+    SetInvalidEdge): the tips pass then reads the unfiltered bitmap (not every edge is valid), and
+    the peel's compact slots cover only the edges valid after the filter. Stats, the valid bitmap
+    afterwards and the results equal the oracle run on the same bits."""
+    spec, k, prm = CONFIGS["pe_err"]
+    packed, offs = M.synth_host(spec)
+    reads = M.Reads.synth(gpu_ctx, spec)
+    g = M.Graph.build(gpu_ctx, reads, k)
+    og = _oracle_graph(packed, offs, k)
+    rng = np.random.default_rng(int(frac * 100))
+    drop = np.sort(rng.choice(g.size, size=int(frac * g.size), replace=False)).astype(np.uint64)
+    g.set_valid(drop, False)
+    v = og.valid().astype(np.uint8)
+    v[drop.astype(np.int64)] = 0
+    og.set_valid(v)
+    res = g.cycle_finder(prm)
+    ores = og.cycle_finder(threshold_multiplicity=prm.threshold_multiplicity, low_abundance=prm.low_abundance,
+                           cycle_max_length=prm.cycle_max_length, cycle_min_length=prm.cycle_min_length, threads=1)
+    assert res.stats[:6] == ores["stats"]
+    assert res.candidates == ores["candidates"] and res.buckets == ores["buckets"]
+    _, _, valid = g.download()
+    assert np.array_equal(valid, og.valid())
+    assert [(s, c) for s, c in res.entries] == [tuple(e) for e in ores["entries"]]

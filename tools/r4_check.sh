@@ -5,3 +5,6 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 tail -2 gpurun_out/gpu_suite.log
 bash tools/abq.sh default ab/nocoop.so
 MCAAT_KNOBS=cf.compact=0 bash tools/abq.sh default
+MCAAT_KNOBS=cf.dls_persist=0 bash tools/abq.sh default
+CFG=c5 bash tools/abq.sh default
+CFG=c5 MCAAT_KNOBS=cf.compact=0,cf.dls_persist=0 bash tools/abq.sh default
