@@ -855,7 +855,21 @@ __device__ __forceinline__ uint32_t edge_slot(uint64_t c) {
 // edge table twice the size, one 1024-thread workgroup per CU (96 KB of LDS)
 constexpr int kCapBig = 8192;
 constexpr int kCapMaxBig = kCapBig * 85 / 100 - kCWaves * 64;
-constexpr int cap_lg(int cap) { return cap == 4096 ? 12 : cap == 8192 ? 13 : -1; }
+// (round 4) the middle tier: 6144 slots (72 KB), still two 1024-thread workgroups per CU, for
+// partitions of ~3-4K distinct edges (C5: ~3700) that overflow 4096 slots; slots are taken by a
+// multiply-high of the hash (not a power of two)
+constexpr int kCapMid = 6144;
+constexpr int kCapMaxMid = kCapMid * 85 / 100 - kCWaves * 64;
+constexpr int cap_lg(int cap) { return cap == 4096 ? 12 : cap == 8192 ? 13 : cap == kCapMid ? 0 : -1; }
+template <int CAP>
+__device__ __forceinline__ uint32_t edge_slot_n(uint64_t c) {
+    if constexpr ((CAP & (CAP - 1)) == 0) {
+        return edge_slot<cap_lg(CAP)>(c);
+    } else {
+        const uint32_t h = ((uint32_t)c ^ (uint32_t)(c >> 32)) * 0x9E3779B1u;
+        return (uint32_t)(((uint64_t)h * (uint64_t)CAP) >> 32);
+    }
+}
 __device__ __forceinline__ uint32_t desc_slot(uint64_t w0, uint64_t w1) {
     const uint64_t x = (w0 ^ (w1 * 0x9E3779B97F4A7C15ULL)) * 0xD6E8FEB86659FD93ULL;
     return (uint32_t)(x >> (64 - 11));
@@ -870,8 +884,7 @@ __global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_coun
                                                          unsigned long long *out_cursor, uint32_t *ovf_list,
                                                          unsigned long long *ovf_n, uint32_t cap_max, uint32_t dmax,
                                                          unsigned long long *split_n, unsigned long long *prof) {
-    constexpr int LG = cap_lg(kCap);
-    static_assert(LG > 0, "edge table of 4096 or 8192 slots");
+    static_assert(cap_lg(kCap) >= 0, "edge table of 4096, 6144 or 8192 slots");
     // The descriptor table (phase 1) and the edge table (phases 2-3) share one LDS region:
     // between the phases each thread keeps its two descriptor slots in registers. 48 KB per
     // workgroup, so two 1024-thread workgroups share a CU and one's loads overlap the other's
@@ -908,7 +921,7 @@ __global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_coun
 
     // add weight to canonical edge c; false once the table has overflowed
     auto insert = [&](uint64_t c, uint32_t weight) {
-        uint32_t h = edge_slot<LG>(c);
+        uint32_t h = edge_slot_n<kCap>(c);
         for (int probe = 0; probe < kCap; ++probe) {
             const unsigned long long cur = keys[h];
             if (cur == c) {
@@ -927,7 +940,7 @@ __global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_coun
                     return;
                 }
             }
-            h = (h + 1) & (kCap - 1);
+            h = h + 1 == (uint32_t)kCap ? 0 : h + 1;
         }
         ovf = 1;  // defensive: never spin on a full table
     };
@@ -1596,10 +1609,13 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
         (uint64_t)knob(ctx, "nc.group_budget", (int64_t)std::max<uint64_t>(n_live / 4 + 1, 1ULL << 28));  // descriptors per group
     const uint32_t cap_max = (uint32_t)std::min<int64_t>(kCapMax, std::max<int64_t>(1, knob(ctx, "nc.edge_cap", kCapMax)));
     const uint32_t cap_max_big = (uint32_t)std::min<int64_t>(kCapMaxBig, std::max<int64_t>(1, knob(ctx, "nc.edge_cap", kCapMaxBig)));
-    // big edge tables: knob nc.big_table 0 never, 1 always, default: from the next group on once
-    // a group split more than 1 in 8 of its partitions into classes (error-rich data)
+    const uint32_t cap_max_mid = (uint32_t)std::min<int64_t>(kCapMaxMid, std::max<int64_t>(1, knob(ctx, "nc.edge_cap", kCapMaxMid)));
+    // larger edge tables: tier 0 = 4096 slots, 1 = 6144 (two workgroups per CU), 2 = 8192 (one).
+    // knob nc.big_table fixes the tier (0, 1 = 8192 as in round 3, 2 = 6144); default: from the
+    // next group on, one tier up once a group split more than 1 in 8 of its partitions into
+    // classes (error-rich data)
     const int64_t big_knob = knob(ctx, "nc.big_table", -1);
-    bool big = big_knob == 1;
+    int tier = big_knob == 1 ? 2 : big_knob == 2 ? 1 : 0;
     const uint32_t dmax = (uint32_t)std::min<int64_t>(kDMax, std::max<int64_t>(1, knob(ctx, "nc.desc_cap", kDMax)));
     // groups of L1 buckets; with the overlap knob (default on) group g+1's pass B runs on the
     // side stream while group g's pass C counts on the main stream (two groups' fine
@@ -1663,11 +1679,13 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
             HIP_OK(hipMemsetAsync(dcnt.p + 1, 0, 16, st));
             {
                 KernelTimer kt(ctx, "lds_count", 16.0 * (double)gn);
-                const unsigned wg = (unsigned)std::min<uint64_t>(p1 - p0, (uint64_t)(big ? 1 : kCPerCu) * ctx->n_cu);
-                auto kern = big ? (prof_c ? k_lds_count<true, kCapBig, 1> : k_lds_count<false, kCapBig, 1>)
+                const unsigned wg = (unsigned)std::min<uint64_t>(p1 - p0, (uint64_t)(tier == 2 ? 1 : kCPerCu) * ctx->n_cu);
+                auto kern = tier == 2 ? (prof_c ? k_lds_count<true, kCapBig, 1> : k_lds_count<false, kCapBig, 1>)
+                          : tier == 1 ? (prof_c ? k_lds_count<true, kCapMid, kCPerCu> : k_lds_count<false, kCapMid, kCPerCu>)
                                 : (prof_c ? k_lds_count<true, kCap, kCPerCu> : k_lds_count<false, kCap, kCPerCu>);
                 hipLaunchKernelGGL(kern, dim3(wg), dim3(kCThreads), 0, st, fine.p, gbase, dfine.p, p0, p1, E, out.keys.p,
-                                   out.counts.p, out_cap, dcnt.p, ovf_list.p, dcnt.p + 1, big ? cap_max_big : cap_max, dmax,
+                                   out.counts.p, out_cap, dcnt.p, ovf_list.p, dcnt.p + 1,
+                                   tier == 2 ? cap_max_big : tier == 1 ? cap_max_mid : cap_max, dmax,
                                    dcnt.p + 2, prof_c ? dprof.p : nullptr);
                 LAUNCH_OK();
                 kt.stop();
@@ -1677,7 +1695,7 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
             HIP_OK(hipStreamSynchronize(st));
             const uint64_t n_ovf = hc[1];
             ctx->kstats["lds_count_split_partitions"].launches += hc[2];
-            if (big_knob < 0 && !big && hc[2] * 8 > p1 - p0) big = true;
+            if (big_knob < 0 && tier < 2 && hc[2] * 8 > p1 - p0) tier = tier + 1;
             ctx->kstats["lds_count_overflow_partitions"].launches += n_ovf;
             if (n_ovf) {
                 // global-table fallback for the partitions whose distinct edges overflowed LDS,

@@ -46,6 +46,9 @@ KNOBS = {
     # pass C with the 8192-slot edge table (error-rich variant), alone and with its class split
     "big_table": {"nc.big_table": 1},
     "big_table_split": {"nc.big_table": 1, "nc.edge_cap": 600, "nc.group_budget": 1},
+    # (round 4) the 6144-slot middle tier (two workgroups per CU), alone and with its class split
+    "mid_table": {"nc.big_table": 2},
+    "mid_table_split": {"nc.big_table": 2, "nc.edge_cap": 600, "nc.group_budget": 1},
     # every partition overflows the descriptor table: class split, then the raw path
     "desc_raw": {"nc.desc_cap": 2, "nc.fine_bits": 9},
     # level-3 buckets through the 256-thread LDS sort, the 1024-thread one, and the radix fallback

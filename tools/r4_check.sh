@@ -7,4 +7,4 @@ bash tools/abq.sh default ab/nocoop.so
 MCAAT_KNOBS=cf.compact=0 bash tools/abq.sh default
 MCAAT_KNOBS=cf.dls_persist=0 bash tools/abq.sh default
 CFG=c5 bash tools/abq.sh default
-CFG=c5 MCAAT_KNOBS=cf.compact=0,cf.dls_persist=0 bash tools/abq.sh default
+CFG=c5 MCAAT_KNOBS=cf.compact=0,cf.dls_persist=0,nc.big_table=1 bash tools/abq.sh default
