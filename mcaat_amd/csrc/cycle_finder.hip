@@ -1802,9 +1802,12 @@ static std::vector<uint64_t> run_dls_dev(mcaat_graph *g, const uint64_t *dcand, 
     hipStream_t st = ctx->stream;
     std::vector<uint64_t> pass;
     if (!n) return pass;
-    // (round 4) cf.dls_persist: per-lane scratch, candidates strided over the lanes (default);
-    // 0: one scratch slot per candidate in batches
-    const bool persist = knob(ctx, "cf.dls_persist", 1) != 0;
+    // (round 4) cf.dls_persist=1: per-lane scratch, candidates strided over the lanes; 0 (default):
+    // one scratch slot per candidate in batches
+    // measured: C3 2.6 ms either way, C5 49.0 ms against 42.4 for the batches (a persistent
+    // wave runs its lanes' candidate sequences to the longest sum, and finished waves leave their
+    // CU idle): off by default
+    const bool persist = knob(ctx, "cf.dls_persist", 0) != 0;
     const bool many = !persist && n * 8ULL * (1024 + 2048) > (8ULL << 30);
     uint32_t cs = (uint32_t)std::max<int64_t>(1, knob(ctx, "cf.dls_stack", many ? 128 : 1024));
     uint32_t cv = (uint32_t)next_pow2((uint64_t)std::max<int64_t>(2, knob(ctx, "cf.dls_visited", many ? 256 : 2048)));
@@ -2265,9 +2268,13 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
     // its own k_peel_init)
     PeelState ps;
     const bool fuse = !comm && knob(ctx, "cf.walk_budget", 0) <= 0 && knob(ctx, "cf.fused_init", 1) != 0 && D;
-    // (round 4) peel arrays over compact slots of the filtered edges (cf.compact=0: one per edge;
-    // the slots are 32-bit prefix counts, so graphs of 2^32 or more edges use one per edge)
-    const bool compact = knob(ctx, "cf.compact", 1) != 0 && D && D < (1ULL << 32) && knob(ctx, "cf.walk_budget", 0) <= 0;
+    // (round 4) cf.compact=1: peel arrays over compact slots of the filtered edges (default one per
+    // edge; the slots are 32-bit prefix counts, so graphs of 2^32 or more edges use one per edge)
+    // Measured (C3): compact slots 36.1 ms of peel against 23.2 with one slot per edge — the
+    // removal walks of long chains pay a binary search per edge (PeelArrays::gid) and the tips
+    // pass a prefix load per successor; C5 68.1 either way. Off by default (the memory saving
+    // stays available: C5's peel state 63 -> 12 GB).
+    const bool compact = knob(ctx, "cf.compact", 0) != 0 && D && D < (1ULL << 32) && knob(ctx, "cf.walk_budget", 0) <= 0;
     // the recount's counts and ChunkStartNodes' filter come from the tips / filter pass
     // (cf.recount = 1: the separate post-peel pass of round 2)
     const bool fold = knob(ctx, "cf.recount", 0) == 0;

@@ -1612,7 +1612,7 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
     const uint32_t cap_max_mid = (uint32_t)std::min<int64_t>(kCapMaxMid, std::max<int64_t>(1, knob(ctx, "nc.edge_cap", kCapMaxMid)));
     // larger edge tables: tier 0 = 4096 slots, 1 = 6144 (two workgroups per CU), 2 = 8192 (one).
     // knob nc.big_table fixes the tier (0, 1 = 8192 as in round 3, 2 = 6144); default: from the
-    // next group on, one tier up once a group split more than 1 in 8 of its partitions into
+    // next group on, 8192 slots once a group split more than 1 in 8 of its partitions into
     // classes (error-rich data)
     const int64_t big_knob = knob(ctx, "nc.big_table", -1);
     int tier = big_knob == 1 ? 2 : big_knob == 2 ? 1 : 0;
@@ -1695,7 +1695,9 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
             HIP_OK(hipStreamSynchronize(st));
             const uint64_t n_ovf = hc[1];
             ctx->kstats["lds_count_split_partitions"].launches += hc[2];
-            if (big_knob < 0 && tier < 2 && hc[2] * 8 > p1 - p0) tier = tier + 1;
+            // measured at C5: the 6144-slot tier still splits more than 1 in 8 partitions (183.6 ms
+            // of pass C either way), so the default goes straight to 8192 slots
+            if (big_knob < 0 && tier < 2 && hc[2] * 8 > p1 - p0) tier = 2;
             ctx->kstats["lds_count_overflow_partitions"].launches += n_ovf;
             if (n_ovf) {
                 // global-table fallback for the partitions whose distinct edges overflowed LDS,

@@ -307,8 +307,8 @@ def test_graph_from_sorted_rejects_bad_keys(gpu_ctx):
         assert ei.value.code == -1
 
 
-@pytest.mark.parametrize("frac", [0.02, 0.3])
-def test_cycle_finder_on_a_graph_with_invalid_edges(gpu_ctx, frac):
+@pytest.mark.parametrize("frac,compact", [(0.02, 0), (0.3, 0), (0.02, 1), (0.3, 1)])
+def test_cycle_finder_on_a_graph_with_invalid_edges(gpu_ctx, frac, compact):
     """CycleFinder on a graph whose valid bits were cleared before it runs (the host's
     SetInvalidEdge): the tips pass then reads the unfiltered bitmap (not every edge is valid), and
     the peel's compact slots cover only the edges valid after the filter. Stats, the valid bitmap
@@ -324,7 +324,8 @@ def test_cycle_finder_on_a_graph_with_invalid_edges(gpu_ctx, frac):
     v = og.valid().astype(np.uint8)
     v[drop.astype(np.int64)] = 0
     og.set_valid(v)
-    res = g.cycle_finder(prm)
+    with gpu_ctx.knobs(cf__compact=compact):
+        res = g.cycle_finder(prm)
     ores = og.cycle_finder(threshold_multiplicity=prm.threshold_multiplicity, low_abundance=prm.low_abundance,
                            cycle_max_length=prm.cycle_max_length, cycle_min_length=prm.cycle_min_length, threads=1)
     assert res.stats[:6] == ores["stats"]

@@ -92,15 +92,15 @@ KNOBS = {
     "dls_dev_regrow": {"cf.dls_stack": 1, "cf.dls_visited": 2},
     # the peel's first pass as its own kernel instead of inside the tips / filter pass
     "peel_own_init": {"cf.fused_init": 0},
-    # (round 4) peel arrays indexed by edge id instead of compact slots, with and without the
-    # fused first pass; the tips pass reading the unfiltered bitmap although every edge is valid
-    "peel_identity": {"cf.compact": 0},
-    "peel_identity_own_init": {"cf.compact": 0, "cf.fused_init": 0},
+    # (round 4) peel arrays over compact slots instead of edge ids, with and without the fused
+    # first pass; the tips pass reading the unfiltered bitmap although every edge is valid
+    "peel_compact": {"cf.compact": 1},
+    "peel_compact_own_init": {"cf.compact": 1, "cf.fused_init": 0},
     "tips_not_fresh": {"cf.fresh": 0},
-    "compact_lists_regrow": {"cf.peel_list_cap": 1, "cf.cand_cap": 1, "cf.fresh": 0},
-    # (round 4) DepthLevelSearch in per-candidate batches instead of per-lane scratch
-    "dls_batches": {"cf.dls_persist": 0},
-    "dls_batches_regrow": {"cf.dls_persist": 0, "cf.dls_stack": 1, "cf.dls_visited": 2},
+    "compact_lists_regrow": {"cf.compact": 1, "cf.peel_list_cap": 1, "cf.cand_cap": 1, "cf.fresh": 0},
+    # (round 4) DepthLevelSearch with per-lane scratch instead of per-candidate batches
+    "dls_persist": {"cf.dls_persist": 1},
+    "dls_persist_regrow": {"cf.dls_persist": 1, "cf.dls_stack": 1, "cf.dls_visited": 2},
     # passes B and C of successive groups in turn on one stream
     "nc_no_overlap": {"nc.overlap": 0, "nc.group_budget": 1 << 14},
     # adjacency: per-edge global directory searches; the owner-side runs (default) with every
