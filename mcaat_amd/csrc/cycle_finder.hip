@@ -279,10 +279,10 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_
                 }
                 cl.push(c, e);
             }
+            // (an edge invalid after the filter gets no kind byte: prep reads the filtered bitmap
+            // first, and every other pass reaches only valid edges)
             if (peel && e < g.D && w < w_hi) {
-                if (!vpf) {
-                    if (!pa.wpre) pa.kind(e) = kInvalid;  // (compact slots exist for valid edges only)
-                } else {
+                if (vpf) {
                     const uint64_t ce = pa.wpre ? (uint64_t)pa.wpre[w] + __popcll(pv[u] & lt) : e;
                     // compact slot of successor lo + i: its word is lo's or the next one
                     auto cs = [&](int i) -> uint64_t {
@@ -401,10 +401,7 @@ __device__ __forceinline__ bool peel_super_hash(uint64_t r) { return (mix64(r ^ 
 __global__ void __launch_bounds__(kBlock) k_peel_init(GraphView g, PeelArrays pa) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < g.D; e += stride) {
-        if (!bit_get(g.valid, e)) {
-            if (!pa.wpre) pa.kind(e) = kInvalid;
-            continue;
-        }
+        if (!bit_get(g.valid, e)) continue;  // no kind byte: prep reads the bitmap first
         uint64_t out[4];
         const int n = dev_outgoing(g, e, out);
         const uint64_t ce = pa.cidx(e);
