@@ -129,6 +129,9 @@ int mcaat_graph_download(const mcaat_graph *g, uint64_t *keys, uint16_t *mult, u
 /* the same for edges [first, first+count) (paged host views of graphs larger than host RAM) */
 int mcaat_graph_download_range(const mcaat_graph *g, uint64_t first, uint64_t count, uint64_t *keys, uint16_t *mult,
                                uint8_t *valid);
+/* the valid bitmap as it is on the device: (n_edges + 63) / 64 words, edge e at bit e % 64 of
+ * word e / 64 (the host SDBG mirror's IsValidEdge without a byte per edge: C3 126 MB, not 1 GB) */
+int mcaat_graph_valid_words(const mcaat_graph *g, uint64_t *words);
 /* Keeps device valid bits coherent with host SetInvalidEdge/SetValidEdge
  * (spacer_ordering.cpp:96-138 mutates them downstream). */
 int mcaat_graph_set_valid(mcaat_graph *g, const uint64_t *ids, size_t n, int valid);

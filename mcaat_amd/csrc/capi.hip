@@ -739,6 +739,14 @@ int mcaat_graph_download(const mcaat_graph *g, uint64_t *keys, uint16_t *mult, u
     });
 }
 
+int mcaat_graph_valid_words(const mcaat_graph *g, uint64_t *words) {
+    return guarded([&] {
+        require(g != nullptr && (words || g->D == 0), "null argument");
+        HIP_OK(hipSetDevice(g->ctx->device));
+        if (g->D) HIP_OK(hipMemcpy(words, g->valid.p, 8 * g->n_words(), hipMemcpyDeviceToHost));
+    });
+}
+
 int mcaat_graph_download_range(const mcaat_graph *g, uint64_t first, uint64_t count, uint64_t *keys, uint16_t *mult,
                                uint8_t *valid) {
     return guarded([&] {

@@ -108,11 +108,19 @@ std::vector<std::vector<uint64_t>> find_strongly_connected_components(const SDBG
 // (the reference's k rounds over the whole set reach exactly the k-hop neighbourhood), then
 // every valid edge outside that set is invalidated.
 void keep_crispr_regions_extended_by_k(SDBG &sdbg, const size_t &k, const std::vector<std::vector<uint64_t>> &cycles) {
-    std::unordered_set<uint64_t> region;
+    IdMap<char> region;  // membership (the order of `keep` does not matter: one bitmap AND)
+    std::vector<uint64_t> keep;
+    auto insert = [&](uint64_t e) {
+        char &c = region[e];
+        if (c) return false;
+        c = 1;
+        keep.push_back(e);
+        return true;
+    };
     std::vector<uint64_t> frontier;
     for (const auto &cycle : cycles)
         for (uint64_t e : cycle)
-            if (region.insert(e).second) frontier.push_back(e);
+            if (insert(e)) frontier.push_back(e);
     std::vector<uint64_t> nb;
     std::vector<int32_t> cnt;
     for (size_t hop = 0; hop < k && !frontier.empty(); ++hop) {
@@ -124,11 +132,10 @@ void keep_crispr_regions_extended_by_k(SDBG &sdbg, const size_t &k, const std::v
             sdbg.NeighborsBatch(expand, dir == 0, nb, cnt);
             for (size_t i = 0; i < expand.size(); ++i)
                 for (int j = 0; j < cnt[i]; ++j)
-                    if (region.insert(nb[4 * i + j]).second) next.push_back(nb[4 * i + j]);
+                    if (insert(nb[4 * i + j])) next.push_back(nb[4 * i + j]);
         }
         frontier.swap(next);
     }
-    std::vector<uint64_t> keep(region.begin(), region.end());
     sdbg.KeepOnly(keep);
     // every node the SCC split and the subgraphs query from here on is one of these: their
     // out-neighbours (valid-only, after the AND) and labels in two device calls
@@ -142,15 +149,27 @@ void keep_crispr_regions_extended_by_k(SDBG &sdbg, const size_t &k, const std::v
 // spacer_ordering.cpp:140-173: one Graph per SCC, edges inside the component only
 std::vector<Graph> divide_graph_into_subgraphs(const SDBG &sdbg) {
     std::vector<Graph> subgraphs;
-    for (const auto &comp : find_strongly_connected_components(sdbg)) {
-        const std::unordered_set<uint64_t> inside(comp.begin(), comp.end());
+    const auto comps = find_strongly_connected_components(sdbg);
+    // component of every node (components are disjoint), one flat map for all of them
+    IdMap<uint32_t> comp_of;
+    size_t total = 0;
+    for (const auto &c : comps) total += c.size();
+    comp_of.reserve(total);
+    for (uint32_t ci = 0; ci < comps.size(); ++ci)
+        for (uint64_t e : comps[ci]) comp_of[e] = ci + 1;
+    for (uint32_t ci = 0; ci < comps.size(); ++ci) {
+        const auto &comp = comps[ci];
         Graph sub;
+        sub.nodes.reserve(comp.size());
+        sub.adjacency_list.reserve(comp.size());
         for (uint64_t e : comp) {
             if (!sdbg.IsValidEdge(e) || sdbg.EdgeOutdegree(e) <= 0) continue;
             uint64_t out[4];
             const int n = sdbg.OutgoingEdges(e, out);
-            for (int i = 0; i < n; ++i)
-                if (inside.count(out[i])) sub.add_edge(e, out[i]);
+            for (int i = 0; i < n; ++i) {
+                const uint32_t *c = comp_of.find(out[i]);
+                if (c && *c == ci + 1) sub.add_edge(e, out[i]);
+            }
         }
         if (!sub.nodes.empty()) subgraphs.push_back(std::move(sub));
     }
@@ -196,14 +215,20 @@ void get_relevant_reads_and_cycles(const std::vector<Graph> &regions, const std:
                                    const std::vector<std::vector<uint64_t>> &all_cycles,
                                    std::vector<std::vector<std::vector<uint64_t>>> &reads_out,
                                    std::vector<std::vector<std::vector<uint64_t>>> &cycles_out) {
-    std::unordered_map<uint64_t, uint32_t> region_of;
+    IdMap<uint32_t> region_of;  // region + 1 (regions are disjoint SCCs)
+    size_t total = 0;
+    for (const auto &r : regions) total += r.nodes.size();
+    region_of.reserve(total);
     for (uint32_t i = 0; i < regions.size(); ++i)
-        for (uint64_t x : regions[i].nodes) region_of.emplace(x, i);
+        for (uint64_t x : regions[i].nodes) {
+            uint32_t &v = region_of[x];
+            if (!v) v = i + 1;
+        }
     reads_out.assign(regions.size(), {});
     cycles_out.assign(regions.size(), {});
     auto find = [&](uint64_t x) {
-        auto it = region_of.find(x);
-        return it == region_of.end() ? UINT32_MAX : it->second;
+        const uint32_t *v = region_of.find(x);
+        return v ? *v - 1 : UINT32_MAX;
     };
     for (const auto &r : all_reads) {
         const uint32_t a = find(r.at(0)), b = find(r.at(r.size() - 1));

@@ -146,7 +146,7 @@ void SDBG::LoadFromDevice(mcaat_graph *g) {
     ocache_.clear();
     std::vector<uint64_t>().swap(key_);
     std::vector<uint16_t>().swap(mult_);
-    std::vector<uint8_t>().swap(valid_);
+    std::vector<uint64_t>().swap(vbits_);
 }
 
 void SDBG::LoadFromFile(const char *path) {
@@ -172,7 +172,9 @@ void SDBG::LoadFromArrays(int k, std::vector<uint64_t> keys, std::vector<uint16_
     D_ = keys.size();
     key_ = std::move(keys);
     mult_ = std::move(mult);
-    valid_ = std::move(valid);
+    vbits_.assign((D_ + 63) / 64, 0);
+    for (uint64_t e = 0; e < D_; ++e)
+        if (valid[e]) vbits_[e >> 6] |= 1ULL << (e & 63);
     have_arrays_ = have_valid_ = true;
     kcache_.clear();
     ocache_.clear();
@@ -193,13 +195,13 @@ const std::vector<uint16_t> &SDBG::host_mult() const {
     return mult_;
 }
 
-const std::vector<uint8_t> &SDBG::host_valid() const {
+const std::vector<uint64_t> &SDBG::host_valid() const {
     if (!have_valid_ && g_) {
-        valid_.resize(D_);
-        mcaat_check(mcaat_graph_download(g_, nullptr, nullptr, valid_.data()), "mcaat_graph_download");
+        vbits_.resize((D_ + 63) / 64);
+        mcaat_check(mcaat_graph_valid_words(g_, vbits_.data()), "mcaat_graph_valid_words");
         have_valid_ = true;
     }
-    return valid_;
+    return vbits_;
 }
 
 void SDBG::SyncFromDevice() {
@@ -214,22 +216,22 @@ void SDBG::KeepOnly(const std::vector<uint64_t> &ids) {
         // array)
         std::vector<uint64_t> live;
         for (uint64_t e : ids)
-            if (e < valid_.size() && valid_[e]) live.push_back(e);
-        std::fill(valid_.begin(), valid_.end(), 0);
-        for (uint64_t e : live) valid_[e] = 1;
+            if (e < D_ && ((vbits_[e >> 6] >> (e & 63)) & 1)) live.push_back(e);
+        std::fill(vbits_.begin(), vbits_.end(), 0);
+        for (uint64_t e : live) vbits_[e >> 6] |= 1ULL << (e & 63);
     }
     if (g_) mcaat_check(mcaat_graph_keep_only(g_, ids.data(), ids.size()), "mcaat_graph_keep_only");
 }
 
 void SDBG::SetInvalidEdge(uint64_t e) {
     ocache_.clear();
-    if (have_valid_ || !g_) valid_[e] = 0;
+    if (have_valid_ || !g_) vbits_[e >> 6] &= ~(1ULL << (e & 63));
     if (g_) mcaat_check(mcaat_graph_set_valid(g_, &e, 1, 0), "mcaat_graph_set_valid");
 }
 
 void SDBG::SetValidEdge(uint64_t e) {
     ocache_.clear();
-    if (have_valid_ || !g_) valid_[e] = 1;
+    if (have_valid_ || !g_) vbits_[e >> 6] |= 1ULL << (e & 63);
     if (g_) mcaat_check(mcaat_graph_set_valid(g_, &e, 1, 1), "mcaat_graph_set_valid");
 }
 
@@ -240,34 +242,33 @@ uint64_t SDBG::lower(uint64_t q) const {
 
 int SDBG::OutgoingEdges(uint64_t e, uint64_t *out) const {
     if (!ocache_.empty()) {
-        auto it = ocache_.find(e);
-        if (it != ocache_.end()) {
-            const int n = (int)it->second[0];
-            for (int i = 0; i < n; ++i) out[i] = it->second[1 + i];
+        if (const auto *a = ocache_.find(e)) {
+            const int n = (int)(*a)[0];
+            for (int i = 0; i < n; ++i) out[i] = (*a)[1 + i];
             return n;
         }
     }
     const auto &key_ = host_key();
-    const auto &valid_ = host_valid();
+    const auto &vb = host_valid();
     const uint64_t K = key_[e], W = K & 3, R = K >> 2;
     const uint64_t Rt = (W << (2 * (k_ - 1))) | (R >> 2);
     uint64_t tmp[4];
     int n = 0;
     for (uint64_t i = lower(Rt << 2); i < size() && (key_[i] >> 2) == Rt; ++i)
-        if (valid_[i]) tmp[n++] = i;
+        if ((vb[i >> 6] >> (i & 63)) & 1) tmp[n++] = i;
     for (int i = 0; i < n; ++i) out[i] = tmp[n - 1 - i];
     return n;
 }
 
 int SDBG::IncomingEdges(uint64_t e, uint64_t *in) const {
     const auto &key_ = host_key();
-    const auto &valid_ = host_valid();
+    const auto &vb = host_valid();
     const uint64_t K = key_[e];
     const uint64_t c = (K >> (2 * k_)) & 3;
     const uint64_t G = (K >> 2) & ((1ULL << (2 * (k_ - 1))) - 1);
     int n = 0;
     for (uint64_t i = lower(G << 4); i < size() && (key_[i] >> 4) == G; ++i)
-        if ((key_[i] & 3) == c && valid_[i]) in[n++] = i;
+        if ((key_[i] & 3) == c && ((vb[i >> 6] >> (i & 63)) & 1)) in[n++] = i;
     return n;
 }
 
@@ -289,11 +290,12 @@ void SDBG::PrefetchKeys(const std::vector<uint64_t> &ids) {
     if (!g_ || ids.empty()) return;
     std::vector<uint64_t> want;
     for (uint64_t e : ids)
-        if (!kcache_.count(e)) want.push_back(e);
+        if (!kcache_.contains(e)) want.push_back(e);
     if (want.empty()) return;
     std::vector<uint64_t> kk(want.size());
     std::vector<uint16_t> mm(want.size());
     mcaat_check(mcaat_graph_gather(g_, want.data(), want.size(), kk.data(), mm.data()), "mcaat_graph_gather");
+    kcache_.reserve(kcache_.size() + want.size());
     for (size_t i = 0; i < want.size(); ++i) kcache_[want[i]] = {kk[i], mm[i]};
 }
 
@@ -302,6 +304,7 @@ void SDBG::PrefetchOutgoing(const std::vector<uint64_t> &ids) {
     std::vector<uint64_t> nb;
     std::vector<int32_t> cnt;
     NeighborsBatch(ids, false, nb, cnt);
+    ocache_.reserve(ocache_.size() + ids.size());
     for (size_t i = 0; i < ids.size(); ++i) {
         std::array<uint64_t, 5> a{(uint64_t)cnt[i], 0, 0, 0, 0};
         for (int j = 0; j < cnt[i]; ++j) a[1 + j] = nb[4 * i + j];
@@ -312,23 +315,14 @@ void SDBG::PrefetchOutgoing(const std::vector<uint64_t> &ids) {
 std::vector<uint64_t> SDBG::ValidIds() const {
     const auto &v = host_valid();
     std::vector<uint64_t> out;
-    const uint64_t n = v.size(), nw = n / 8;
-    const uint8_t *p = v.data();
-    for (uint64_t w = 0; w < nw; ++w) {  // eight bytes at a time, all-zero words skipped
-        uint64_t x;
-        memcpy(&x, p + 8 * w, 8);
-        if (!x) continue;
-        for (int j = 0; j < 8; ++j)
-            if (p[8 * w + j]) out.push_back(8 * w + j);
-    }
-    for (uint64_t e = 8 * nw; e < n; ++e)
-        if (p[e]) out.push_back(e);
+    for (uint64_t w = 0; w < v.size(); ++w)  // all-zero words skipped
+        for (uint64_t x = v[w]; x; x &= x - 1) out.push_back(64 * w + (uint64_t)__builtin_ctzll(x));
     return out;
 }
 
 uint32_t SDBG::GetLabel(uint64_t e, uint8_t *seq) const {
-    auto it = kcache_.find(e);
-    const uint64_t R = (it != kcache_.end() ? it->second.first : host_key()[e]) >> 2;
+    const auto *kc = kcache_.find(e);
+    const uint64_t R = (kc ? kc->first : host_key()[e]) >> 2;
     for (int i = 0; i < k_; ++i) seq[i] = (uint8_t)(((R >> (2 * i)) & 3) + 1);
     return (uint32_t)k_;
 }

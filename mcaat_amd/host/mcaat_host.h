@@ -48,6 +48,65 @@ class SDBGBuild {
     mcaat_graph *graph_ = nullptr;
 };
 
+// Open-addressing map from edge ids (never ~0) to V, linear probing in a power-of-two table
+// kept at most half full: the host caches of the downstream steps hold ~1M entries at C3, where
+// std::unordered_map's node allocations dominated step 7.
+template <class V>
+class IdMap {
+   public:
+    void clear() {
+        keys_.clear();
+        vals_.clear();
+        n_ = 0;
+    }
+    bool empty() const { return n_ == 0; }
+    size_t size() const { return n_; }
+    void reserve(size_t n) {
+        size_t cap = 16;
+        while (cap < 2 * n + 2) cap <<= 1;
+        if (cap > keys_.size()) rehash(cap);
+    }
+    const V *find(uint64_t k) const {
+        if (keys_.empty()) return nullptr;
+        for (size_t i = slot(k);; i = (i + 1) & (keys_.size() - 1)) {
+            if (keys_[i] == k) return &vals_[i];
+            if (keys_[i] == kEmpty) return nullptr;
+        }
+    }
+    bool contains(uint64_t k) const { return find(k) != nullptr; }
+    V &operator[](uint64_t k) {
+        if (2 * (n_ + 1) > keys_.size()) rehash(keys_.empty() ? 16 : 2 * keys_.size());
+        size_t i = slot(k);
+        for (; keys_[i] != k; i = (i + 1) & (keys_.size() - 1))
+            if (keys_[i] == kEmpty) {
+                keys_[i] = k;
+                vals_[i] = V{};
+                ++n_;
+                break;
+            }
+        return vals_[i];
+    }
+
+   private:
+    static constexpr uint64_t kEmpty = ~0ULL;
+    size_t slot(uint64_t k) const {
+        uint64_t x = k * 0x9E3779B97F4A7C15ULL;
+        return (size_t)(x ^ (x >> 29)) & (keys_.size() - 1);
+    }
+    void rehash(size_t cap) {
+        std::vector<uint64_t> ok(cap, kEmpty);
+        std::vector<V> ov(cap);
+        ok.swap(keys_);
+        ov.swap(vals_);
+        n_ = 0;
+        for (size_t i = 0; i < ok.size(); ++i)
+            if (ok[i] != kEmpty) (*this)[ok[i]] = ov[i];
+    }
+    std::vector<uint64_t> keys_;
+    std::vector<V> vals_;
+    size_t n_ = 0;
+};
+
 // MEGAHIT SDBG API subset, valid-only neighbour semantics (DESIGN.md "SDBG conventions").
 // Queries run on a host mirror of the device arrays; SetInvalidEdge/SetValidEdge update both.
 class SDBG {
@@ -71,7 +130,7 @@ class SDBG {
 
     uint64_t size() const { return D_; }
     int k() const { return k_; }
-    bool IsValidEdge(uint64_t e) const { return host_valid()[e] != 0; }
+    bool IsValidEdge(uint64_t e) const { return (host_valid()[e >> 6] >> (e & 63)) & 1; }
     void SetInvalidEdge(uint64_t e);
     void SetValidEdge(uint64_t e);
     uint16_t EdgeMultiplicity(uint64_t e) const { return host_mult()[e]; }
@@ -110,16 +169,17 @@ class SDBG {
     // are re-read after a device-side mutation.
     const std::vector<uint64_t> &host_key() const;
     const std::vector<uint16_t> &host_mult() const;
-    const std::vector<uint8_t> &host_valid() const;
+    // the valid bits as a bitmap (edge e: bit e % 64 of word e / 64), 1 bit per edge on the host
+    const std::vector<uint64_t> &host_valid() const;
     mcaat_graph *g_ = nullptr;
     int k_ = 0;
     uint64_t D_ = 0;
     mutable bool have_arrays_ = false, have_valid_ = false;
     mutable std::vector<uint64_t> key_;
     mutable std::vector<uint16_t> mult_;
-    mutable std::vector<uint8_t> valid_;
-    std::unordered_map<uint64_t, std::pair<uint64_t, uint16_t>> kcache_;  // id -> (key, mult)
-    std::unordered_map<uint64_t, std::array<uint64_t, 5>> ocache_;       // id -> (n, out[4])
+    mutable std::vector<uint64_t> vbits_;
+    IdMap<std::pair<uint64_t, uint16_t>> kcache_;  // id -> (key, mult)
+    IdMap<std::array<uint64_t, 5>> ocache_;       // id -> (n, out[4])
 };
 
 // Reference: CycleFinder(Settings&) runs FindApproximateCRISPRArrays in the constructor and

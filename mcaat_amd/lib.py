@@ -116,6 +116,7 @@ SIGNATURES = {
     "mcaat_graph_save": (C.c_int, [C.c_void_p, C.c_char_p]),
     "mcaat_graph_load": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_void_p)]),
     "mcaat_graph_download_range": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, _u64p, _u16p, _u8p]),
+    "mcaat_graph_valid_words": (C.c_int, [C.c_void_p, _u64p]),
     "mcaat_comm_unique_id": (C.c_int, [_u8p]),
     "mcaat_comm_init_rccl": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p, C.POINTER(C.c_void_p)]),
     "mcaat_comm_init_shm": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_char_p, C.c_uint64, C.POINTER(C.c_void_p)]),

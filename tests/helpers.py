@@ -73,3 +73,42 @@ def brute_neighbors(edges, k):
         preds = [index[x + e[:k]] for x in "ACGT" if (x + e[:k]) in index]
         inc.append(sorted(preds))
     return out, inc
+
+
+class HipBuffer:
+    """A device buffer from the HIP runtime libmcaat_gpu.so itself links (libamdhip64), for tests
+    that hand device pointers to the C ABI. (torch ships its own HIP runtime; two runtimes in one
+    process do not reliably share the device, so tests do not mix torch in.)"""
+
+    _hip = None
+
+    @classmethod
+    def hip(cls):
+        if cls._hip is None:
+            import ctypes
+
+            import mcaat_amd as M
+
+            M.load_library()  # the runtime it links is then in the process: reuse that very file
+            path = next(ln.split()[-1] for ln in open("/proc/self/maps") if "libamdhip64" in ln)
+            cls._hip = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+        return cls._hip
+
+    def __init__(self, arr: np.ndarray):
+        import ctypes
+
+        arr = np.ascontiguousarray(arr)
+        h = self.hip()
+        self.ptr = ctypes.c_void_p()
+        assert h.hipMalloc(ctypes.byref(self.ptr), ctypes.c_size_t(max(arr.nbytes, 8))) == 0
+        assert h.hipMemcpy(self.ptr, arr.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(arr.nbytes), 1) == 0
+        assert h.hipDeviceSynchronize() == 0
+
+    @property
+    def addr(self) -> int:
+        return int(self.ptr.value)
+
+    def __del__(self):
+        if getattr(self, "ptr", None) is not None and self.ptr.value:
+            self.hip().hipFree(self.ptr)
+            self.ptr = None

@@ -270,19 +270,16 @@ def test_graph_from_sorted_rejects_bad_keys(gpu_ctx):
     """mcaat_graph_from_sorted takes sorted unique BOSS keys below 4^(k+1). The directory pass
     checks both and a violation is MCAAT_E_INVALID, not a silently wrong directory (the round-3
     clamp in k_dir kept out-of-range prefixes from writing past it, but built a wrong graph)."""
-    import torch
+    from tests.helpers import HipBuffer
 
     spec = M.SynthSpec()
     k = 23
     reads = M.Reads.synth(gpu_ctx, spec)
     keys, mult, _ = M.Graph.build(gpu_ctx, reads, k).download()
-    dev = torch.device("cuda", 0)
 
     def build(kk):
-        tk = torch.from_numpy(kk.view(np.int64).copy()).to(dev)
-        tm = torch.from_numpy(mult.view(np.int16).copy()).to(dev)
-        torch.cuda.synchronize()
-        return M.Graph.from_sorted(gpu_ctx, k, tk.data_ptr(), tm.data_ptr(), int(kk.size))
+        tk, tm = HipBuffer(kk), HipBuffer(mult)
+        return M.Graph.from_sorted(gpu_ctx, k, tk.addr, tm.addr, int(kk.size))
 
     g = build(keys)  # the good keys build the same graph
     k2, m2, _ = g.download()
