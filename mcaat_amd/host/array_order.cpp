@@ -147,9 +147,12 @@ void keep_crispr_regions_extended_by_k(SDBG &sdbg, const size_t &k, const std::v
 }
 
 // spacer_ordering.cpp:140-173: one Graph per SCC, edges inside the component only
+static double g_scc_s = 0;  // TIMING_REGIONS detail
 std::vector<Graph> divide_graph_into_subgraphs(const SDBG &sdbg) {
     std::vector<Graph> subgraphs;
+    const auto t0 = std::chrono::high_resolution_clock::now();
     const auto comps = find_strongly_connected_components(sdbg);
+    g_scc_s = std::chrono::duration<double>(std::chrono::high_resolution_clock::now() - t0).count();
     // component of every node (components are disjoint), one flat map for all of them
     IdMap<uint32_t> comp_of;
     size_t total = 0;
@@ -184,7 +187,8 @@ std::vector<Graph> get_crispr_regions_extended_by_k(SDBG &sdbg, const size_t &k,
     const auto t1 = clk::now();
     auto out = divide_graph_into_subgraphs(sdbg);
     std::cout << "TIMING_REGIONS grow_s=" << std::chrono::duration<double>(t1 - t0).count()
-              << " divide_s=" << std::chrono::duration<double>(clk::now() - t1).count() << std::endl;
+              << " divide_s=" << std::chrono::duration<double>(clk::now() - t1).count() << " scc_s=" << g_scc_s
+              << std::endl;
     return out;
 }
 
@@ -627,13 +631,18 @@ struct WeightedConstraints {
 static WeightedConstraints generate_constraints_weighted(const std::vector<std::vector<uint64_t>> &reads,
                                                          const std::unordered_map<uint64_t, uint32_t> &node_to_cycle_map) {
     WeightedConstraints wc;
+    // the map's lookups (every node of every read) from a flat copy: the unordered_map itself
+    // only matters for its iteration order (get_all_cycle_indices)
+    IdMap<uint32_t> n2c;
+    n2c.reserve(node_to_cycle_map.size());
+    for (const auto &kv : node_to_cycle_map) n2c[kv.first] = kv.second;
     std::vector<uint32_t> seq;                   // cycle index per node, NOT_IN_ANY_CYCLE_INDEX outside
     std::vector<std::pair<uint32_t, int64_t>> runs;  // runs of the in-cycle subsequence
     for (const auto &r : reads) {
         seq.clear();
         for (uint64_t x : r) {
-            auto it = node_to_cycle_map.find(x);
-            seq.push_back(it == node_to_cycle_map.end() ? NOT_IN_ANY_CYCLE_INDEX : it->second);
+            const uint32_t *c = n2c.find(x);
+            seq.push_back(c ? *c : NOT_IN_ANY_CYCLE_INDEX);
         }
         runs.clear();
         for (uint32_t v : seq) {

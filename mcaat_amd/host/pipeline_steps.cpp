@@ -61,11 +61,16 @@ std::vector<FoundSystem> run_and_debug_spacer_ordering(const std::vector<std::ve
     };
     std::vector<Sub> subs(regions.size());
     const auto t_split = std::chrono::high_resolution_clock::now();
+    std::atomic<int64_t> ns_cover{0}, ns_order{0};  // CPU time of the two parts, summed over threads
     auto solve = [&](size_t ri) {
+        using hc = std::chrono::high_resolution_clock;
         Sub &s = subs[ri];
         auto rr = std::move(region_reads[ri]);
         s.cycles = std::move(region_cycles[ri]);
+        const auto a = hc::now();
         get_minimum_cycles_for_full_coverage(s.cycles);
+        const auto b = hc::now();
+        ns_cover += std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
         // the reverse-complement twin of a region is expected to carry no relevant reads
         if (rr.empty() || s.cycles.size() < 3) return;
         s.kept = true;
@@ -73,6 +78,7 @@ std::vector<FoundSystem> run_and_debug_spacer_ordering(const std::vector<std::ve
         std::ostringstream log;
         s.order = order_cycles(regions[ri], rr, s.cycles, s.conf_resolution, s.conf_sort, log);
         s.log = log.str();
+        ns_order += std::chrono::duration_cast<std::chrono::nanoseconds>(hc::now() - b).count();
     };
     if (threads == 0) threads = 1;
     threads = (unsigned)std::min<size_t>(threads, std::max<size_t>(1, regions.size()));
@@ -135,7 +141,8 @@ std::vector<FoundSystem> run_and_debug_spacer_ordering(const std::vector<std::ve
         const auto t_end = std::chrono::high_resolution_clock::now();
         std::cout << "TIMING_STEP7 regions_s=" << sec(t_regions - t0).count()
                   << " split_s=" << sec(t_split - t_regions).count() << " solve_s=" << sec(t_solved - t_split).count()
-                  << " emit_s=" << sec(t_end - t_solved).count() << " threads=" << threads << std::endl;
+                  << " emit_s=" << sec(t_end - t_solved).count() << " threads=" << threads
+                  << " cover_cpu_s=" << ns_cover.load() * 1e-9 << " order_cpu_s=" << ns_order.load() * 1e-9 << std::endl;
     }
     print_elapsed(t0);
     return found;
