@@ -216,8 +216,7 @@ std::vector<std::vector<uint64_t>> get_relevant_cycles(const Graph &graph,
 // the region holding its first node. Per region the lists are the same, in the same order, as
 // get_relevant_reads / get_relevant_cycles give (800 regions x 367K reads at C3: 27 s -> <1 s).
 void get_relevant_reads_and_cycles(const std::vector<Graph> &regions, const std::vector<std::vector<uint64_t>> &all_reads,
-                                   const std::vector<std::vector<uint64_t>> &all_cycles,
-                                   std::vector<std::vector<std::vector<uint64_t>>> &reads_out,
+                                   const std::vector<std::vector<uint64_t>> &all_cycles, std::vector<ReadRefs> &reads_out,
                                    std::vector<std::vector<std::vector<uint64_t>>> &cycles_out) {
     IdMap<uint32_t> region_of;  // region + 1 (regions are disjoint SCCs)
     size_t total = 0;
@@ -236,8 +235,8 @@ void get_relevant_reads_and_cycles(const std::vector<Graph> &regions, const std:
     };
     for (const auto &r : all_reads) {
         const uint32_t a = find(r.at(0)), b = find(r.at(r.size() - 1));
-        if (a != UINT32_MAX) reads_out[a].push_back(r);
-        if (b != UINT32_MAX && b != a) reads_out[b].push_back(r);
+        if (a != UINT32_MAX) reads_out[a].push_back(&r);
+        if (b != UINT32_MAX && b != a) reads_out[b].push_back(&r);
     }
     for (const auto &c : all_cycles) {
         if (c.empty()) {  // vacuously inside every region
@@ -628,7 +627,7 @@ struct WeightedConstraints {
     }
 };
 
-static WeightedConstraints generate_constraints_weighted(const std::vector<std::vector<uint64_t>> &reads,
+static WeightedConstraints generate_constraints_weighted(const ReadRefs &reads,
                                                          const std::unordered_map<uint64_t, uint32_t> &node_to_cycle_map) {
     WeightedConstraints wc;
     // the map's lookups (every node of every read) from a flat copy: the unordered_map itself
@@ -638,7 +637,8 @@ static WeightedConstraints generate_constraints_weighted(const std::vector<std::
     for (const auto &kv : node_to_cycle_map) n2c[kv.first] = kv.second;
     std::vector<uint32_t> seq;                   // cycle index per node, NOT_IN_ANY_CYCLE_INDEX outside
     std::vector<std::pair<uint32_t, int64_t>> runs;  // runs of the in-cycle subsequence
-    for (const auto &r : reads) {
+    for (const auto *rp : reads) {
+        const auto &r = *rp;
         seq.clear();
         for (uint64_t x : r) {
             const uint32_t *c = n2c.find(x);
@@ -734,7 +734,16 @@ static std::vector<uint32_t> solve_topological_weighted(const WeightedConstraint
 
 std::vector<uint32_t> order_cycles(const Graph &graph, const std::vector<std::vector<uint64_t>> &reads,
                                    const std::vector<std::vector<uint64_t>> &cycles, float &confidence_cycle_resolution,
-                                   float &confidence_topological_sort, std::ostream &log) {  // spacer_ordering.cpp:719-754
+                                   float &confidence_topological_sort, std::ostream &log) {
+    ReadRefs refs;
+    refs.reserve(reads.size());
+    for (const auto &r : reads) refs.push_back(&r);
+    return order_cycles(graph, refs, cycles, confidence_cycle_resolution, confidence_topological_sort, log);
+}
+
+std::vector<uint32_t> order_cycles(const Graph &graph, const ReadRefs &reads, const std::vector<std::vector<uint64_t>> &cycles,
+                                   float &confidence_cycle_resolution, float &confidence_topological_sort,
+                                   std::ostream &log) {  // spacer_ordering.cpp:719-754
     const auto node_to_cycle = get_node_to_unique_cycle_map(cycles);
     const auto cycle_ids = get_all_cycle_indices(node_to_cycle);
     const char *ref = getenv("MCAAT_ORDER_REF");
@@ -751,7 +760,10 @@ std::vector<uint32_t> order_cycles(const Graph &graph, const std::vector<std::ve
                   << std::setprecision(2) << (confidence_cycle_resolution * 100) << "%)" << std::endl;
         return solve_topological_weighted(wc, heuristic, cycle_ids, confidence_topological_sort);
     }
-    auto constraints = generate_constraints(graph, reads, node_to_cycle);
+    std::vector<std::vector<uint64_t>> copies;  // the list form (MCAAT_ORDER_REF=1) takes the reads themselves
+    copies.reserve(reads.size());
+    for (const auto *r : reads) copies.push_back(*r);
+    auto constraints = generate_constraints(graph, copies, node_to_cycle);
     log << "      ▸ " << constraints.size() << " constraints derived" << std::endl;
     std::unordered_map<uint32_t, int> heuristic;
     for (uint32_t c : cycle_ids) heuristic[c] = 0;

@@ -72,9 +72,11 @@ std::vector<std::vector<uint64_t>> get_relevant_reads(const Graph &graph,
                                                       const std::vector<std::vector<uint64_t>> &all_reads);
 std::vector<std::vector<uint64_t>> get_relevant_cycles(const Graph &graph,
                                                        const std::vector<std::vector<uint64_t>> &all_cycles);
+// a region's relevant reads as pointers into the relevant-read list (C3: 367K reads of 124 ids;
+// copying them per region was 365 MB of copies in step 7)
+using ReadRefs = std::vector<const std::vector<uint64_t> *>;
 void get_relevant_reads_and_cycles(const std::vector<Graph> &regions, const std::vector<std::vector<uint64_t>> &all_reads,
-                                   const std::vector<std::vector<uint64_t>> &all_cycles,
-                                   std::vector<std::vector<std::vector<uint64_t>>> &reads_out,
+                                   const std::vector<std::vector<uint64_t>> &all_cycles, std::vector<ReadRefs> &reads_out,
                                    std::vector<std::vector<std::vector<uint64_t>>> &cycles_out);
 void get_minimum_cycles_for_full_coverage(std::vector<std::vector<uint64_t>> &cycles);
 std::vector<size_t> solve_min_cover_problem(const std::unordered_set<uint32_t> &universe,
@@ -101,6 +103,9 @@ std::vector<uint32_t> solve_constraints_with_topological_sort(
 std::vector<uint32_t> order_cycles(const Graph &graph, const std::vector<std::vector<uint64_t>> &reads,
                                    const std::vector<std::vector<uint64_t>> &cycles, float &confidence_cycle_resolution,
                                    float &confidence_topological_sort, std::ostream &log = std::cout);
+std::vector<uint32_t> order_cycles(const Graph &graph, const ReadRefs &reads, const std::vector<std::vector<uint64_t>> &cycles,
+                                   float &confidence_cycle_resolution, float &confidence_topological_sort,
+                                   std::ostream &log = std::cout);
 std::vector<std::vector<uint64_t>> get_ordered_cycles(const std::vector<uint32_t> &cycle_order,
                                                       const std::vector<std::vector<uint64_t>> &cycles);
 

@@ -48,9 +48,10 @@ class SDBGBuild {
     mcaat_graph *graph_ = nullptr;
 };
 
-// Open-addressing map from edge ids (never ~0) to V, linear probing in a power-of-two table
-// kept at most half full: the host caches of the downstream steps hold ~1M entries at C3, where
-// std::unordered_map's node allocations dominated step 7.
+// Open-addressing map from edge ids to V, linear probing in a power-of-two table kept at most
+// half full: the host caches of the downstream steps hold ~1M entries at C3, where
+// std::unordered_map's node allocations dominated step 7. The empty-slot marker ~0 is also a
+// key callers use (a read's absent label, the reference's -1): it lives beside the table.
 template <class V>
 class IdMap {
    public:
@@ -58,6 +59,7 @@ class IdMap {
         keys_.clear();
         vals_.clear();
         n_ = 0;
+        has_max_ = false;
     }
     bool empty() const { return n_ == 0; }
     size_t size() const { return n_; }
@@ -67,6 +69,7 @@ class IdMap {
         if (cap > keys_.size()) rehash(cap);
     }
     const V *find(uint64_t k) const {
+        if (k == kEmpty) return has_max_ ? &max_val_ : nullptr;
         if (keys_.empty()) return nullptr;
         for (size_t i = slot(k);; i = (i + 1) & (keys_.size() - 1)) {
             if (keys_[i] == k) return &vals_[i];
@@ -75,6 +78,14 @@ class IdMap {
     }
     bool contains(uint64_t k) const { return find(k) != nullptr; }
     V &operator[](uint64_t k) {
+        if (k == kEmpty) {
+            if (!has_max_) {
+                has_max_ = true;
+                max_val_ = V{};
+                ++n_;
+            }
+            return max_val_;
+        }
         if (2 * (n_ + 1) > keys_.size()) rehash(keys_.empty() ? 16 : 2 * keys_.size());
         size_t i = slot(k);
         for (; keys_[i] != k; i = (i + 1) & (keys_.size() - 1))
@@ -98,13 +109,15 @@ class IdMap {
         std::vector<V> ov(cap);
         ok.swap(keys_);
         ov.swap(vals_);
-        n_ = 0;
+        n_ = has_max_ ? 1 : 0;
         for (size_t i = 0; i < ok.size(); ++i)
             if (ok[i] != kEmpty) (*this)[ok[i]] = ov[i];
     }
     std::vector<uint64_t> keys_;
     std::vector<V> vals_;
     size_t n_ = 0;
+    bool has_max_ = false;
+    V max_val_{};
 };
 
 // MEGAHIT SDBG API subset, valid-only neighbour semantics (DESIGN.md "SDBG conventions").

@@ -49,7 +49,8 @@ std::vector<FoundSystem> run_and_debug_spacer_ordering(const std::vector<std::ve
     const auto t_regions = std::chrono::high_resolution_clock::now();
 
     std::cout << "  🔄 Filtering subproblems:" << std::endl;
-    std::vector<std::vector<std::vector<uint64_t>>> region_reads, region_cycles;
+    std::vector<ReadRefs> region_reads;
+    std::vector<std::vector<std::vector<uint64_t>>> region_cycles;
     get_relevant_reads_and_cycles(regions, reads, cycles, region_reads, region_cycles);
     struct Sub {
         bool kept = false;
