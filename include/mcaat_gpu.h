@@ -145,6 +145,10 @@ int mcaat_graph_gather(const mcaat_graph *g, const uint64_t *ids, size_t n, uint
 /* valid &= {ids}: keep_crispr_regions_extended_by_k (spacer_ordering.cpp:129-137) invalidates
  * every valid edge outside the extended cycle set; here one bitmap AND on the device. */
 int mcaat_graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n);
+/* keep_crispr_regions_extended_by_k (spacer_ordering.cpp:78-138) whole on the device: the seeds
+ * grown by `hops` rounds over the valid in- and out-neighbours of the valid frontier nodes, then
+ * valid &= that region (one call instead of a host BFS of 2 x hops neighbour queries). */
+int mcaat_graph_keep_region(mcaat_graph *g, const uint64_t *seeds, size_t n, uint64_t hops);
 /* Checkpoint / resume. Replaces: the on-disk graph between SDBGBuild and CycleFinder
  * (MEGAHIT graph.sdbg* + SDBG::LoadFromFile, main.cpp:386-393, 522-530). The library's own
  * format (MEGAHIT's is unpinned offline): sorted BOSS keys, multiplicities and valid bits with

@@ -802,6 +802,13 @@ int mcaat_graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n) {
         graph_keep_only(g, ids, n);
     });
 }
+int mcaat_graph_keep_region(mcaat_graph *g, const uint64_t *seeds, size_t n, uint64_t hops) {
+    return guarded([&] {
+        require(g != nullptr && (n == 0 || seeds), "null argument");
+        HIP_OK(hipSetDevice(g->ctx->device));
+        graph_keep_region(g, seeds, n, hops);
+    });
+}
 
 int mcaat_graph_save(const mcaat_graph *g, const char *path) {
     return guarded([&] {

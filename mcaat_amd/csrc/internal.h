@@ -403,6 +403,7 @@ void graph_set_valid(mcaat_graph *g, const uint64_t *ids, size_t n, int valid);
 void graph_gather(const mcaat_graph *g, const uint64_t *ids, size_t n, uint64_t *keys, uint16_t *mult);
 void graph_download_valid(const mcaat_graph *g, uint8_t *valid);
 void graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n);
+void graph_keep_region(mcaat_graph *g, const uint64_t *seeds, size_t n, uint64_t hops);
 // FASTQ(.gz) inputs parsed on the GPU (fastq_ingest.hip)
 // ranges: per file, the byte range [first, second) to read (a rank's part; null: whole files)
 void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_reads *r,

@@ -213,6 +213,75 @@ void map_reads(const mcaat_graph *g, const mcaat_reads *r, const uint64_t *nodes
 
 // valid &= {ids}: keep_crispr_regions_extended_by_k's invalidation of every edge outside
 // the extended cycle set (spacer_ordering.cpp:129-137) as one bitmap AND
+// keep_crispr_regions_extended_by_k (spacer_ordering.cpp:78-138) on the device: the seeds grown
+// by `hops` rounds over the valid in- and out-edges of the valid frontier nodes, then valid &=
+// region. One launch per hop over the frontier (each node adds at most 4 + 4 neighbours, so the
+// next frontier is sized exactly); membership is a bitmap set by atomicOr, and the node whose
+// atomicOr set a bit appends it to the next frontier.
+__global__ void __launch_bounds__(kBlock) k_grow_seed(uint64_t *reg, const uint64_t *ids, uint64_t n, uint64_t D,
+                                                       uint64_t *front, unsigned long long *nf) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t e = ids[i];
+        if (e >= D) continue;
+        const unsigned long long b = 1ull << (e & 63);
+        if (!(atomicOr((unsigned long long *)&reg[e >> 6], b) & b)) front[atomicAdd(nf, 1ull)] = e;
+    }
+}
+__global__ void __launch_bounds__(kBlock) k_grow_hop(GraphView g, uint64_t *reg, const uint64_t *front, uint64_t nf,
+                                                      uint64_t *next, unsigned long long *nn) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += stride) {
+        const uint64_t e = front[i];
+        if (!bit_get(g.valid, e)) continue;
+        uint64_t nb[8];
+        int m = dev_outgoing(g, e, nb);
+        m += dev_incoming(g, e, nb + m);
+        for (int j = 0; j < m; ++j) {
+            const uint64_t x = nb[j];
+            const unsigned long long b = 1ull << (x & 63);
+            if (!(atomicOr((unsigned long long *)&reg[x >> 6], b) & b)) next[atomicAdd(nn, 1ull)] = x;
+        }
+    }
+}
+
+void graph_keep_region(mcaat_graph *g, const uint64_t *seeds, size_t n, uint64_t hops) {
+    hipStream_t st = g->ctx->stream;
+    const uint64_t nw = g->n_words();
+    if (!nw) return;
+    DevBuf<uint64_t> reg(nw);
+    HIP_OK(hipMemsetAsync(reg.p, 0, 8 * nw, st));
+    DevBuf<unsigned long long> cnt(1);
+    HIP_OK(hipMemsetAsync(cnt.p, 0, 8, st));
+    DevBuf<uint64_t> front(n ? n : 1);
+    uint64_t nf = 0;
+    if (n) {
+        DevBuf<uint64_t> di(n);
+        HIP_OK(hipMemcpyAsync(di.p, seeds, 8 * n, hipMemcpyHostToDevice, st));
+        hipLaunchKernelGGL(k_grow_seed, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, reg.p, di.p, (uint64_t)n, g->D,
+                           front.p, cnt.p);
+        LAUNCH_OK();
+        unsigned long long hn = 0;
+        d2h(g->ctx, &hn, cnt.p, 8);
+        nf = hn;
+    }
+    for (uint64_t h = 0; h < hops && nf; ++h) {
+        DevBuf<uint64_t> next(8 * nf);
+        HIP_OK(hipMemsetAsync(cnt.p, 0, 8, st));
+        hipLaunchKernelGGL(k_grow_hop, dim3(grid_for(nf, kBlock)), dim3(kBlock), 0, st, g->view(), reg.p,
+                           (const uint64_t *)front.p, nf, next.p, cnt.p);
+        LAUNCH_OK();
+        unsigned long long hn = 0;
+        d2h(g->ctx, &hn, cnt.p, 8);
+        nf = hn;
+        front = std::move(next);
+    }
+    hipLaunchKernelGGL(k_and_bits, dim3(grid_for(nw, kBlock)), dim3(kBlock), 0, st, g->valid.p, reg.p, nw);
+    g->all_valid = false;
+    LAUNCH_OK();
+    HIP_OK(hipStreamSynchronize(st));
+}
+
 void graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n) {
     hipStream_t st = g->ctx->stream;
     const uint64_t nw = g->n_words();

@@ -31,9 +31,13 @@ struct Tarjan {
     std::vector<uint32_t> stack;
     std::vector<std::vector<uint64_t>> components;
     int counter = 0;
+    IdMap<uint32_t> at;  // id -> position in ids (a flat map: a binary search per edge was most of the SCC time)
     Tarjan(const SDBG &s, const std::vector<uint64_t> &v)
-        : g(s), ids(v), index(v.size(), -1), low(v.size(), 0), on_stack(v.size(), 0) {}
-    uint32_t pos(uint64_t e) const { return (uint32_t)(std::lower_bound(ids.begin(), ids.end(), e) - ids.begin()); }
+        : g(s), ids(v), index(v.size(), -1), low(v.size(), 0), on_stack(v.size(), 0) {
+        at.reserve(v.size());
+        for (uint32_t i = 0; i < v.size(); ++i) at[v[i]] = i;
+    }
+    uint32_t pos(uint64_t e) const { return *at.find(e); }
 
     struct Frame {
         uint32_t v;
@@ -108,6 +112,15 @@ std::vector<std::vector<uint64_t>> find_strongly_connected_components(const SDBG
 // (the reference's k rounds over the whole set reach exactly the k-hop neighbourhood), then
 // every valid edge outside that set is invalidated.
 void keep_crispr_regions_extended_by_k(SDBG &sdbg, const size_t &k, const std::vector<std::vector<uint64_t>> &cycles) {
+    if (sdbg.device()) {  // the whole growth and the AND on the GPU, one call
+        std::vector<uint64_t> seeds;
+        for (const auto &cycle : cycles) seeds.insert(seeds.end(), cycle.begin(), cycle.end());
+        sdbg.KeepRegion(seeds, k);
+        const std::vector<uint64_t> live = sdbg.ValidIds();
+        sdbg.PrefetchOutgoing(live);
+        sdbg.PrefetchKeys(live);
+        return;
+    }
     IdMap<char> region;  // membership (the order of `keep` does not matter: one bitmap AND)
     std::vector<uint64_t> keep;
     auto insert = [&](uint64_t e) {

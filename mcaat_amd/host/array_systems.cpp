@@ -46,15 +46,29 @@ std::tuple<std::string, std::vector<std::string>, std::string> get_systems(
     int shortest = ordered_cycles.at(0).size();
     for (const auto &c : ordered_cycles) shortest = std::min<int>(shortest, c.size());
 
+    // one symbol of a node's label (fetch_node_label(...).at(0) / .back()) without building the
+    // label string: C3 has 800 regions of ~24 cycles of ~70 nodes, and a k-symbol string per look
+    // was most of the step's emit time
+    const int kk = sdbg.k();
+    auto symbol = [&](uint64_t node, bool last_symbol) {
+        uint8_t seq[64];
+        sdbg.GetLabel(node, seq);
+        return "ACGT"[seq[last_symbol ? kk - 1 : 0] - 1];
+    };
     // label symbol at `pos` of every cycle (front: first symbol, back: last symbol)
     auto distinct_at = [&](bool from_end, int i, bool last_symbol) {
-        std::unordered_set<char> seen;
+        bool seen[4] = {false, false, false, false};
+        size_t n = 0;
         for (const auto &c : ordered_cycles) {
             const uint64_t node = from_end ? c.at(c.size() - i - 1) : c.at(i);
-            const std::string label = fetch_node_label(sdbg, node);
-            seen.insert(last_symbol ? label.back() : label.at(0));
+            const char ch = symbol(node, last_symbol);
+            const int b = ch == 'A' ? 0 : ch == 'C' ? 1 : ch == 'G' ? 2 : 3;
+            if (!seen[b]) {
+                seen[b] = true;
+                ++n;
+            }
         }
-        return seen.size();
+        return n;
     };
     int right = 0;
     for (int i = 0; i < shortest - 1; ++i) {
@@ -77,7 +91,7 @@ std::tuple<std::string, std::vector<std::string>, std::string> get_systems(
         std::string spacer, repeat;
         const int shift = c.size() - left;
         for (int i = 0; i < (int)c.size(); ++i) {
-            const char last = fetch_node_label(sdbg, c.at((shift + i) % c.size())).back();
+            const char last = symbol(c.at((shift + i) % c.size()), true);
             (i < repeat_length ? repeat : spacer) += last;
         }
         spacers.push_back(spacer);

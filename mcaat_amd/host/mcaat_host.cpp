@@ -223,6 +223,13 @@ void SDBG::KeepOnly(const std::vector<uint64_t> &ids) {
     if (g_) mcaat_check(mcaat_graph_keep_only(g_, ids.data(), ids.size()), "mcaat_graph_keep_only");
 }
 
+void SDBG::KeepRegion(const std::vector<uint64_t> &seeds, uint64_t hops) {
+    if (!g_) throw std::runtime_error("SDBG::KeepRegion: no device graph");
+    ocache_.clear();
+    mcaat_check(mcaat_graph_keep_region(g_, seeds.data(), seeds.size(), hops), "mcaat_graph_keep_region");
+    have_valid_ = false;
+}
+
 void SDBG::SetInvalidEdge(uint64_t e) {
     ocache_.clear();
     if (have_valid_ || !g_) vbits_[e >> 6] &= ~(1ULL << (e & 63));

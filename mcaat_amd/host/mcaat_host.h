@@ -139,6 +139,9 @@ class SDBG {
     void SyncFromDevice();
     // valid &= {ids} on the host mirror and the device graph (one bitmap AND on the GPU)
     void KeepOnly(const std::vector<uint64_t> &ids);
+    // device graphs: valid &= the seeds grown by `hops` rounds over valid neighbours, on the GPU
+    // (mcaat_graph_keep_region); the host mirror re-reads the bits on its next query
+    void KeepRegion(const std::vector<uint64_t> &seeds, uint64_t hops);
     mcaat_graph *device() const { return g_; }
 
     uint64_t size() const { return D_; }

@@ -117,6 +117,7 @@ SIGNATURES = {
     "mcaat_graph_load": (C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_void_p)]),
     "mcaat_graph_download_range": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, _u64p, _u16p, _u8p]),
     "mcaat_graph_valid_words": (C.c_int, [C.c_void_p, _u64p]),
+    "mcaat_graph_keep_region": (C.c_int, [C.c_void_p, _u64p, C.c_size_t, C.c_uint64]),
     "mcaat_comm_unique_id": (C.c_int, [_u8p]),
     "mcaat_comm_init_rccl": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p, C.POINTER(C.c_void_p)]),
     "mcaat_comm_init_shm": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_char_p, C.c_uint64, C.POINTER(C.c_void_p)]),
@@ -637,6 +638,11 @@ class Graph:
         mm = np.zeros(max(ids.size, 1), dtype=np.uint16)
         _check(self.ctx._lib.mcaat_graph_gather(self.h, _ptr(ids, _u64p), ids.size, _ptr(kk, _u64p), _ptr(mm, _u16p)))
         return kk[: ids.size], mm[: ids.size]
+
+    def keep_region(self, seeds: np.ndarray, hops: int) -> None:
+        """valid &= seeds grown by `hops` rounds over valid neighbours (mcaat_graph_keep_region)."""
+        seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
+        _check(self.ctx._lib.mcaat_graph_keep_region(self.h, _ptr(seeds, _u64p), seeds.size, hops))
 
     def keep_only(self, ids: np.ndarray) -> None:
         """valid &= {ids} (keep_crispr_regions_extended_by_k, spacer_ordering.cpp:129-137)."""

@@ -330,3 +330,40 @@ def test_cycle_finder_on_a_graph_with_invalid_edges(gpu_ctx, frac, compact):
     _, _, valid = g.download()
     assert np.array_equal(valid, og.valid())
     assert [(s, c) for s, c in res.entries] == [tuple(e) for e in ores["entries"]]
+
+
+@pytest.mark.parametrize("hops", [0, 1, 5, 40])
+def test_keep_region_equals_host_growth(gpu_ctx, hops):
+    """mcaat_graph_keep_region (step 7's keep_crispr_regions_extended_by_k on the device) equals the
+    host growth: seeds grown `hops` rounds over valid in/out neighbours of valid frontier nodes,
+    then valid &= region."""
+    spec, k, prm = CONFIGS["pe_err"]
+    reads = M.Reads.synth(gpu_ctx, spec)
+    g = M.Graph.build(gpu_ctx, reads, k)
+    rng = np.random.default_rng(hops)
+    # some invalid edges first, and seeds both valid and invalid
+    g.set_valid(np.sort(rng.choice(g.size, size=g.size // 10, replace=False)).astype(np.uint64), False)
+    _, _, v0 = g.download()
+    seeds = rng.choice(g.size, size=200, replace=False).astype(np.uint64)
+    region = set(int(x) for x in seeds)
+    frontier = list(region)
+    for _ in range(hops):
+        expand = np.array([e for e in frontier if v0[e]], dtype=np.uint64)
+        nxt = []
+        if expand.size:
+            for inc in (False, True):
+                nb, cnt = g.neighbors(expand, incoming=inc)
+                for i in range(expand.size):
+                    for j in range(cnt[i]):
+                        x = int(nb[i, j])
+                        if x not in region:
+                            region.add(x)
+                            nxt.append(x)
+        frontier = nxt
+    want = v0.copy()
+    keep = np.zeros_like(want)
+    keep[np.array(sorted(region), dtype=np.int64)] = 1
+    want &= keep.astype(want.dtype)
+    g.keep_region(seeds, hops)
+    _, _, v1 = g.download()
+    assert np.array_equal(v1.astype(bool), want.astype(bool))
