@@ -197,7 +197,7 @@ def measure_e2e(cfg: dict, spec, fastq: str, threads: int, n_kmers: int) -> dict
         if mt:
             tail = {kv.split("=")[0]: round(float(kv.split("=")[1]), 3) for kv in mt.group(1).split()}
             tail["process_start_and_exit_s"] = round(wall - tail.get("main_s", 0.0), 3)
-        for tag in ("TIMING_REGIONS", "TIMING_STEP7"):  # step 7's own split (array_order.cpp, pipeline_steps.cpp)
+        for tag in ("TIMING_REGIONS", "TIMING_STEP7", "TIMING_GROW"):  # step 7's own split (array_order.cpp, pipeline_steps.cpp)
             ms = re.search(tag + r" (.*)", p.stdout)
             if ms:
                 tail[tag.lower()[7:]] = {kv.split("=")[0]: round(float(kv.split("=")[1]), 3)

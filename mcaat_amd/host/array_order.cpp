@@ -100,11 +100,19 @@ std::vector<uint32_t> merge_runs(const std::vector<uint32_t> &v) {  // A,A,B,C,C
 
 }  // namespace
 
+static double g_ids_s = 0, g_scc_s = 0, g_map_s = 0;  // TIMING_REGIONS detail
+static uint64_t g_n_ids = 0;
 std::vector<std::vector<uint64_t>> find_strongly_connected_components(const SDBG &sdbg) {
+    using clk = std::chrono::high_resolution_clock;
+    const auto t0 = clk::now();
     const std::vector<uint64_t> ids = sdbg.ValidIds();
+    const auto t1 = clk::now();
     Tarjan t(sdbg, ids);
     for (uint32_t v = 0; v < ids.size(); ++v)  // valid nodes in ascending id order
         if (t.index[v] < 0) t.run(v);
+    g_ids_s = std::chrono::duration<double>(t1 - t0).count();
+    g_scc_s = std::chrono::duration<double>(clk::now() - t1).count();
+    g_n_ids = ids.size();
     return std::move(t.components);
 }
 
@@ -115,10 +123,18 @@ void keep_crispr_regions_extended_by_k(SDBG &sdbg, const size_t &k, const std::v
     if (sdbg.device()) {  // the whole growth and the AND on the GPU, one call
         std::vector<uint64_t> seeds;
         for (const auto &cycle : cycles) seeds.insert(seeds.end(), cycle.begin(), cycle.end());
+        using clk = std::chrono::high_resolution_clock;
+        const auto a = clk::now();
         sdbg.KeepRegion(seeds, k);
+        const auto b = clk::now();
         const std::vector<uint64_t> live = sdbg.ValidIds();
+        const auto c = clk::now();
         sdbg.PrefetchOutgoing(live);
         sdbg.PrefetchKeys(live);
+        std::cout << "TIMING_GROW keep_s=" << std::chrono::duration<double>(b - a).count()
+                  << " ids_s=" << std::chrono::duration<double>(c - b).count()
+                  << " prefetch_s=" << std::chrono::duration<double>(clk::now() - c).count() << " live=" << live.size()
+                  << std::endl;
         return;
     }
     IdMap<char> region;  // membership (the order of `keep` does not matter: one bitmap AND)
@@ -160,12 +176,10 @@ void keep_crispr_regions_extended_by_k(SDBG &sdbg, const size_t &k, const std::v
 }
 
 // spacer_ordering.cpp:140-173: one Graph per SCC, edges inside the component only
-static double g_scc_s = 0;  // TIMING_REGIONS detail
 std::vector<Graph> divide_graph_into_subgraphs(const SDBG &sdbg) {
     std::vector<Graph> subgraphs;
-    const auto t0 = std::chrono::high_resolution_clock::now();
     const auto comps = find_strongly_connected_components(sdbg);
-    g_scc_s = std::chrono::duration<double>(std::chrono::high_resolution_clock::now() - t0).count();
+    const auto t0 = std::chrono::high_resolution_clock::now();
     // component of every node (components are disjoint), one flat map for all of them
     IdMap<uint32_t> comp_of;
     size_t total = 0;
@@ -173,6 +187,7 @@ std::vector<Graph> divide_graph_into_subgraphs(const SDBG &sdbg) {
     comp_of.reserve(total);
     for (uint32_t ci = 0; ci < comps.size(); ++ci)
         for (uint64_t e : comps[ci]) comp_of[e] = ci + 1;
+    g_map_s = std::chrono::duration<double>(std::chrono::high_resolution_clock::now() - t0).count();
     for (uint32_t ci = 0; ci < comps.size(); ++ci) {
         const auto &comp = comps[ci];
         Graph sub;
@@ -200,8 +215,8 @@ std::vector<Graph> get_crispr_regions_extended_by_k(SDBG &sdbg, const size_t &k,
     const auto t1 = clk::now();
     auto out = divide_graph_into_subgraphs(sdbg);
     std::cout << "TIMING_REGIONS grow_s=" << std::chrono::duration<double>(t1 - t0).count()
-              << " divide_s=" << std::chrono::duration<double>(clk::now() - t1).count() << " scc_s=" << g_scc_s
-              << std::endl;
+              << " divide_s=" << std::chrono::duration<double>(clk::now() - t1).count() << " ids_s=" << g_ids_s
+              << " scc_s=" << g_scc_s << " map_s=" << g_map_s << " n_ids=" << g_n_ids << std::endl;
     return out;
 }
 
