@@ -149,6 +149,11 @@ int mcaat_graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n);
  * grown by `hops` rounds over the valid in- and out-neighbours of the valid frontier nodes, then
  * valid &= that region (one call instead of a host BFS of 2 x hops neighbour queries). */
 int mcaat_graph_keep_region(mcaat_graph *g, const uint64_t *seeds, size_t n, uint64_t hops);
+/* The valid edges and their valid out-edges as a dense graph (step 7's SCC split, Tarjan over a
+ * few hundred thousand edges): *n_valid valid edge ids ascending into ids[], and for each its
+ * out-neighbours (OutgoingEdges order, DESCENDING ids) as positions in ids[] at nbr[4i..4i+counts[i]).
+ * With ids, nbr and counts all NULL only *n_valid is set (size the arrays, call again). */
+int mcaat_graph_valid_subgraph(const mcaat_graph *g, uint64_t *n_valid, uint64_t *ids, uint32_t *nbr, uint8_t *counts);
 /* Checkpoint / resume. Replaces: the on-disk graph between SDBGBuild and CycleFinder
  * (MEGAHIT graph.sdbg* + SDBG::LoadFromFile, main.cpp:386-393, 522-530). The library's own
  * format (MEGAHIT's is unpinned offline): sorted BOSS keys, multiplicities and valid bits with

@@ -802,6 +802,15 @@ int mcaat_graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n) {
         graph_keep_only(g, ids, n);
     });
 }
+int mcaat_graph_valid_subgraph(const mcaat_graph *g, uint64_t *n_valid, uint64_t *ids, uint32_t *nbr, uint8_t *counts) {
+    return guarded([&] {
+        require(g != nullptr && n_valid != nullptr, "null argument");
+        require((ids == nullptr) == (nbr == nullptr) && (ids == nullptr) == (counts == nullptr), "all outputs or none");
+        HIP_OK(hipSetDevice(g->ctx->device));
+        *n_valid = graph_valid_out_ranks(g, ids, nbr, counts);
+    });
+}
+
 int mcaat_graph_keep_region(mcaat_graph *g, const uint64_t *seeds, size_t n, uint64_t hops) {
     return guarded([&] {
         require(g != nullptr && (n == 0 || seeds), "null argument");

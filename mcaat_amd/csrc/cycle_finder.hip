@@ -2528,6 +2528,60 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
     HIP_OK(hipStreamSynchronize(st));
     timer.finish();
 }
+// the valid edges in ascending id order (their rank = their position) and each one's valid
+// out-neighbours as ranks, DESCENDING ids as OutgoingEdges (step 7's SCC split over a small
+// valid set: dense arrays instead of a hash lookup per neighbour)
+__global__ void __launch_bounds__(kBlock) k_word_popc(const uint64_t *bm, uint64_t nw, uint64_t *cnt) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) cnt[w] = __popcll(bm[w]);
+}
+__global__ void __launch_bounds__(kBlock) k_valid_out_ranks(GraphView g, const uint64_t *wpre, uint64_t *ids,
+                                                            uint32_t *nbr, uint8_t *cnt) {
+    const uint64_t nw = (g.D + 63) / 64, stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; e < nw * 64; e += stride) {
+        const uint64_t w = e >> 6, word = g.valid[w];
+        if (!((word >> (e & 63)) & 1)) continue;
+        const uint64_t r = wpre[w] + __popcll(word & ((1ull << (e & 63)) - 1));
+        ids[r] = e;
+        uint64_t out[4];
+        const int n = dev_outgoing(g, e, out);
+        for (int j = 0; j < n; ++j) {
+            const uint64_t y = out[j], wy = g.valid[y >> 6];
+            nbr[4 * r + j] = (uint32_t)(wpre[y >> 6] + __popcll(wy & ((1ull << (y & 63)) - 1)));
+        }
+        cnt[r] = (uint8_t)n;
+    }
+}
+
+uint64_t graph_valid_out_ranks(const mcaat_graph *g, uint64_t *ids, uint32_t *nbr, uint8_t *cnt) {
+    hipStream_t st = g->ctx->stream;
+    const uint64_t nw = g->n_words();
+    if (!nw) return 0;
+    DevBuf<uint64_t> pc(nw + 1), wpre(nw + 1);
+    HIP_OK(hipMemsetAsync(pc.p + nw, 0, 8, st));
+    hipLaunchKernelGGL(k_word_popc, dim3(grid_for(nw, kBlock, (unsigned)g->ctx->n_cu * 16)), dim3(kBlock), 0, st,
+                       (const uint64_t *)g->valid.p, nw, pc.p);
+    LAUNCH_OK();
+    size_t tmp = 0;
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, pc.p, wpre.p, (size_t)(nw + 1), st));
+    DevBuf<uint8_t> t(tmp);
+    HIP_OK(hipcub::DeviceScan::ExclusiveSum(t.p, tmp, pc.p, wpre.p, (size_t)(nw + 1), st));
+    uint64_t n = 0;
+    d2h(g->ctx, &n, wpre.p + nw, 8);
+    if (!ids || !n) return n;
+    if (n >= (1ULL << 32)) throw Error(MCAAT_E_CAPACITY, "valid subgraph of 2^32 or more edges");
+    DevBuf<uint64_t> di(n);
+    DevBuf<uint32_t> dn(4 * n);
+    DevBuf<uint8_t> dc(n);
+    hipLaunchKernelGGL(k_valid_out_ranks, dim3(grid_for(nw * 64, kBlock, (unsigned)g->ctx->n_cu * 32)), dim3(kBlock), 0,
+                       st, g->view(), (const uint64_t *)wpre.p, di.p, dn.p, dc.p);
+    LAUNCH_OK();
+    d2h(g->ctx, ids, di.p, 8 * n);
+    d2h(g->ctx, nbr, dn.p, 16 * n);
+    d2h(g->ctx, cnt, dc.p, n);
+    return n;
+}
+
 void graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, int incoming, uint64_t *out,
                      int32_t *counts) {
     if (!n) return;

@@ -404,6 +404,9 @@ void graph_gather(const mcaat_graph *g, const uint64_t *ids, size_t n, uint64_t 
 void graph_download_valid(const mcaat_graph *g, uint8_t *valid);
 void graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n);
 void graph_keep_region(mcaat_graph *g, const uint64_t *seeds, size_t n, uint64_t hops);
+// valid edge ids (ascending) and each one's valid out-neighbours as ranks among them; null ids:
+// only the count
+uint64_t graph_valid_out_ranks(const mcaat_graph *g, uint64_t *ids, uint32_t *nbr, uint8_t *cnt);
 // FASTQ(.gz) inputs parsed on the GPU (fastq_ingest.hip)
 // ranges: per file, the byte range [first, second) to read (a rank's part; null: whole files)
 void ingest_fastq(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_reads *r,

@@ -21,27 +21,22 @@ namespace {
 
 // Tarjan's SCC from `root` (spacer_ordering.cpp:3-51) with an explicit frame stack visiting
 // successors in OutgoingEdges order, exactly as the recursion does. The nodes it can reach are
-// the valid ones (ids, ascending), so index / low / on-stack are dense arrays over their
-// positions in that list instead of hash maps keyed by edge id.
+// the valid ones, taken as a dense graph (SDBG::ValidSubgraph: positions in the ascending list
+// of valid ids, out-neighbours as positions), so index / low / on-stack are arrays and a step
+// reads no hash table.
 struct Tarjan {
-    const SDBG &g;
-    const std::vector<uint64_t> &ids;  // valid ids, ascending
+    const std::vector<uint32_t> &nbr;  // 4 per node
+    const std::vector<uint8_t> &cnt;
     std::vector<int> index, low;       // -1: not visited
     std::vector<char> on_stack;
     std::vector<uint32_t> stack;
-    std::vector<std::vector<uint64_t>> components;
+    std::vector<std::vector<uint32_t>> components;  // positions
     int counter = 0;
-    IdMap<uint32_t> at;  // id -> position in ids (a flat map: a binary search per edge was most of the SCC time)
-    Tarjan(const SDBG &s, const std::vector<uint64_t> &v)
-        : g(s), ids(v), index(v.size(), -1), low(v.size(), 0), on_stack(v.size(), 0) {
-        at.reserve(v.size());
-        for (uint32_t i = 0; i < v.size(); ++i) at[v[i]] = i;
-    }
-    uint32_t pos(uint64_t e) const { return *at.find(e); }
+    Tarjan(const std::vector<uint32_t> &nb, const std::vector<uint8_t> &c)
+        : nbr(nb), cnt(c), index(c.size(), -1), low(c.size(), 0), on_stack(c.size(), 0) {}
 
     struct Frame {
         uint32_t v;
-        uint64_t nb[4];
         int n, next;
     };
     void open(std::vector<Frame> &frames, uint32_t v) {
@@ -50,9 +45,7 @@ struct Tarjan {
         ++counter;
         stack.push_back(v);
         on_stack[v] = 1;
-        Frame f{v, {0, 0, 0, 0}, 0, 0};
-        if (g.EdgeOutdegree(ids[v]) > 0) f.n = std::max(0, g.OutgoingEdges(ids[v], f.nb));
-        frames.push_back(f);
+        frames.push_back(Frame{v, (int)cnt[v], 0});
     }
     void run(uint32_t root) {
         std::vector<Frame> frames;
@@ -60,9 +53,7 @@ struct Tarjan {
         while (!frames.empty()) {
             Frame &f = frames.back();
             if (f.next < f.n) {
-                const uint64_t we = f.nb[f.next++];
-                if (!g.IsValidEdge(we)) continue;
-                const uint32_t w = pos(we);  // a valid edge is in ids
+                const uint32_t w = nbr[4 * (size_t)f.v + f.next++];
                 if (index[w] < 0) {
                     open(frames, w);  // invalidates f
                 } else if (on_stack[w]) {
@@ -72,13 +63,13 @@ struct Tarjan {
             }
             const uint32_t v = f.v;
             if (low[v] == index[v]) {
-                std::vector<uint64_t> comp;
+                std::vector<uint32_t> comp;
                 uint32_t w;
                 do {
                     w = stack.back();
                     stack.pop_back();
                     on_stack[w] = 0;
-                    comp.push_back(ids[w]);
+                    comp.push_back(w);
                 } while (w != v);
                 if (comp.size() > 1) components.push_back(std::move(comp));
             }
@@ -102,18 +93,32 @@ std::vector<uint32_t> merge_runs(const std::vector<uint32_t> &v) {  // A,A,B,C,C
 
 static double g_ids_s = 0, g_scc_s = 0, g_map_s = 0;  // TIMING_REGIONS detail
 static uint64_t g_n_ids = 0;
-std::vector<std::vector<uint64_t>> find_strongly_connected_components(const SDBG &sdbg) {
+// components as positions in ids (the valid edges, ascending), in the recursion's order
+static std::vector<std::vector<uint32_t>> scc_positions(const SDBG &sdbg, std::vector<uint64_t> &ids,
+                                                        std::vector<uint32_t> &nbr, std::vector<uint8_t> &cnt) {
     using clk = std::chrono::high_resolution_clock;
     const auto t0 = clk::now();
-    const std::vector<uint64_t> ids = sdbg.ValidIds();
+    sdbg.ValidSubgraph(ids, nbr, cnt);
     const auto t1 = clk::now();
-    Tarjan t(sdbg, ids);
+    Tarjan t(nbr, cnt);
     for (uint32_t v = 0; v < ids.size(); ++v)  // valid nodes in ascending id order
         if (t.index[v] < 0) t.run(v);
     g_ids_s = std::chrono::duration<double>(t1 - t0).count();
     g_scc_s = std::chrono::duration<double>(clk::now() - t1).count();
     g_n_ids = ids.size();
     return std::move(t.components);
+}
+
+std::vector<std::vector<uint64_t>> find_strongly_connected_components(const SDBG &sdbg) {
+    std::vector<uint64_t> ids;
+    std::vector<uint32_t> nbr;
+    std::vector<uint8_t> cnt;
+    std::vector<std::vector<uint64_t>> out;
+    for (const auto &c : scc_positions(sdbg, ids, nbr, cnt)) {
+        out.emplace_back();
+        for (uint32_t v : c) out.back().push_back(ids[v]);
+    }
+    return out;
 }
 
 // spacer_ordering.cpp:78-138: the cycle nodes grown by k hops over valid in- and out-edges
@@ -178,30 +183,25 @@ void keep_crispr_regions_extended_by_k(SDBG &sdbg, const size_t &k, const std::v
 // spacer_ordering.cpp:140-173: one Graph per SCC, edges inside the component only
 std::vector<Graph> divide_graph_into_subgraphs(const SDBG &sdbg) {
     std::vector<Graph> subgraphs;
-    const auto comps = find_strongly_connected_components(sdbg);
+    std::vector<uint64_t> ids;
+    std::vector<uint32_t> nbr;
+    std::vector<uint8_t> cnt;
+    const auto comps = scc_positions(sdbg, ids, nbr, cnt);
     const auto t0 = std::chrono::high_resolution_clock::now();
-    // component of every node (components are disjoint), one flat map for all of them
-    IdMap<uint32_t> comp_of;
-    size_t total = 0;
-    for (const auto &c : comps) total += c.size();
-    comp_of.reserve(total);
+    std::vector<uint32_t> comp_of(ids.size(), 0);  // component + 1 by position (components are disjoint)
     for (uint32_t ci = 0; ci < comps.size(); ++ci)
-        for (uint64_t e : comps[ci]) comp_of[e] = ci + 1;
+        for (uint32_t v : comps[ci]) comp_of[v] = ci + 1;
     g_map_s = std::chrono::duration<double>(std::chrono::high_resolution_clock::now() - t0).count();
     for (uint32_t ci = 0; ci < comps.size(); ++ci) {
         const auto &comp = comps[ci];
         Graph sub;
         sub.nodes.reserve(comp.size());
         sub.adjacency_list.reserve(comp.size());
-        for (uint64_t e : comp) {
-            if (!sdbg.IsValidEdge(e) || sdbg.EdgeOutdegree(e) <= 0) continue;
-            uint64_t out[4];
-            const int n = sdbg.OutgoingEdges(e, out);
-            for (int i = 0; i < n; ++i) {
-                const uint32_t *c = comp_of.find(out[i]);
-                if (c && *c == ci + 1) sub.add_edge(e, out[i]);
+        for (uint32_t v : comp)  // every node of a component is valid; its out-edges in OutgoingEdges order
+            for (int j = 0; j < cnt[v]; ++j) {
+                const uint32_t w = nbr[4 * (size_t)v + j];
+                if (comp_of[w] == ci + 1) sub.add_edge(ids[v], ids[w]);
             }
-        }
         if (!sub.nodes.empty()) subgraphs.push_back(std::move(sub));
     }
     return subgraphs;

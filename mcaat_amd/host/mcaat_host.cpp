@@ -327,6 +327,28 @@ std::vector<uint64_t> SDBG::ValidIds() const {
     return out;
 }
 
+void SDBG::ValidSubgraph(std::vector<uint64_t> &ids, std::vector<uint32_t> &nbr, std::vector<uint8_t> &cnt) const {
+    if (g_) {
+        uint64_t n = 0;
+        mcaat_check(mcaat_graph_valid_subgraph(g_, &n, nullptr, nullptr, nullptr), "mcaat_graph_valid_subgraph");
+        ids.assign(n, 0);
+        nbr.assign(4 * n, 0);
+        cnt.assign(n, 0);
+        if (n) mcaat_check(mcaat_graph_valid_subgraph(g_, &n, ids.data(), nbr.data(), cnt.data()), "mcaat_graph_valid_subgraph");
+        return;
+    }
+    ids = ValidIds();
+    nbr.assign(4 * ids.size(), 0);
+    cnt.assign(ids.size(), 0);
+    for (size_t i = 0; i < ids.size(); ++i) {
+        uint64_t out[4];
+        const int n = OutgoingEdges(ids[i], out);
+        cnt[i] = (uint8_t)n;
+        for (int j = 0; j < n; ++j)
+            nbr[4 * i + j] = (uint32_t)(std::lower_bound(ids.begin(), ids.end(), out[j]) - ids.begin());
+    }
+}
+
 uint32_t SDBG::GetLabel(uint64_t e, uint8_t *seq) const {
     const auto *kc = kcache_.find(e);
     const uint64_t R = (kc ? kc->first : host_key()[e]) >> 2;

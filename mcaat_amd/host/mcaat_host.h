@@ -175,6 +175,9 @@ class SDBG {
     void PrefetchOutgoing(const std::vector<uint64_t> &ids);
     // valid edge ids in ascending order
     std::vector<uint64_t> ValidIds() const;
+    // the valid edges (ascending) and each one's valid out-neighbours (OutgoingEdges order) as
+    // positions in that list, nbr[4i .. 4i + cnt[i]) (one device call on a device graph)
+    void ValidSubgraph(std::vector<uint64_t> &ids, std::vector<uint32_t> &nbr, std::vector<uint8_t> &cnt) const;
     int64_t IndexBinarySearch(const uint8_t *seq) const;    // -1 if absent
     static constexpr uint64_t kNullID = ~0ULL;
 

@@ -118,6 +118,8 @@ SIGNATURES = {
     "mcaat_graph_download_range": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, _u64p, _u16p, _u8p]),
     "mcaat_graph_valid_words": (C.c_int, [C.c_void_p, _u64p]),
     "mcaat_graph_keep_region": (C.c_int, [C.c_void_p, _u64p, C.c_size_t, C.c_uint64]),
+    "mcaat_graph_valid_subgraph": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), _u64p, C.POINTER(C.c_uint32),
+                                             _u8p]),
     "mcaat_comm_unique_id": (C.c_int, [_u8p]),
     "mcaat_comm_init_rccl": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p, C.POINTER(C.c_void_p)]),
     "mcaat_comm_init_shm": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_char_p, C.c_uint64, C.POINTER(C.c_void_p)]),
@@ -643,6 +645,19 @@ class Graph:
         """valid &= seeds grown by `hops` rounds over valid neighbours (mcaat_graph_keep_region)."""
         seeds = np.ascontiguousarray(seeds, dtype=np.uint64)
         _check(self.ctx._lib.mcaat_graph_keep_region(self.h, _ptr(seeds, _u64p), seeds.size, hops))
+
+    def valid_subgraph(self):
+        """(ids, nbr[n, 4], counts): valid edges ascending, out-neighbours as positions in ids."""
+        n = C.c_uint64(0)
+        _check(self.ctx._lib.mcaat_graph_valid_subgraph(self.h, C.byref(n), None, None, None))
+        ids = np.zeros(max(n.value, 1), dtype=np.uint64)
+        nbr = np.zeros(4 * max(n.value, 1), dtype=np.uint32)
+        cnt = np.zeros(max(n.value, 1), dtype=np.uint8)
+        if n.value:
+            _check(self.ctx._lib.mcaat_graph_valid_subgraph(self.h, C.byref(n), _ptr(ids, _u64p),
+                                                            nbr.ctypes.data_as(C.POINTER(C.c_uint32)),
+                                                            _ptr(cnt, _u8p)))
+        return ids[: n.value], nbr.reshape(-1, 4)[: n.value], cnt[: n.value]
 
     def keep_only(self, ids: np.ndarray) -> None:
         """valid &= {ids} (keep_crispr_regions_extended_by_k, spacer_ordering.cpp:129-137)."""

@@ -367,3 +367,22 @@ def test_keep_region_equals_host_growth(gpu_ctx, hops):
     g.keep_region(seeds, hops)
     _, _, v1 = g.download()
     assert np.array_equal(v1.astype(bool), want.astype(bool))
+
+
+def test_valid_subgraph_equals_neighbors(gpu_ctx):
+    """mcaat_graph_valid_subgraph (step 7's SCC input) lists the valid edges ascending and, for each,
+    its valid out-neighbours in OutgoingEdges order as positions in that list — the same sets
+    mcaat_graph_neighbors gives edge by edge."""
+    spec, k, prm = CONFIGS["pe_err"]
+    reads = M.Reads.synth(gpu_ctx, spec)
+    g = M.Graph.build(gpu_ctx, reads, k)
+    rng = np.random.default_rng(7)
+    g.set_valid(np.sort(rng.choice(g.size, size=g.size // 4, replace=False)).astype(np.uint64), False)
+    _, _, v = g.download()
+    ids, nbr, cnt = g.valid_subgraph()
+    assert np.array_equal(ids, np.flatnonzero(v).astype(np.uint64))
+    nb, c = g.neighbors(ids)
+    assert np.array_equal(cnt.astype(np.int32), c)
+    got = np.where(np.arange(4)[None, :] < cnt[:, None], ids[np.minimum(nbr, ids.size - 1)], 0)
+    want = np.where(np.arange(4)[None, :] < c[:, None], nb, 0)
+    assert np.array_equal(got, want)
