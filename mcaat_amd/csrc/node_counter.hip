@@ -173,7 +173,9 @@ __device__ __forceinline__ void hash_step(uint64_t win, int m, uint32_t mmask, u
             f &= mmask;
             r &= mmask;
         }
-#if MCAAT_HASH == 1
+#if MCAAT_HASH == 2
+        h[t] = (min(f, r) ^ salt) * 0x9E3779B1u;  // A/B: the multiply alone
+#elif MCAAT_HASH == 1
         // multiply-xorshift: a bijection, and only the minimizer order depends on it (the
         // buckets and sub-partitions come from a re-hash), so a short one suffices
         uint32_t x = (min(f, r) ^ salt) * 0x9E3779B1u;
@@ -218,6 +220,10 @@ constexpr uint16_t kDeadSub = 0xffff;  // sub-partition mark of an inert (n = 0)
 #ifndef MCAAT_WB
 #define MCAAT_WB 4
 #endif
+#ifndef MCAAT_APF
+#define MCAAT_APF 1
+#endif
+constexpr int kAPF = MCAAT_APF;  // scan steps of window words in flight (1 or 2)
 constexpr int kWB = MCAAT_WB;  // write batch (entries per thread per round: 3 loads each in flight)
 
 // 8-byte pre-entry of a closed super-k-mer: minimizer hash (low 32 bits); above it the
@@ -294,6 +300,7 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
     // per-lane scan state (wave-uniform: active, c, ph, nck, fill, par, bsf)
     uint32_t H[3 * kCk];  // ring of three 8-hash groups; step c reads groups c, c+1, c+2 (mod 3)
     uint64_t cw[3], pa = 0, pb = 0;  // the item's first words; the next step's window words
+    uint64_t qa = 0, qb = 0;         // kAPF == 2: the step after next's
     uint64_t s = 0;
     int np = 0, c = 0, ph = 0, nck = 0;
     uint32_t prev_hm = 0, h_open = 0, p7 = 0, ihc = 0, fill = 0, par = 1, bsf = 0;
@@ -316,7 +323,13 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
         c = __builtin_amdgcn_readfirstlane(c);
         const int rb = kCk * c + 2 * kCk;
         const uint64_t win = win32(pa, pb, s + rb);
-        {
+        if constexpr (kAPF == 2) {  // the step after next's window words; the next step's were loaded a step ago
+            pa = qa;
+            pb = qb;
+            const u64x2 nx = *(const u64x2 *)(packed + ((s + rb + 2 * kCk) >> 5));
+            qa = nx.a;
+            qb = nx.b;
+        } else {
             const u64x2 nx = *(const u64x2 *)(packed + ((s + rb + kCk) >> 5));  // next step's window words
             pa = nx.a;
             pb = nx.b;
@@ -373,6 +386,11 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
             const u64x2 nx = *(const u64x2 *)(packed + ((s + 2 * kCk) >> 5));
             pa = nx.a;
             pb = nx.b;
+        }
+        if constexpr (kAPF == 2) {
+            const u64x2 nx = *(const u64x2 *)(packed + ((s + 3 * kCk) >> 5));
+            qa = nx.a;
+            qb = nx.b;
         }
         int mx = np;
 #pragma unroll
@@ -870,11 +888,16 @@ __device__ __forceinline__ uint32_t edge_slot_n(uint64_t c) {
         return (uint32_t)(((uint64_t)h * (uint64_t)CAP) >> 32);
     }
 }
+// descriptor-table slots of an edge-table tier: the 8192-slot tier's 96-KB region holds a
+// 4096-slot descriptor table (80 KB), so error-rich partitions (C5: ~2000 distinct descriptors)
+// collapse in one pass instead of being re-read as four classes
+constexpr int dcap_for(int cap) { return cap == kCapBig ? 2 * kDCap : kDCap; }
+template <int DCAP>
 __device__ __forceinline__ uint32_t desc_slot(uint64_t w0, uint64_t w1) {
+    static_assert(DCAP == 2048 || DCAP == 4096, "11 or 12 slot bits");
     const uint64_t x = (w0 ^ (w1 * 0x9E3779B97F4A7C15ULL)) * 0xD6E8FEB86659FD93ULL;
-    return (uint32_t)(x >> (64 - 11));
+    return (uint32_t)(x >> (64 - (DCAP == 4096 ? 12 : 11)));
 }
-static_assert(kDCap == 2048, "desc_slot yields 11 bits");
 
 template <bool PROF, int kCap, int PERCU>
 __global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_count(const uint4 *__restrict__ data, uint64_t gbase,
@@ -885,6 +908,7 @@ __global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_coun
                                                          unsigned long long *ovf_n, uint32_t cap_max, uint32_t dmax,
                                                          unsigned long long *split_n, unsigned long long *prof) {
     static_assert(cap_lg(kCap) >= 0, "edge table of 4096, 6144 or 8192 slots");
+    constexpr int kDCap = dcap_for(kCap);  // descriptor slots of this tier
     // The descriptor table (phase 1) and the edge table (phases 2-3) share one LDS region:
     // between the phases each thread keeps its two descriptor slots in registers. 48 KB per
     // workgroup, so two 1024-thread workgroups share a CU and one's loads overlap the other's
@@ -979,7 +1003,7 @@ __global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_coun
                     dovf = 1;
                 return;
             }
-            uint32_t h = desc_slot(w0, w1);
+            uint32_t h = desc_slot<kDCap>(w0, w1);
             for (int probe = 0; probe < kDProbe; ++probe, h = (h + 1) & (kDCap - 1)) {
                 unsigned long long k1 = dk1[h];
                 if (k1 == kEmpty) {
@@ -1617,6 +1641,8 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
     const int64_t big_knob = knob(ctx, "nc.big_table", -1);
     int tier = big_knob == 1 ? 2 : big_knob == 2 ? 1 : 0;
     const uint32_t dmax = (uint32_t)std::min<int64_t>(kDMax, std::max<int64_t>(1, knob(ctx, "nc.desc_cap", kDMax)));
+    constexpr int kDMaxBig = dcap_for(kCapBig) * 3 / 4;
+    const uint32_t dmax_big = (uint32_t)std::min<int64_t>(kDMaxBig, std::max<int64_t>(1, knob(ctx, "nc.desc_cap", kDMaxBig)));
     // groups of L1 buckets; with the overlap knob (default on) group g+1's pass B runs on the
     // side stream while group g's pass C counts on the main stream (two groups' fine
     // partitions alive at once, so groups are half the size)
@@ -1629,7 +1655,10 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
     std::vector<Group> groups;
     for (int b0 = 0; b0 < 256;) {
         int b1 = b0 + 1;
-        const uint64_t gb = overlap && !knob_set(ctx, "nc.group_budget") ? group_budget / 2 + 1 : group_budget;
+        uint64_t gb = overlap && !knob_set(ctx, "nc.group_budget") ? group_budget / 2 + 1 : group_budget;
+        // the first group is a small probe: the edge-table tier is chosen from its class splits,
+        // so on error-rich data only 1/16 of the descriptors take the re-read of a split
+        if (b0 == 0 && big_knob < 0 && !knob_set(ctx, "nc.group_budget")) gb = gb / 8 + 1;
         while (b1 < 256 && hfine[(uint64_t)(b1 + 1) * S] - hfine[(uint64_t)b0 * S] <= gb) ++b1;
         groups.push_back(Group{b0, b1, {}, nullptr});
         b0 = b1;
@@ -1685,7 +1714,7 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
                                 : (prof_c ? k_lds_count<true, kCap, kCPerCu> : k_lds_count<false, kCap, kCPerCu>);
                 hipLaunchKernelGGL(kern, dim3(wg), dim3(kCThreads), 0, st, fine.p, gbase, dfine.p, p0, p1, E, out.keys.p,
                                    out.counts.p, out_cap, dcnt.p, ovf_list.p, dcnt.p + 1,
-                                   tier == 2 ? cap_max_big : tier == 1 ? cap_max_mid : cap_max, dmax,
+                                   tier == 2 ? cap_max_big : tier == 1 ? cap_max_mid : cap_max, tier == 2 ? dmax_big : dmax,
                                    dcnt.p + 2, prof_c ? dprof.p : nullptr);
                 LAUNCH_OK();
                 kt.stop();
