@@ -835,6 +835,7 @@ constexpr int kCPerCu = MCAAT_CPERCU;                      // resident workgroup
 #endif
 constexpr uint32_t kSplitLg = MCAAT_CSPLIT;                // log2 classes of an overflowing partition (<= 3 spare hash bits)
 static_assert(kSplitLg <= 3, "the sub-partition takes the top 11 of the 14 stored hash bits");
+constexpr uint32_t kSplitMax = 3;                          // spare hash bits: deepest class split
 #ifndef MCAAT_CRING
 #define MCAAT_CRING 0
 #endif
@@ -906,7 +907,8 @@ __global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_coun
                                                          uint64_t *out_keys, uint32_t *out_cnt, uint64_t out_cap,
                                                          unsigned long long *out_cursor, uint32_t *ovf_list,
                                                          unsigned long long *ovf_n, uint32_t cap_max, uint32_t dmax,
-                                                         unsigned long long *split_n, unsigned long long *prof) {
+                                                         unsigned long long *split_n, uint32_t split_first,
+                                                         uint32_t split_max, unsigned long long *prof) {
     static_assert(cap_lg(kCap) >= 0, "edge table of 4096, 6144 or 8192 slots");
     constexpr int kDCap = dcap_for(kCap);  // descriptor slots of this tier
     // The descriptor table (phase 1) and the edge table (phases 2-3) share one LDS region:
@@ -929,6 +931,8 @@ __global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_coun
     __shared__ uint32_t n_deferred;
     __shared__ uint32_t n_distinct, n_ddistinct;
     __shared__ int ovf, dovf;
+    __shared__ uint32_t todo[16];
+    __shared__ int ntodo;
     __shared__ uint32_t wsum[kCWaves];
     __shared__ unsigned long long obase;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -970,12 +974,36 @@ __global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_coun
     };
 
     for (uint64_t p = p0 + blockIdx.x; p < F; p += gridDim.x) {
-      // a partition whose distinct descriptors overflow the table is counted again as
-      // 2^kSplitLg edge-disjoint classes (spare minimizer-hash bits: every occurrence of a
-      // canonical edge carries the same minimizer), each collapsed, expanded and emitted alone
-      uint32_t lgn = 0;
-      for (uint32_t cls = 0; cls < (1u << lgn); ++cls) {
+      // a partition whose distinct descriptors or edges overflow a table is counted again as
+      // edge-disjoint classes (spare minimizer-hash bits: every occurrence of a canonical edge
+      // carries the same minimizer), each collapsed, expanded and emitted alone
+      // (round 4) the classes still to count, a stack of (cls | lgn << 4): a class that
+      // overflows either table is split on its next spare hash bits — split_first bits the
+      // first time, one bit after that — until split_max bits, past which an edge overflow goes to
+      // the fallback and a descriptor overflow expands raw. Round 3 split once, 2^kSplitLg ways.
+      if (threadIdx.x == 0) {
+          todo[0] = 0;
+          ntodo = 1;
+      }
+      __syncthreads();
+      for (;;) {
+        const int nt = ntodo;
+        const uint32_t item = nt ? todo[nt - 1] : 0u;
+        // every thread has read the top before thread 0 pops it (or, on an empty stack, before it
+        // starts the next partition's)
+        __syncthreads();
+        if (nt == 0) break;
+        const uint32_t cls = item & 15, lgn = item >> 4;
         const uint32_t cmask = (1u << lgn) - 1;
+        // children of this class, pushed by thread 0 when it overflows (every thread has read
+        // ntodo/todo: the clear below ends with a barrier before any push)
+        auto split = [&]() {
+            if (threadIdx.x == 0) {
+                atomicAdd(split_n, 1ull);
+                const uint32_t b = lgn == 0 ? split_first : 1u;
+                for (uint32_t j = (1u << b); j-- > 0;) todo[ntodo++] = (cls + (j << lgn)) | ((lgn + b) << 4);
+            }
+        };
         for (int i = threadIdx.x; i < kDCap; i += kCThreads) {
             dk0[i] = dk1[i] = kEmpty;
             dcnt[i] = 0;
@@ -983,6 +1011,7 @@ __global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_coun
         if (threadIdx.x == 0) {
             n_distinct = n_ddistinct = n_deferred = 0;
             ovf = dovf = 0;
+            ntodo = nt - 1;  // popped
         }
         __syncthreads();
         tick(0);
@@ -1089,11 +1118,9 @@ __global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_coun
         }
         __syncthreads();
         tick(1);
-        if (dovf && lgn == 0 && !n_deferred_over(n_deferred)) {
-            if (threadIdx.x == 0) atomicAdd(split_n, 1ull);
-            lgn = kSplitLg;
-            cls = ~0u;  // -> class 0 of 2^kSplitLg
-            __syncthreads();  // every thread has read dovf before the next clear resets it
+        if (dovf && lgn + (lgn == 0 ? split_first : 1u) <= split_max && !n_deferred_over(n_deferred)) {
+            split();
+            __syncthreads();  // every thread has read dovf and the stack before the next clear
             continue;
         }
         if (PROF && threadIdx.x == 0) {
@@ -1186,10 +1213,8 @@ __global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_coun
             // too many distinct edges for the LDS table: count the partition again as
             // edge-disjoint classes (shallow or error-rich data); a class that still overflows
             // goes to the global-table fallback
-            if (lgn == 0) {
-                if (threadIdx.x == 0) atomicAdd(split_n, 1ull);
-                lgn = kSplitLg;
-                cls = ~0u;
+            if (lgn + (lgn == 0 ? split_first : 1u) <= split_max) {
+                split();
             } else if (threadIdx.x == 0) {
                 ovf_list[atomicAdd(ovf_n, 1ull)] = (uint32_t)p | (cls << 24) | (lgn << 28);
             }
@@ -1626,7 +1651,7 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
     out.counts.alloc(out_cap);
     DevBuf<unsigned long long> dcnt(4);
     HIP_OK(hipMemsetAsync(dcnt.p, 0, dcnt.bytes(), st));
-    DevBuf<uint32_t> ovf_list(F << kSplitLg);  // one entry per (partition, class)
+    DevBuf<uint32_t> ovf_list(F << kSplitMax);  // one entry per (partition, class)
     static const bool prof_c = getenv("MCAAT_PROF_C") && getenv("MCAAT_PROF_C")[0] == '1';
     if (prof_c) HIP_OK(hipMemsetAsync(dprof.p, 0, dprof.bytes(), st));
     const uint64_t group_budget =
@@ -1642,6 +1667,12 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
     int tier = big_knob == 1 ? 2 : big_knob == 2 ? 1 : 0;
     const uint32_t dmax = (uint32_t)std::min<int64_t>(kDMax, std::max<int64_t>(1, knob(ctx, "nc.desc_cap", kDMax)));
     constexpr int kDMaxBig = dcap_for(kCapBig) * 3 / 4;
+    // bits of a partition's first class split: round 3's four-way split in the 4096-slot tier (C2:
+    // partitions far over it); two-way in the 8192-slot tier, whose overflowing partitions (C5)
+    // are mostly just over it, so halves fit and each re-read is half as many passes
+    const uint32_t split_first = (uint32_t)std::min<int64_t>(kSplitMax, std::max<int64_t>(1, knob(ctx, "nc.split_first", kSplitLg)));
+    const uint32_t split_big = (uint32_t)std::min<int64_t>(kSplitMax, std::max<int64_t>(1, knob(ctx, "nc.split_first", 1)));
+    const uint32_t split_max = (uint32_t)std::min<int64_t>(kSplitMax, std::max<int64_t>(1, knob(ctx, "nc.split_max", kSplitMax)));
     const uint32_t dmax_big = (uint32_t)std::min<int64_t>(kDMaxBig, std::max<int64_t>(1, knob(ctx, "nc.desc_cap", kDMaxBig)));
     // groups of L1 buckets; with the overlap knob (default on) group g+1's pass B runs on the
     // side stream while group g's pass C counts on the main stream (two groups' fine
@@ -1715,7 +1746,7 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
                 hipLaunchKernelGGL(kern, dim3(wg), dim3(kCThreads), 0, st, fine.p, gbase, dfine.p, p0, p1, E, out.keys.p,
                                    out.counts.p, out_cap, dcnt.p, ovf_list.p, dcnt.p + 1,
                                    tier == 2 ? cap_max_big : tier == 1 ? cap_max_mid : cap_max, tier == 2 ? dmax_big : dmax,
-                                   dcnt.p + 2, prof_c ? dprof.p : nullptr);
+                                   dcnt.p + 2, tier == 2 ? split_big : split_first, split_max, prof_c ? dprof.p : nullptr);
                 LAUNCH_OK();
                 kt.stop();
             }

@@ -329,3 +329,31 @@ def test_host_pack_off_matches_on(gpu_ctx, tmp_path, monkeypatch):
     (p0, o0), i0, q0 = got[1]
     nw = (int(o1[-1]) + 31) // 32
     assert i1 == i0 and q1 == q0 and np.array_equal(o1, o0) and np.array_equal(p1[:nw], p0[:nw])
+
+
+@pytest.mark.gpu
+def test_host_pack_on_a_second_device(gpu_ctx, tmp_path, monkeypatch):
+    """ The packer's worker threads bind the context's device before making
+    their events: a context on device 1 packs the same library as one on device 0. Needs two
+    GPUs (skipped on a one-GPU box)."""
+    import mcaat_amd as M
+
+    if M.device_count() < 2:
+        pytest.skip("one GPU: the second-device case needs two")
+    monkeypatch.setenv("MCAAT_PACK_THREADS", "6")
+    rng = np.random.default_rng(5)
+    text = _fastq_text(_acgt_records(rng, 4000, [150]))
+    path = _write(tmp_path / "a.fq", text)
+    ctx1 = M.Context(1)
+    try:
+        ctx1.reset_timing()
+        r1 = M.Reads.from_fastx(ctx1, [path])
+        assert _packed_by_host(ctx1)
+        r0 = M.Reads.from_fastx(gpu_ctx, [path])
+        (p1, o1), (p0, o0) = r1.download(), r0.download()
+        nw = (int(o1[-1]) + 31) // 32
+        assert r1.info() == r0.info() and np.array_equal(o1, o0) and np.array_equal(p1[:nw], p0[:nw])
+        r1.free()
+        r0.free()
+    finally:
+        ctx1.close()

@@ -51,6 +51,10 @@ KNOBS = {
     "mid_table_split": {"nc.big_table": 2, "nc.edge_cap": 600, "nc.group_budget": 1},
     # every partition overflows the descriptor table: class split, then the raw path
     "desc_raw": {"nc.desc_cap": 2, "nc.fine_bits": 9},
+    # (round 4) splits one bit at a time down to three bits, then the fallback / the raw path
+    "split_by_halves": {"nc.split_first": 1, "nc.edge_cap": 600, "nc.group_budget": 1},
+    "split_by_halves_desc": {"nc.split_first": 1, "nc.desc_cap": 40, "nc.fine_bits": 9},
+    "split_eight_ways_big": {"nc.split_first": 3, "nc.big_table": 1, "nc.edge_cap": 300},
     # level-3 buckets through the 256-thread LDS sort, the 1024-thread one, and the radix fallback
     "sort_mid": {"sort.msd": 1, "sort.wave_limit": 0},
     "sort_mid_bitonic": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_counting": 0},
