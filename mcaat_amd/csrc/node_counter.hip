@@ -224,7 +224,11 @@ constexpr uint16_t kDeadSub = 0xffff;  // sub-partition mark of an inert (n = 0)
 #define MCAAT_APF 1
 #endif
 constexpr int kAPF = MCAAT_APF;  // scan steps of window words in flight (1 or 2)
-constexpr int kWB = MCAAT_WB;  // write batch (entries per thread per round: 3 loads each in flight)
+constexpr int kWB = MCAAT_WB;
+#ifndef MCAAT_WPIPE
+#define MCAAT_WPIPE 0
+#endif
+constexpr bool kWPipe = MCAAT_WPIPE != 0;  // write phase: the next batch's loads before this batch's stores  // write batch (entries per thread per round: 3 loads each in flight)
 
 // 8-byte pre-entry of a closed super-k-mer: minimizer hash (low 32 bits); above it the
 // close position (7 bits), the first position (7), batch parity (1) and lane (6), all in
@@ -509,47 +513,73 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
         uint32_t total = 0;
 #pragma unroll
         for (int w = 0; w < kAWaves; ++w) total += wtot[w];
-        for (uint32_t j0 = threadIdx.x; j0 < total; j0 += kWB * kAThreads) {
-            uint64_t q[kWB], B0[kWB], x[kWB][3];
+        // a batch of kWB entries per thread: first its stage reads and base loads, then the
+        // descriptors; with kWPipe the next batch's loads are issued before this batch's
+        // descriptors are built (two batches of registers, slots fixed at compile time)
+        uint64_t q[2][kWB], B0[2][kWB], x[2][kWB][3];
+        auto load_batch = [&](auto Sc, uint32_t j0) {
+            constexpr int S = decltype(Sc)::value;
 #pragma unroll
             for (int k = 0; k < kWB; ++k) {
                 const uint32_t j = j0 + k * kAThreads;
-                q[k] = 0;
-                B0[k] = 0;
+                q[S][k] = 0;
+                B0[S][k] = 0;
                 if (j < total) {
                     const uint32_t i = perm[j];
-                    q[k] = stage[i];
-                    const uint32_t hi = (uint32_t)(q[k] >> 32);
+                    q[S][k] = stage[i];
+                    const uint32_t hi = (uint32_t)(q[S][k] >> 32);
                     const uint32_t ln = (hi >> kPeLane) & 63, pr = (hi >> kPePar) & 1;
-                    B0[k] = sbase[i / kSeg][pr][ln] + ((hi >> kPeP) & 127);
+                    B0[S][k] = sbase[i / kSeg][pr][ln] + ((hi >> kPeP) & 127);
                 }
                 // the first two words in one 16-B load; the third only when the bases reach
                 // it (these loads are uncoalesced, so the vector L1 pays per lane and line)
-                const int L = (int)(((uint32_t)(q[k] >> 32) & 127) - (((uint32_t)(q[k] >> 32) >> kPeP) & 127)) + P.E - 1;
-                const u64x2 x01 = *(const u64x2 *)(packed + (B0[k] >> 5));
-                x[k][0] = x01.a;
-                x[k][1] = x01.b;
-                x[k][2] = j < total && 2 * (int)(B0[k] & 31) + 2 * L > 128 ? packed[(B0[k] >> 5) + 2] : 0;
+                const int L = (int)(((uint32_t)(q[S][k] >> 32) & 127) - (((uint32_t)(q[S][k] >> 32) >> kPeP) & 127)) + P.E - 1;
+                const u64x2 x01 = *(const u64x2 *)(packed + (B0[S][k] >> 5));
+                x[S][k][0] = x01.a;
+                x[S][k][1] = x01.b;
+                x[S][k][2] = j < total && 2 * (int)(B0[S][k] & 31) + 2 * L > 128 ? packed[(B0[S][k] >> 5) + 2] : 0;
             }
+        };
+        auto store_batch = [&](auto Sc, uint32_t j0) {
+            constexpr int S = decltype(Sc)::value;
 #pragma unroll
             for (int k = 0; k < kWB; ++k) {
                 const uint32_t j = j0 + k * kAThreads;
                 if (j >= total) continue;
                 const uint32_t i = perm[j];
                 const int b = stage_l1[i];
-                const uint32_t hi = (uint32_t)(q[k] >> 32);
+                const uint32_t hi = (uint32_t)(q[S][k] >> 32);
                 const uint32_t n = (hi & 127) - ((hi >> kPeP) & 127);
-                const int sh = 2 * (int)(B0[k] & 31);
+                const int sh = 2 * (int)(B0[S][k] & 31);
                 // bases past the last edge are zeroed, so every copy of a super-k-mer is the
                 // same 128-bit descriptor whatever follows it in its read
                 const int L = (int)n + P.E - 1;
-                const uint64_t w0 = (sh ? (x[k][0] >> sh) | (x[k][1] << (64 - sh)) : x[k][0]) & mask_bits(2 * L);
-                uint64_t w1 = (sh ? (x[k][1] >> sh) | (x[k][2] << (64 - sh)) : x[k][1]) &
+                const uint64_t w0 = (sh ? (x[S][k][0] >> sh) | (x[S][k][1] << (64 - sh)) : x[S][k][0]) & mask_bits(2 * L);
+                uint64_t w1 = (sh ? (x[S][k][1] >> sh) | (x[S][k][2] << (64 - sh)) : x[S][k][1]) &
                               mask_bits(L > 32 ? 2 * (L - 32) : 0);
-                const uint32_t h = part_mix((uint32_t)q[k]);
+                const uint32_t h = part_mix((uint32_t)q[S][k]);
                 w1 |= ((uint64_t)n << kNShift) | ((uint64_t)((h >> (24 - kHBits)) & ((1u << kHBits) - 1)) << kHShift);
                 put(b, rpos[b] + (j - boff[b]),
                     make_uint4((uint32_t)w0, (uint32_t)(w0 >> 32), (uint32_t)w1, (uint32_t)(w1 >> 32)));
+            }
+        };
+        constexpr uint32_t kStep = kWB * kAThreads;
+        using S0 = std::integral_constant<int, 0>;
+        using S1 = std::integral_constant<int, 1>;
+        if constexpr (kWPipe) {
+            uint32_t j0 = threadIdx.x;
+            if (j0 < total) load_batch(S0(), j0);
+            for (; j0 < total; j0 += 2 * kStep) {
+                if (j0 + kStep < total) load_batch(S1(), j0 + kStep);
+                store_batch(S0(), j0);
+                if (j0 + kStep >= total) break;
+                if (j0 + 2 * kStep < total) load_batch(S0(), j0 + 2 * kStep);
+                store_batch(S1(), j0 + kStep);
+            }
+        } else {
+            for (uint32_t j0 = threadIdx.x; j0 < total; j0 += kStep) {
+                load_batch(S0(), j0);
+                store_batch(S0(), j0);
             }
         }
         if (tb < 256) bcur[tb] = 0;

@@ -1,6 +1,5 @@
 set -e
 mkdir -p gpurun_out
-CFG=c5 STEPS=2 bash tools/abq.sh default ab/prep8.so
-MCAAT_KNOBS=cf.scan_u=1 CFG=c5 STEPS=2 bash tools/abq.sh default
-CFG=c3 STEPS=3 bash tools/abq.sh ab/prep8.so
-MCAAT_KNOBS=cf.scan_u=1 CFG=c3 STEPS=3 bash tools/abq.sh default
+CFG=c3 STEPS=3 bash tools/abq.sh default ab/wpipe2.so default ab/wpipe2.so
+MCAAT_PROF_A=1 MCAAT_LIB=$PWD/ab/wpipe2.so timeout -k 10 300 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-post --no-e2e --ingest-reads 0 2> gpurun_out/pa2.err > /dev/null
+grep "pass A" gpurun_out/pa2.err | tail -1
