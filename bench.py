@@ -9,15 +9,15 @@ k-mers = N_occ = sum over reads of (L - k) edge occurrences.
 Workload (N=1): config C3 — ~300M x 150 bp reads, k=27, threshold_multiplicity=20,
 error rate tuned so the SDBG has ~1e9 edges (D).
 N>1, default --mode shard (config C4): the SAME C3 dataset is split over
-the ranks; each counts its slice, the oriented edges are routed to their owner rank by a
-BOSS-key-range all-to-all, owners sort and sum, an exact-size all-gather in rank order gives
-every rank the single-GPU graph, and CycleFinder runs over the ranks (pruning on every rank,
-candidate scan by id range, DLS and FindCycle starts dealt round-robin with one ordered
-commit). All of it is the library's native path (mcaat_build_graph_sharded,
-mcaat_cycle_finder_comm) over an RCCL communicator whose id travels over torch.distributed
-(gloo, control plane only); MCAAT_COMM_BACKEND=gloo uses the shared-memory transport instead
-(ranks sharing one GPU); --shard-impl torch keeps the Python orchestration (mcaat_amd/shard.py,
-torch.distributed collectives) with CycleFinder replicated. Scaling "strong": total work fixed.
+the ranks; each runs pass A of the counter on its slice, the super-k-mer descriptors go to the
+owners of their minimizer-hash (L1 bucket) ranges by one all-to-all, owners count them to final
+counts, the oriented edges are routed to their BOSS-key-range owners and sorted, an exact-size
+all-gather in rank order gives every rank the single-GPU graph, and CycleFinder runs over the
+ranks (pruning on every rank, candidate scan by id range, DLS and FindCycle starts dealt
+round-robin with one ordered commit). All of it is the library's native path
+(mcaat_build_graph_sharded, mcaat_cycle_finder_comm) over an RCCL communicator whose id travels
+over torch.distributed (gloo, control plane only); MCAAT_COMM_BACKEND=gloo uses the
+shared-memory transport instead (ranks sharing one GPU). Scaling "strong": total work fixed.
 --mode replicas: every rank runs its own independent C3-sized sample, no collective on the
 data path (scaling "weak").
 value = all k-mers processed / max-over-ranks step time.
@@ -365,8 +365,6 @@ def main() -> int:
                     help="untimed FASTQ ingest measurement on a file of this many reads (0: skip)")
     ap.add_argument("--mode", default="shard", choices=["shard", "replicas"],
                     help="N>1: one dataset hash-range sharded over the ranks, or one dataset per rank")
-    ap.add_argument("--shard-impl", default="native", choices=["native", "torch"],
-                    help="shard mode: the library's native path (RCCL communicator) or the Python orchestration")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU-only rehearsal of the control flow (ranks, barrier, max-reduce, JSON); no GPU work")
     args = ap.parse_args()
@@ -379,18 +377,11 @@ def main() -> int:
 
     dist = None
     cdev = torch.device("cpu")
-    native = sharded and args.shard_impl == "native"
+    native = sharded
     if world > 1:
         import torch.distributed as dist
 
-        if sharded and not native and not args.dry_run and os.environ.get("MCAAT_COMM_BACKEND", "nccl") == "nccl":
-            # data path: RCCL all-to-all / all-gather of device tensors (MCAAT_COMM_BACKEND=gloo
-            # stages them through host memory instead: a rehearsal with ranks sharing one GPU)
-            torch.cuda.set_device(local)
-            dist.init_process_group("nccl")
-            cdev = torch.device("cuda", local)
-        else:  # control plane only (barrier, max of times)
-            dist.init_process_group("gloo")
+        dist.init_process_group("gloo")  # control plane only (barrier, max of times, the RCCL id)
 
     cfg = dict(CONFIGS[args.config])
     spec = M.SynthSpec(**cfg["spec"].__dict__)
@@ -442,11 +433,6 @@ def main() -> int:
         if native:
             g = M.Graph.build_sharded(ctx, comm, reads, k)
             st_build = ctx.stage_times()
-        elif sharded:
-            from mcaat_amd import shard
-
-            st_build = {}
-            g = shard.sharded_build(shard.DeviceOps(ctx, k), reads, times=st_build)
         else:
             g = M.Graph.build(ctx, reads, k)
             st_build = ctx.stage_times()
@@ -530,9 +516,7 @@ def main() -> int:
     kmers_rank = count * max(0, spec.read_len - k)
     kmers_total = n_occ(spec, k) if sharded else kmers_rank * world
     value = kmers_total / dt
-    if not native:
-        impl = "torch.distributed collectives, CycleFinder replicated"
-    elif os.environ.get("MCAAT_COMM_BACKEND", "nccl") == "nccl":
+    if os.environ.get("MCAAT_COMM_BACKEND", "nccl") == "nccl":
         impl = "native RCCL communicator, CycleFinder over the ranks"
     else:
         impl = "native shared-memory communicator, CycleFinder over the ranks"
@@ -563,7 +547,7 @@ def main() -> int:
                 "kmers_per_gpu": kmers_rank,
                 "kmers_total": kmers_total,
                 "sdbg_edges_D": D,
-                "parallelism": (f"shard{world} (BOSS-key-range all-to-all + all-gather; {impl})"
+                "parallelism": (f"shard{world} (minimizer-range descriptor all-to-all, BOSS-key-range all-to-all + all-gather; {impl})"
                                 if sharded else f"replicas{world}"),
                 "cycle_entries": len(res.entries) if res else 0,
                 "cycles": res.stats[5] if res else 0,

@@ -108,6 +108,16 @@ class HipBuffer:
     def addr(self) -> int:
         return int(self.ptr.value)
 
+    def to_numpy(self, dtype, n: int) -> np.ndarray:
+        """The first n elements of the buffer, copied to the host."""
+        import ctypes
+
+        out = np.zeros(max(n, 1), dtype=dtype)
+        h = self.hip()
+        assert h.hipDeviceSynchronize() == 0
+        assert h.hipMemcpy(out.ctypes.data_as(ctypes.c_void_p), self.ptr, ctypes.c_size_t(out.itemsize * n), 2) == 0
+        return out[:n]
+
     def __del__(self):
         if getattr(self, "ptr", None) is not None and self.ptr.value:
             self.hip().hipFree(self.ptr)

@@ -386,3 +386,48 @@ def test_valid_subgraph_equals_neighbors(gpu_ctx):
     got = np.where(np.arange(4)[None, :] < cnt[:, None], ids[np.minimum(nbr, ids.size - 1)], 0)
     want = np.where(np.arange(4)[None, :] < c[:, None], nb, 0)
     assert np.array_equal(got, want)
+
+
+def test_sharded_build_blocks_two_owners_equal_one_gpu(gpu_ctx):
+    """The C-ABI building blocks a host with its own collectives drives (include/mcaat_gpu.h,
+    "multi-GPU build"): two read halves counted apart (mcaat_count_local), owner ranges of the
+    BOSS key from the summed histogram, each half's pairs grouped by owner
+    (mcaat_counts_partition), the 'exchange' done here through host copies, each owner's pairs
+    sorted and summed (mcaat_edges_reduce), and the owners' ranges in owner order built into a
+    graph (mcaat_graph_from_sorted): the single-GPU keys and multiplicities."""
+    from tests.helpers import HipBuffer
+
+    spec, k, prm = CONFIGS["pe_err"]
+    want_k, want_m, _ = M.Graph.build(gpu_ctx, M.Reads.synth(gpu_ctx, spec), k).download()
+    half = spec.n_reads // 2
+    parts = [M.Reads.synth_range(gpu_ctx, spec, 0, half), M.Reads.synth_range(gpu_ctx, spec, half, spec.n_reads - half)]
+    counts = [M.Counts.count(gpu_ctx, r, k) for r in parts]
+    bits = 10
+    hist = sum(c.histogram(bits).astype(np.int64) for c in counts)
+    cut = int(np.searchsorted(np.cumsum(hist), hist.sum() // 2))  # bins below go to owner 0
+    assert 0 < cut < (1 << bits)
+    splits = np.array([cut << (2 * (k + 1) - bits)], dtype=np.uint64)
+    sent = []  # per source rank: its owner-major keys and counts, and the owners' sizes
+    for c in counts:
+        cap = 2 * c.n + 1
+        kd, cd = HipBuffer(np.zeros(cap, np.uint64)), HipBuffer(np.zeros(cap, np.uint32))
+        sizes = c.partition(splits, kd.addr, cd.addr, cap).astype(np.int64)
+        n = int(sizes.sum())
+        sent.append((kd.to_numpy(np.uint64, n), cd.to_numpy(np.uint32, n), sizes))
+    got_k, got_m = [], []
+    for o in range(2):
+        ks = np.concatenate([kk[sz[:o].sum():sz[:o + 1].sum()] for kk, _, sz in sent])
+        cs = np.concatenate([cc[sz[:o].sum():sz[:o + 1].sum()] for _, cc, sz in sent])
+        kb, cb = HipBuffer(ks), HipBuffer(cs)
+        ko, mo = HipBuffer(np.zeros(max(1, ks.size), np.uint64)), HipBuffer(np.zeros(max(1, ks.size), np.uint16))
+        n = M.edges_reduce(gpu_ctx, k, kb.addr, cb.addr, ks.size, ko.addr, mo.addr)
+        got_k.append(ko.to_numpy(np.uint64, n))
+        got_m.append(mo.to_numpy(np.uint16, n))
+    keys, mult = np.concatenate(got_k), np.concatenate(got_m)
+    assert np.all(got_k[0][-1:] < splits[0]) and np.all(got_k[1][:1] >= splits[0])
+    kb, mb = HipBuffer(keys), HipBuffer(mult)
+    g = M.Graph.from_sorted(gpu_ctx, k, kb.addr, mb.addr, keys.size)
+    gk, gm, _ = g.download()
+    assert np.array_equal(gk, want_k) and np.array_equal(gm, want_m)
+    for c in counts:
+        c.free()
