@@ -65,3 +65,11 @@ def test_sanitized_oracle_and_downstream(driver, tmp_path, name):
     n = DS.crispr_arrays(k, keys, mult, valid, cycles, reads, str(want))
     assert int(line[10]) == n
     assert report.read_text() == want.read_text()
+
+
+def test_sanitized_idmap(driver):
+    """The host mirror's open-addressing map against std::unordered_map, ~0 keys included
+    (tests/sanitize/idmap_test.cpp, same sanitizer build)."""
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1", UBSAN_OPTIONS="print_stacktrace=1")
+    p = subprocess.run([os.path.join(SAN, "build", "idmap_test")], capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0 and "idmap ok" in p.stdout, (p.stdout + p.stderr)[-3000:]
