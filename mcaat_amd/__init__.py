@@ -9,12 +9,14 @@ from .lib import (  # noqa: F401
     CfParams,
     Comm,
     Context,
+    Counts,
     CycleResult,
     Graph,
     McaatError,
     Reads,
     SynthSpec,
     count_edges,
+    edges_reduce,
     device_count,
     load_library,
     synth_arrays,

@@ -164,16 +164,21 @@ def test_cluster_bound_and_step_cap(gpu_ctx):
 
 
 def test_lds_overflow_fallback_low_coverage(gpu_ctx):
-    """Low coverage: almost every edge is distinct, every LDS partition overflows and the
-    global-table fallback counts it; results must still equal the oracle."""
+    """Low coverage: almost every edge is distinct and every LDS partition overflows. By default
+    the partitions are split down to eight classes (round 4); with the split depth of round 3
+    (two bits) the global-table fallback counts the classes still over. Both equal the oracle."""
     spec = M.SynthSpec(seed=31, n_genomes=50, genome_len=1_000_000, arrays_per_genome=0, n_reads=60_000,
                        error_rate=0.01)
     packed, offs = M.synth_host(spec)
     reads = M.Reads.synth(gpu_ctx, spec)
-    gk, gc = M.count_edges(gpu_ctx, reads, 27)
     ok, oc = O.count_canonical(packed, offs, 27, threads=4)
-    assert np.array_equal(gk, ok) and np.array_equal(gc, oc)
-    assert gpu_ctx.kernel_timing("lds_count_overflow_partitions")[1] > 0
+    for depth in (3, 2):
+        gpu_ctx.reset_timing()
+        with gpu_ctx.knobs(nc__split_max=depth):
+            gk, gc = M.count_edges(gpu_ctx, reads, 27)
+        assert np.array_equal(gk, ok) and np.array_equal(gc, oc), depth
+        if depth == 2:
+            assert gpu_ctx.kernel_timing("lds_count_overflow_partitions")[1] > 0
 
 
 @pytest.mark.parametrize("mini_w", ["", "14", "16"])

@@ -61,7 +61,27 @@ def main() -> int:
     ap.add_argument("--digest", default="", help="write checksums here (JSON) instead of comparing")
     ap.add_argument("--single", action="store_true", help="the one-GPU path alone (with --digest)")
     ap.add_argument("--knob", action="append", default=[], help="name=value knob on every rank's context")
+    ap.add_argument("--repeat", type=int, default=1, help="--config: sharded builds in a row (stages of the last)")
     a = ap.parse_args()
+
+    def make_comm(ctx):
+        if a.comm == "shm":
+            return M.Comm.shm(ctx, a.world, a.rank, a.name, a.slot)
+        if a.rank == 0:
+            uid = M.Comm.unique_id()
+            tmp = a.uid_file + ".tmp"
+            with open(tmp, "wb") as f:
+                f.write(uid)
+            os.replace(tmp, a.uid_file)
+        else:
+            t0 = time.time()
+            while not os.path.exists(a.uid_file):
+                if time.time() - t0 > 120:
+                    raise SystemExit("no unique id file")
+                time.sleep(0.05)
+        with open(a.uid_file, "rb") as f:
+            uid = f.read()
+        return M.Comm.rccl(ctx, a.world, a.rank, uid)
 
     if a.config:
         import json
@@ -82,13 +102,16 @@ def main() -> int:
             res = g.cycle_finder(prm, as_arrays=False)
             comm = None
         else:
-            comm = M.Comm.shm(ctx, a.world, a.rank, a.name, a.slot) if a.comm == "shm" else None
-            assert comm is not None, "--config runs use the shared-memory transport"
+            comm = make_comm(ctx)
             first = a.rank * spec.n_reads // a.world
             count = (a.rank + 1) * spec.n_reads // a.world - first
             mine = M.Reads.synth_range(ctx, spec, first, count)
-            g = M.Graph.build_sharded(ctx, comm, mine, k)
-            build_stages = {kk: round(vv, 2) for kk, vv in ctx.stage_times().items()}
+            for rep in range(a.repeat):  # stage times of the last build (the first pays allocations)
+                if rep:
+                    g.free()
+                ctx.stage_times()
+                g = M.Graph.build_sharded(ctx, comm, mine, k)
+                build_stages = {kk: round(vv, 2) for kk, vv in ctx.stage_times().items()}
             mine.free()
             res = g.cycle_finder(prm, comm=comm)
         d = checksums(g, res)
@@ -117,24 +140,7 @@ def main() -> int:
     for kv in a.knob:
         kn, kval = kv.split("=")
         ctx.set_knob(kn, int(kval))
-    if a.comm == "shm":
-        comm = M.Comm.shm(ctx, a.world, a.rank, a.name, a.slot)
-    else:
-        if a.rank == 0:
-            uid = M.Comm.unique_id()
-            tmp = a.uid_file + ".tmp"
-            with open(tmp, "wb") as f:
-                f.write(uid)
-            os.replace(tmp, a.uid_file)
-        else:
-            t0 = time.time()
-            while not os.path.exists(a.uid_file):
-                if time.time() - t0 > 120:
-                    raise SystemExit("no unique id file")
-                time.sleep(0.05)
-        with open(a.uid_file, "rb") as f:
-            uid = f.read()
-        comm = M.Comm.rccl(ctx, a.world, a.rank, uid)
+    comm = make_comm(ctx)
     assert (comm.world, comm.rank) == (a.world, a.rank)
 
     first = a.rank * spec.n_reads // a.world
