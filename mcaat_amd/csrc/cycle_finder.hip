@@ -213,13 +213,20 @@ __global__ void __launch_bounds__(kBlock) k_word_pop(const uint64_t *bm, uint64_
 template <int kScanU>
 // fresh: every edge is valid before the filter (mcaat_graph::all_valid), so an edge is a tip
 // iff it has no out-edges at all, and no window of the unfiltered bitmap is read
+// pull (round 4, with the peel's arrays): an edge writes its own predecessor flags instead of
+// each predecessor setting a byte at its successors' slots. All predecessors of y share y's
+// source node, so their filtered out-degree is the number of filter-valid siblings of y (the
+// out-edges of that node: consecutive ids, and with any predecessor present exactly the ids
+// around y whose in_info word equals y's), and y has one iff its in-edge window holds a
+// filter-valid edge. One 4-byte store per edge, no scattered byte stores and no clearing pass.
 __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_lo, uint64_t w_hi, uint64_t *tip_bm,
                                                         const uint64_t *post, unsigned long long *counts, PeelArrays pa,
-                                                        uint64_t thr, uint64_t *cand, uint64_t cap, bool fresh) {
+                                                        uint64_t thr, uint64_t *cand, uint64_t cap, bool fresh, bool pull) {
     const int lane = threadIdx.x & 63;
     const uint64_t nw = (g.D + 63) / 64;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const bool peel = pa.nf != nullptr, fold = cand != nullptr;
+    pull = pull && peel;
     const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     __shared__ uint64_t cbuf[kBlock / 64][128];
     WaveList cl{cbuf[threadIdx.x >> 6], cand, counts + 3, cap};
@@ -242,7 +249,7 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_
         for (int u = 0; u < kScanU; ++u) {
             const uint64_t w = wb + u * wstride, e = w * 64 + lane;
             // the candidate filter's in-edge window, for post-filter valid edges above thr
-            const bool cv = fold && e < g.D && w < w_hi && ((pv[u] >> lane) & 1) && (uint64_t)mu[u] > thr;
+            const bool cv = e < g.D && w < w_hi && ((pv[u] >> lane) & 1) && (pull || (fold && (uint64_t)mu[u] > thr));
             ii[u] = cv ? g.in_info[e] : 0;
         }
 #pragma unroll
@@ -250,7 +257,38 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_
             const uint64_t lo = oi[u] & kIdxMask;
             if (!fresh) a[u] = word_pair(g.valid, lo, nw);
             if (peel || fold) a2[u] = word_pair(post, lo, nw);
-            if (fold) b[u] = word_pair(post, ii[u] & kIdxMask, nw);
+            if (fold || pull) b[u] = word_pair(post, ii[u] & kIdxMask, nw);
+        }
+        // pull: filter-valid siblings of each edge (equal in_info words within 3 ids); the ids
+        // outside the wave's word come from the neighbouring words, read only by the lanes at
+        // its ends that need them
+        uint32_t sib[kScanU];
+        if (pull) {
+#pragma unroll
+            for (int u = 0; u < kScanU; ++u) {
+                const uint64_t w = wb + u * wstride, e = w * 64 + lane;
+                const uint64_t my = ii[u];
+                uint32_t c = 0;
+#pragma unroll
+                for (int d = -3; d <= 3; ++d) {
+                    if (!d) continue;
+                    const int nl = lane + d;
+                    const uint64_t x = __shfl(my, nl & 63);  // every lane shuffles (uniform)
+                    if (nl >= 0 && nl < 64) c += x == my;
+                }
+                const bool edge_lane = lane < 3 || lane > 60;
+                if (edge_lane && my && ((pv[u] >> lane) & 1) && w < w_hi) {
+                    for (int d = -3; d <= 3; ++d) {
+                        const int nl = lane + d;
+                        if (nl >= 0 && nl < 64) continue;
+                        const int64_t y = (int64_t)e + d;
+                        if (y < 0 || (uint64_t)y >= g.D) continue;
+                        if (!((post[(uint64_t)y >> 6] >> (y & 63)) & 1)) continue;
+                        c += g.in_info[y] == my;
+                    }
+                }
+                sib[u] = c + 1;  // and the edge itself
+            }
         }
 #pragma unroll
         for (int u = 0; u < kScanU; ++u) {
@@ -298,14 +336,22 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_
                             ++od;
                             i1 = i;
                         }
-                    pa.kind(ce) = (uint8_t)od;
-                    if (od == 1) {
-                        const uint64_t cy = cs(i1);
-                        pa.nxk[ce] = cy;
-                        pa.upred(cy) = 1;
+                    if (pull) {
+                        const uint64_t l = ii[u] & kIdxMask;
+                        const bool haspred = (bits16(b[u].a, b[u].b, l) & (uint32_t)((ii[u] >> kIdxBits) & 0xFFFF)) != 0;
+                        const uint32_t up = haspred && sib[u] == 1, bp = haspred && sib[u] >= 2;
+                        *(uint32_t *)(pa.nf + 4 * ce) = (uint32_t)od | (up << (8 * kFUpred)) | (bp << (8 * kFBpred));
+                        if (od == 1) pa.nxk[ce] = cs(i1);
                     } else {
-                        for (int i = (int)cnt - 1; i >= 0; --i)
-                            if ((pfo >> i) & 1) pa.bpred(cs(i)) = 1;
+                        pa.kind(ce) = (uint8_t)od;
+                        if (od == 1) {
+                            const uint64_t cy = cs(i1);
+                            pa.nxk[ce] = cy;
+                            pa.upred(cy) = 1;
+                        } else {
+                            for (int i = (int)cnt - 1; i >= 0; --i)
+                                if ((pfo >> i) & 1) pa.bpred(cs(i)) = 1;
+                        }
                     }
                 }
             }
@@ -2282,6 +2328,11 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
     uint64_t n_cand = 0, tips_after = 0;
     // every edge valid (as built): the passes before the filter read no unfiltered bitmap
     const bool fresh = g->all_valid && knob(ctx, "cf.fresh", 1) != 0;
+    // (round 4) cf.pull_flags=1: the tips pass writes each edge's predecessor flags from its own
+    // side (k_tips_filter). Measured slower, off: C3 tips 14.4 -> 25.5 ms, C5 55.1 -> 69.6 ms (the
+    // in-edge window gather and in_info read for every filter-valid edge cost more than the
+    // scattered flag bytes and the clearing pass they replace)
+    const bool pull = knob(ctx, "cf.pull_flags", 0) != 0;
     g->all_valid = false;  // the filter and the peel clear bits from here on
     // the filtered bitmap (whole graph); the peel's compact slots index it, so it stays unchanged
     // until the peel is done (the graph's own copy is the one the peel clears)
@@ -2329,7 +2380,7 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
             const uint64_t S = std::max<uint64_t>(compact ? ps.slots : D, 1);
             ps.nf.alloc(4 * S);
             ps.nxk.alloc(S);
-            HIP_OK(hipMemsetAsync(ps.nf.p, 0, ps.nf.bytes(), st));
+            if (!pull) HIP_OK(hipMemsetAsync(ps.nf.p, 0, ps.nf.bytes(), st));  // pull: every slot read is written
             ps.ready = true;
         }
         // 1. CollectTips (before the filter: the seeds of the reduction), with the peel's first
@@ -2346,7 +2397,7 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
             auto kern = scan_u == 1 ? k_tips_filter<1> : scan_u == 4 ? k_tips_filter<4> : k_tips_filter<kScanUDefault>;
             hipLaunchKernelGGL(kern, dim3(wgrid), dim3(kBlock), 0, st, v, w_lo, w_hi, comm ? mseeds.p : seeds.p + w_lo,
                                (const uint64_t *)post.p, c2.p, fa, (uint64_t)p.threshold_multiplicity,
-                               fold ? clist.p : (uint64_t *)nullptr, ccap, fresh);
+                               fold ? clist.p : (uint64_t *)nullptr, ccap, fresh, pull);
             LAUNCH_OK();
         }
         unsigned long long hc[4];
@@ -2354,7 +2405,7 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
         HIP_OK(hipStreamSynchronize(st));
         if (fold && hc[3] > ccap) {  // more candidates than the list held: the pass again (idempotent), sized
             ccap = hc[3];
-            if (fuse) HIP_OK(hipMemsetAsync(ps.nf.p, 0, ps.nf.bytes(), st));  // its flag bytes are set again
+            if (fuse && !pull) HIP_OK(hipMemsetAsync(ps.nf.p, 0, ps.nf.bytes(), st));  // its flag bytes are set again
             continue;
         }
         n_cand = fold ? hc[3] : 0;

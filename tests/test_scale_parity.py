@@ -102,6 +102,10 @@ KNOBS = {
     "peel_compact_own_init": {"cf.compact": 1, "cf.fused_init": 0},
     "tips_not_fresh": {"cf.fresh": 0},
     "compact_lists_regrow": {"cf.compact": 1, "cf.peel_list_cap": 1, "cf.cand_cap": 1, "cf.fresh": 0},
+    # (round 4) predecessor flags written from each edge's own side, per-id and compact slots,
+    # fresh and with the candidate list regrown (the pass runs twice without clearing)
+    "pull_flags": {"cf.pull_flags": 1},
+    "pull_flags_compact_regrow": {"cf.pull_flags": 1, "cf.compact": 1, "cf.cand_cap": 1, "cf.fresh": 0},
     # (round 4) DepthLevelSearch with per-lane scratch instead of per-candidate batches
     "dls_persist": {"cf.dls_persist": 1},
     "dls_persist_regrow": {"cf.dls_persist": 1, "cf.dls_stack": 1, "cf.dls_visited": 2},
