@@ -232,7 +232,7 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_
     WaveList cl{cbuf[threadIdx.x >> 6], cand, counts + 3, cap};
     unsigned long long acc = 0, tips_pf = 0;
     for (uint64_t wb = w_lo + (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6); wb < w_hi; wb += kScanU * wstride) {
-        uint64_t sv[kScanU], pv[kScanU], oi[kScanU];
+        uint64_t sv[kScanU], pv[kScanU], oi[kScanU], xb[kScanU];
         WordPair a[kScanU], a2[kScanU];
         uint32_t mu[kScanU];
 #pragma unroll
@@ -242,6 +242,16 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_
             pv[u] = w < w_hi ? post[w] : 0;
             oi[u] = e < g.D && w < w_hi ? g.out_info[e] : 0;
             mu[u] = e < g.D && w < w_hi && fold ? g.mult[e] : 0;
+            // pull: lanes 0..2 and 61..63 hold the in_info words of the 3 ids on either side of
+            // the word (0 unless filter-valid), for their neighbours' sibling counts
+            xb[u] = 0;
+            if (pull && w < w_hi && (lane < 3 || lane > 60)) {
+                const int64_t y = lane < 3 ? (int64_t)(w * 64) - 3 + lane : (int64_t)(w * 64) + 64 + (lane - 61);
+                if (y >= 0 && (uint64_t)y < g.D) {  // both loads issued together
+                    const uint64_t x = g.in_info[y], pw = post[(uint64_t)y >> 6];
+                    xb[u] = ((pw >> (y & 63)) & 1) ? x : 0;
+                }
+            }
         }
         uint64_t ii[kScanU];
         WordPair b[kScanU];
@@ -273,20 +283,13 @@ __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_
                 for (int d = -3; d <= 3; ++d) {
                     if (!d) continue;
                     const int nl = lane + d;
-                    const uint64_t x = __shfl(my, nl & 63);  // every lane shuffles (uniform)
-                    if (nl >= 0 && nl < 64) c += x == my;
+                    // every lane shuffles (uniform): the neighbour's word from its lane, or from the
+                    // lane holding that id outside the word (xb, loaded with the scan's other loads)
+                    const uint64_t x = __shfl(my, nl & 63);
+                    const uint64_t xo = __shfl(xb[u], nl < 0 ? nl + 3 : (nl - 64 + 61) & 63);
+                    c += (nl >= 0 && nl < 64 ? x : xo) == my;
                 }
-                const bool edge_lane = lane < 3 || lane > 60;
-                if (edge_lane && my && ((pv[u] >> lane) & 1) && w < w_hi) {
-                    for (int d = -3; d <= 3; ++d) {
-                        const int nl = lane + d;
-                        if (nl >= 0 && nl < 64) continue;
-                        const int64_t y = (int64_t)e + d;
-                        if (y < 0 || (uint64_t)y >= g.D) continue;
-                        if (!((post[(uint64_t)y >> 6] >> (y & 63)) & 1)) continue;
-                        c += g.in_info[y] == my;
-                    }
-                }
+                (void)e;
                 sib[u] = c + 1;  // and the edge itself
             }
         }
@@ -2329,7 +2332,7 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
     // every edge valid (as built): the passes before the filter read no unfiltered bitmap
     const bool fresh = g->all_valid && knob(ctx, "cf.fresh", 1) != 0;
     // (round 4) cf.pull_flags=1: the tips pass writes each edge's predecessor flags from its own
-    // side (k_tips_filter). Measured slower, off: C3 tips 14.4 -> 25.5 ms, C5 55.1 -> 69.6 ms (the
+    // side (k_tips_filter). Measured slower, off: C3 tips 14.3 -> 15.8 ms, C5 55.2 -> 61.9 ms (the
     // in-edge window gather and in_info read for every filter-valid edge cost more than the
     // scattered flag bytes and the clearing pass they replace)
     const bool pull = knob(ctx, "cf.pull_flags", 0) != 0;

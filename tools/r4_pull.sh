@@ -1,8 +1,8 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests/test_gpu_parity.py tests/test_scale_parity.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/t8.log 2>&1 || { tail -30 gpurun_out/t8.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_scale_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "pull or compact or fresh or peel or knob" > gpurun_out/t8.log 2>&1 || { tail -30 gpurun_out/t8.log; exit 1; }
 tail -1 gpurun_out/t8.log
 CFG=c3 STEPS=3 bash tools/abq.sh default
-MCAAT_KNOBS=cf.pull_flags=0 CFG=c3 STEPS=3 bash tools/abq.sh default
+MCAAT_KNOBS=cf.pull_flags=1 CFG=c3 STEPS=3 bash tools/abq.sh default
 CFG=c5 STEPS=2 bash tools/abq.sh default
-MCAAT_KNOBS=cf.pull_flags=0 CFG=c5 STEPS=2 bash tools/abq.sh default
+MCAAT_KNOBS=cf.pull_flags=1 CFG=c5 STEPS=2 bash tools/abq.sh default
