@@ -1006,7 +1006,7 @@ int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value) {
         "nc.overlap",      "sort.l3_counting",   "cf.peel_list_div", "cf.peel_list_cap", "cf.cand_cap",
         "fq.hostpack",     "sort.mid_counting", "nc.big_table", "cf.fused_init", "sort.mid_occ", "cf.scan_u", "cf.prep_batch", "cf.dls_lanes", "dist.oriented",
         "sort.small_mid", "sort.small_limit", "cf.recount", "cf.dls_host",
-        "dist.desc",      "cf.compact",         "cf.fresh",   "cf.dls_persist", "nc.split_first", "nc.split_max", "cf.pull_flags"};
+        "dist.desc",      "cf.compact",         "cf.fresh",   "cf.dls_persist", "nc.split_first", "nc.split_max", "cf.pull_flags", "cf.dls_budget", "nc.grow_early"};
     return guarded([&] {
         require(ctx && name, "null argument");
         bool ok = false;

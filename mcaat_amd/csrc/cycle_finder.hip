@@ -1854,7 +1854,9 @@ static std::vector<uint64_t> run_dls_dev(mcaat_graph *g, const uint64_t *dcand, 
     // wave runs its lanes' candidate sequences to the longest sum, and finished waves leave their
     // CU idle): off by default
     const bool persist = knob(ctx, "cf.dls_persist", 0) != 0;
-    const bool many = !persist && n * 8ULL * (1024 + 2048) > (8ULL << 30);
+    // scratch budget of one launch (knob cf.dls_budget, GB)
+    const uint64_t budget = (uint64_t)std::max<int64_t>(1, knob(ctx, "cf.dls_budget", 8)) << 30;
+    const bool many = !persist && n * 8ULL * (1024 + 2048) > budget;
     uint32_t cs = (uint32_t)std::max<int64_t>(1, knob(ctx, "cf.dls_stack", many ? 128 : 1024));
     uint32_t cv = (uint32_t)next_pow2((uint64_t)std::max<int64_t>(2, knob(ctx, "cf.dls_visited", many ? 256 : 2048)));
     const int lanes = (int)std::max<int64_t>(1, std::min<int64_t>(64, knob(ctx, "cf.dls_lanes", 16)));
@@ -1865,7 +1867,7 @@ static std::vector<uint64_t> run_dls_dev(mcaat_graph *g, const uint64_t *dcand, 
     LAUNCH_OK();
     uint64_t nt = n;
     for (bool first = true; nt; first = false) {
-        const uint64_t batch_cap = std::max<uint64_t>(64, (8ULL << 30) / (8ULL * (cs + cv)));
+        const uint64_t batch_cap = std::max<uint64_t>(64, budget / (8ULL * (cs + cv)));
         const uint64_t *src = dcand;
         if (!first) {  // the candidates to search again, in candidate order
             hipLaunchKernelGGL(k_gather_ids, dim3(grid_for(nt, kBlock)), dim3(kBlock), 0, st, dcand,

@@ -1855,12 +1855,13 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
             out_cap = ncap;
             const unsigned long long keep = n_out;
             HIP_OK(hipMemcpyAsync(dcnt.p, &keep, 8, hipMemcpyHostToDevice, st));
+            HIP_OK(hipStreamSynchronize(st));  // keep is a host local; the old buffers are already free
         }
         // (round 4) the output is sized from n_occ / 32 (C3: 0.53 G distinct of 1.15 G); an
         // error-rich input (C5: ~2 G) used to overflow it mid-run, re-count a whole group and copy
         // everything counted so far. The groups are hash ranges, so the first (the small probe)
         // already tells the total: grow once, early, while little is copied.
-        if (gi + 1 < groups.size() && !knob_set(ctx, "nc.out_cap") && hfine[p1] > 0) {
+        if (gi + 1 < groups.size() && (!knob_set(ctx, "nc.out_cap") || knob(ctx, "nc.grow_early", 0)) && hfine[p1] > 0) {
             const double frac = (double)hfine[p1] / (double)std::max<uint64_t>(n_live, 1);
             const uint64_t est = (uint64_t)((double)n_out / frac * 1.08) + (1u << 20);
             if (est > out_cap) {
@@ -1868,6 +1869,9 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
                 DevBuf<uint32_t> c2(est);
                 HIP_OK(hipMemcpyAsync(k2.p, out.keys.p, 8 * n_out, hipMemcpyDeviceToDevice, st));
                 HIP_OK(hipMemcpyAsync(c2.p, out.counts.p, 4 * n_out, hipMemcpyDeviceToDevice, st));
+                // the arena reuses freed memory at once, and the next group's pass B (side stream)
+                // may be handed the old buffers: the copies land before they are freed
+                HIP_OK(hipStreamSynchronize(st));
                 out.keys = std::move(k2);
                 out.counts = std::move(c2);
                 out_cap = est;

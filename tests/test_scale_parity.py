@@ -38,6 +38,9 @@ CASES = {
 KNOBS = {
     # one L1 bucket per pass-B/C group, the count output regrown (and the group recounted)
     "multi_group": {"nc.group_budget": 1, "nc.out_cap": 1},
+    # (round 4) the output grown once after the first group, while the next group's pass B runs
+    # on the side stream (the old buffers must not be reused before their copy lands)
+    "grow_early": {"nc.group_budget": 1, "nc.out_cap": 64, "nc.grow_early": 1},
     # L1 buckets undersized on the first pass-A attempt: resize and re-run
     "l1_resize": {"nc.l1_slots": 64, "nc.fine_bits": 12},
     # every partition overflows the LDS edge table: class split, then the class-filtered global
@@ -157,7 +160,7 @@ def test_forced_branches_match_oracle(gpu_ctx, name, knobset):
     ref = _oracle(name)
     reads = M.Reads.synth(gpu_ctx, spec)
     with gpu_ctx.knobs(**{n.replace(".", "__"): v for n, v in KNOBS[knobset].items()}):
-        if knobset.startswith(("multi", "l1", "fallback", "desc")):
+        if knobset.startswith(("multi", "l1", "fallback", "desc", "grow")):
             gk, gc = M.count_edges(gpu_ctx, reads, k)
             assert np.array_equal(gk, ref["ck"]) and np.array_equal(gc, ref["cc"]), (name, knobset)
         g = M.Graph.build(gpu_ctx, reads, k)
