@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--settle", type=float, default=0.0, help="seconds to wait after writing the FASTQ")
     ap.add_argument("--preread", action="store_true", help="read the file once (8 threads) before the runs")
+    ap.add_argument("--gap", type=float, default=0.0, help="seconds between runs (the driver scrubs freed VRAM)")
     a = ap.parse_args()
     cfg = bench.CONFIGS[a.config]
     spec = M.SynthSpec(**cfg["spec"].__dict__)
@@ -68,7 +69,9 @@ def main():
         st = os.path.join(work, "s.txt")
         with open(st, "w") as f:
             f.write(f"kmer_k={cfg['k']}\nthreshold_multiplicity={cfg['thr']}\n")
-        for var in (a.variants.split(";") if a.variants else [""]):
+        for vi, var in enumerate(a.variants.split(";") if a.variants else [""]):
+            if vi and a.gap:
+                time.sleep(a.gap)
             env = dict(os.environ)
             for kv in filter(None, var.split(",")):
                 k, v = kv.split("=", 1)
