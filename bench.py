@@ -220,8 +220,9 @@ def measure_e2e(cfg: dict, spec, fastq: str, threads: int, n_kmers: int) -> dict
             "fastq_bytes": os.path.getsize(fastq), "fastq_GBps": round(os.path.getsize(fastq) / lib / 1e9, 2),
             "cli_wall_s": round(wall, 3), "cli_phases_s": tail, "crispr_systems": n_arr, "planted_recall": recall,
             "note": "fresh CLI process on a GPU no earlier process of this job used, FASTQ in tmpfs (/dev/shm, "
-                    "pages settled by one untimed read); the span excludes process start, HIP runtime init (input "
-                    "check) and the downstream steps 6-8 (cli_wall_s includes them)",
+                    "pages settled by one untimed read); the span excludes process start, HIP runtime init and the "
+                    "kernels' code-object load (input check, mcaat_preload) and the downstream steps 6-8 "
+                    "(cli_wall_s includes them)",
         }
     finally:
         shutil.rmtree(work, ignore_errors=True)

@@ -49,6 +49,9 @@ void mcaat_finalize(mcaat_ctx *ctx);
 void mcaat_trim(mcaat_ctx *ctx);
 const char *mcaat_last_error(void);
 int mcaat_device_count(int *n);
+/* load the hot path's kernel code objects on `device` now rather than at each one's first launch
+ * (HIP's deferred loading); the CLI calls it with the runtime init, before its timed span */
+int mcaat_preload(int device);
 
 /* ---- reads ----------------------------------------------------------------
  * Replaces: SDBGBuild::BuildLib / SequenceLibCollection::Build (sdbg_build.cpp:82-115):

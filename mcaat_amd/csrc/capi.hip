@@ -352,6 +352,23 @@ int mcaat_device_count(int *n) {
     });
 }
 
+int mcaat_preload(int device) {
+    return guarded([&] {
+        int c = 0;
+        if (hipGetDeviceCount(&c) != hipSuccess || device < 0 || device >= c) {
+            (void)hipGetLastError();
+            throw Error(MCAAT_E_HIP, "no such HIP device");
+        }
+        HIP_OK(hipSetDevice(device));
+        mcaat::preload_fastq_pack();
+        mcaat::preload_node_counter();
+        mcaat::preload_sdbg_build();
+        mcaat::preload_cycle_finder();
+        mcaat::preload_read_mapping();
+        (void)hipGetLastError();
+    });
+}
+
 int mcaat_init(int device, mcaat_ctx **out) {
     return guarded([&] {
         require(out != nullptr, "null argument");

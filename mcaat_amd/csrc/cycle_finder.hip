@@ -2700,4 +2700,10 @@ void graph_download_valid(const mcaat_graph *g, uint8_t *valid) {
     HIP_OK(hipStreamSynchronize(st));
 }
 
+// loads this file's code object now (HIP defers it to the first launch of one of its kernels)
+void preload_cycle_finder() {
+    hipFuncAttributes a;
+    (void)hipFuncGetAttributes(&a, (const void *)k_word_pop);
+}
+
 }  // namespace mcaat

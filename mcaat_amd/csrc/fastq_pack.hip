@@ -551,4 +551,10 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
     return true;
 }
 
+// loads this file's code object now (HIP defers it to the first launch of one of its kernels)
+void preload_fastq_pack() {
+    hipFuncAttributes a;
+    (void)hipFuncGetAttributes(&a, (const void *)k_offsets_fixed);
+}
+
 }  // namespace mcaat

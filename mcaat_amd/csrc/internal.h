@@ -47,6 +47,11 @@ void *dev_alloc(size_t bytes);
 void dev_free(void *p, size_t bytes, int device);
 int current_device();
 void dev_trim();
+void preload_node_counter();
+void preload_sdbg_build();
+void preload_cycle_finder();
+void preload_fastq_pack();
+void preload_read_mapping();
 
 // owning device buffer
 template <class T>

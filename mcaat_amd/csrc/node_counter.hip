@@ -1913,4 +1913,10 @@ void sort_counts(mcaat_ctx *ctx, CountResult &c, int k) {
     c.counts = std::move(c2);
 }
 
+// loads this file's code object now (HIP defers it to the first launch of one of its kernels)
+void preload_node_counter() {
+    hipFuncAttributes a;
+    (void)hipFuncGetAttributes(&a, (const void *)k_l2_hist);
+}
+
 }  // namespace mcaat

@@ -302,4 +302,10 @@ void graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n) {
     HIP_OK(hipStreamSynchronize(st));
 }
 
+// loads this file's code object now (HIP defers it to the first launch of one of its kernels)
+void preload_read_mapping() {
+    hipFuncAttributes a;
+    (void)hipFuncGetAttributes(&a, (const void *)k_label_set);
+}
+
 }  // namespace mcaat

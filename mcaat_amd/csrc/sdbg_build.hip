@@ -1298,4 +1298,10 @@ void sdbg_finish(mcaat_ctx *ctx, mcaat_graph *g) {
     HIP_OK(hipStreamSynchronize(st));
 }
 
+// loads this file's code object now (HIP defers it to the first launch of one of its kernels)
+void preload_sdbg_build() {
+    hipFuncAttributes a;
+    (void)hipFuncGetAttributes(&a, (const void *)k_count_pal);
+}
+
 }  // namespace mcaat

@@ -221,6 +221,10 @@ static int run(Settings &settings, Ranks &ranks) {
         // it has written data.lib as the reference does)
         int n_dev = 0;
         (void)mcaat_device_count(&n_dev);
+        // and loads the kernels' code objects (HIP otherwise loads each file's at the first launch
+        // of one of its kernels, inside the span); MCAAT_PRELOAD=0 leaves that to HIP
+        const char *pl = getenv("MCAAT_PRELOAD");
+        if (n_dev > 0 && !(pl && pl[0] == '0')) (void)mcaat_preload(mcaat_rank_device(settings));
     }
     if (settings.gpus > 1) {
         if (const char *e = getenv("MCAAT_TEST_RANK_EXIT"))  // test hook: this rank dies before joining
