@@ -61,6 +61,7 @@ SIGNATURES = {
     "mcaat_finalize": (None, [C.c_void_p]),
     "mcaat_last_error": (C.c_char_p, []),
     "mcaat_device_count": (C.c_int, [C.POINTER(C.c_int)]),
+    "mcaat_preload": (C.c_int, [C.c_int]),
     "mcaat_reads_from_host": (C.c_int, [C.c_void_p, _u64p, C.c_uint64, _u64p, C.c_uint64, C.POINTER(C.c_void_p)]),
     "mcaat_reads_from_fastx": (C.c_int, [C.c_void_p, C.POINTER(C.c_char_p), C.c_int, C.POINTER(C.c_void_p)]),
     "mcaat_reads_info": (C.c_int, [C.c_void_p, _u64p, _u64p]),
