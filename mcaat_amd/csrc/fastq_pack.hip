@@ -38,7 +38,14 @@ namespace {
 
 constexpr size_t kBlk = 16u << 20;        // bytes read per pread() block
 constexpr size_t kMaxRecord = 1u << 20;   // longest record the fast path takes
-constexpr size_t kStageWords = 1u << 20;  // packed words per pinned staging buffer (8 MB)
+// packed words per pinned staging buffer (2 MB; round 3's 8 MB made the first call pin 256 MB
+// for 16 threads, 52 ms inside the span, for no faster upload)
+constexpr size_t kStageWords = 1u << 18;
+// upload streams shared by the threads (thread t uses stream t % kUpStreams; 0: the context's
+// own stream). Round 3 created one per thread, ~4.5 ms each (77 ms for 16, inside the span);
+// the uploads (~10 GB/s in all) need no more than one: 0 / 2 / 4 streams measured build_lib
+// 1.15-1.19 / 1.24-1.29 / 1.23-1.24 s at C3 (the packing itself unchanged)
+constexpr int kUpStreams = 0;
 constexpr int kPB = 256;
 
 // ---------------------------------------------------------------- packing
@@ -431,7 +438,9 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
         outs[t].cap = (parts[t].e - parts[t].b) / 64 + 64;
         rw += outs[t].cap;
     }
+    verbose_mark(ctx, "fq.parts");
     DevBuf<uint64_t> regions(rw);
+    verbose_mark(ctx, "fq.regions");
     const size_t stage_bytes = (size_t)P * 2 * kStageWords * 8;
     if (ctx->pack_pinned_bytes < stage_bytes) {
         if (ctx->pack_pinned) HIP_OK(hipHostFree(ctx->pack_pinned));
@@ -440,19 +449,29 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
         HIP_OK(hipHostMalloc((void **)&ctx->pack_pinned, stage_bytes, hipHostMallocDefault));
         ctx->pack_pinned_bytes = stage_bytes;
     }
-    std::vector<hipStream_t> streams(P, nullptr);
+    verbose_mark(ctx, "fq.pinned");
+    // MCAAT_UP_STREAMS (A/B): upload streams; 0 = the context's own stream, none created
+    int ns = kUpStreams;
+    if (const char *e = getenv("MCAAT_UP_STREAMS")) ns = std::max(0, atoi(e));
+    std::vector<hipStream_t> streams(std::min(P, std::max(ns, 1)), nullptr);
     struct Streams {
         std::vector<hipStream_t> &s;
+        hipStream_t own;
         ~Streams() {
             for (auto x : s)
-                if (x) {
+                if (x && x != own) {
                     (void)hipStreamSynchronize(x);
                     (void)hipStreamDestroy(x);
                 }
         }
-    } sguard{streams};
-    for (auto &s : streams) HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    } sguard{streams, st};
+    if (ns == 0) {
+        streams[0] = st;  // not destroyed: the guard below skips it
+    } else {
+        for (auto &s : streams) HIP_OK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    }
 
+    verbose_mark(ctx, "fq.streams");
     Shared sh;
     std::vector<int> ok(P, 0);
     std::vector<std::string> err(P);
@@ -462,7 +481,7 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
             // context's device, as its stream does
             HIP_OK(hipSetDevice(ctx->device));
             uint64_t *s0 = (uint64_t *)ctx->pack_pinned + (size_t)t * 2 * kStageWords;
-            PartPacker pk(regions.p + outs[t].region, s0, s0 + kStageWords, streams[t], outs[t]);
+            PartPacker pk(regions.p + outs[t].region, s0, s0 + kStageWords, streams[t % streams.size()], outs[t]);
             const bool good = pack_part(files[parts[t].file], parts[t].b, parts[t].e, parts[t].file_end, pk, sh, outs[t]);
             if (good) pk.finish();
             ok[t] = good;
@@ -478,6 +497,7 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
         job(0);
         for (auto &th : pool) th.join();
     }
+    verbose_mark(ctx, "fq.pack");
     for (int t = 0; t < P; ++t)
         if (!err[t].empty()) throw Error(MCAAT_E_HIP, "FASTQ packing: " + err[t]);
     for (int t = 0; t < P; ++t)
@@ -527,6 +547,7 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
         h2d(ctx, r->offsets.p, off.data(), 8 * off.size());
     }
     HIP_OK(hipStreamSynchronize(st));
+    verbose_mark(ctx, "fq.concat");
     regions.release();
     r->ctx = ctx;
     r->n_reads = n_reads;
