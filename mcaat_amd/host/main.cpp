@@ -224,7 +224,11 @@ static int run(Settings &settings, Ranks &ranks) {
         // and loads the kernels' code objects (HIP otherwise loads each file's at the first launch
         // of one of its kernels, inside the span); MCAAT_PRELOAD=0 leaves that to HIP
         const char *pl = getenv("MCAAT_PRELOAD");
-        if (n_dev > 0 && !(pl && pl[0] == '0')) (void)mcaat_preload(mcaat_rank_device(settings));
+        if (n_dev > 0 && !(pl && pl[0] == '0')) {
+            (void)mcaat_preload(mcaat_rank_device(settings));
+            // the rank's GPU context (its streams) is set up with the runtime as well
+            if (settings.gpus <= 1) (void)mcaat_host_ctx(mcaat_rank_device(settings));
+        }
     }
     if (settings.gpus > 1) {
         if (const char *e = getenv("MCAAT_TEST_RANK_EXIT"))  // test hook: this rank dies before joining
