@@ -19,6 +19,7 @@
 // are i * L when every read has length L, else uploaded; the mapping view of paired inputs
 // (files after the first reverse-complemented, reads.cpp:20-31) is built on the device from
 // the counting view.
+#include <chrono>
 #include <fcntl.h>
 #include <immintrin.h>
 #include <sys/mman.h>
@@ -411,7 +412,10 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
     const int T = pack_threads();
     hipStream_t st = ctx->stream;
 
-    // parts: per file, T byte ranges cut at record starts
+    // parts: per file, T x K byte ranges cut at record starts (MCAAT_PACK_SPLIT = K, default 1),
+    // taken by min(parts, T) worker threads from a shared counter
+    int K = 1;
+    if (const char *e = getenv("MCAAT_PACK_SPLIT")) K = std::max(1, std::min(16, atoi(e)));
     struct Part {
         int file;
         uint64_t b, e;
@@ -427,12 +431,13 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
         if (b >= e) continue;
         // a file must start with a record (leading blank lines: the GPU parser trims them)
         std::vector<uint64_t> cut{b};
-        for (int t = 1; t < T; ++t) {
-            const uint64_t c = fastq_record_start(files[f], b + (uint64_t)((unsigned __int128)(e - b) * t / T));
+        const int TK = T * K;
+        for (int t = 1; t < TK; ++t) {
+            const uint64_t c = fastq_record_start(files[f], b + (uint64_t)((unsigned __int128)(e - b) * t / TK));
             cut.push_back(std::max(cut.back(), std::min(c, e)));
         }
         cut.push_back(e);
-        for (int t = 0; t < T; ++t)
+        for (int t = 0; t < TK; ++t)
             if (cut[t + 1] > cut[t]) parts.push_back({f, cut[t], cut[t + 1], cut[t + 1] == S});
     }
     if (parts.empty()) return false;  // empty inputs: the GPU path's conventions
@@ -449,7 +454,8 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
     verbose_mark(ctx, "fq.parts");
     DevBuf<uint64_t> regions(rw);
     verbose_mark(ctx, "fq.regions");
-    const size_t stage_bytes = (size_t)P * 2 * kStageWords * 8;
+    const int NW = K > 1 ? std::min(P, T) : P;  // worker threads (K = 1: one per part, as before)
+    const size_t stage_bytes = (size_t)NW * 2 * kStageWords * 8;
     if (ctx->pack_pinned_bytes < stage_bytes) {
         if (ctx->pack_pinned) HIP_OK(hipHostFree(ctx->pack_pinned));
         ctx->pack_pinned = nullptr;
@@ -483,27 +489,38 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
     Shared sh;
     std::vector<int> ok(P, 0);
     std::vector<std::string> err(P);
-    auto job = [&](int t) {
-        try {
-            // the HIP current device is per thread: a worker's events must belong to the
-            // context's device, as its stream does
-            HIP_OK(hipSetDevice(ctx->device));
-            uint64_t *s0 = (uint64_t *)ctx->pack_pinned + (size_t)t * 2 * kStageWords;
-            PartPacker pk(regions.p + outs[t].region, s0, s0 + kStageWords, streams[t % streams.size()], outs[t]);
-            const bool good = pack_part(files[parts[t].file], parts[t].b, parts[t].e, parts[t].file_end, pk, sh, outs[t]);
-            if (good) pk.finish();
-            ok[t] = good;
-            if (!good) sh.decline.store(true);
-        } catch (const std::exception &x) {
-            err[t] = x.what();
-            sh.decline.store(true);
+    std::atomic<int> next{0};
+    std::vector<double> busy(NW, 0.0);
+    auto job = [&](int wk) {
+        const auto t0 = std::chrono::steady_clock::now();
+        // the HIP current device is per thread: a worker's events must belong to the
+        // context's device, as its stream does
+        (void)hipSetDevice(ctx->device);
+        uint64_t *s0 = (uint64_t *)ctx->pack_pinned + (size_t)wk * 2 * kStageWords;
+        for (int t = next.fetch_add(1); t < P; t = next.fetch_add(1)) {
+            try {
+                PartPacker pk(regions.p + outs[t].region, s0, s0 + kStageWords, streams[wk % streams.size()], outs[t]);
+                const bool good = pack_part(files[parts[t].file], parts[t].b, parts[t].e, parts[t].file_end, pk, sh, outs[t]);
+                if (good) pk.finish();
+                ok[t] = good;
+                if (!good) sh.decline.store(true);
+            } catch (const std::exception &x) {
+                err[t] = x.what();
+                sh.decline.store(true);
+            }
         }
+        busy[wk] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     };
     {
         std::vector<std::thread> pool;
-        for (int t = 1; t < P; ++t) pool.emplace_back(job, t);
+        for (int w = 1; w < NW; ++w) pool.emplace_back(job, w);
         job(0);
         for (auto &th : pool) th.join();
+    }
+    static const bool verbose = getenv("MCAAT_VERBOSE") && getenv("MCAAT_VERBOSE")[0] == '1';
+    if (verbose) {
+        const auto mm = std::minmax_element(busy.begin(), busy.end());
+        fprintf(stderr, "[mcaat] fq: %d parts, %d workers, busy %.3f .. %.3f s\n", P, NW, *mm.first, *mm.second);
     }
     verbose_mark(ctx, "fq.pack");
     for (int t = 0; t < P; ++t)
