@@ -412,9 +412,11 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
     const int T = pack_threads();
     hipStream_t st = ctx->stream;
 
-    // parts: per file, T x K byte ranges cut at record starts (MCAAT_PACK_SPLIT = K, default 1),
-    // taken by min(parts, T) worker threads from a shared counter
-    int K = 1;
+    // parts: per file, T x K byte ranges cut at record starts (MCAAT_PACK_SPLIT = K), taken by
+    // min(parts, T) worker threads from a shared counter. The threads read the page cache at
+    // different speeds (C3, one part each: busy 0.83-1.10 s), so parts of ~1/256 of the file
+    // let the fast ones take more: K = 1 / 8 / 16 -> pack 1.04-1.10 / 1.01-1.07 / 0.99-1.03 s
+    int K = 16;
     if (const char *e = getenv("MCAAT_PACK_SPLIT")) K = std::max(1, std::min(16, atoi(e)));
     struct Part {
         int file;
@@ -454,7 +456,7 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
     verbose_mark(ctx, "fq.parts");
     DevBuf<uint64_t> regions(rw);
     verbose_mark(ctx, "fq.regions");
-    const int NW = K > 1 ? std::min(P, T) : P;  // worker threads (K = 1: one per part, as before)
+    const int NW = K > 1 ? std::min(P, T) : P;  // worker threads (K = 1: one per part, as round 3)
     const size_t stage_bytes = (size_t)NW * 2 * kStageWords * 8;
     if (ctx->pack_pinned_bytes < stage_bytes) {
         if (ctx->pack_pinned) HIP_OK(hipHostFree(ctx->pack_pinned));
