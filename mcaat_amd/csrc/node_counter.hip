@@ -1844,6 +1844,9 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
                 break;
             }
             if (attempt > 0) throw Error(MCAAT_E_CAPACITY, "node_counter: output sizing failed");
+            if (getenv("MCAAT_VERBOSE") && getenv("MCAAT_VERBOSE")[0] == '1')
+                fprintf(stderr, "[mcaat] node_counter: group %zu overflowed the output (%llu > %llu): re-count\n", gi,
+                        (unsigned long long)total, (unsigned long long)out_cap);
             // grow (keeping the groups already counted) and count this group again
             const uint64_t ncap = total + (total - n_out) * (uint64_t)(256 - b1) / (uint64_t)(b1 - b0) + (1u << 20);
             DevBuf<uint64_t> k2(ncap);
@@ -1865,6 +1868,9 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
             const double frac = (double)hfine[p1] / (double)std::max<uint64_t>(n_live, 1);
             const uint64_t est = (uint64_t)((double)n_out / frac * 1.08) + (1u << 20);
             if (est > out_cap) {
+                if (getenv("MCAAT_VERBOSE") && getenv("MCAAT_VERBOSE")[0] == '1')
+                    fprintf(stderr, "[mcaat] node_counter: output grown after group %zu (%llu distinct, %.4f of the descriptors): %llu -> %llu\n",
+                            gi, (unsigned long long)n_out, frac, (unsigned long long)out_cap, (unsigned long long)est);
                 DevBuf<uint64_t> k2(est);
                 DevBuf<uint32_t> c2(est);
                 HIP_OK(hipMemcpyAsync(k2.p, out.keys.p, 8 * n_out, hipMemcpyDeviceToDevice, st));
