@@ -354,6 +354,14 @@ void mcaat_reset_timing(mcaat_ctx *ctx);
  *                      target key range staged (maximum 1024) */
 int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value);
 
+/* ---- allocator check ----------------------------------------------------------------------
+ * Replaces: nothing in the reference. The device arena's stream order (csrc/alloc.hip): a block
+ * is freed while a kernel queued on the context's main stream still writes it, then taken for
+ * a kernel on the side stream. out[0] = 1 when the side allocation got the same block, out[1] =
+ * 1 when every word holds the side kernel's value afterwards (the side kernel waited for the
+ * fence), out[2] = the arena's fence waits during the check. */
+int mcaat_arena_check(mcaat_ctx *ctx, int64_t *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -394,6 +394,9 @@ int mcaat_init(int device, mcaat_ctx **out) {
             delete ctx;
             throw Error(MCAAT_E_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(se));
         }
+        // frees fence these streams while they have work queued (stream-ordered arena, alloc.hip)
+        mcaat::watch_stream(device, ctx->stream);
+        mcaat::watch_stream(device, ctx->side);
         *out = ctx;
     });
 }
@@ -402,6 +405,9 @@ void mcaat_finalize(mcaat_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     mcaat::dev_trim();
+    mcaat::unwatch_stream(ctx->device, ctx->side);
+    mcaat::unwatch_stream(ctx->device, ctx->stream);
+    if (mcaat::alloc_stream() == ctx->stream) mcaat::set_alloc_stream(nullptr);
     for (auto *&p : ctx->pinned)
         if (p) (void)hipHostFree(p);
     for (hipEvent_t e : ctx->events) (void)hipEventDestroy(e);
@@ -416,7 +422,7 @@ int mcaat_reads_from_host(mcaat_ctx *ctx, const uint64_t *packed, uint64_t n_wor
                           uint64_t n_reads, mcaat_reads **out) {
     return guarded([&] {
         require(ctx && out && offsets && (packed || n_words == 0), "null argument");
-        HIP_OK(hipSetDevice(ctx->device));
+        mcaat::bind(ctx);
         auto *r = new mcaat_reads;
         try {
             upload_reads(ctx, packed, n_words, offsets, n_reads, r);
@@ -431,7 +437,7 @@ int mcaat_reads_from_host(mcaat_ctx *ctx, const uint64_t *packed, uint64_t n_wor
 int mcaat_reads_from_fastx(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_reads **out) {
     return guarded([&] {
         require(ctx && out && files && n_files > 0, "null argument");
-        HIP_OK(hipSetDevice(ctx->device));
+        mcaat::bind(ctx);
         // empty (or blank) files go with either format: they hold no records, and keep their
         // place in the file order (a second file's records are reverse-complemented)
         int n_fastq = 0, n_fasta = 0;
@@ -502,7 +508,7 @@ int mcaat_reads_info(const mcaat_reads *r, uint64_t *n_reads, uint64_t *n_bases)
 int mcaat_reads_download(const mcaat_reads *r, uint64_t *packed, uint64_t *offsets) {
     return guarded([&] {
         require(r != nullptr, "null argument");
-        HIP_OK(hipSetDevice(r->ctx->device));
+        mcaat::bind(r->ctx);
         if (packed) HIP_OK(hipMemcpy(packed, r->packed.p, 8 * r->n_words, hipMemcpyDeviceToHost));
         if (offsets) HIP_OK(hipMemcpy(offsets, r->offsets.p, 8 * (r->n_reads + 1), hipMemcpyDeviceToHost));
     });
@@ -511,7 +517,7 @@ int mcaat_reads_download(const mcaat_reads *r, uint64_t *packed, uint64_t *offse
 int mcaat_reads_write_fastq(const mcaat_reads *r, const char *path, int threads) {
     return guarded([&] {
         require(r && path, "null argument");
-        HIP_OK(hipSetDevice(r->ctx->device));
+        mcaat::bind(r->ctx);
         write_fastq(r, path, threads);
     });
 }
@@ -522,7 +528,7 @@ int mcaat_reads_synth(mcaat_ctx *ctx, const mcaat_synth_spec *spec, mcaat_reads 
     return guarded([&] {
         require(ctx && spec && out, "null argument");
         check_spec(*spec);
-        HIP_OK(hipSetDevice(ctx->device));
+        mcaat::bind(ctx);
         auto *r = new mcaat_reads;
         try {
             synth_reads(ctx, *spec, r, 0, spec->n_reads);
@@ -540,7 +546,7 @@ int mcaat_reads_synth_range(mcaat_ctx *ctx, const mcaat_synth_spec *spec, uint64
         require(ctx && spec && out, "null argument");
         check_spec(*spec);
         require(first <= spec->n_reads && count <= spec->n_reads - first, "read range outside the spec");
-        HIP_OK(hipSetDevice(ctx->device));
+        mcaat::bind(ctx);
         auto *r = new mcaat_reads;
         try {
             synth_reads(ctx, *spec, r, first, count);
@@ -613,7 +619,7 @@ int mcaat_count_edges(mcaat_ctx *ctx, const mcaat_reads *r, int k, uint64_t *n_d
     return guarded([&] {
         require(ctx && r && n_distinct && keys && counts, "null argument");
         require(k >= 2 && k <= kMaxK, "k must be in [2, 30]");
-        HIP_OK(hipSetDevice(ctx->device));
+        mcaat::bind(ctx);
         CountResult c;
         node_counter(ctx, r, k, c);
         sort_counts(ctx, c, k);
@@ -634,7 +640,7 @@ int mcaat_build_graph(mcaat_ctx *ctx, const mcaat_reads *r, int k, mcaat_graph *
     return guarded([&] {
         require(ctx && r && out, "null argument");
         require(k >= 2 && k <= kMaxK, "k must be in [2, 30]");
-        HIP_OK(hipSetDevice(ctx->device));
+        mcaat::bind(ctx);
         verbose_mark(ctx, "build.enter");
         auto *g = new mcaat_graph;
         g->ctx = ctx;
@@ -661,7 +667,7 @@ int mcaat_count_local(mcaat_ctx *ctx, const mcaat_reads *r, int k, mcaat_counts 
     return guarded([&] {
         require(ctx && r && out, "null argument");
         require(k >= 2 && k <= kMaxK, "k must be in [2, 30]");
-        HIP_OK(hipSetDevice(ctx->device));
+        mcaat::bind(ctx);
         auto *c = new mcaat_counts;
         c->ctx = ctx;
         c->k = k;
@@ -690,7 +696,7 @@ int mcaat_counts_histogram(const mcaat_counts *c, int bits, uint64_t *hist) {
     return guarded([&] {
         require(c && hist, "null argument");
         require(bits >= 1 && bits <= 13 && bits <= 2 * (c->k + 1), "histogram bits must be in [1, min(13, 2(k+1))]");
-        HIP_OK(hipSetDevice(c->ctx->device));
+        mcaat::bind(c->ctx);
         counts_histogram(c->ctx, c->c, c->k, bits, hist);
     });
 }
@@ -701,7 +707,7 @@ int mcaat_counts_partition(const mcaat_counts *c, int n_owners, const uint64_t *
         require(c && sizes && (n_owners == 1 || splits), "null argument");
         require(n_owners >= 1 && n_owners <= 64, "n_owners must be in [1, 64]");
         for (int i = 1; i + 1 < n_owners; ++i) require(splits[i - 1] <= splits[i], "splits must be ascending");
-        HIP_OK(hipSetDevice(c->ctx->device));
+        mcaat::bind(c->ctx);
         counts_partition(c->ctx, c->c, c->k, n_owners, splits, sizes, keys_dev, counts_dev, cap);
     });
 }
@@ -714,7 +720,7 @@ int mcaat_edges_reduce(mcaat_ctx *ctx, int k, const uint64_t *keys_dev, const ui
     return guarded([&] {
         require(ctx && n_out && (n == 0 || (keys_dev && counts_dev && keys_out_dev && mult_out_dev)), "null argument");
         require(k >= 2 && k <= kMaxK, "k must be in [2, 30]");
-        HIP_OK(hipSetDevice(ctx->device));
+        mcaat::bind(ctx);
         *n_out = edges_reduce(ctx, k, keys_dev, counts_dev, n, keys_out_dev, mult_out_dev);
     });
 }
@@ -724,7 +730,7 @@ int mcaat_graph_from_sorted(mcaat_ctx *ctx, int k, const uint64_t *keys_dev, con
     return guarded([&] {
         require(ctx && out && (D == 0 || (keys_dev && mult_dev)), "null argument");
         require(k >= 2 && k <= kMaxK, "k must be in [2, 30]");
-        HIP_OK(hipSetDevice(ctx->device));
+        mcaat::bind(ctx);
         verbose_mark(ctx, "build.enter");
         auto *g = new mcaat_graph;
         g->ctx = ctx;
@@ -753,7 +759,7 @@ int mcaat_graph_info(const mcaat_graph *g, int *k, uint64_t *n_edges) {
 int mcaat_graph_download(const mcaat_graph *g, uint64_t *keys, uint16_t *mult, uint8_t *valid) {
     return guarded([&] {
         require(g != nullptr, "null argument");
-        HIP_OK(hipSetDevice(g->ctx->device));
+        mcaat::bind(g->ctx);
         if (keys && g->D) HIP_OK(hipMemcpy(keys, g->key.p, 8 * g->D, hipMemcpyDeviceToHost));
         if (mult && g->D) HIP_OK(hipMemcpy(mult, g->mult.p, 2 * g->D, hipMemcpyDeviceToHost));
         if (valid) graph_download_valid(g, valid);
@@ -763,7 +769,7 @@ int mcaat_graph_download(const mcaat_graph *g, uint64_t *keys, uint16_t *mult, u
 int mcaat_graph_valid_words(const mcaat_graph *g, uint64_t *words) {
     return guarded([&] {
         require(g != nullptr && (words || g->D == 0), "null argument");
-        HIP_OK(hipSetDevice(g->ctx->device));
+        mcaat::bind(g->ctx);
         if (g->D) HIP_OK(hipMemcpy(words, g->valid.p, 8 * g->n_words(), hipMemcpyDeviceToHost));
     });
 }
@@ -774,7 +780,7 @@ int mcaat_graph_download_range(const mcaat_graph *g, uint64_t first, uint64_t co
         require(g != nullptr, "null argument");
         require(first <= g->D && count <= g->D - first, "edge range out of bounds");
         if (!count) return;
-        HIP_OK(hipSetDevice(g->ctx->device));
+        mcaat::bind(g->ctx);
         if (keys) HIP_OK(hipMemcpy(keys, g->key.p + first, 8 * count, hipMemcpyDeviceToHost));
         if (mult) HIP_OK(hipMemcpy(mult, g->mult.p + first, 2 * count, hipMemcpyDeviceToHost));
         if (valid) {
@@ -792,7 +798,7 @@ int mcaat_graph_download_range(const mcaat_graph *g, uint64_t first, uint64_t co
 int mcaat_graph_set_valid(mcaat_graph *g, const uint64_t *ids, size_t n, int valid) {
     return guarded([&] {
         require(g && (ids || n == 0), "null argument");
-        HIP_OK(hipSetDevice(g->ctx->device));
+        mcaat::bind(g->ctx);
         graph_set_valid(g, ids, n, valid);
     });
 }
@@ -802,7 +808,7 @@ int mcaat_graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, i
     return guarded([&] {
         require(g && (n == 0 || (ids && out && counts)), "null argument");
         for (size_t i = 0; i < n; ++i) require(ids[i] < g->D, "edge id out of range");
-        HIP_OK(hipSetDevice(g->ctx->device));
+        mcaat::bind(g->ctx);
         graph_neighbors(g, ids, n, incoming, out, counts);
     });
 }
@@ -811,7 +817,7 @@ int mcaat_graph_gather(const mcaat_graph *g, const uint64_t *ids, size_t n, uint
     return guarded([&] {
         require(g && (n == 0 || ids), "null argument");
         for (size_t i = 0; i < n; ++i) require(ids[i] < g->D, "edge id out of range");
-        HIP_OK(hipSetDevice(g->ctx->device));
+        mcaat::bind(g->ctx);
         graph_gather(g, ids, n, keys, mult);
     });
 }
@@ -819,7 +825,7 @@ int mcaat_graph_gather(const mcaat_graph *g, const uint64_t *ids, size_t n, uint
 int mcaat_graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n) {
     return guarded([&] {
         require(g && (ids || n == 0), "null argument");
-        HIP_OK(hipSetDevice(g->ctx->device));
+        mcaat::bind(g->ctx);
         graph_keep_only(g, ids, n);
     });
 }
@@ -827,7 +833,7 @@ int mcaat_graph_valid_subgraph(const mcaat_graph *g, uint64_t *n_valid, uint64_t
     return guarded([&] {
         require(g != nullptr && n_valid != nullptr, "null argument");
         require((ids == nullptr) == (nbr == nullptr) && (ids == nullptr) == (counts == nullptr), "all outputs or none");
-        HIP_OK(hipSetDevice(g->ctx->device));
+        mcaat::bind(g->ctx);
         *n_valid = graph_valid_out_ranks(g, ids, nbr, counts);
     });
 }
@@ -835,7 +841,7 @@ int mcaat_graph_valid_subgraph(const mcaat_graph *g, uint64_t *n_valid, uint64_t
 int mcaat_graph_keep_region(mcaat_graph *g, const uint64_t *seeds, size_t n, uint64_t hops) {
     return guarded([&] {
         require(g != nullptr && (n == 0 || seeds), "null argument");
-        HIP_OK(hipSetDevice(g->ctx->device));
+        mcaat::bind(g->ctx);
         graph_keep_region(g, seeds, n, hops);
     });
 }
@@ -843,7 +849,7 @@ int mcaat_graph_keep_region(mcaat_graph *g, const uint64_t *seeds, size_t n, uin
 int mcaat_graph_save(const mcaat_graph *g, const char *path) {
     return guarded([&] {
         require(g && path, "null argument");
-        HIP_OK(hipSetDevice(g->ctx->device));
+        mcaat::bind(g->ctx);
         graph_save(g, path);
     });
 }
@@ -851,7 +857,7 @@ int mcaat_graph_save(const mcaat_graph *g, const char *path) {
 int mcaat_graph_load(mcaat_ctx *ctx, const char *path, mcaat_graph **out) {
     return guarded([&] {
         require(ctx && path && out, "null argument");
-        HIP_OK(hipSetDevice(ctx->device));
+        mcaat::bind(ctx);
         auto *g = new mcaat_graph;
         try {
             graph_load(ctx, path, g);
@@ -883,7 +889,7 @@ int mcaat_map_reads(const mcaat_graph *g, const mcaat_reads *r, const uint64_t *
     return guarded([&] {
         require(g && r && out && (cycle_nodes || n_nodes == 0), "null argument");
         require(g->ctx == r->ctx, "graph and reads belong to different contexts");
-        HIP_OK(hipSetDevice(g->ctx->device));
+        mcaat::bind(g->ctx);
         auto *m = new mcaat_mapped;
         try {
             map_reads(g, r, cycle_nodes, n_nodes, max_batch_ids ? max_batch_ids : (uint64_t)1 << 28, m);
@@ -1027,7 +1033,8 @@ int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value) {
         "nc.overlap",      "sort.l3_counting",   "cf.peel_list_div", "cf.peel_list_cap", "cf.cand_cap",
         "fq.hostpack",     "sort.mid_counting", "nc.big_table", "cf.fused_init", "sort.mid_occ", "cf.scan_u", "cf.prep_batch", "cf.dls_lanes", "dist.oriented",
         "sort.small_mid", "sort.small_limit", "cf.recount", "cf.dls_host",
-        "dist.desc",      "cf.compact",         "cf.fresh",   "cf.dls_persist", "nc.split_first", "nc.split_max", "cf.pull_flags", "cf.dls_budget", "nc.grow_early"};
+        "dist.desc",      "cf.compact",         "cf.fresh",   "cf.dls_persist", "nc.split_first", "nc.split_max", "cf.pull_flags", "cf.dls_budget", "nc.grow_early",
+        "nc.free_sync"};
     return guarded([&] {
         require(ctx && name, "null argument");
         bool ok = false;
@@ -1050,7 +1057,7 @@ int mcaat_comm_init_rccl(mcaat_ctx *ctx, int world, int rank, const uint8_t *id,
     return guarded([&] {
         require(ctx && id && out, "null argument");
         require(world >= 1 && rank >= 0 && rank < world, "rank must be in [0, world)");
-        HIP_OK(hipSetDevice(ctx->device));
+        mcaat::bind(ctx);
         auto *c = new mcaat_comm;
         try {
             c->c = comm_rccl(ctx, world, rank, id);
@@ -1068,7 +1075,7 @@ int mcaat_comm_init_shm(mcaat_ctx *ctx, int world, int rank, const char *name, u
         require(name && out, "null argument");
         require(name[0] == '/' && !strchr(name + 1, '/'), "shared-memory name must be \"/name\"");
         require(world >= 1 && rank >= 0 && rank < world, "rank must be in [0, world)");
-        if (ctx) HIP_OK(hipSetDevice(ctx->device));
+        if (ctx) mcaat::bind(ctx);
         auto *c = new mcaat_comm;
         try {
             c->c = comm_shm(ctx, world, rank, name, slot_bytes ? slot_bytes : (256ULL << 20));
@@ -1124,7 +1131,7 @@ int mcaat_reads_from_fastx_part(mcaat_ctx *ctx, const char *const *files, int n_
     return guarded([&] {
         require(n_parts >= 1 && part >= 0 && part < n_parts, "part must be in [0, n_parts)");
         require(ctx && out && files && n_files > 0, "null argument");
-        HIP_OK(hipSetDevice(ctx->device));
+        mcaat::bind(ctx);
         std::vector<std::pair<uint64_t, uint64_t>> ranges;
         for (int i = 0; i < n_files; ++i) {
             const int c = sniff_format(files[i]);
@@ -1174,7 +1181,7 @@ int mcaat_build_graph_sharded(mcaat_ctx *ctx, mcaat_comm *comm, const mcaat_read
     return guarded([&] {
         require(ctx && comm && r && out, "null argument");
         require(k >= 2 && k <= kMaxK, "k must be in [2, 30]");
-        HIP_OK(hipSetDevice(ctx->device));
+        mcaat::bind(ctx);
         auto *g = new mcaat_graph;
         g->ctx = ctx;
         try {
@@ -1193,7 +1200,7 @@ int mcaat_cycle_finder_comm(mcaat_graph *g, mcaat_comm *comm, const mcaat_cf_par
         require(p->cycle_max_length >= 2 && p->cycle_max_length <= 250, "cycle_max_length must be in [2, 250]");
         require(p->cluster_bound >= 1 && p->cluster_bound <= 65535, "cluster_bound must be in [1, 65535]");
         require(p->step_cap >= 1, "step_cap must be positive");
-        HIP_OK(hipSetDevice(g->ctx->device));
+        mcaat::bind(g->ctx);
         auto *c = new mcaat_cycles;
         try {
             cycle_finder(g, *p, c, comm ? comm->c.get() : nullptr);
@@ -1207,3 +1214,11 @@ int mcaat_cycle_finder_comm(mcaat_graph *g, mcaat_comm *comm, const mcaat_cf_par
 }
 
 }  // extern "C"
+
+int mcaat_arena_check(mcaat_ctx *ctx, int64_t *out) {
+    return guarded([&] {
+        require(ctx && out, "null argument");
+        mcaat::bind(ctx);
+        mcaat::arena_check(ctx, out);
+    });
+}

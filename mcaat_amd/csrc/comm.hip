@@ -98,7 +98,7 @@ struct RcclComm final : Comm {
         rank = rank_;
         ncclUniqueId u;
         memcpy(u.internal, id, NCCL_UNIQUE_ID_BYTES);
-        HIP_OK(hipSetDevice(ctx->device));
+        mcaat::bind(ctx);
         NCCL_OK(rccl().CommInitRank(&comm, world, u, rank));
     }
     ~RcclComm() override {
@@ -356,7 +356,7 @@ struct ShmComm final : Comm {
 
     void need_ctx() const {
         if (!ctx) throw Error(MCAAT_E_INVALID, "shared-memory comm without a context moves host memory only");
-        HIP_OK(hipSetDevice(ctx->device));
+        mcaat::bind(ctx);
         HIP_OK(hipStreamSynchronize(ctx->stream));
     }
 

@@ -320,6 +320,8 @@ bool pack_part(const char *path, uint64_t b, uint64_t e, bool file_end, PartPack
 }
 
 // ---------------------------------------------------------------- device kernels
+// part tables of k_concat_parts held in LDS up to this many parts ((2P + 1) x 8 B = 32 KB)
+constexpr int kConcatLdsParts = 2047;
 // out word W = bases [32W, 32W + 32) of the concatenation of the parts (part t: n_t bases at
 // base offset start[t], stored from word region[t] of src)
 __global__ void k_concat_parts(const uint64_t *src, const uint64_t *region_g, const uint64_t *start_g, int T,
@@ -327,11 +329,17 @@ __global__ void k_concat_parts(const uint64_t *src, const uint64_t *region_g, co
     // (round 4) the parts' starts and regions in LDS, and each thread's part carried from its
     // previous word (its words ascend): 16.7 -> 6.3 ms at C3 (11.5 GB), from a scan of the
     // global start table per word
+    // Above kConcatLdsParts parts (many files x many threads) the tables stay in global memory:
+    // the launch then asks for no dynamic LDS (64 KB per workgroup is the limit)
     extern __shared__ uint64_t sh_parts[];
-    uint64_t *start = sh_parts, *region = sh_parts + T + 1;
-    for (int i = threadIdx.x; i <= T; i += blockDim.x) start[i] = start_g[i];
-    for (int i = threadIdx.x; i < T; i += blockDim.x) region[i] = region_g[i];
-    __syncthreads();
+    const uint64_t *start = start_g, *region = region_g;
+    if (T <= kConcatLdsParts) {
+        for (int i = threadIdx.x; i <= T; i += blockDim.x) sh_parts[i] = start_g[i];
+        for (int i = threadIdx.x; i < T; i += blockDim.x) sh_parts[T + 1 + i] = region_g[i];
+        __syncthreads();
+        start = sh_parts;
+        region = sh_parts + T + 1;
+    }
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     int t = 0;
     for (uint64_t W = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; W < n_words; W += stride) {
@@ -418,6 +426,8 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
     // let the fast ones take more: K = 1 / 8 / 16 -> pack 1.04-1.10 / 1.01-1.07 / 0.99-1.03 s
     int K = 16;
     if (const char *e = getenv("MCAAT_PACK_SPLIT")) K = std::max(1, std::min(16, atoi(e)));
+    // keep the part tables of the concatenation in LDS where the file and thread counts allow
+    K = std::max(1, std::min(K, kConcatLdsParts / std::max(1, n_files * T)));
     struct Part {
         int file;
         uint64_t b, e;
@@ -555,7 +565,7 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
     if (n_words) {
         KernelTimer kt(ctx, "fq_concat", 16.0 * (double)n_words);
         hipLaunchKernelGGL(k_concat_parts, dim3(grid_for(n_words, kPB, (unsigned)ctx->n_cu * 8)), dim3(kPB),
-                           (size_t)(2 * P + 1) * 8, st, regions.p, dregion.p, dstart.p, P, n_words, n_bases, r->packed.p);
+                           P <= kConcatLdsParts ? (size_t)(2 * P + 1) * 8 : (size_t)0, st, regions.p, dregion.p, dstart.p, P, n_words, n_bases, r->packed.p);
         LAUNCH_OK();
         kt.stop();
     }

@@ -47,6 +47,22 @@ void *dev_alloc(size_t bytes);
 void dev_free(void *p, size_t bytes, int device);
 int current_device();
 void dev_trim();
+// stream-ordered reuse (alloc.hip): frees fence the watched streams that still have work queued,
+// and an allocation waits (on its stream) for the fences of the other streams
+void watch_stream(int device, hipStream_t s);
+void unwatch_stream(int device, hipStream_t s);
+hipStream_t alloc_stream();  // this thread's allocation stream (null: the host waits)
+void set_alloc_stream(hipStream_t s);
+void arena_stats(uint64_t *fences, uint64_t *waits);
+void arena_check(::mcaat_ctx *ctx, int64_t *out);  // mcaat_arena_check
+// allocations inside the scope are for work queued on stream s
+struct AllocStreamScope {
+    hipStream_t prev;
+    explicit AllocStreamScope(hipStream_t s) : prev(alloc_stream()) { set_alloc_stream(s); }
+    ~AllocStreamScope() { set_alloc_stream(prev); }
+    AllocStreamScope(const AllocStreamScope &) = delete;
+    AllocStreamScope &operator=(const AllocStreamScope &) = delete;
+};
 void preload_node_counter();
 void preload_sdbg_build();
 void preload_cycle_finder();
@@ -154,6 +170,14 @@ struct mcaat_ctx {
     uint8_t *pack_pinned = nullptr;
     size_t pack_pinned_bytes = 0;
 };
+
+namespace mcaat {
+// a C-ABI entry's context: its device, and its main stream as this thread's allocation stream
+inline void bind(mcaat_ctx *ctx) {
+    HIP_OK(hipSetDevice(ctx->device));
+    set_alloc_stream(ctx->stream);
+}
+}  // namespace mcaat
 
 struct mcaat_reads {
     mcaat_ctx *ctx = nullptr;

@@ -1708,6 +1708,7 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
     // side stream while group g's pass C counts on the main stream (two groups' fine
     // partitions alive at once, so groups are half the size)
     const bool overlap = knob(ctx, "nc.overlap", 1) != 0;
+    const bool free_sync = knob(ctx, "nc.free_sync", 0) != 0;
     struct Group {
         int b0, b1;
         DevBuf<uint4> fine;
@@ -1737,7 +1738,10 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
         const uint64_t p0 = (uint64_t)g.b0 * S, p1 = (uint64_t)g.b1 * S;
         const uint64_t gbase = hfine[p0], gn = hfine[p1] - gbase;
         const uint64_t c0 = bchunk[g.b0], c1 = bchunk[g.b1];
-        g.fine.alloc(gn ? gn : 1);
+        {
+            AllocStreamScope scope(sb);  // written by pass B on the side stream
+            g.fine.alloc(gn ? gn : 1);
+        }
         auto *kt = new KernelTimer(ctx, "l2_partition", 34.0 * (double)gn, sb);  // sub rows + descriptors read, descriptors written
         if (c1 > c0) {
             hipLaunchKernelGGL(k_l2_scatter, dim3((unsigned)(c1 - c0)), dim3(kBThreads), 0, sb, l1.p, l1s.p,
@@ -1856,9 +1860,12 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
             out.keys = std::move(k2);
             out.counts = std::move(c2);
             out_cap = ncap;
-            const unsigned long long keep = n_out;
-            HIP_OK(hipMemcpyAsync(dcnt.p, &keep, 8, hipMemcpyHostToDevice, st));
-            HIP_OK(hipStreamSynchronize(st));  // keep is a host local; the old buffers are already free
+            // the counter restarts at n_out (two 32-bit device writes: no host buffer to keep alive)
+            HIP_OK(hipMemsetD32Async((hipDeviceptr_t)dcnt.p, (int)(uint32_t)n_out, 1, st));
+            HIP_OK(hipMemsetD32Async((hipDeviceptr_t)((uint32_t *)dcnt.p + 1), (int)(uint32_t)(n_out >> 32), 1, st));
+            // (round 4 placed a synchronise here before the old buffers went back to the arena;
+            // the arena's fences order their reuse now, nc.free_sync=1 restores it for A/B)
+            if (free_sync) HIP_OK(hipStreamSynchronize(st));
         }
         // (round 4) the output is sized from n_occ / 32 (C3: 0.53 G distinct of 1.15 G); an
         // error-rich input (C5: ~2 G) used to overflow it mid-run, re-count a whole group and copy
@@ -1878,9 +1885,9 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
                 DevBuf<uint32_t> c2(est);
                 HIP_OK(hipMemcpyAsync(k2.p, out.keys.p, 8 * n_out, hipMemcpyDeviceToDevice, st));
                 HIP_OK(hipMemcpyAsync(c2.p, out.counts.p, 4 * n_out, hipMemcpyDeviceToDevice, st));
-                // the arena reuses freed memory at once, and the next group's pass B (side stream)
-                // may be handed the old buffers: the copies land before they are freed
-                HIP_OK(hipStreamSynchronize(st));
+                // the next group's pass B (side stream) may be handed the old buffers: the arena
+                // makes it wait for these copies (round 4 synchronised here: nc.free_sync=1)
+                if (free_sync) HIP_OK(hipStreamSynchronize(st));
                 out.keys = std::move(k2);
                 out.counts = std::move(c2);
                 out_cap = est;

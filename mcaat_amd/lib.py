@@ -134,6 +134,7 @@ SIGNATURES = {
     "mcaat_reads_file_records": (C.c_int, [C.c_void_p, C.c_int, _u64p]),
     "mcaat_build_graph_sharded": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
     "mcaat_cycle_finder_comm": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(_CfParams), C.POINTER(C.c_void_p)]),
+    "mcaat_arena_check": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64)]),
 }
 
 _lib: Optional[C.CDLL] = None
@@ -272,6 +273,13 @@ class Context:
     def trim(self) -> None:
         """Release device memory the arena keeps but nothing uses (mcaat_trim)."""
         self._lib.mcaat_trim(self.h)
+
+    def arena_check(self) -> Tuple[bool, bool, int]:
+        """The device arena's stream order (mcaat_arena_check): (same block reused, the side
+        stream's writes survived the main stream's queued ones, fence waits)."""
+        out = (C.c_int64 * 3)()
+        _check(self._lib.mcaat_arena_check(self.h, out))
+        return bool(out[0]), bool(out[1]), int(out[2])
 
     def set_knob(self, name: str, value: int) -> None:
         """Size limit that picks a code path (include/mcaat_gpu.h, mcaat_set_knob); value < 0

@@ -290,6 +290,21 @@ def test_host_pack_paired_end(gpu_ctx, tmp_path, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_host_pack_many_files_many_threads(gpu_ctx, tmp_path, monkeypatch):
+    """ 40 files x 64 threads: the per-thread split is clamped to 1 and the
+    2560 parts exceed the concatenation's LDS table (2047 parts), so its part tables are read
+    from global memory instead of failing the launch; same library as the restatement."""
+    monkeypatch.setenv("MCAAT_PACK_THREADS", "64")
+    rng = np.random.default_rng(17)
+    texts = [_fastq_text(_acgt_records(rng, 100, [150, 90])) for _ in range(40)]
+    files = [_write(tmp_path / f"f{i}.fq", t) for i, t in enumerate(texts)]
+    gpu_ctx.reset_timing()
+    reads = _check(gpu_ctx, files, texts, monkeypatch, 0)
+    assert _packed_by_host(gpu_ctx)
+    reads.free()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("bad", ["N", "lower", "crlf", "empty", "blank_end"])
 def test_host_pack_declines_to_the_text_parser(gpu_ctx, tmp_path, monkeypatch, bad):
     """Inputs outside the fast path's form go to the GPU text parser, with its results."""

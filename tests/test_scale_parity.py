@@ -39,8 +39,10 @@ KNOBS = {
     # one L1 bucket per pass-B/C group, the count output regrown (and the group recounted)
     "multi_group": {"nc.group_budget": 1, "nc.out_cap": 1},
     # (round 4) the output grown once after the first group, while the next group's pass B runs
-    # on the side stream (the old buffers must not be reused before their copy lands)
+    # on the side stream (the old buffers must not be reused before their copy lands). Round 5:
+    # no synchronise at the site (the stream-ordered arena orders the reuse); free_sync restores it
     "grow_early": {"nc.group_budget": 1, "nc.out_cap": 64, "nc.grow_early": 1},
+    "grow_early_free_sync": {"nc.group_budget": 1, "nc.out_cap": 64, "nc.grow_early": 1, "nc.free_sync": 1},
     # L1 buckets undersized on the first pass-A attempt: resize and re-run
     "l1_resize": {"nc.l1_slots": 64, "nc.fine_bits": 12},
     # every partition overflows the LDS edge table: class split, then the class-filtered global

@@ -1,0 +1,26 @@
+# Parameterised GPU job (replaces round 4's one-off tools/r4_*.sh wrappers).
+#   bash tools/gpu_check.sh tests "<pytest -k expr>"   selected GPU tests
+#   bash tools/gpu_check.sh suite                       the whole GPU suite + smoke
+#   bash tools/gpu_check.sh abq [c3|c2|c5] [steps]      quick timing (tools/abq.sh)
+#   bash tools/gpu_check.sh bench                       the driver's default bench line
+# Every GPU step has its own time limit; the first failure ends the job.
+set -e
+mkdir -p gpurun_out
+what=$1; shift || true
+case "$what" in
+  tests)
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "$1" \
+      > gpurun_out/gpu_tests.log 2>&1 || { tail -40 gpurun_out/gpu_tests.log; exit 1; }
+    tail -3 gpurun_out/gpu_tests.log ;;
+  suite)
+    timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+      > gpurun_out/gpu_suite.log 2>&1 || { tail -40 gpurun_out/gpu_suite.log; exit 1; }
+    tail -1 gpurun_out/gpu_suite.log
+    timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && tail -1 gpurun_out/smoke.log ;;
+  abq)
+    CFG=${1:-c3} STEPS=${2:-3} bash tools/abq.sh default ;;
+  bench)
+    timeout -k 10 900 python -u bench.py > gpurun_out/bench.log 2>&1 || { tail -30 gpurun_out/bench.log; exit 1; }
+    tail -1 gpurun_out/bench.log ;;
+  *) echo "unknown job $what"; exit 2 ;;
+esac
