@@ -281,6 +281,17 @@ int mcaat_build_graph_sharded(mcaat_ctx *ctx, mcaat_comm *comm, const mcaat_read
  * round-robin with one ordered commit; every rank gets the results mcaat_cycle_finder gives
  * (comm NULL: mcaat_cycle_finder). Replaces cycle_finder.cpp:394-419, 468-487. */
 int mcaat_cycle_finder_comm(mcaat_graph *g, mcaat_comm *comm, const mcaat_cf_params *p, mcaat_cycles **out);
+/* (round 5) Per-shard graphs. By default (knob dist.shard_cf = 1) mcaat_build_graph_sharded
+ * leaves each rank its BOSS-key range of the edges (ids [first, first + n_local)) with its
+ * adjacency built by one request/response exchange, and mcaat_cycle_finder_comm on such a graph
+ * runs CycleFinder per shard (filter, tips, degrees and the RecursiveReduction fixpoint over
+ * the ranks' ranges with message exchanges; DepthLevelSearch and FindCycle on gathered
+ * search-region replicas): the same results as mcaat_cycle_finder. Entry points that read the
+ * whole graph (download, neighbours, regions, read mapping, save) refuse a sharded graph until
+ * mcaat_graph_unshard (collective) gathers it on every rank, valid bits included.
+ * Replaces cycle_finder.cpp:346-492 over a graph split by ranges. */
+int mcaat_graph_shard_info(const mcaat_graph *g, int *sharded, uint64_t *first, uint64_t *n_local);
+int mcaat_graph_unshard(mcaat_graph *g, mcaat_comm *comm);
 
 /* ---- measurement -------------------------------------------------------------
  * Per-stage device time of the last build/cycle_finder call on this ctx, measured
@@ -353,6 +364,12 @@ void mcaat_reset_timing(mcaat_ctx *ctx);
  *                      a larger run clears its slots and writes them directly); mode 2: largest
  *                      target key range staged (maximum 1024) */
 int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value);
+
+/*   dist.shard_cf     0: the sharded build all-gathers the whole graph on every rank and
+ *                      CycleFinder runs over the ranks on replicas (round 4; default 1: per shard)
+ *   dist.ruler_mask   per-shard peel: 1 in (mask + 1) unary edges is a ruler besides the chain
+ *                      heads (default 15)
+ *   dist.adj_chunk    sharded adjacency: edges per request/response exchange (default 2^27) */
 
 /* ---- allocator check ----------------------------------------------------------------------
  * Replaces: nothing in the reference. The device arena's stream order (csrc/alloc.hip): a block

@@ -748,6 +748,31 @@ int mcaat_graph_from_sorted(mcaat_ctx *ctx, int k, const uint64_t *keys_dev, con
     });
 }
 
+// entry points that read the whole graph: a sharded graph (each rank its range) is gathered first
+static void require_whole(const mcaat_graph *g) {
+    if (g->sharded)
+        throw Error(MCAAT_E_INVALID, "the graph is sharded over the ranks: call mcaat_graph_unshard first");
+}
+
+int mcaat_graph_shard_info(const mcaat_graph *g, int *sharded, uint64_t *first, uint64_t *n_local) {
+    return guarded([&] {
+        require(g != nullptr, "null argument");
+        if (sharded) *sharded = g->sharded ? 1 : 0;
+        if (first) *first = g->sharded ? g->id_lo : 0;
+        if (n_local) *n_local = g->sharded ? g->D_local : g->D;
+    });
+}
+
+int mcaat_graph_unshard(mcaat_graph *g, mcaat_comm *comm) {
+    return guarded([&] {
+        require(g != nullptr, "null argument");
+        if (!g->sharded) return;
+        require(comm != nullptr, "a sharded graph is gathered over its communicator");
+        mcaat::bind(g->ctx);
+        graph_unshard(g, *comm->c);
+    });
+}
+
 int mcaat_graph_info(const mcaat_graph *g, int *k, uint64_t *n_edges) {
     return guarded([&] {
         require(g != nullptr, "null argument");
@@ -759,6 +784,7 @@ int mcaat_graph_info(const mcaat_graph *g, int *k, uint64_t *n_edges) {
 int mcaat_graph_download(const mcaat_graph *g, uint64_t *keys, uint16_t *mult, uint8_t *valid) {
     return guarded([&] {
         require(g != nullptr, "null argument");
+        require_whole(g);
         mcaat::bind(g->ctx);
         if (keys && g->D) HIP_OK(hipMemcpy(keys, g->key.p, 8 * g->D, hipMemcpyDeviceToHost));
         if (mult && g->D) HIP_OK(hipMemcpy(mult, g->mult.p, 2 * g->D, hipMemcpyDeviceToHost));
@@ -769,6 +795,7 @@ int mcaat_graph_download(const mcaat_graph *g, uint64_t *keys, uint16_t *mult, u
 int mcaat_graph_valid_words(const mcaat_graph *g, uint64_t *words) {
     return guarded([&] {
         require(g != nullptr && (words || g->D == 0), "null argument");
+        require_whole(g);
         mcaat::bind(g->ctx);
         if (g->D) HIP_OK(hipMemcpy(words, g->valid.p, 8 * g->n_words(), hipMemcpyDeviceToHost));
     });
@@ -780,6 +807,7 @@ int mcaat_graph_download_range(const mcaat_graph *g, uint64_t first, uint64_t co
         require(g != nullptr, "null argument");
         require(first <= g->D && count <= g->D - first, "edge range out of bounds");
         if (!count) return;
+        require_whole(g);
         mcaat::bind(g->ctx);
         if (keys) HIP_OK(hipMemcpy(keys, g->key.p + first, 8 * count, hipMemcpyDeviceToHost));
         if (mult) HIP_OK(hipMemcpy(mult, g->mult.p + first, 2 * count, hipMemcpyDeviceToHost));
@@ -798,6 +826,7 @@ int mcaat_graph_download_range(const mcaat_graph *g, uint64_t first, uint64_t co
 int mcaat_graph_set_valid(mcaat_graph *g, const uint64_t *ids, size_t n, int valid) {
     return guarded([&] {
         require(g && (ids || n == 0), "null argument");
+        require_whole(g);
         mcaat::bind(g->ctx);
         graph_set_valid(g, ids, n, valid);
     });
@@ -808,6 +837,7 @@ int mcaat_graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, i
     return guarded([&] {
         require(g && (n == 0 || (ids && out && counts)), "null argument");
         for (size_t i = 0; i < n; ++i) require(ids[i] < g->D, "edge id out of range");
+        require_whole(g);
         mcaat::bind(g->ctx);
         graph_neighbors(g, ids, n, incoming, out, counts);
     });
@@ -817,6 +847,7 @@ int mcaat_graph_gather(const mcaat_graph *g, const uint64_t *ids, size_t n, uint
     return guarded([&] {
         require(g && (n == 0 || ids), "null argument");
         for (size_t i = 0; i < n; ++i) require(ids[i] < g->D, "edge id out of range");
+        require_whole(g);
         mcaat::bind(g->ctx);
         graph_gather(g, ids, n, keys, mult);
     });
@@ -825,6 +856,7 @@ int mcaat_graph_gather(const mcaat_graph *g, const uint64_t *ids, size_t n, uint
 int mcaat_graph_keep_only(mcaat_graph *g, const uint64_t *ids, size_t n) {
     return guarded([&] {
         require(g && (ids || n == 0), "null argument");
+        require_whole(g);
         mcaat::bind(g->ctx);
         graph_keep_only(g, ids, n);
     });
@@ -833,6 +865,7 @@ int mcaat_graph_valid_subgraph(const mcaat_graph *g, uint64_t *n_valid, uint64_t
     return guarded([&] {
         require(g != nullptr && n_valid != nullptr, "null argument");
         require((ids == nullptr) == (nbr == nullptr) && (ids == nullptr) == (counts == nullptr), "all outputs or none");
+        require_whole(g);
         mcaat::bind(g->ctx);
         *n_valid = graph_valid_out_ranks(g, ids, nbr, counts);
     });
@@ -841,6 +874,7 @@ int mcaat_graph_valid_subgraph(const mcaat_graph *g, uint64_t *n_valid, uint64_t
 int mcaat_graph_keep_region(mcaat_graph *g, const uint64_t *seeds, size_t n, uint64_t hops) {
     return guarded([&] {
         require(g != nullptr && (n == 0 || seeds), "null argument");
+        require_whole(g);
         mcaat::bind(g->ctx);
         graph_keep_region(g, seeds, n, hops);
     });
@@ -849,6 +883,7 @@ int mcaat_graph_keep_region(mcaat_graph *g, const uint64_t *seeds, size_t n, uin
 int mcaat_graph_save(const mcaat_graph *g, const char *path) {
     return guarded([&] {
         require(g && path, "null argument");
+        require_whole(g);
         mcaat::bind(g->ctx);
         graph_save(g, path);
     });
@@ -889,6 +924,7 @@ int mcaat_map_reads(const mcaat_graph *g, const mcaat_reads *r, const uint64_t *
     return guarded([&] {
         require(g && r && out && (cycle_nodes || n_nodes == 0), "null argument");
         require(g->ctx == r->ctx, "graph and reads belong to different contexts");
+        require_whole(g);
         mcaat::bind(g->ctx);
         auto *m = new mcaat_mapped;
         try {
@@ -1034,7 +1070,7 @@ int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value) {
         "fq.hostpack",     "sort.mid_counting", "nc.big_table", "cf.fused_init", "sort.mid_occ", "cf.scan_u", "cf.prep_batch", "cf.dls_lanes", "dist.oriented",
         "sort.small_mid", "sort.small_limit", "cf.recount", "cf.dls_host",
         "dist.desc",      "cf.compact",         "cf.fresh",   "cf.dls_persist", "nc.split_first", "nc.split_max", "cf.pull_flags", "cf.dls_budget", "nc.grow_early",
-        "nc.free_sync"};
+        "nc.free_sync", "dist.shard_cf", "dist.ruler_mask", "dist.adj_chunk"};
     return guarded([&] {
         require(ctx && name, "null argument");
         bool ok = false;
@@ -1201,9 +1237,11 @@ int mcaat_cycle_finder_comm(mcaat_graph *g, mcaat_comm *comm, const mcaat_cf_par
         require(p->cluster_bound >= 1 && p->cluster_bound <= 65535, "cluster_bound must be in [1, 65535]");
         require(p->step_cap >= 1, "step_cap must be positive");
         mcaat::bind(g->ctx);
+        require(!g->sharded || comm, "a sharded graph runs CycleFinder over its communicator");
         auto *c = new mcaat_cycles;
         try {
-            cycle_finder(g, *p, c, comm ? comm->c.get() : nullptr);
+            if (g->sharded) cycle_finder_sharded(g, *p, c, *comm->c);
+            else cycle_finder(g, *p, c, comm ? comm->c.get() : nullptr);
             verbose_mark(g->ctx, "cf.return");
         } catch (...) {
             delete c;

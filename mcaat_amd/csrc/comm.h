@@ -25,6 +25,16 @@ struct Comm {
                                const uint64_t *recv_bytes) = 0;
     // rank r's sizes[r] bytes at `send`, concatenated in rank order into recv (sizes known to all)
     virtual void allgatherv_dev(const void *send, void *recv, const uint64_t *sizes) = 0;
+    // all-to-all of device segments: to each rank d this rank sends the segments send[d] in order;
+    // from each rank s it receives the segments of byte sizes recv[s] (what s sends here), placed
+    // back to back, sources in rank order, from `out`. No staging copy on the sending side
+    // (round 5: pass A's L1 buckets go out from where pass A wrote them).
+    struct Seg {
+        const void *p;
+        uint64_t bytes;
+    };
+    virtual void alltoallv_dev_segs(const std::vector<std::vector<Seg>> &send, void *out,
+                                    const std::vector<std::vector<uint64_t>> &recv) = 0;
 
     // typed helpers over allgatherv_host
     template <class T>

@@ -165,6 +165,59 @@ struct RcclComm final : Comm {
         sync();
     }
 
+    // Segments in rounds: round j holds, for every peer, the j-th send segment and the j-th
+    // receive segment (pieces of 1 GiB), so the k-th operation between two ranks sits in the
+    // same round on both sides (ncclGroupEnd of one round completes before the next starts on
+    // the stream; a round-agnostic split could wait on a peer's later round).
+    void alltoallv_dev_segs(const std::vector<std::vector<Seg>> &send, void *out,
+                            const std::vector<std::vector<uint64_t>> &recv) override {
+        struct Op {
+            const uint8_t *s;
+            uint8_t *d;
+            uint64_t n;
+        };
+        std::vector<std::vector<Op>> sends(world), recvs(world);
+        uint8_t *d = (uint8_t *)out;
+        for (int q = 0; q < world; ++q) {
+            for (const uint64_t n : recv[q]) {
+                if (q != rank)
+                    for (uint64_t c0 = 0; c0 < n; c0 += kPiece) recvs[q].push_back({nullptr, d + c0, std::min(kPiece, n - c0)});
+                d += n;
+            }
+        }
+        // own segments: copies on the stream, in place
+        {
+            uint8_t *o = (uint8_t *)out;
+            for (int q = 0; q < rank; ++q)
+                for (const uint64_t n : recv[q]) o += n;
+            if (send[rank].size() != recv[rank].size()) throw Error(MCAAT_E_INVALID, "alltoallv_segs: self segments differ");
+            for (size_t i = 0; i < send[rank].size(); ++i) {
+                if (send[rank][i].bytes != recv[rank][i]) throw Error(MCAAT_E_INVALID, "alltoallv_segs: self sizes differ");
+                if (send[rank][i].bytes)
+                    HIP_OK(hipMemcpyAsync(o, send[rank][i].p, send[rank][i].bytes, hipMemcpyDeviceToDevice, ctx->stream));
+                o += send[rank][i].bytes;
+            }
+        }
+        size_t rounds = 0;
+        for (int q = 0; q < world; ++q) {
+            if (q == rank) continue;
+            for (const Seg &g : send[q])
+                for (uint64_t c0 = 0; c0 < g.bytes; c0 += kPiece)
+                    sends[q].push_back({(const uint8_t *)g.p + c0, nullptr, std::min(kPiece, g.bytes - c0)});
+            rounds = std::max({rounds, sends[q].size(), recvs[q].size()});
+        }
+        for (size_t j = 0; j < rounds; ++j) {
+            NCCL_OK(rccl().GroupStart());
+            for (int q = 0; q < world; ++q) {
+                if (q == rank) continue;
+                if (j < sends[q].size()) NCCL_OK(rccl().Send(sends[q][j].s, sends[q][j].n, ncclUint8, q, comm, ctx->stream));
+                if (j < recvs[q].size()) NCCL_OK(rccl().Recv(recvs[q][j].d, recvs[q][j].n, ncclUint8, q, comm, ctx->stream));
+            }
+            NCCL_OK(rccl().GroupEnd());
+        }
+        sync();
+    }
+
     // exact-size all-gather: one broadcast per root into its place in the output, grouped
     void allgatherv_dev(const void *send, void *recv, const uint64_t *sizes) override {
         const auto off = offsets_of(sizes, world);
@@ -389,6 +442,29 @@ struct ShmComm final : Comm {
     void allgatherv_dev(const void *send, void *recv, const uint64_t *sizes) override {
         need_ctx();
         gather_through_slots(send, recv, sizes, true);
+    }
+
+    // the rehearsal transport stages device data through the host anyway: each peer's segments
+    // are packed into one device buffer and sent by the plain all-to-all
+    void alltoallv_dev_segs(const std::vector<std::vector<Seg>> &send, void *out,
+                            const std::vector<std::vector<uint64_t>> &recv) override {
+        need_ctx();
+        std::vector<uint64_t> sb(world, 0), rb(world, 0);
+        for (int q = 0; q < world; ++q) {
+            for (const Seg &g : send[q]) sb[q] += g.bytes;
+            for (const uint64_t n : recv[q]) rb[q] += n;
+        }
+        uint64_t tot = 0;
+        for (uint64_t x : sb) tot += x;
+        DevBuf<uint8_t> st(tot ? tot : 1);
+        uint64_t o = 0;
+        for (int q = 0; q < world; ++q)
+            for (const Seg &g : send[q]) {
+                if (g.bytes) HIP_OK(hipMemcpyAsync(st.p + o, g.p, g.bytes, hipMemcpyDeviceToDevice, ctx->stream));
+                o += g.bytes;
+            }
+        HIP_OK(hipStreamSynchronize(ctx->stream));
+        alltoallv_dev(st.p, sb.data(), out, rb.data());
     }
 };
 

@@ -76,6 +76,9 @@ struct GraphView {
     const uint64_t *out_info;
     const uint64_t *in_info;
     uint64_t *valid;
+    // search-region replicas of a sharded graph (round 5): compact id -> edge id; null: ids are
+    // edge ids. Only FindCycle's frame order (the libstdc++ bucket, id mod 13) reads it.
+    const uint64_t *gid = nullptr;
 };
 
 __device__ __forceinline__ bool bit_get(const uint64_t *bm, uint64_t i) { return (bm[i >> 6] >> (i & 63)) & 1; }

@@ -1126,7 +1126,7 @@ struct FcThread {
             if (sl < 0) continue;
             if (!background_ok(node, x, rm, mu[i], (qb >> i) & 1)) continue;
             // 13 buckets, hash(x) = x: before the first element of x's bucket, else at front
-            const uint32_t xm = mod13(x);
+            const uint32_t xm = mod13(g.gid ? g.gid[x] : x);  // region replicas: the edge id's bucket
             int pos = 0;
             bool hit = false;
 #pragma unroll
@@ -2286,6 +2286,30 @@ static std::vector<uint64_t> gather_sorted(Comm *comm, const std::vector<uint64_
     std::vector<uint64_t> all = comm->allgather_vec(mine);
     std::sort(all.begin(), all.end());
     return all;
+}
+
+std::vector<uint64_t> cf_depth_level_search(mcaat_graph *g, const std::vector<uint64_t> &cand, int limit, Comm *comm) {
+    if (comm && comm->world == 1) comm = nullptr;
+    if (comm) {  // candidate i is searched on rank i % N
+        std::vector<uint64_t> mine;
+        for (size_t i = comm->rank; i < cand.size(); i += comm->world) mine.push_back(cand[i]);
+        return gather_sorted(comm, run_dls(g, mine, limit));
+    }
+    if (knob(g->ctx, "cf.dls_host", 0) != 0 || cand.empty()) return run_dls(g, cand, limit);
+    DevBuf<uint64_t> d(cand.size());
+    h2d(g->ctx, d.p, cand.data(), 8 * cand.size());
+    return run_dls_dev(g, d.p, cand.size(), limit);
+}
+
+void cf_find_cycles(mcaat_graph *g, const mcaat_cf_params &p, const std::vector<uint64_t> &starts, mcaat_cycles *out,
+                    Comm *comm) {
+    if (comm && comm->world == 1) comm = nullptr;
+    FcRunner fr(g, p, out, comm);
+    // with threads=1 the reference's bucket loop is one ordered sequence of starts, so the
+    // speculative windows run across bucket boundaries
+    fr.run_bucket(starts);
+    out->stats[6] = fr.rounds;
+    out->stats[7] = fr.reruns;
 }
 
 void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, Comm *comm) {

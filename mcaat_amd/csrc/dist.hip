@@ -1,23 +1,19 @@
 // dist.hip — the hash-range sharded graph build of a multi-GPU run, natively over a Comm
-// (RCCL or shared memory; comm.hip). The C++ counterpart of mcaat_amd/shard.py with the same
-// steps and the same result:
-//   1. every rank counts its own reads (node_counter; the LDS collapse pre-aggregates);
-//   2. the ranks sum a histogram of the top BOSS-key bits and cut it into `world` owner
-//      ranges of equal weight, contiguous in BOSS order;
-//   3. each rank sends every canonical edge once, with its partial count saturated to 16 bits,
-//      to the owner of the smaller of its two BOSS keys (one all-to-all of keys and counts);
-//   4. that owner sorts and sums them, expands each to its oriented edges (multiplicity
-//      saturated at 65535) and routes each to the owner of its BOSS range (a second, small
-//      all-to-all); each owner sorts what it holds — its range, every key exactly once;
-//   5. an exact-size all-gather in rank order concatenates the owners' ranges into the
-//      single-GPU edge array (edge ids bit-identical), and every rank builds the adjacency.
-// Round 3: at high coverage every rank's reads hold nearly every edge, so the round-2 exchange
-// of both orientations with 32-bit counts (knob dist.oriented=1, kept for comparison) sent
-// 2 x D_local x 12 B per rank and each owner sorted ~2 x D_local pairs whatever N; steps 3-4
-// send D_local x 10 B and sort D_local, then D / N.
-// Round 4 (default): steps 1 and 3-4 become pass A on every rank, the descriptors routed to the
-// owners of their L1 buckets (hash ranges of the minimizer), passes B and C there (final counts),
-// and the oriented edges routed to their BOSS-range owners (exchange_descriptors).
+// (RCCL or shared memory; comm.hip); SURVEY.md §8e, DESIGN.md §7. Default route (round 4):
+//   1. every rank runs pass A of the counter (node_counter_a) on its reads: super-k-mer
+//      descriptors in 256 L1 buckets (hash ranges of the minimizer);
+//   2. the buckets are cut into `world` contiguous owner ranges of equal descriptor weight and
+//      each bucket's descriptors go to its owner (exchange_descriptors; round 5: straight from
+//      pass A's buffers, one segment per bucket); every occurrence of a canonical edge has the
+//      same minimizer, so the owner's passes B and C give final counts;
+//   3. the ranks sum a histogram of the top BOSS-key bits and cut it into owner ranges,
+//      contiguous in BOSS order; the counted canonical edges expand to their oriented edges and
+//      go to their BOSS-range owners (route_oriented, one all-to-all), which sort their ranges;
+//   4. an exact-size all-gather in rank order concatenates the ranges into the single-GPU edge
+//      array (edge ids bit-identical), and every rank builds the adjacency (sdbg_finish).
+// dist.desc=0 keeps round 3's route (each rank counts its own reads, partial counts to the owner
+// of the smaller BOSS key, summed there: canon_reduce), dist.oriented=1 round 2's (both
+// orientations with 32-bit partial counts).
 // Replaces: Read2SdbgS2::Run driven from sdbg_build.cpp:171-187, for reads split over ranks.
 #include <algorithm>
 #include <vector>
@@ -64,13 +60,19 @@ std::vector<uint64_t> choose_splits(const std::vector<uint64_t> &hist, int world
 // reservations (whole 1024-slot runs, inert padding included) to b's owner, which keeps one
 // region per (bucket, source rank) for pass B.
 // Replaces: the S2 counting of Read2SdbgS2::Run (sdbg_build.cpp:171-187) over reads split by rank.
+// Round 5: the buckets go out from where pass A wrote them (one segment per bucket, grouped per
+// owner: Comm::alltoallv_dev_segs), with no full-size send buffer; one rank keeps its buckets.
 static void exchange_descriptors(mcaat_ctx *ctx, Comm &comm, NcBuckets &bk, NcBuckets &own, uint64_t occ_total) {
-    hipStream_t st = ctx->stream;
     const int N = comm.world, R = comm.rank;
     std::vector<uint64_t> mine(256, 0);
     for (int b = 0; b < 256; ++b) {
         if (bk.regions[b].size() > 1) throw Error(MCAAT_E_INVALID, "descriptor exchange: one region per bucket expected");
         for (const auto &rg : bk.regions[b]) mine[b] += rg.second;
+    }
+    if (N == 1) {  // every bucket is this rank's: nothing moves
+        own = std::move(bk);
+        own.n_occ = occ_total;
+        return;
     }
     const std::vector<uint64_t> all = comm.allgather_vec(mine);  // [rank][bucket]
     std::vector<double> cum(256);
@@ -86,52 +88,34 @@ static void exchange_descriptors(mcaat_ctx *ctx, Comm &comm, NcBuckets &bk, NcBu
         int b = acc > 0 ? (int)(std::lower_bound(cum.begin(), cum.end(), acc * o / N) - cum.begin()) + 1 : 256;
         lo[o] = std::min(std::max(b, lo[o - 1]), 256);
     }
-    // send buffer: each owner's buckets, ascending, back to back
-    uint64_t n_send = 0;
-    for (int b = 0; b < 256; ++b) n_send += mine[b];
-    DevBuf<uint4> sd(n_send ? n_send : 1);
-    DevBuf<uint16_t> ss(n_send ? n_send : 8);
-    std::vector<uint64_t> sb16(N, 0), sb2(N, 0);
-    {
-        uint64_t o = 0;
-        for (int q = 0; q < N; ++q)
-            for (int b = lo[q]; b < lo[q + 1]; ++b) {
-                for (const auto &rg : bk.regions[b]) {
-                    HIP_OK(hipMemcpyAsync(sd.p + o, bk.data.p + rg.first, 16 * rg.second, hipMemcpyDeviceToDevice, st));
-                    HIP_OK(hipMemcpyAsync(ss.p + o, bk.sub.p + rg.first, 2 * rg.second, hipMemcpyDeviceToDevice, st));
-                    o += rg.second;
-                }
-                sb16[q] += 16 * mine[b];
-                sb2[q] += 2 * mine[b];
+    // to owner q: one segment per non-empty bucket of its range, descriptors and sub rows
+    std::vector<std::vector<Comm::Seg>> s16(N), s2(N);
+    for (int q = 0; q < N; ++q)
+        for (int b = lo[q]; b < lo[q + 1]; ++b)
+            for (const auto &rg : bk.regions[b]) {
+                s16[q].push_back({bk.data.p + rg.first, 16 * rg.second});
+                s2[q].push_back({bk.sub.p + rg.first, 2 * rg.second});
             }
-    }
-    bk.data.release();
-    bk.sub.release();
-    // what this rank receives: from each source, its slots of buckets [lo[R], lo[R+1])
-    std::vector<uint64_t> rb16(N, 0), rb2(N, 0);
+    // from source q: its non-empty buckets of [lo[R], lo[R+1]), in bucket order
+    std::vector<std::vector<uint64_t>> r16(N), r2(N);
     uint64_t n_recv = 0;
-    for (int q = 0; q < N; ++q) {
-        uint64_t n = 0;
-        for (int b = lo[R]; b < lo[R + 1]; ++b) n += all[(uint64_t)q * 256 + b];
-        rb16[q] = 16 * n;
-        rb2[q] = 2 * n;
-        n_recv += n;
-    }
+    own.regions.assign(256, {});
+    for (int q = 0; q < N; ++q)
+        for (int b = lo[R]; b < lo[R + 1]; ++b) {
+            const uint64_t n = all[(uint64_t)q * 256 + b];
+            if (!n) continue;
+            r16[q].push_back(16 * n);
+            r2[q].push_back(2 * n);
+            own.regions[b].push_back({n_recv, n});
+            n_recv += n;
+        }
     own.data.alloc(n_recv ? n_recv : 1);
     own.sub.alloc(n_recv ? n_recv : 8);
-    HIP_OK(hipStreamSynchronize(st));
-    comm.alltoallv_dev(sd.p, sb16.data(), own.data.p, rb16.data());
-    comm.alltoallv_dev(ss.p, sb2.data(), own.sub.p, rb2.data());
-    own.regions.assign(256, {});
-    {
-        uint64_t o = 0;
-        for (int q = 0; q < N; ++q)
-            for (int b = lo[R]; b < lo[R + 1]; ++b) {
-                const uint64_t n = all[(uint64_t)q * 256 + b];
-                if (n) own.regions[b].push_back({o, n});
-                o += n;
-            }
-    }
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    comm.alltoallv_dev_segs(s16, own.data.p, r16);
+    comm.alltoallv_dev_segs(s2, own.sub.p, r2);
+    bk.data.release();
+    bk.sub.release();
     own.l2_bits = bk.l2_bits;
     // occurrences behind this owner's descriptors (sizes its output buffer), by its share
     own.n_occ = acc > 0 ? (uint64_t)((double)occ_total * (double)n_recv / acc) + 1 : 0;
@@ -280,6 +264,28 @@ void build_graph_sharded(mcaat_ctx *ctx, Comm &comm, const mcaat_reads *r, int k
     g->ctx = ctx;
     g->k = k;
     g->D = D;
+    // (round 5, default) the graph stays sharded: this rank keeps its range, builds its edges'
+    // adjacency by one exchange with the target owners, and CycleFinder runs per shard
+    // (shard_cf.hip). dist.shard_cf=0: the exact-size all-gather below, every rank the whole graph.
+    if (knob(ctx, "dist.shard_cf", 1) != 0 && desc_route) {
+        g->sharded = true;
+        g->rank_lo.assign(N + 1, 0);
+        for (int r = 0; r < N; ++r) g->rank_lo[r + 1] = g->rank_lo[r] + ns[r];
+        g->key_split = splits;
+        g->id_lo = g->rank_lo[R];
+        g->D_local = u;
+        g->key = std::move(uk);
+        g->mult.alloc(mcaat_graph::mult_entries(u));
+        HIP_OK(hipMemcpyAsync(g->mult.p, um.p, 2 * u, hipMemcpyDeviceToDevice, st));
+        HIP_OK(hipStreamSynchronize(st));
+        um.release();
+        timer.mark("shard_all_gather");
+        sdbg_finish_sharded(ctx, comm, g);
+        timer.mark("sdbg_build");
+        HIP_OK(hipStreamSynchronize(st));
+        timer.finish();
+        return;
+    }
     g->key.alloc(D ? D : 1);
     g->mult.alloc(mcaat_graph::mult_entries(D));
     std::vector<uint64_t> b8(N), b2(N);

@@ -216,10 +216,25 @@ struct mcaat_graph {
     // radix directory over the top bits of the BOSS key (label lookups after the build)
     mcaat::DevBuf<uint64_t> dir;
     int dir_shift = 0;
+    // (round 5) a sharded graph (mcaat_build_graph_sharded, knob dist.shard_cf): this rank holds
+    // the edges [id_lo, id_lo + D_local) of the D edges, its BOSS-key range; key, mult, out_info,
+    // in_info (global ids) and valid are indexed by local position; rank_lo holds every rank's
+    // first id (N + 1 entries), key_split the N - 1 BOSS-key splits (owner of a key: the number of
+    // splits at or below it). CycleFinder runs per shard (shard_cf.hip); mcaat_graph_unshard
+    // gathers the whole graph for the host steps after it.
+    bool sharded = false;
+    uint64_t id_lo = 0, D_local = 0;
+    std::vector<uint64_t> rank_lo, key_split;
+    uint64_t dir_base = 0;  // sharded: the local directory's prefixes are (key - dir_base) >> dir_shift
+    uint64_t dir_n = 0;     // sharded: its prefix count
+    // search-region replicas (shard_cf.hip): compact id -> edge id, read for FindCycle's frame
+    // order (the libstdc++ bucket of an id) and to name results
+    mcaat::DevBuf<uint64_t> gid;
     mcaat::GraphView view() const {
-        return mcaat::GraphView{k, D, key.p, mult.p, out_info.p, in_info.p, valid.p};
+        return mcaat::GraphView{k, sharded ? D_local : D, key.p, mult.p, out_info.p, in_info.p, valid.p,
+                                gid.n ? gid.p : nullptr};
     }
-    uint64_t n_words() const { return (D + 63) / 64; }
+    uint64_t n_words() const { return ((sharded ? D_local : D) + 63) / 64; }
     // allocation sizes: a valid/visited bitmap keeps one word past its last, and mult 8
     // entries past its last, so a neighbour window is one 16-B / 12-B load (common.h win16,
     // mult4) even at the end of the graph
@@ -391,6 +406,9 @@ struct NcBuckets {
     // per L1 bucket: its regions (first slot, slots) in data/sub, each a whole number of
     // 1024-slot reservations (so every region starts 16-B aligned in sub)
     std::vector<std::vector<std::pair<uint64_t, uint64_t>>> regions;
+    // pass A's layout: bucket b's slots start at base[b] (257 entries; a bucket's reserved but
+    // unused tail is not part of its region). Empty when the regions came from an exchange.
+    std::vector<uint64_t> base;
     int l2_bits = 0;        // fine partitions = 256 << l2_bits
     uint64_t n_occ = 0;     // edge occurrences behind the descriptors (sizes the output)
 };
@@ -424,6 +442,21 @@ struct Comm;  // comm.h
 // comm: the ranks of a multi-GPU run that each hold this graph (null: one GPU); every rank
 // gets the same results
 void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, Comm *comm = nullptr);
+// CycleFinder's searches over a search graph (cycle_finder.hip; the whole graph, or a region
+// replica of a sharded one): DepthLevelSearch of the ascending candidate ids, split over the
+// ranks (returns the passing ids, ascending, on every rank) ...
+std::vector<uint64_t> cf_depth_level_search(mcaat_graph *g, const std::vector<uint64_t> &cand, int limit, Comm *comm);
+// ... and the bucket loop of FindCycle over the starts in the reference's order (out->starts,
+// flat, offsets, stats[5..7])
+void cf_find_cycles(mcaat_graph *g, const mcaat_cf_params &p, const std::vector<uint64_t> &starts, mcaat_cycles *out,
+                    Comm *comm);
+// (round 5) the per-shard CycleFinder over a sharded graph (shard_cf.hip)
+void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, Comm &comm);
+// the sharded build's adjacency: every rank its range's out_info / in_info by one request /
+// response exchange with the owners of the targets (shard_cf.hip)
+void sdbg_finish_sharded(mcaat_ctx *ctx, Comm &comm, mcaat_graph *g);
+// a sharded graph -> the whole graph on every rank (valid bits kept)
+void graph_unshard(mcaat_graph *g, Comm &comm);
 void synth_reads(mcaat_ctx *ctx, const mcaat_synth_spec &s, mcaat_reads *out, uint64_t first, uint64_t count);
 void synth_genome_host(const mcaat_synth_spec &s, std::vector<uint64_t> &genome);
 void graph_neighbors(const mcaat_graph *g, const uint64_t *ids, size_t n, int incoming, uint64_t *out,

@@ -1585,6 +1585,7 @@ void node_counter_a(mcaat_ctx *ctx, const mcaat_reads *r, int k, const std::func
         for (int b = 0; b < 256; ++b) cap[b] = (tot[b] + 8) & ~7ull;  // exact on the second run (cursors count every grab)
     }
     uint64_t n_desc = 0;
+    bk.base = base;
     for (int b = 0; b < 256; ++b) {
         n_desc += tot[b];
         if (tot[b]) bk.regions[b].push_back({base[b], tot[b]});  // tot: whole 1024-slot reservations

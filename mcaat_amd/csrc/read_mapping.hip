@@ -266,7 +266,8 @@ void graph_keep_region(mcaat_graph *g, const uint64_t *seeds, size_t n, uint64_t
         nf = hn;
     }
     for (uint64_t h = 0; h < hops && nf; ++h) {
-        DevBuf<uint64_t> next(8 * nf);
+        // membership is a bitmap, so each edge enters a frontier at most once: at most D entries
+        DevBuf<uint64_t> next(std::min<uint64_t>(8 * nf, g->D));
         HIP_OK(hipMemsetAsync(cnt.p, 0, 8, st));
         hipLaunchKernelGGL(k_grow_hop, dim3(grid_for(nf, kBlock)), dim3(kBlock), 0, st, g->view(), reg.p,
                            (const uint64_t *)front.p, nf, next.p, cnt.p);

@@ -281,7 +281,7 @@ void get_relevant_reads_and_cycles(const std::vector<Graph> &regions, const std:
 // reference's removal loop compares the ORIGINAL kept indices against positions in the
 // shrinking vector (its bound and index both use the current size); that exact walk is
 // restated here, because it decides which cycles survive when the cover drops some.
-void get_minimum_cycles_for_full_coverage(std::vector<std::vector<uint64_t>> &cycles) {
+void get_minimum_cycles_for_full_coverage(std::vector<std::vector<uint64_t>> &cycles, std::ostream &log) {
     if (cycles.empty()) return;
     std::unordered_map<uint64_t, uint32_t> dense;
     uint32_t next_id = 0;
@@ -304,7 +304,7 @@ void get_minimum_cycles_for_full_coverage(std::vector<std::vector<uint64_t>> &cy
         sets.push_back(std::move(s));
     }
     if (universe.empty() || sets.empty()) return;
-    const std::vector<size_t> kept = solve_min_cover_problem(universe, sets);
+    const std::vector<size_t> kept = solve_min_cover_problem(universe, sets, log);
     const std::unordered_set<size_t> keep(kept.begin(), kept.end());
     for (size_t i = 0; i < cycles.size(); ++i) {
         const size_t pos = cycles.size() - 1 - i;
@@ -320,21 +320,21 @@ void get_minimum_cycles_for_full_coverage(std::vector<std::vector<uint64_t>> &cy
 // index first), bounded by a node budget after which the best cover found (greedy seed) is
 // kept. The returned indices are ascending; callers only use them as a set.
 std::vector<size_t> solve_min_cover_problem(const std::unordered_set<uint32_t> &universe,
-                                            const std::vector<std::vector<uint32_t>> &sets) {
+                                            const std::vector<std::vector<uint32_t>> &sets, std::ostream &log) {
     if (universe.empty() || sets.empty()) {
-        std::cout << "Error: Unable to find min cover as the universe or sets are empty" << std::endl;
+        log << "Error: Unable to find min cover as the universe or sets are empty" << std::endl;
         return {};
     }
     const size_t n = universe.size();
     for (uint32_t x : universe)
         if (x >= n) {
-            std::cout << "Error: Unable to find min cover as the universe elements are invalid" << std::endl;
+            log << "Error: Unable to find min cover as the universe elements are invalid" << std::endl;
             return {};
         }
     for (const auto &s : sets)
         for (uint32_t x : s)
             if (x >= n) {
-                std::cout << "Error: Unable to find min cover as the sets elements are invalid" << std::endl;
+                log << "Error: Unable to find min cover as the sets elements are invalid" << std::endl;
                 return {};
             }
     // element -> covering sets (ascending, deduplicated)

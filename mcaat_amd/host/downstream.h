@@ -78,9 +78,11 @@ using ReadRefs = std::vector<const std::vector<uint64_t> *>;
 void get_relevant_reads_and_cycles(const std::vector<Graph> &regions, const std::vector<std::vector<uint64_t>> &all_reads,
                                    const std::vector<std::vector<uint64_t>> &all_cycles, std::vector<ReadRefs> &reads_out,
                                    std::vector<std::vector<std::vector<uint64_t>>> &cycles_out);
-void get_minimum_cycles_for_full_coverage(std::vector<std::vector<uint64_t>> &cycles);
+// (round 5) `log`: where the cover's diagnostics go (std::cout by default; step 7's worker
+// threads pass a per-region stream that is printed in region order)
+void get_minimum_cycles_for_full_coverage(std::vector<std::vector<uint64_t>> &cycles, std::ostream &log = std::cout);
 std::vector<size_t> solve_min_cover_problem(const std::unordered_set<uint32_t> &universe,
-                                            const std::vector<std::vector<uint32_t>> &sets);
+                                            const std::vector<std::vector<uint32_t>> &sets, std::ostream &log = std::cout);
 std::unordered_map<uint64_t, uint32_t> get_node_to_unique_cycle_map(const std::vector<std::vector<uint64_t>> &cycles);
 std::vector<uint32_t> get_all_cycle_indices(const std::unordered_map<uint64_t, uint32_t> &node_to_cycle_map);
 std::vector<std::tuple<uint32_t, uint32_t>> every_possible_combination(const std::vector<uint32_t> &v);

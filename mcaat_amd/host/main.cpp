@@ -258,6 +258,16 @@ static int run(Settings &settings, Ranks &ranks) {
             std::cout << line << std::endl;
         }
         const double t_span_end = since(g_main_start);
+        // a graph built and searched per shard is gathered on every rank for the steps after
+        // the span (read mapping, spacer ordering read the whole graph); no-op on one GPU
+        if (settings.gpus > 1 && settings.mcomm) {
+            int sharded = 0;
+            mcaat_check(mcaat_graph_shard_info(sdbg.device(), &sharded, nullptr, nullptr), "graph shard info");
+            if (sharded) {
+                mcaat_check(mcaat_graph_unshard(sdbg.device(), settings.mcomm), "gathering the sharded graph");
+                sdbg.SyncFromDevice();
+            }
+        }
         auto cycles_map = cycle_finder.results;
         std::cout << "Number of nodes in results: " << cycles_map.size() << std::endl;
         auto cycles = cycles_map_to_cycles(cycles_map);        // main.cpp:542

@@ -123,6 +123,8 @@ void SDBGBuild::BuildSDBG() {
                         "building the SDBG over the ranks");
         else
             mcaat_check(mcaat_build_graph(ctx, reads_, settings.kmer_k, &graph_), "building the SDBG");
+        if (settings.keep_graph && settings.gpus > 1 && settings.mcomm)  // the whole graph is saved
+            mcaat_check(mcaat_graph_unshard(graph_, settings.mcomm), "gathering the sharded graph");
         if (settings.keep_graph && settings.rank == 0) {
             const std::string out = settings.graph_folder + "/graph.mcaat_sdbg";
             mcaat_check(mcaat_graph_save(graph_, out.c_str()), "saving the graph");

@@ -59,6 +59,7 @@ std::vector<FoundSystem> run_and_debug_spacer_ordering(const std::vector<std::ve
         std::vector<uint32_t> order;
         float conf_resolution = 1.0, conf_sort = 1.0;
         std::string log;  // order_cycles' lines
+        std::string cover_log;  // the set cover's diagnostics (printed in region order)
     };
     std::vector<Sub> subs(regions.size());
     const auto t_split = std::chrono::high_resolution_clock::now();
@@ -69,7 +70,11 @@ std::vector<FoundSystem> run_and_debug_spacer_ordering(const std::vector<std::ve
         auto rr = std::move(region_reads[ri]);
         s.cycles = std::move(region_cycles[ri]);
         const auto a = hc::now();
-        get_minimum_cycles_for_full_coverage(s.cycles);
+        {
+            std::ostringstream clog;
+            get_minimum_cycles_for_full_coverage(s.cycles, clog);
+            s.cover_log = clog.str();
+        }
         const auto b = hc::now();
         ns_cover += std::chrono::duration_cast<std::chrono::nanoseconds>(b - a).count();
         // the reverse-complement twin of a region is expected to carry no relevant reads
@@ -102,7 +107,10 @@ std::vector<FoundSystem> run_and_debug_spacer_ordering(const std::vector<std::ve
             if (!e.empty()) throw std::runtime_error(e);
     }
     size_t n_kept = 0;
-    for (const Sub &s : subs) n_kept += s.kept;
+    for (const Sub &s : subs) {
+        n_kept += s.kept;
+        std::cout << s.cover_log;  // region order, whatever thread solved it
+    }
     std::cout << "  ✅ Filtered out " << regions.size() - n_kept << "/" << regions.size() << " subproblems" << std::endl;
     const auto t_solved = std::chrono::high_resolution_clock::now();
     std::cout << "  🔄 Solving " << n_kept << " subproblems..." << std::endl;

@@ -135,6 +135,8 @@ SIGNATURES = {
     "mcaat_build_graph_sharded": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
     "mcaat_cycle_finder_comm": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(_CfParams), C.POINTER(C.c_void_p)]),
     "mcaat_arena_check": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64)]),
+    "mcaat_graph_shard_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), _u64p, _u64p]),
+    "mcaat_graph_unshard": (C.c_int, [C.c_void_p, C.c_void_p]),
 }
 
 _lib: Optional[C.CDLL] = None
@@ -615,6 +617,17 @@ class Graph:
     @property
     def size(self) -> int:
         return self.info()[1]
+
+    def shard_info(self) -> Tuple[bool, int, int]:
+        """(sharded, first id, edges held here) — mcaat_graph_shard_info."""
+        sh = C.c_int(0)
+        a, n = C.c_uint64(0), C.c_uint64(0)
+        _check(self.ctx._lib.mcaat_graph_shard_info(self.h, C.byref(sh), C.byref(a), C.byref(n)))
+        return bool(sh.value), a.value, n.value
+
+    def unshard(self, comm: "Comm") -> None:
+        """Gather a sharded graph on every rank (collective; mcaat_graph_unshard)."""
+        _check(self.ctx._lib.mcaat_graph_unshard(self.h, comm.h))
 
     def download(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         _, d = self.info()

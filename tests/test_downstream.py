@@ -279,3 +279,32 @@ def test_cli_rank_dying_before_it_joins_ends_the_run(tmp_path, comm):
                           "--comm", comm], capture_output=True, text=True, timeout=300, env=env)
     assert out.returncode != 0
     assert time.time() - t0 < 120, "the run waited for a rank that had already died"
+
+
+@pytest.mark.gpu
+def test_cli_step7_threads_equal_serial_on_a_device_graph(tmp_path):
+    """ The CLI's device-graph path (GPU region growth and valid subgraph, then
+    the regions solved on the job's threads) with --threads 1 and --threads 8 on a multi-array
+    input: the same CRISPR_Arrays.txt and the same step-7 log, line for line."""
+    spec = M.SynthSpec(seed=21, n_genomes=3, genome_len=20_000, arrays_per_genome=2, spacers_per_array=9,
+                       repeat_len_min=30, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36, n_reads=24_000,
+                       error_rate=0.001)
+    packed, offs = M.synth_host(spec)
+    p = tmp_path / "r.fq"
+    with open(p, "w") as f:
+        for i in range(len(offs) - 1):
+            s = unpack_read(packed, int(offs[i]), int(offs[i + 1]))
+            f.write(f"@r{i}\n{s}\n+\n{'I' * len(s)}\n")
+    got = {}
+    for t in (1, 8):
+        o = tmp_path / f"o{t}"
+        out = subprocess.run([CLI, "-i", str(p), "--output-folder", str(o), "--threads", str(t), "--ram", "2G"],
+                             capture_output=True, text=True, timeout=600)
+        assert out.returncode == 0, out.stderr + out.stdout[-2000:]
+        lines = out.stdout.splitlines()
+        a = next(i for i, x in enumerate(lines) if "Filtered out" in x)
+        b = next(i for i, x in enumerate(lines) if "Completed each subproblem" in x)
+        got[t] = ((o / "CRISPR_Arrays.txt").read_text(), lines[a:b + 1])
+    assert got[1][0] == got[8][0]
+    assert got[1][1] == got[8][1]
+    assert "Number of Systems:" in got[1][0] and got[1][1][0].split()[-1] != "0/0"

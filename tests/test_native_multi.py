@@ -93,12 +93,34 @@ def _ranks(world, comm, extra=(), timeout=600):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world,extra", [(1, ()), (2, ()), (3, ("--window", "16", "--slot", "65536")), (4, ()),
-                                         (3, ("--knob", "dist.oriented=1")), (3, ("--knob", "dist.desc=0"))])
+                                         (3, ("--knob", "dist.oriented=1")), (3, ("--knob", "dist.desc=0")),
+                                         # round 4's replicated CycleFinder (every rank the whole graph)
+                                         (2, ("--knob", "dist.shard_cf=0")), (3, ("--knob", "dist.shard_cf=0")),
+                                         # per-shard peel with every unary edge a ruler / sparse rulers,
+                                         # adjacency and window exchanges in many small chunks
+                                         (2, ("--knob", "dist.ruler_mask=0")), (3, ("--knob", "dist.ruler_mask=1023")),
+                                         (3, ("--knob", "dist.adj_chunk=1024"))])
 def test_sharded_build_and_cycle_finder_ranks_share_one_gpu(world, extra):
+    """(round 5: per-shard CycleFinder by default) the sharded build + CycleFinder over 1-4 ranks
+    sharing the GPU equal the one-GPU path: keys, multiplicities, valid bits after CycleFinder,
+    entries, candidates, buckets, stats."""
     outs = _ranks(world, "shm", extra)
     for rc, o, e in outs:
         assert rc == 0, (o[-2000:], e[-3000:])
         assert "NATIVE_MULTI_OK" in o, o
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["pe_err", "low_thr", "c3_sample", "c5_sample"])
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_per_shard_cycle_finder_parity_cases(case, world):
+    """ The per-shard CycleFinder on the parity cases (paired-end with errors,
+    threshold 2, the C3 and C5 coverage-matched samples) through 1, 2 and 4 shared-memory ranks
+    equals the one-GPU path: valid bitmap, candidates, buckets, entries, stats."""
+    outs = _ranks(world, "shm", ("--case", case, "--slot", "0"))
+    for rc, o, e in outs:
+        assert rc == 0, (o[-2000:], e[-3000:])
+        assert "NATIVE_MULTI_OK" in o and "sharded=True" in o, o
 
 
 @pytest.mark.gpu

@@ -62,6 +62,8 @@ def main() -> int:
     ap.add_argument("--single", action="store_true", help="the one-GPU path alone (with --digest)")
     ap.add_argument("--knob", action="append", default=[], help="name=value knob on every rank's context")
     ap.add_argument("--repeat", type=int, default=1, help="--config: sharded builds in a row (stages of the last)")
+    ap.add_argument("--case", default="default", choices=["default", "pe_err", "low_thr", "c3_sample", "c5_sample"],
+                    help="the dataset of the in-process comparison")
     a = ap.parse_args()
 
     def make_comm(ctx):
@@ -114,10 +116,13 @@ def main() -> int:
                 build_stages = {kk: round(vv, 2) for kk, vv in ctx.stage_times().items()}
             mine.free()
             res = g.cycle_finder(prm, comm=comm)
+            cf_stages = {kk: round(vv, 2) for kk, vv in ctx.stage_times().items()}
+            g.unshard(comm)  # a per-shard graph is gathered for the checksums (no-op otherwise)
         d = checksums(g, res)
         d["seconds"] = round(time.time() - t0, 1)
         if not a.single:
             d["build_stages_ms"] = build_stages
+            d["cf_stages_ms"] = cf_stages
         g.free()
         if comm is not None:
             comm.barrier()
@@ -132,7 +137,20 @@ def main() -> int:
     spec = M.SynthSpec(seed=11, n_genomes=3, genome_len=40_000, arrays_per_genome=2, spacers_per_array=10,
                        repeat_len_min=30, repeat_len_max=34, spacer_len_min=30, spacer_len_max=36,
                        n_reads=a.reads, error_rate=2e-3)
-    k = 27
+    k, thr = 27, 20
+    if a.case != "default":  # the parity cases of tests/test_scale_parity.py (CASES, SAMPLES)
+        from mcaat_amd.configs import CONFIGS
+
+        spec, k, thr = {
+            "pe_err": (M.SynthSpec(seed=7, n_genomes=4, genome_len=20_000, arrays_per_genome=2, spacers_per_array=8,
+                                   repeat_len_min=32, repeat_len_max=36, spacer_len_min=30, spacer_len_max=36,
+                                   n_reads=24_000, error_rate=0.002, paired=True), 23, 5),
+            "low_thr": (M.SynthSpec(seed=11, n_genomes=3, genome_len=15_000, arrays_per_genome=2, spacers_per_array=10,
+                                    repeat_len_min=30, repeat_len_max=34, spacer_len_min=30, spacer_len_max=34,
+                                    n_reads=12_000, error_rate=0.004), 23, 2),
+            "c3_sample": (CONFIGS["c3"]["sample"], 27, 20),
+            "c5_sample": (CONFIGS["c5"]["sample"], 27, 2),
+        }[a.case]
     dev = a.rank % max(1, M.device_count()) if a.comm == "rccl" else 0
     ctx = M.Context(dev)
     if a.window:
@@ -146,10 +164,12 @@ def main() -> int:
     first = a.rank * spec.n_reads // a.world
     count = (a.rank + 1) * spec.n_reads // a.world - first
     mine = M.Reads.synth_range(ctx, spec, first, count)
-    prm = M.CfParams(threshold_multiplicity=20)
+    prm = M.CfParams(threshold_multiplicity=thr)
     g = M.Graph.build_sharded(ctx, comm, mine, k)
-    keys, mult, _ = g.download()
+    sharded = g.shard_info()[0]
     res = g.cycle_finder(prm, comm=comm)
+    g.unshard(comm)
+    keys, mult, valid = g.download()
     g.free()
     mine.free()
 
@@ -157,17 +177,22 @@ def main() -> int:
     g1 = M.Graph.build(ctx, whole, k)
     k1, m1, _ = g1.download()
     r1 = g1.cycle_finder(prm)
+    _, _, v1 = g1.download()
     g1.free()
     whole.free()
 
-    ok = np.array_equal(keys, k1) and np.array_equal(mult, m1)
+    ok = np.array_equal(keys, k1) and np.array_equal(mult, m1) and np.array_equal(valid, v1)
     ok = ok and res.entries == r1.entries and res.stats[:6] == r1.stats[:6]
     ok = ok and list(res.candidates) == list(r1.candidates) and list(res.buckets) == list(r1.buckets)
     # every rank holds the same results
     digest = repr((res.entries, res.stats[:6])).encode()
     same = len(set(comm.allgather_bytes(digest))) == 1
     print(f"rank {a.rank}: D={len(keys)} (single {len(k1)}) entries={len(res.entries)} cycles={res.stats[5]} "
-          f"rounds={res.stats[6]} reruns={res.stats[7]} match={ok} ranks_agree={same}", flush=True)
+          f"rounds={res.stats[6]} reruns={res.stats[7]} sharded={sharded} match={ok} ranks_agree={same}", flush=True)
+    if not ok:
+        print(f"rank {a.rank}: keys {np.array_equal(keys, k1)} mult {np.array_equal(mult, m1)} valid "
+              f"{np.array_equal(valid, v1)} ({int((valid != v1).sum())} differ) stats {res.stats[:6]} vs {r1.stats[:6]} "
+              f"entries {res.entries == r1.entries} cand {list(res.candidates) == list(r1.candidates)}", flush=True)
     comm.barrier()
     comm.close()
     ctx.close()
