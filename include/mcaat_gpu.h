@@ -369,7 +369,8 @@ int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value);
  *                      CycleFinder runs over the ranks on replicas (round 4; default 1: per shard)
  *   dist.ruler_mask   per-shard peel: 1 in (mask + 1) unary edges is a ruler besides the chain
  *                      heads (default 15)
- *   dist.adj_chunk    sharded adjacency: edges per request/response exchange (default 2^27) */
+ *   dist.adj_chunk    sharded adjacency: edges per request/response exchange (default 2^26)
+ *   dist.dir_edges    sharded adjacency: edges per prefix of the range's radix directory (default 2) */
 
 /* ---- allocator check ----------------------------------------------------------------------
  * Replaces: nothing in the reference. The device arena's stream order (csrc/alloc.hip): a block
@@ -378,6 +379,10 @@ int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value);
  * 1 when every word holds the side kernel's value afterwards (the side kernel waited for the
  * fence), out[2] = the arena's fence waits during the check. */
 int mcaat_arena_check(mcaat_ctx *ctx, int64_t *out);
+/* Device memory of the library on the ctx's GPU (the arena behind every buffer): bytes in use
+ * now, the most in use since the last reset (reset_peak != 0 starts a new window after
+ * reading), and the chunks the arena holds. Null outputs are skipped. */
+int mcaat_arena_usage(mcaat_ctx *ctx, int reset_peak, uint64_t *in_use, uint64_t *peak, uint64_t *reserved);
 
 #ifdef __cplusplus
 }

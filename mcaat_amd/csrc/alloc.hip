@@ -60,6 +60,7 @@ struct Arena {
     std::vector<Watched> streams;
     std::vector<hipEvent_t> event_pool;
     uint64_t serial = 0;
+    uint64_t in_use = 0, peak = 0;  // bytes handed out now / most since the last reset
     uint64_t fences_recorded = 0, waits = 0;
 
     hipEvent_t new_event() {
@@ -148,6 +149,8 @@ struct Arena {
             s.size = bytes;
             add_free(p + bytes, sz - bytes, s.chunk, fences);  // the rest keeps the fences
         }
+        in_use += segs[p].size;
+        peak = std::max(peak, in_use);
         wait_fences(fences, on);
         return p;
     }
@@ -155,6 +158,7 @@ struct Arena {
         auto it = segs.find(p);
         if (it == segs.end()) return;
         it->second.free = true;
+        in_use -= it->second.size;
         it->second.fences = std::move(fences);
         // coalesce with the next segment of the same chunk
         auto nx = std::next(it);
@@ -337,6 +341,17 @@ void arena_check(mcaat_ctx *ctx, int64_t *out) {
     out[0] = b.p == first;
     out[1] = all2;
     out[2] = (int64_t)(w1 - w0);
+}
+
+void arena_usage(uint64_t *in_use, uint64_t *peak, uint64_t *reserved, bool reset_peak) {
+    std::lock_guard<std::mutex> lk(pools().mu);
+    Arena &a = pools().by_device[current_device()];
+    uint64_t r = 0;
+    for (const auto &c : a.chunks) r += c.second;
+    if (in_use) *in_use = a.in_use;
+    if (peak) *peak = a.peak;
+    if (reserved) *reserved = r;
+    if (reset_peak) a.peak = a.in_use;
 }
 
 void arena_stats(uint64_t *fences, uint64_t *waits) {

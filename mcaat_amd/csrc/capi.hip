@@ -1070,7 +1070,7 @@ int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value) {
         "fq.hostpack",     "sort.mid_counting", "nc.big_table", "cf.fused_init", "sort.mid_occ", "cf.scan_u", "cf.prep_batch", "cf.dls_lanes", "dist.oriented",
         "sort.small_mid", "sort.small_limit", "cf.recount", "cf.dls_host",
         "dist.desc",      "cf.compact",         "cf.fresh",   "cf.dls_persist", "nc.split_first", "nc.split_max", "cf.pull_flags", "cf.dls_budget", "nc.grow_early",
-        "nc.free_sync", "dist.shard_cf", "dist.ruler_mask", "dist.adj_chunk"};
+        "nc.free_sync", "dist.shard_cf", "dist.ruler_mask", "dist.adj_chunk", "dist.dir_edges"};
     return guarded([&] {
         require(ctx && name, "null argument");
         bool ok = false;
@@ -1258,5 +1258,13 @@ int mcaat_arena_check(mcaat_ctx *ctx, int64_t *out) {
         require(ctx && out, "null argument");
         mcaat::bind(ctx);
         mcaat::arena_check(ctx, out);
+    });
+}
+
+int mcaat_arena_usage(mcaat_ctx *ctx, int reset_peak, uint64_t *in_use, uint64_t *peak, uint64_t *reserved) {
+    return guarded([&] {
+        require(ctx != nullptr, "null argument");
+        mcaat::bind(ctx);
+        mcaat::arena_usage(in_use, peak, reserved, reset_peak != 0);
     });
 }

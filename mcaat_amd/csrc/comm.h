@@ -21,8 +21,11 @@ struct Comm {
                                  std::vector<uint64_t> &sizes) = 0;
     // rank r sends send_bytes[d] bytes (at the prefix-sum offset) to each rank d and receives
     // recv_bytes[s] bytes from each rank s into recv (prefix-sum offsets, rank order)
+    // (send_off / recv_off: explicit byte offsets per rank instead of the prefix sums; a rank
+    // with 0 bytes each way is skipped, so a caller that moved its own share already passes 0)
     virtual void alltoallv_dev(const void *send, const uint64_t *send_bytes, void *recv,
-                               const uint64_t *recv_bytes) = 0;
+                               const uint64_t *recv_bytes, const uint64_t *send_off = nullptr,
+                               const uint64_t *recv_off = nullptr) = 0;
     // rank r's sizes[r] bytes at `send`, concatenated in rank order into recv (sizes known to all)
     virtual void allgatherv_dev(const void *send, void *recv, const uint64_t *sizes) = 0;
     // all-to-all of device segments: to each rank d this rank sends the segments send[d] in order;

@@ -137,9 +137,11 @@ struct RcclComm final : Comm {
         sync();
     }
 
-    void alltoallv_dev(const void *send, const uint64_t *send_bytes, void *recv,
-                       const uint64_t *recv_bytes) override {
-        const auto so = offsets_of(send_bytes, world), ro = offsets_of(recv_bytes, world);
+    void alltoallv_dev(const void *send, const uint64_t *send_bytes, void *recv, const uint64_t *recv_bytes,
+                       const uint64_t *send_off, const uint64_t *recv_off) override {
+        auto so = offsets_of(send_bytes, world), ro = offsets_of(recv_bytes, world);
+        if (send_off) so.assign(send_off, send_off + world);
+        if (recv_off) ro.assign(recv_off, recv_off + world);
         const uint8_t *s = (const uint8_t *)send;
         uint8_t *d = (uint8_t *)recv;
         if (send_bytes[rank] != recv_bytes[rank]) throw Error(MCAAT_E_INVALID, "alltoallv: self sizes differ");
@@ -413,10 +415,12 @@ struct ShmComm final : Comm {
         HIP_OK(hipStreamSynchronize(ctx->stream));
     }
 
-    void alltoallv_dev(const void *send, const uint64_t *send_bytes, void *recv,
-                       const uint64_t *recv_bytes) override {
+    void alltoallv_dev(const void *send, const uint64_t *send_bytes, void *recv, const uint64_t *recv_bytes,
+                       const uint64_t *send_off, const uint64_t *recv_off) override {
         need_ctx();
-        const auto so = offsets_of(send_bytes, world), ro = offsets_of(recv_bytes, world);
+        auto so = offsets_of(send_bytes, world), ro = offsets_of(recv_bytes, world);
+        if (send_off) so.assign(send_off, send_off + world);
+        if (recv_off) ro.assign(recv_off, recv_off + world);
         // shift s: this rank sends to rank+s and receives from rank-s
         for (int s = 0; s < world; ++s) {
             const int to = (rank + s) % world, from = (rank - s + world) % world;
@@ -444,8 +448,25 @@ struct ShmComm final : Comm {
         gather_through_slots(send, recv, sizes, true);
     }
 
-    // the rehearsal transport stages device data through the host anyway: each peer's segments
-    // are packed into one device buffer and sent by the plain all-to-all
+    // bytes [a, a + n) of the concatenation of segments `sg` (device) into host memory
+    void put_range(uint8_t *dst, const std::vector<Seg> &sg, uint64_t a, uint64_t n) {
+        uint64_t o = 0;
+        for (const Seg &g : sg) {
+            if (n == 0) break;
+            if (a < o + g.bytes) {
+                const uint64_t off = a - o, m = std::min(n, g.bytes - off);
+                HIP_OK(hipMemcpyAsync(dst, (const uint8_t *)g.p + off, m, hipMemcpyDeviceToHost, ctx->stream));
+                dst += m;
+                a += m;
+                n -= m;
+            }
+            o += g.bytes;
+        }
+        HIP_OK(hipStreamSynchronize(ctx->stream));
+    }
+
+    // the segments go through the slots as the plain all-to-all's messages do (no device staging
+    // copy: ranks sharing one GPU cannot afford a third copy of the descriptors)
     void alltoallv_dev_segs(const std::vector<std::vector<Seg>> &send, void *out,
                             const std::vector<std::vector<uint64_t>> &recv) override {
         need_ctx();
@@ -454,17 +475,29 @@ struct ShmComm final : Comm {
             for (const Seg &g : send[q]) sb[q] += g.bytes;
             for (const uint64_t n : recv[q]) rb[q] += n;
         }
-        uint64_t tot = 0;
-        for (uint64_t x : sb) tot += x;
-        DevBuf<uint8_t> st(tot ? tot : 1);
-        uint64_t o = 0;
-        for (int q = 0; q < world; ++q)
-            for (const Seg &g : send[q]) {
-                if (g.bytes) HIP_OK(hipMemcpyAsync(st.p + o, g.p, g.bytes, hipMemcpyDeviceToDevice, ctx->stream));
-                o += g.bytes;
+        const auto ro = offsets_of(rb.data(), world);
+        for (int s = 0; s < world; ++s) {
+            const int to = (rank + s) % world, from = (rank - s + world) % world;
+            uint8_t *dst = (uint8_t *)out + ro[from];
+            if (s == 0) {
+                if (sb[rank] != rb[rank]) throw Error(MCAAT_E_INVALID, "alltoallv_segs: self sizes differ");
+                for (const Seg &g : send[rank]) {
+                    if (g.bytes) HIP_OK(hipMemcpyAsync(dst, g.p, g.bytes, hipMemcpyDeviceToDevice, ctx->stream));
+                    dst += g.bytes;
+                }
+                HIP_OK(hipStreamSynchronize(ctx->stream));
+                continue;
             }
-        HIP_OK(hipStreamSynchronize(ctx->stream));
-        alltoallv_dev(st.p, sb.data(), out, rb.data());
+            const auto out_n = exchange(sb[to]);
+            uint64_t most = 0;
+            for (int r = 0; r < world; ++r) most = std::max(most, out_n[r]);
+            for (uint64_t c0 = 0; c0 < most; c0 += slot) {
+                if (sb[to] > c0) put_range(slot_of(rank), send[to], c0, std::min(slot, sb[to] - c0));
+                barrier();
+                if (rb[from] > c0) get(dst + c0, slot_of(from), std::min(slot, rb[from] - c0), true);
+                barrier();
+            }
+        }
     }
 };
 

@@ -54,6 +54,8 @@ void unwatch_stream(int device, hipStream_t s);
 hipStream_t alloc_stream();  // this thread's allocation stream (null: the host waits)
 void set_alloc_stream(hipStream_t s);
 void arena_stats(uint64_t *fences, uint64_t *waits);
+// device bytes handed out now, the most since the last reset, and the chunks held (this device)
+void arena_usage(uint64_t *in_use, uint64_t *peak, uint64_t *reserved, bool reset_peak);
 void arena_check(::mcaat_ctx *ctx, int64_t *out);  // mcaat_arena_check
 // allocations inside the scope are for work queued on stream s
 struct AllocStreamScope {

@@ -85,57 +85,154 @@ Owners owners_of(const mcaat_graph *g, const Comm &comm) {
 __device__ __forceinline__ bool bit_of(const uint64_t *bm, uint64_t i) { return (bm[i >> 6] >> (i & 63)) & 1; }
 
 // ---------------------------------------------------------------- Router
-// Records of W 64-bit words with a destination rank each go to their ranks in one all-to-all
-// (grouped by destination on the device: a block reserves its per-destination ranges with one
-// atomic per destination). perm keeps, for a request / response pattern, which record went out
-// at each send position, so the answers (in the order the owner received them) come back to
-// their requests. Order within a destination is not fixed; nothing here depends on it.
-__global__ void __launch_bounds__(kBlk) k_dest_count(const uint8_t *dest, uint64_t n, unsigned long long *cnt, int N) {
-    __shared__ unsigned int h[64];
-    for (int i = threadIdx.x; i < N; i += blockDim.x) h[i] = 0;
+// Request / message slots of W 64-bit words, each with a destination rank (kNoDest: an empty
+// slot), go to their ranks in one all-to-all. The grouping by destination is atomic-free and
+// deterministic: the slots are cut into one contiguous range per block, every block counts its
+// range's destinations with wave ballots, one small kernel turns the per-block counts into
+// per-block send offsets, and the scatter ranks each slot among its block's slots of the same
+// destination (ballot + mbcnt). The placement is stable (slot order within a destination), so the
+// answers, which come back in the order the owner received the requests, are gathered into their
+// slots by walking the same offsets again (no permutation array).
+constexpr uint8_t kNoDest = 0xFF;
+constexpr int kRBlocks = 1024;  // most blocks of a routing pass (the offsets kernel scans them in one block)
+
+// the slots' destination bytes, eight per thread at a time (each byte compared to d with a
+// zero-byte test): per-block counts per destination, no atomics
+__device__ __forceinline__ uint32_t bytes_equal(uint64_t x, uint32_t d) {
+    const uint64_t y = x ^ (0x0101010101010101ULL * d);
+    return (uint32_t)__popcll(~(((y & 0x7F7F7F7F7F7F7F7FULL) + 0x7F7F7F7F7F7F7F7FULL) | y | 0x7F7F7F7F7F7F7F7FULL));
+}
+__global__ void __launch_bounds__(kBlk) k_route_count(const uint8_t *dest, uint64_t n, uint64_t per, int N, uint32_t *cnt) {
+    __shared__ uint32_t h[64];
+    for (int q = threadIdx.x; q < N; q += blockDim.x) h[q] = 0;
     __syncthreads();
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) atomicAdd(&h[dest[i]], 1u);
+    const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = min(n, b0 + per);  // b0 is a multiple of 8
+    uint32_t c[64];
+    for (int q = 0; q < N; ++q) c[q] = 0;
+    for (uint64_t t = b0 + 8 * (uint64_t)threadIdx.x; t < b1; t += 8 * (uint64_t)kBlk) {
+        uint64_t x;
+        if (t + 8 <= b1) {
+            x = *(const uint64_t *)(dest + t);
+        } else {
+            x = ~0ULL;  // kNoDest padding
+            for (uint64_t i = t; i < b1; ++i) x = (x & ~(0xFFULL << (8 * (i - t)))) | ((uint64_t)dest[i] << (8 * (i - t)));
+        }
+        for (int q = 0; q < N; ++q) c[q] += bytes_equal(x, (uint32_t)q);
+    }
+    for (int q = 0; q < N; ++q) {
+        uint32_t v = c[q];
+        for (int o = 32; o; o >>= 1) v += __shfl_down(v, o);
+        if ((threadIdx.x & 63) == 0 && v) atomicAdd(&h[q], v);
+    }
     __syncthreads();
-    for (int i = threadIdx.x; i < N; i += blockDim.x)
-        if (h[i]) atomicAdd(&cnt[i], (unsigned long long)h[i]);
+    for (int q = threadIdx.x; q < N; q += blockDim.x) cnt[(uint64_t)blockIdx.x * N + q] = h[q];
 }
 
-__global__ void __launch_bounds__(kBlk) k_dest_scatter(const uint64_t *rec, int W, const uint8_t *dest, uint64_t n,
-                                                       const uint64_t *off, unsigned long long *cur, uint64_t *out,
-                                                       uint32_t *perm, int N) {
-    __shared__ unsigned int h[64];
-    __shared__ unsigned long long base[64];
-    for (uint64_t t0 = (uint64_t)blockIdx.x * blockDim.x; t0 < n; t0 += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t i = t0 + threadIdx.x;
-        for (int q = threadIdx.x; q < N; q += blockDim.x) h[q] = 0;
+// base[b * N + d] = where block b's slots for destination d start in the send buffer
+// (destinations back to back, blocks in order within one); tot[d] = all slots for d
+__global__ void __launch_bounds__(1024) k_route_offsets(const uint32_t *cnt, int G, int N, uint64_t *base, uint64_t *tot) {
+    __shared__ uint64_t sc[1024];
+    __shared__ uint64_t run;
+    if (threadIdx.x == 0) run = 0;
+    __syncthreads();
+    for (int d = 0; d < N; ++d) {
+        const uint64_t v = (int)threadIdx.x < G ? cnt[(uint64_t)threadIdx.x * N + d] : 0;
+        sc[threadIdx.x] = v;
         __syncthreads();
-        const int d = i < n ? dest[i] : 0;
-        const unsigned int r = i < n ? atomicAdd(&h[d], 1u) : 0u;
+        for (int o = 1; o < 1024; o <<= 1) {  // inclusive scan
+            const uint64_t x = threadIdx.x >= (unsigned)o ? sc[threadIdx.x - o] : 0;
+            __syncthreads();
+            sc[threadIdx.x] += x;
+            __syncthreads();
+        }
+        if ((int)threadIdx.x < G) base[(uint64_t)threadIdx.x * N + d] = run + sc[threadIdx.x] - v;
         __syncthreads();
-        for (int q = threadIdx.x; q < N; q += blockDim.x) base[q] = h[q] ? atomicAdd(&cur[q], (unsigned long long)h[q]) : 0ull;
-        __syncthreads();
-        if (i < n) {
-            const uint64_t pos = off[d] + base[d] + r;
-            for (int w = 0; w < W; ++w) out[pos * W + w] = rec[i * W + w];
-            if (perm) perm[pos] = (uint32_t)i;
+        if (threadIdx.x == 0) {
+            tot[d] = sc[1023];
+            run += sc[1023];
         }
         __syncthreads();
     }
 }
 
-__global__ void __launch_bounds__(kBlk) k_unperm(const uint64_t *ans, int W, const uint32_t *perm, uint64_t n, uint64_t *out) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += stride)
-        for (int w = 0; w < W; ++w) out[(uint64_t)perm[k] * W + w] = ans[k * W + w];
+// kRT slots per thread per tile: fewer barriers per slot; a slot's send position depends only on
+// the slots before it (stable within a destination), so the same walk also gathers the answers
+// back in slot order (GATHER: out[slot] = back[position]) without a permutation array
+constexpr int kRT = 8;
+// self: this rank; its records are placed straight into the receive buffer (self_buf, from
+// position self_pos0 of the send order) and its answers gathered from there, so the exchange
+// copies nothing for them
+template <bool GATHER>
+__global__ void __launch_bounds__(kBlk) k_route_place(const uint64_t *rec, int W, const uint8_t *dest, uint64_t n,
+                                                      uint64_t per, int N, const uint64_t *base, uint64_t *out,
+                                                      int self, uint64_t *self_buf, uint64_t self_pos0) {
+    __shared__ uint64_t run[64];
+    __shared__ uint32_t tile_tot[64];
+    __shared__ uint32_t wc[kRT * (kBlk / 64)][64];  // per (u, wave): counts, then exclusive prefixes
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = min(n, b0 + per);
+    if (threadIdx.x < N) run[threadIdx.x] = base[(uint64_t)blockIdx.x * N + threadIdx.x];
+    __syncthreads();
+    for (uint64_t t = b0; t < b1; t += (uint64_t)kBlk * kRT) {
+        int d[kRT];
+        uint32_t rank[kRT];
+#pragma unroll
+        for (int u = 0; u < kRT; ++u) {
+            const uint64_t i = t + (uint64_t)u * kBlk + threadIdx.x;
+            d[u] = i < b1 ? dest[i] : kNoDest;
+        }
+#pragma unroll
+        for (int u = 0; u < kRT; ++u) {
+            uint32_t c = 0;
+            rank[u] = 0;
+            for (int q = 0; q < N; ++q) {
+                const unsigned long long m = __ballot(d[u] == q);
+                if (d[u] == q) rank[u] = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                if (lane == q) c = (uint32_t)__popcll(m);
+            }
+            wc[u * (kBlk / 64) + wave][lane] = c;
+        }
+        __syncthreads();
+        // slot order is (u, wave, lane): exclusive prefix over (u, wave) per destination
+        if (threadIdx.x < N) {
+            uint32_t acc = 0;
+            for (int k = 0; k < kRT * (kBlk / 64); ++k) {
+                const uint32_t v = wc[k][threadIdx.x];
+                wc[k][threadIdx.x] = acc;
+                acc += v;
+            }
+            tile_tot[threadIdx.x] = acc;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kRT; ++u) {
+            if (d[u] == kNoDest) continue;
+            const uint64_t i = t + (uint64_t)u * kBlk + threadIdx.x;
+            const uint64_t pos = run[d[u]] + wc[u * (kBlk / 64) + wave][d[u]] + rank[u];
+            if (GATHER) {
+                const uint64_t *src = d[u] == self ? self_buf + (pos - self_pos0) * W : rec + pos * W;
+                for (int x = 0; x < W; ++x) out[i * W + x] = src[x];
+            } else {
+                uint64_t *dst = d[u] == self ? self_buf + (pos - self_pos0) * W : out + pos * W;
+                for (int x = 0; x < W; ++x) dst[x] = rec[i * W + x];
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < N) run[threadIdx.x] += tile_tot[threadIdx.x];
+        __syncthreads();
+    }
 }
 
 struct Routed {
     int W = 1;
-    uint64_t n = 0, n_in = 0, total = 0;  // sent, received, sent by all ranks
+    uint64_t n = 0, sent = 0, n_in = 0, total = 0;  // slots, records sent, received, sent by all ranks
     std::vector<uint64_t> out_cnt, in_cnt;
-    DevBuf<uint32_t> perm;
-    DevBuf<uint64_t> in;  // received records, sources in rank order
+    const uint8_t *dest = nullptr;  // the slots' destinations (reply: the caller keeps them alive)
+    DevBuf<uint64_t> base;          // per (block, destination) send offsets (reply walks them again)
+    uint64_t per = 0;
+    int G = 0;
+    std::vector<uint64_t> out_off, in_off;  // prefix sums of out_cnt / in_cnt
+    DevBuf<uint64_t> in;            // received records, sources in rank order
 };
 
 struct Router {
@@ -144,60 +241,81 @@ struct Router {
     uint64_t rounds = 0, records = 0;  // collectives and records moved (diagnostics)
     Router(mcaat_ctx *c, Comm &cm) : ctx(c), comm(cm) {}
 
-    void send(const uint64_t *rec, int W, const uint8_t *dest, uint64_t n, Routed &rt, bool keep_perm) {
+    // n slots (rec: n x W words; dest[i] a rank or kNoDest). keep: a reply follows (dest must
+    // stay valid until it). Records for this rank go straight to the receive buffer.
+    void send(const uint64_t *rec, int W, const uint8_t *dest, uint64_t n, Routed &rt, bool keep) {
         hipStream_t st = ctx->stream;
         const int N = comm.world, R = comm.rank;
-        if (n >= (1ULL << 32)) throw Error(MCAAT_E_CAPACITY, "shard router: 2^32 or more records in one exchange");
         rt.W = W;
         rt.n = n;
+        rt.dest = dest;
         rt.out_cnt.assign(N, 0);
-        DevBuf<unsigned long long> cnt(2 * N);
-        HIP_OK(hipMemsetAsync(cnt.p, 0, 16 * N, st));
+        rt.per = std::max<uint64_t>(kBlk * kRT, ((n + kRBlocks - 1) / kRBlocks + kBlk * kRT - 1) / (kBlk * kRT) * (kBlk * kRT));
+        rt.G = n ? (int)((n + rt.per - 1) / rt.per) : 0;
+        DevBuf<uint32_t> cnt((uint64_t)std::max(rt.G, 1) * N);
+        rt.base.alloc((uint64_t)std::max(rt.G, 1) * N);
+        DevBuf<uint64_t> tot(N);
         if (n) {
-            hipLaunchKernelGGL(k_dest_count, dim3(grid_for(n, kBlk, (unsigned)ctx->n_cu * 8)), dim3(kBlk), 0, st, dest, n,
-                               cnt.p, N);
+            hipLaunchKernelGGL(k_route_count, dim3(rt.G), dim3(kBlk), 0, st, dest, n, rt.per, N, cnt.p);
             LAUNCH_OK();
-            d2h(ctx, rt.out_cnt.data(), cnt.p, 8 * N);
-        }
-        std::vector<uint64_t> off(N + 1, 0);
-        for (int q = 0; q < N; ++q) off[q + 1] = off[q] + rt.out_cnt[q];
-        DevBuf<uint64_t> sendb((n ? n : 1) * W);
-        if (keep_perm) rt.perm.alloc(n ? n : 1);
-        if (n) {
-            DevBuf<uint64_t> doff(N);
-            HIP_OK(hipMemcpyAsync(doff.p, off.data(), 8 * N, hipMemcpyHostToDevice, st));
-            hipLaunchKernelGGL(k_dest_scatter, dim3(grid_for(n, kBlk, (unsigned)ctx->n_cu * 8)), dim3(kBlk), 0, st, rec, W,
-                               dest, n, doff.p, cnt.p + N, sendb.p, keep_perm ? rt.perm.p : nullptr, N);
+            hipLaunchKernelGGL(k_route_offsets, dim3(1), dim3(1024), 0, st, (const uint32_t *)cnt.p, rt.G, N, rt.base.p, tot.p);
             LAUNCH_OK();
+            d2h(ctx, rt.out_cnt.data(), tot.p, 8 * N);
         }
+        rt.sent = 0;
+        for (uint64_t x : rt.out_cnt) rt.sent += x;
         const std::vector<uint64_t> mat = comm.allgather_vec(rt.out_cnt);
         rt.in_cnt.assign(N, 0);
         rt.n_in = rt.total = 0;
-        for (int s = 0; s < N; ++s) {
-            rt.in_cnt[s] = mat[(uint64_t)s * N + R];
-            rt.n_in += rt.in_cnt[s];
-            for (int d = 0; d < N; ++d) rt.total += mat[(uint64_t)s * N + d];
+        for (int s2 = 0; s2 < N; ++s2) {
+            rt.in_cnt[s2] = mat[(uint64_t)s2 * N + R];
+            rt.n_in += rt.in_cnt[s2];
+            for (int d = 0; d < N; ++d) rt.total += mat[(uint64_t)s2 * N + d];
+        }
+        rt.out_off.assign(N + 1, 0);
+        rt.in_off.assign(N + 1, 0);
+        for (int q = 0; q < N; ++q) {
+            rt.out_off[q + 1] = rt.out_off[q] + rt.out_cnt[q];
+            rt.in_off[q + 1] = rt.in_off[q] + rt.in_cnt[q];
         }
         rt.in.alloc((rt.n_in ? rt.n_in : 1) * W);
-        std::vector<uint64_t> sb(N), rb(N);
-        for (int q = 0; q < N; ++q) sb[q] = 8ULL * W * rt.out_cnt[q], rb[q] = 8ULL * W * rt.in_cnt[q];
+        // the send buffer has a hole where this rank's own records would be (they go to rt.in)
+        DevBuf<uint64_t> sendb((N > 1 && rt.sent ? rt.sent : 1) * W);
+        if (rt.sent) {
+            hipLaunchKernelGGL(k_route_place<false>, dim3(rt.G), dim3(kBlk), 0, st, rec, W, dest, n, rt.per, N,
+                               (const uint64_t *)rt.base.p, sendb.p, R, rt.in.p + rt.in_off[R] * W, rt.out_off[R]);
+            LAUNCH_OK();
+        }
+        if (!keep) rt.base.release();
+        std::vector<uint64_t> sb(N), rb(N), so(N), ro(N);
+        for (int q = 0; q < N; ++q) {
+            sb[q] = 8ULL * W * rt.out_cnt[q], rb[q] = 8ULL * W * rt.in_cnt[q];
+            so[q] = 8ULL * W * rt.out_off[q], ro[q] = 8ULL * W * rt.in_off[q];
+        }
+        sb[R] = rb[R] = 0;  // placed already
         HIP_OK(hipStreamSynchronize(st));
-        if (rt.total) comm.alltoallv_dev(sendb.p, sb.data(), rt.in.p, rb.data());
+        if (N > 1) comm.alltoallv_dev(sendb.p, sb.data(), rt.in.p, rb.data(), so.data(), ro.data());
         ++rounds;
-        records += n;
+        records += rt.sent;
     }
-    // answers (Wa words per received record, in received order) back to the requests: out[i * Wa ..]
-    void reply(Routed &rt, const uint64_t *ans, int Wa, uint64_t *out) {
+    // answers (Wa words per received record, in received order) back to their slots: out[slot * Wa ..]
+    // (slots without a request keep what out held); this rank's own answers are read in place
+    void reply(Routed &rt, uint64_t *ans, int Wa, uint64_t *out) {
         hipStream_t st = ctx->stream;
-        const int N = comm.world;
-        DevBuf<uint64_t> back((rt.n ? rt.n : 1) * Wa);
-        std::vector<uint64_t> sb(N), rb(N);
-        for (int q = 0; q < N; ++q) sb[q] = 8ULL * Wa * rt.in_cnt[q], rb[q] = 8ULL * Wa * rt.out_cnt[q];
+        const int N = comm.world, R = comm.rank;
+        DevBuf<uint64_t> back((N > 1 && rt.sent ? rt.sent : 1) * Wa);
+        std::vector<uint64_t> sb(N), rb(N), so(N), ro(N);
+        for (int q = 0; q < N; ++q) {
+            sb[q] = 8ULL * Wa * rt.in_cnt[q], rb[q] = 8ULL * Wa * rt.out_cnt[q];
+            so[q] = 8ULL * Wa * rt.in_off[q], ro[q] = 8ULL * Wa * rt.out_off[q];
+        }
+        sb[R] = rb[R] = 0;  // read in place
         HIP_OK(hipStreamSynchronize(st));
-        if (rt.total) comm.alltoallv_dev(ans, sb.data(), back.p, rb.data());
-        if (rt.n) {
-            hipLaunchKernelGGL(k_unperm, dim3(grid_for(rt.n, kBlk, (unsigned)ctx->n_cu * 16)), dim3(kBlk), 0, st,
-                               (const uint64_t *)back.p, Wa, (const uint32_t *)rt.perm.p, rt.n, out);
+        if (N > 1) comm.alltoallv_dev(ans, sb.data(), back.p, rb.data(), so.data(), ro.data());
+        if (rt.sent) {
+            hipLaunchKernelGGL(k_route_place<true>, dim3(rt.G), dim3(kBlk), 0, st, (const uint64_t *)back.p, Wa, rt.dest,
+                               rt.n, rt.per, N, (const uint64_t *)rt.base.p, out, R, ans + rt.in_off[R] * Wa,
+                               rt.out_off[R]);
             LAUNCH_OK();
         }
         HIP_OK(hipStreamSynchronize(st));
@@ -337,33 +455,22 @@ __global__ void __launch_bounds__(kBlk) k_sh_filter(const uint16_t *mult, const 
     block_add(cnt + 1, low);
 }
 
-// window requests: every filter-valid edge with out-edges asks the 16 filtered bits at its
-// target node's first edge; filter-valid edges above the threshold ask their predecessor group's
-// (ChunkStartNodes' in-degree); src = local index | 1 << 63 for the in-window
+// window requests, two slots per local edge of the chunk [a0, a1): slot 2j asks the 16
+// filtered bits at its target node's first edge (a filter-valid edge with out-edges), slot 2j+1
+// its predecessor group's (a filter-valid edge above the threshold: ChunkStartNodes' in-degree)
 __global__ void __launch_bounds__(kBlk) k_win_req(const uint64_t *post, const uint16_t *mult, const uint64_t *out_info,
-                                                  const uint64_t *in_info, uint64_t a0, uint64_t n, uint64_t thr, Owners o,
-                                                  uint64_t *q, uint8_t *dest, uint64_t *src, unsigned long long *cur) {
+                                                  const uint64_t *in_info, uint64_t a0, uint64_t a1, uint64_t thr, Owners o,
+                                                  uint64_t *q, uint8_t *dest) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i0 = a0 + (uint64_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
-        const uint64_t i = i0 + threadIdx.x;
-        const bool pv = i < n && bit_of(post, i);
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < a1 - a0; j += stride) {
+        const uint64_t i = a0 + j;
+        const bool pv = bit_of(post, i);
         const uint64_t oi = pv ? out_info[i] : 0;
-        const bool wo = pv && ((oi >> kIdxBits) & 0xF);
         const uint64_t ii = pv && (uint64_t)mult[i] > thr ? in_info[i] : 0;
-        const bool wi = (ii >> kIdxBits) != 0;
-        unsigned long long m;
-        uint64_t at = wave_reserve(wo, cur, m);
-        if (wo) {
-            q[at] = oi & kIdM;
-            dest[at] = (uint8_t)owner_of_id(o, oi & kIdM);
-            src[at] = i;
-        }
-        at = wave_reserve(wi, cur, m);
-        if (wi) {
-            q[at] = ii & kIdM;
-            dest[at] = (uint8_t)owner_of_id(o, ii & kIdM);
-            src[at] = i | (1ULL << 63);
-        }
+        q[2 * j] = oi & kIdM;
+        dest[2 * j] = (oi >> kIdxBits) & 0xF ? (uint8_t)owner_of_id(o, oi & kIdM) : kNoDest;
+        q[2 * j + 1] = ii & kIdM;
+        dest[2 * j + 1] = (ii >> kIdxBits) ? (uint8_t)owner_of_id(o, ii & kIdM) : kNoDest;
     }
 }
 
@@ -385,60 +492,47 @@ __global__ void __launch_bounds__(kBlk) k_win_ans(const uint64_t *bm, uint64_t n
 }
 
 // the answers: kind (filtered out-window), unary successor, candidates (in-window)
-__global__ void __launch_bounds__(kBlk) k_win_apply(const uint64_t *src, const uint64_t *ans, uint64_t m,
+__global__ void __launch_bounds__(kBlk) k_win_apply(const uint8_t *dest, const uint64_t *ans, uint64_t a0, uint64_t a1,
                                                     const uint64_t *out_info, const uint64_t *in_info, uint64_t id_lo,
-                                                    uint8_t *kind, uint64_t *nx, uint64_t *cand, unsigned long long *ncand) {
+                                                    uint8_t *kind, uint64_t *nx, uint64_t *cbits) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x; j0 < m; j0 += stride) {
-        const uint64_t j = j0 + threadIdx.x;
-        bool c = false;
-        uint64_t e = 0;
-        if (j < m) {
-            const uint64_t s = src[j], i = s & ~(1ULL << 63);
-            const uint32_t b = (uint32_t)ans[j];
-            if (!(s >> 63)) {
-                const uint64_t oi = out_info[i];
-                const int cnt = __popc((unsigned)(oi >> kIdxBits) & 0xF);
-                const uint32_t pm = b & ((1u << cnt) - 1);
-                kind[i] = (uint8_t)pm;  // the flag bits come later (k_flag_apply)
-                if (__popc(pm) == 1) nx[i] = (oi & kIdM) + (uint64_t)(__ffs(pm) - 1);
-            } else {
-                const uint64_t ii = in_info[i], l = ii & kIdM;
-                const uint32_t in = b & (uint32_t)((ii >> kIdxBits) & 0xFFFF);
-                e = id_lo + i;
-                const bool self = e >= l && e - l < 16 && ((in >> (e - l)) & 1);
-                c = __popc(in) >= 2 && !self;  // _IncomingNotEqualToCurrentNode, indegree >= 2
-            }
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < a1 - a0; j += stride) {
+        const uint64_t i = a0 + j;
+        if (dest[2 * j] != kNoDest) {
+            const uint64_t oi = out_info[i];
+            const int cnt = __popc((unsigned)(oi >> kIdxBits) & 0xF);
+            const uint32_t pm = (uint32_t)ans[2 * j] & ((1u << cnt) - 1);
+            kind[i] = (uint8_t)pm;  // the flag bits come later (k_flag_apply)
+            if (__popc(pm) == 1) nx[i] = (oi & kIdM) + (uint64_t)(__ffs(pm) - 1);
         }
-        unsigned long long mk;
-        const uint64_t at = wave_reserve(c, ncand, mk);
-        if (c) cand[at] = e;
+        if (dest[2 * j + 1] != kNoDest) {
+            const uint64_t ii = in_info[i], l = ii & kIdM, e = id_lo + i;
+            const uint32_t in = (uint32_t)ans[2 * j + 1] & (uint32_t)((ii >> kIdxBits) & 0xFFFF);
+            const bool self = e >= l && e - l < 16 && ((in >> (e - l)) & 1);
+            if (__popc(in) >= 2 && !self)  // _IncomingNotEqualToCurrentNode, indegree >= 2
+                atomicOr((unsigned long long *)&cbits[i >> 6], 1ULL << (i & 63));
+        }
     }
 }
 
 // post-filter tips that are not seeds (counts[2]); predecessor flags as messages to the
-// successors: id | 1 << 62 from a unary edge, id | 1 << 63 from a branch edge
+// successors, four slots per local edge: id | 1 << 62 from a unary edge, id | 1 << 63 from a branch
 __global__ void __launch_bounds__(kBlk) k_flag_msgs(const uint64_t *post, const uint64_t *seed, const uint8_t *kind,
-                                                    const uint64_t *out_info, uint64_t a0, uint64_t n, Owners o, uint64_t *q,
-                                                    uint8_t *dest, unsigned long long *cur, unsigned long long *cnt) {
+                                                    const uint64_t *out_info, uint64_t a0, uint64_t a1, Owners o,
+                                                    uint64_t *q, uint8_t *dest, unsigned long long *cnt) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     unsigned long long tpf = 0;
-    for (uint64_t i0 = a0 + (uint64_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
-        const uint64_t i = i0 + threadIdx.x;
-        const bool pv = i < n && bit_of(post, i);
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < a1 - a0; j += stride) {
+        const uint64_t i = a0 + j;
+        const bool pv = bit_of(post, i);
         const uint32_t pm = pv ? kind[i] & 0xF : 0;
         const int od = __popc(pm);
         if (pv && od == 0 && !bit_of(seed, i)) ++tpf;
         const uint64_t lo = pv ? out_info[i] & kIdM : 0;
         for (int b = 0; b < 4; ++b) {
-            const bool f = (pm >> b) & 1;
-            unsigned long long mk;
-            const uint64_t at = wave_reserve(f, cur, mk);
-            if (f) {
-                const uint64_t y = lo + b;
-                q[at] = y | (od == 1 ? (1ULL << 62) : (1ULL << 63));
-                dest[at] = (uint8_t)owner_of_id(o, y);
-            }
+            const uint64_t y = lo + b;
+            q[4 * j + b] = y | (od == 1 ? (1ULL << 62) : (1ULL << 63));
+            dest[4 * j + b] = (pm >> b) & 1 ? (uint8_t)owner_of_id(o, y) : kNoDest;
         }
     }
     block_add(cnt + 2, tpf);
@@ -460,10 +554,11 @@ __global__ void __launch_bounds__(kBlk) k_flag_apply(const uint64_t *q, uint64_t
 // the non-unary edges (dead ends: removed iff a seed; branches unresolved); lists of rulers
 // and branches (local indices)
 __global__ void __launch_bounds__(kBlk) k_prep(const uint64_t *post, const uint64_t *seed, uint8_t *kind, uint8_t *st,
-                                               uint64_t n, uint64_t id_lo, uint64_t rmask, uint64_t *rl,
-                                               unsigned long long *nr, uint64_t *bl, unsigned long long *nb) {
+                                               uint64_t n, uint64_t id_lo, uint64_t rmask, uint64_t *rbits,
+                                               uint64_t *bbits) {
+    const int lane = threadIdx.x & 63;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
+    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < ((n + 63) & ~63ULL); i0 += stride) {
         const uint64_t i = i0 + threadIdx.x;
         const bool pv = i < n && bit_of(post, i);
         const uint8_t k = pv ? kind[i] : 0;
@@ -474,93 +569,102 @@ __global__ void __launch_bounds__(kBlk) k_prep(const uint64_t *post, const uint6
             if (ruler) kind[i] = k | kRuler;
             st[i] = od == 0 ? (bit_of(seed, i) ? kStRem : kStSurv) : kStUnk;
         }
-        unsigned long long mk;
-        uint64_t at = wave_reserve(ruler, nr, mk);
-        if (ruler) rl[at] = i;
-        at = wave_reserve(branch, nb, mk);
-        if (branch) bl[at] = i;
+        const unsigned long long rm = __ballot(ruler), bm = __ballot(branch);
+        if (lane == 0) {
+            rbits[i >> 6] = rm;
+            bbits[i >> 6] = bm;
+        }
     }
 }
 
-// walkers: {ruler, edge, tortoise, power << 32 | lam}; results: {ruler, reached, 0, 1 << 63}
-// (reached: a non-unary edge, kRef | a ruler, or kNo on a ruler-less unary cycle)
+// the set bits of a local bitmap as a list of local indices (wpre: exclusive prefix of the words' popcounts)
+__global__ void __launch_bounds__(kBlk) k_bits_list(const uint64_t *bm, uint64_t nw, const uint64_t *wpre, uint64_t *out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nw * 64; i += stride) {
+        const uint64_t w = i >> 6, word = bm[w];
+        if ((word >> (i & 63)) & 1) out[wpre[w] + __popcll(word & ((1ULL << (i & 63)) - 1))] = i;
+    }
+}
+
+// walkers: {ruler, edge}; results: {ruler | 1 << 63, reached} (reached: a non-unary edge, kRef |
+// a ruler, or kNo on a unary cycle). A walker claims each non-ruler unary edge it passes by
+// swapping its successor word for kOwn | ruler (compare-and-swap: one claimer per edge); a
+// walker that meets an edge claimed by another ruler r1 stops with kRef | r1 (both chains go on
+// identically from there, so r1's terminal is its terminal), one that meets its own claim has
+// gone round a unary cycle without a ruler (kNo: survives). The claims are also the chain
+// edges' owners for the removal, so there is no owner array and merging chains walk once.
 constexpr uint64_t kResult = 1ULL << 63;
+constexpr uint64_t kOwn = 1ULL << 61;
+__device__ __forceinline__ bool is_claim(uint64_t v) { return v < kPad && !(v & kRef) && (v & kOwn); }
 
 __global__ void __launch_bounds__(kBlk) k_walk_init(const uint64_t *rl, uint64_t nr, const uint64_t *nx, uint64_t id_lo,
                                                     uint64_t *w) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nr; j += stride) {
         const uint64_t i = rl[j];
-        w[4 * j] = id_lo + i;
-        w[4 * j + 1] = nx[i];
-        w[4 * j + 2] = id_lo + i;
-        w[4 * j + 3] = (1ULL << 32) | 1;
+        w[2 * j] = id_lo + i;
+        w[2 * j + 1] = nx[i];
     }
 }
 
-// one round: results land in their rulers' jump words (nx of the ruler, no longer read: a walk
-// stops at a ruler before reading its successor); walkers advance over this rank's edges and
-// leave for the owner of the next one (Brent's cycle check as the one-GPU k_peel_walk)
-__global__ void __launch_bounds__(kBlk) k_walk(const uint64_t *in, uint64_t m, const uint8_t *kind, uint64_t *nx,
-                                               uint64_t *own, Owners o, uint64_t *out, uint8_t *dest,
-                                               unsigned long long *cur) {
+// one round: results land in their rulers' jump words (nx of the ruler: a walk stops at a ruler
+// before reading its word); walkers advance over this rank's edges and leave for the owner of
+// the next one
+__global__ void __launch_bounds__(kBlk) k_walk(const uint64_t *in, uint64_t m, const uint8_t *kind, uint64_t *nx, Owners o,
+                                               uint64_t *out, uint8_t *dest) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x; j0 < m; j0 += stride) {
         const uint64_t j = j0 + threadIdx.x;
         bool emit = false;
-        uint64_t r = 0, x = 0, tort = 0, pl = 0;
+        uint64_t r = 0, x = 0;
         int to = 0;
         if (j < m) {
-            r = in[4 * j];
-            x = in[4 * j + 1];
-            tort = in[4 * j + 2];
-            pl = in[4 * j + 3];
-            if (pl & kResult) {
-                nx[r - o.id_lo] = x;
+            r = in[2 * j];
+            x = in[2 * j + 1];
+            if (r & kResult) {
+                nx[(r & kIdM) - o.id_lo] = x;
             } else {
-                uint64_t power = pl >> 32, lam = pl & 0xFFFFFFFFu;
                 for (;;) {
                     if (x < o.id_lo || x >= o.id_lo + o.n) {  // leaves for the owner of x
                         emit = true;
                         to = owner_of_id(o, x);
-                        pl = (power << 32) | lam;
                         break;
                     }
                     const uint64_t li = x - o.id_lo;
                     const uint8_t k = kind[li];
                     uint64_t res = 0;
                     bool done = true;
-                    if (__popc(k & 0xF) != 1) res = x;
-                    else if (k & kRuler) res = kRef | x;
-                    else if (x == tort) res = kNo;
-                    else done = false;
+                    if (__popc(k & 0xF) != 1) {
+                        res = x;
+                    } else if (k & kRuler) {
+                        res = kRef | x;
+                    } else {
+                        uint64_t v = nx[li];
+                        if (!is_claim(v)) {
+                            const uint64_t prev = atomicCAS((unsigned long long *)&nx[li], v, kOwn | r);
+                            if (prev == v) {
+                                x = v;  // claimed: on to the successor
+                                done = false;
+                            } else {
+                                v = prev;
+                            }
+                        }
+                        if (done) res = (v & kIdM) == r ? kNo : (kRef | (v & kIdM));
+                    }
                     if (done) {
                         emit = true;
                         to = owner_of_id(o, r);
+                        r |= kResult;
                         x = res;
-                        tort = 0;
-                        pl = kResult;
                         break;
                     }
-                    own[li] = r;
-                    if (power == lam) {
-                        tort = x;
-                        power <<= 1;
-                        lam = 0;
-                    }
-                    x = nx[li];
-                    ++lam;
                 }
             }
         }
-        unsigned long long mk;
-        const uint64_t at = wave_reserve(emit, cur, mk);
-        if (emit) {
-            out[4 * at] = r;
-            out[4 * at + 1] = x;
-            out[4 * at + 2] = tort;
-            out[4 * at + 3] = pl;
-            dest[at] = (uint8_t)to;
+        if (j < m) {  // one output slot per input record
+            out[2 * j] = r;
+            out[2 * j + 1] = x;
+            dest[j] = emit ? (uint8_t)to : kNoDest;
         }
     }
 }
@@ -579,104 +683,71 @@ __global__ void __launch_bounds__(kBlk) k_jump_ans(const uint64_t *q, uint64_t m
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += stride) ans[j] = nx[q[j] - id_lo];
 }
-// the new jumps; the rulers still pointing at a ruler stay listed
+// the new jumps; keep[j]: ruler j still points at a ruler
 __global__ void __launch_bounds__(kBlk) k_jump_apply(const uint64_t *al, uint64_t na, const uint64_t *a, uint64_t *nx,
-                                                     uint64_t *al2, unsigned long long *na2) {
+                                                     uint8_t *keep) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x; j0 < na; j0 += stride) {
-        const uint64_t j = j0 + threadIdx.x;
-        bool keep = false;
-        if (j < na) {
-            nx[al[j]] = a[j];
-            keep = a[j] != kNo && (a[j] & kRef);
-        }
-        unsigned long long mk;
-        const uint64_t at = wave_reserve(keep, na2, mk);
-        if (keep) al2[at] = al[j];
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < na; j += stride) {
+        nx[al[j]] = a[j];
+        keep[j] = a[j] != kNo && (a[j] & kRef);
     }
 }
 __global__ void __launch_bounds__(kBlk) k_jump_cycle(const uint64_t *al, uint64_t na, uint64_t *nx) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < na; j += stride) nx[al[j]] = kNo;
 }
-// the rulers whose jump still points at a ruler (kept in `al`) after the walks
-__global__ void __launch_bounds__(kBlk) k_active_rulers(const uint64_t *rl, uint64_t nr, const uint64_t *nx, uint64_t *al,
-                                                        unsigned long long *na) {
+// the rulers whose jump still points at a ruler after the walks
+__global__ void __launch_bounds__(kBlk) k_active_rulers(const uint64_t *rl, uint64_t nr, const uint64_t *nx, uint8_t *keep) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x; j0 < nr; j0 += stride) {
-        const uint64_t j = j0 + threadIdx.x;
-        const bool a = j < nr && nx[rl[j]] != kNo && (nx[rl[j]] & kRef);
-        unsigned long long mk;
-        const uint64_t at = wave_reserve(a, na, mk);
-        if (a) al[at] = rl[j];
-    }
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nr; j += stride)
+        keep[j] = nx[rl[j]] != kNo && (nx[rl[j]] & kRef);
 }
 
-// the references of branch successors: request y (4 slots per branch, kNo past its successors)
+// the references of branch successors: request y, four slots per branch
 __global__ void __launch_bounds__(kBlk) k_bref_req(const uint64_t *bl, uint64_t nb, const uint8_t *kind,
-                                                   const uint64_t *out_info, Owners o, uint64_t *q, uint8_t *dest,
-                                                   uint64_t *src, unsigned long long *cur) {
+                                                   const uint64_t *out_info, Owners o, uint64_t *q, uint8_t *dest) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x; j0 < nb; j0 += stride) {
-        const uint64_t j = j0 + threadIdx.x;
-        const uint32_t pm = j < nb ? kind[bl[j]] & 0xF : 0;
-        const uint64_t lo = j < nb ? out_info[bl[j]] & kIdM : 0;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nb; j += stride) {
+        const uint32_t pm = kind[bl[j]] & 0xF;
+        const uint64_t lo = out_info[bl[j]] & kIdM;
         for (int b = 0; b < 4; ++b) {
-            const bool f = (pm >> b) & 1;
-            unsigned long long mk;
-            const uint64_t at = wave_reserve(f, cur, mk);
-            if (f) {
-                q[at] = lo + b;
-                dest[at] = (uint8_t)owner_of_id(o, lo + b);
-                src[at] = 4 * j + b;
-            }
+            q[4 * j + b] = lo + b;
+            dest[4 * j + b] = (pm >> b) & 1 ? (uint8_t)owner_of_id(o, lo + b) : kNoDest;
         }
     }
 }
 // a successor's reference: itself (non-unary), its ruler's terminal (a ruler), or kRef | the
 // ruler whose walk passed it (kNo: none did — a ruler-less unary cycle)
 __global__ void __launch_bounds__(kBlk) k_bref_ans(const uint64_t *q, uint64_t m, const uint8_t *kind, const uint64_t *nx,
-                                                   const uint64_t *own, uint64_t id_lo, uint64_t *ans) {
+                                                   uint64_t id_lo, uint64_t *ans) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += stride) {
         const uint64_t y = q[j], li = y - id_lo;
         const uint8_t k = kind[li];
+        const uint64_t v = nx[li];
         if (__popc(k & 0xF) != 1) ans[j] = y;
-        else if (k & kRuler) ans[j] = nx[li];
-        else ans[j] = own[li] == kNo ? kNo : (kRef | own[li]);
+        else if (k & kRuler) ans[j] = v;
+        else ans[j] = is_claim(v) ? (kRef | (v & kIdM)) : kNo;  // unclaimed: a unary cycle without a ruler
     }
 }
-__global__ void __launch_bounds__(kBlk) k_scatter_ref(const uint64_t *src, const uint64_t *a, uint64_t m, uint64_t *ref) {
+// second step for successors claimed by a ruler's walk: that ruler's terminal (slot per reference)
+__global__ void __launch_bounds__(kBlk) k_bref_req2(const uint64_t *ref, uint64_t nslots, Owners o, uint64_t *q, uint8_t *dest) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += stride) ref[src[j]] = a[j];
-}
-// second step for successors owned by a passing ruler: that ruler's terminal
-__global__ void __launch_bounds__(kBlk) k_bref_req2(const uint64_t *ref, uint64_t nslots, Owners o, uint64_t *q, uint8_t *dest,
-                                                    uint64_t *src, unsigned long long *cur) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x; j0 < nslots; j0 += stride) {
-        const uint64_t j = j0 + threadIdx.x;
-        const bool f = j < nslots && ref[j] < kPad && (ref[j] & kRef);
-        unsigned long long mk;
-        const uint64_t at = wave_reserve(f, cur, mk);
-        if (f) {
-            q[at] = ref[j] & kIdM;
-            dest[at] = (uint8_t)owner_of_id(o, ref[j] & kIdM);
-            src[at] = j;
-        }
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nslots; j += stride) {
+        const bool f = ref[j] < kPad && (ref[j] & kRef);
+        q[j] = ref[j] & kIdM;
+        dest[j] = f ? (uint8_t)owner_of_id(o, ref[j] & kIdM) : kNoDest;
     }
 }
 
 // branch resolution: a branch with a surviving reference (kNo: a unary cycle) survives at once;
 // otherwise its references' states are requested
 __global__ void __launch_bounds__(kBlk) k_res_req(const uint64_t *bl, const uint64_t *ref, uint64_t nb, uint8_t *st,
-                                                  Owners o, uint64_t *q, uint8_t *dest, uint64_t *src,
-                                                  unsigned long long *cur, unsigned long long *changed) {
+                                                  Owners o, uint64_t *q, uint8_t *dest, unsigned long long *changed) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     unsigned long long ch = 0;
-    for (uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x; j0 < nb; j0 += stride) {
-        const uint64_t j = j0 + threadIdx.x;
-        bool unk = j < nb && st[bl[j]] == kStUnk;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nb; j += stride) {
+        bool unk = st[bl[j]] == kStUnk;
         if (unk) {
             for (int b = 0; b < 4; ++b)
                 if (ref[4 * j + b] == kNo) unk = false;
@@ -686,15 +757,9 @@ __global__ void __launch_bounds__(kBlk) k_res_req(const uint64_t *bl, const uint
             }
         }
         for (int b = 0; b < 4; ++b) {
-            const uint64_t t = unk ? ref[4 * j + b] : kPad;
-            const bool f = t != kPad;
-            unsigned long long mk;
-            const uint64_t at = wave_reserve(f, cur, mk);
-            if (f) {
-                q[at] = t;
-                dest[at] = (uint8_t)owner_of_id(o, t);
-                src[at] = 4 * j + b;
-            }
+            const uint64_t t = ref[4 * j + b];
+            q[4 * j + b] = t;
+            dest[4 * j + b] = unk && t != kPad ? (uint8_t)owner_of_id(o, t) : kNoDest;
         }
     }
     block_add(changed, ch);
@@ -703,27 +768,24 @@ __global__ void __launch_bounds__(kBlk) k_st_ans(const uint64_t *q, uint64_t m, 
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += stride) ans[j] = st[q[j] - id_lo];
 }
-// per branch slot: the state of its reference (written by the answers; kStRem for padding)
-__global__ void __launch_bounds__(kBlk) k_res_apply(const uint64_t *bl, uint64_t nb, const uint8_t *slot_st, uint8_t *st,
-                                                    unsigned long long *changed) {
+// per branch slot: the state of its reference (a[slot], written by the answers; slots without a
+// request read kStRem: padding never keeps a branch alive)
+__global__ void __launch_bounds__(kBlk) k_res_apply(const uint64_t *bl, uint64_t nb, const uint64_t *a, const uint8_t *dest,
+                                                    uint8_t *st, unsigned long long *changed) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     unsigned long long ch = 0;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nb; j += stride) {
         if (st[bl[j]] != kStUnk) continue;
         bool all_rem = true, any_surv = false;
         for (int b = 0; b < 4; ++b) {
-            const uint8_t s = slot_st[4 * j + b];
-            if (s == kStSurv) any_surv = true;
-            if (s != kStRem) all_rem = false;
+            const uint8_t sv = dest[4 * j + b] == kNoDest ? kStRem : (uint8_t)a[4 * j + b];
+            if (sv == kStSurv) any_surv = true;
+            if (sv != kStRem) all_rem = false;
         }
         if (any_surv) { st[bl[j]] = kStSurv; ++ch; }
         else if (all_rem) { st[bl[j]] = kStRem; ++ch; }
     }
     block_add(changed, ch);
-}
-__global__ void __launch_bounds__(kBlk) k_slot_st(const uint64_t *src, const uint64_t *a, uint64_t m, uint8_t *slot_st) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += stride) slot_st[src[j]] = (uint8_t)a[j];
 }
 
 // removal of the non-unary edges resolved kRem (valid starts as the filtered bitmap)
@@ -738,34 +800,25 @@ __global__ void __launch_bounds__(kBlk) k_rm_nonunary(const uint64_t *post, cons
         if (lane == 0) valid[w] = post[w] & ~m;
     }
 }
-// rulers: the state of their terminal (kNo: survive)
+// rulers: the state of their terminal (kNo: survive), one slot per ruler
 __global__ void __launch_bounds__(kBlk) k_term_req(const uint64_t *rl, uint64_t nr, const uint64_t *nx, Owners o, uint64_t *q,
-                                                   uint8_t *dest, uint64_t *src, unsigned long long *cur) {
+                                                   uint8_t *dest) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x; j0 < nr; j0 += stride) {
-        const uint64_t j = j0 + threadIdx.x;
-        const uint64_t t = j < nr ? nx[rl[j]] : kNo;
-        const bool f = t != kNo;
-        unsigned long long mk;
-        const uint64_t at = wave_reserve(f, cur, mk);
-        if (f) {
-            q[at] = t;
-            dest[at] = (uint8_t)owner_of_id(o, t);
-            src[at] = rl[j];
-        }
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nr; j += stride) {
+        const uint64_t t = nx[rl[j]];
+        q[j] = t;
+        dest[j] = t != kNo ? (uint8_t)owner_of_id(o, t) : kNoDest;
     }
 }
-// removed rulers: their own valid bit cleared, their ids listed
-__global__ void __launch_bounds__(kBlk) k_rm_rulers(const uint64_t *src, const uint64_t *a, uint64_t m, uint64_t id_lo,
-                                                    uint64_t *valid, uint64_t *rm, unsigned long long *nrm) {
+// removed rulers (terminal resolved kRem): their own valid bit cleared, flagged for the list
+__global__ void __launch_bounds__(kBlk) k_rm_rulers(const uint64_t *rl, uint64_t nr, const uint64_t *a, const uint8_t *dest,
+                                                    uint64_t *valid, uint64_t id_lo, uint64_t *gid, uint8_t *flag) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x; j0 < m; j0 += stride) {
-        const uint64_t j = j0 + threadIdx.x;
-        const bool r = j < m && a[j] == kStRem;
-        if (r) atomicAnd((unsigned long long *)&valid[src[j] >> 6], ~(1ULL << (src[j] & 63)));
-        unsigned long long mk;
-        const uint64_t at = wave_reserve(r, nrm, mk);
-        if (r) rm[at] = id_lo + src[j];
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nr; j += stride) {
+        const bool r = dest[j] != kNoDest && a[j] == kStRem;
+        if (r) atomicAnd((unsigned long long *)&valid[rl[j] >> 6], ~(1ULL << (rl[j] & 63)));
+        gid[j] = id_lo + rl[j];
+        flag[j] = r;
     }
 }
 // open-addressing set of the removed rulers (every rank holds all of them)
@@ -777,8 +830,8 @@ __global__ void __launch_bounds__(kBlk) k_set_build(const uint64_t *ids, uint64_
             if (prev == kNo || prev == ids[j]) break;
         }
 }
-// non-ruler unary edges passed by a removed ruler's walk
-__global__ void __launch_bounds__(kBlk) k_rm_chains(const uint64_t *post, const uint8_t *kind, const uint64_t *own, uint64_t n,
+// non-ruler unary edges claimed by a removed ruler's walk
+__global__ void __launch_bounds__(kBlk) k_rm_chains(const uint64_t *post, const uint8_t *kind, const uint64_t *nx, uint64_t n,
                                                     const uint64_t *tab, uint64_t cap, uint64_t *valid) {
     const int lane = threadIdx.x & 63;
     const uint64_t nw = (n + 63) / 64, wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
@@ -787,8 +840,8 @@ __global__ void __launch_bounds__(kBlk) k_rm_chains(const uint64_t *post, const 
         bool rm = false;
         if (i < n && bit_of(post, i)) {
             const uint8_t k = kind[i];
-            if (__popc(k & 0xF) == 1 && !(k & kRuler) && own[i] != kNo) {
-                const uint64_t r = own[i];
+            if (__popc(k & 0xF) == 1 && !(k & kRuler) && is_claim(nx[i])) {
+                const uint64_t r = nx[i] & kIdM;
                 for (uint64_t h = mix64(r) & (cap - 1);; h = (h + 1) & (cap - 1)) {
                     const uint64_t x = tab[h];
                     if (x == r) { rm = true; break; }
@@ -808,17 +861,9 @@ __global__ void __launch_bounds__(kBlk) k_popc(const uint64_t *bm, uint64_t nw, 
     block_add(out, c);
 }
 
-// the candidates still valid after the peel (global ids -> local test)
-__global__ void __launch_bounds__(kBlk) k_cand_keep(const uint64_t *cand, uint64_t m, const uint64_t *valid, uint64_t id_lo,
-                                                    uint64_t *out, unsigned long long *n) {
+__global__ void __launch_bounds__(kBlk) k_and_words(uint64_t *a, const uint64_t *b, uint64_t nw) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x; j0 < m; j0 += stride) {
-        const uint64_t j = j0 + threadIdx.x;
-        const bool k = j < m && bit_of(valid, cand[j] - id_lo);
-        unsigned long long mk;
-        const uint64_t at = wave_reserve(k, n, mk);
-        if (k) out[at] = cand[j];
-    }
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) a[w] &= b[w];
 }
 
 // ---------------------------------------------------------------- search regions
@@ -849,6 +894,12 @@ __device__ __forceinline__ void mark_group(const uint64_t *gs, uint64_t n, uint6
     }
 }
 
+__global__ void __launch_bounds__(kBlk) k_set_ids(const uint64_t *ids, uint64_t m, uint64_t *bm) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += stride)
+        atomicOr((unsigned long long *)&bm[ids[j] >> 6], 1ULL << (ids[j] & 63));
+}
+
 // the starts of a BFS: their groups marked, themselves seen and listed (local indices)
 __global__ void __launch_bounds__(kBlk) k_bfs_seed(const uint64_t *ids, uint64_t m, uint64_t id_lo, uint64_t n, const uint64_t *gs,
                                                    uint64_t *reg, uint64_t *seen, uint64_t *front) {
@@ -864,30 +915,22 @@ __global__ void __launch_bounds__(kBlk) k_bfs_seed(const uint64_t *ids, uint64_t
 // predecessors' (backward): first id | position mask << 40
 __global__ void __launch_bounds__(kBlk) k_bfs_req(const uint64_t *front, uint64_t nf, const uint64_t *out_info,
                                                   const uint64_t *in_info, int backward, Owners o, uint64_t *q,
-                                                  uint8_t *dest, unsigned long long *cur) {
+                                                  uint8_t *dest) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x; j0 < nf; j0 += stride) {
-        const uint64_t j = j0 + threadIdx.x;
-        uint64_t lo = 0, pos = 0;
-        if (j < nf) {
-            const uint64_t li = front[j];
-            if (backward) {
-                const uint64_t ii = in_info[li];
-                lo = ii & kIdM;
-                pos = (ii >> kIdxBits) & 0xFFFF;
-            } else {
-                const uint64_t oi = out_info[li];
-                lo = oi & kIdM;
-                pos = (1ULL << __popc((unsigned)(oi >> kIdxBits) & 0xF)) - 1;
-            }
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nf; j += stride) {
+        const uint64_t li = front[j];
+        uint64_t lo, pos;
+        if (backward) {
+            const uint64_t ii = in_info[li];
+            lo = ii & kIdM;
+            pos = (ii >> kIdxBits) & 0xFFFF;
+        } else {
+            const uint64_t oi = out_info[li];
+            lo = oi & kIdM;
+            pos = (1ULL << __popc((unsigned)(oi >> kIdxBits) & 0xF)) - 1;
         }
-        const bool f = pos != 0;
-        unsigned long long mk;
-        const uint64_t at = wave_reserve(f, cur, mk);
-        if (f) {
-            q[at] = lo | (pos << kIdxBits);
-            dest[at] = (uint8_t)owner_of_id(o, lo);
-        }
+        q[j] = lo | (pos << kIdxBits);
+        dest[j] = pos ? (uint8_t)owner_of_id(o, lo) : kNoDest;
     }
 }
 // the owner: the window's group joins the region; its valid, unseen positions join the next frontier
@@ -895,18 +938,35 @@ __global__ void __launch_bounds__(kBlk) k_bfs_claim(const uint64_t *q, uint64_t 
                                                     const uint64_t *valid, uint64_t *reg, uint64_t *seen, uint64_t *next,
                                                     unsigned long long *nn) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += stride) {
-        const uint64_t li = (q[j] & kIdM) - id_lo;
-        uint32_t pos = (uint32_t)(q[j] >> kIdxBits) & 0xFFFF;
-        mark_group(gs, n, li, reg);
-        while (pos) {
-            const int b = __ffs(pos) - 1;
-            pos &= pos - 1;
+    for (uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x; j0 < m; j0 += stride) {
+        const uint64_t j = j0 + threadIdx.x;
+        const uint64_t li = j < m ? (q[j] & kIdM) - id_lo : 0;
+        const uint32_t pos = j < m ? (uint32_t)(q[j] >> kIdxBits) & 0xFFFF : 0;
+        if (j < m) mark_group(gs, n, li, reg);
+        for (int b = 0; b < 16; ++b) {
             const uint64_t y = li + b;
-            if (y >= n || !bit_of(valid, y)) continue;
-            const unsigned long long bit = 1ULL << (y & 63);
-            if (atomicOr((unsigned long long *)&seen[y >> 6], bit) & bit) continue;
-            next[atomicAdd(nn, 1ull)] = y;
+            bool f = ((pos >> b) & 1) && y < n && bit_of(valid, y);
+            if (f) {
+                const unsigned long long bit = 1ULL << (y & 63);
+                f = !(atomicOr((unsigned long long *)&seen[y >> 6], bit) & bit);
+            }
+            unsigned long long mk;
+            const uint64_t at = wave_reserve(f, nn, mk);
+            if (f) next[at] = y;
+        }
+    }
+}
+
+// a BFS hop on a region replica (compact ids, every rank alike): the valid successors not seen yet
+__global__ void __launch_bounds__(kBlk) k_cbfs(GraphView g, const uint64_t *front, uint64_t nf, uint64_t *seen, uint64_t *next,
+                                               unsigned long long *nn) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nf; j += stride) {
+        uint64_t out[4];
+        const int od = dev_outgoing(g, front[j], out);
+        for (int b = 0; b < od; ++b) {
+            const uint64_t x = out[b], bit = 1ULL << (x & 63);
+            if (!(atomicOr((unsigned long long *)&seen[x >> 6], bit) & bit)) next[atomicAdd(nn, 1ull)] = x;
         }
     }
 }
@@ -993,6 +1053,38 @@ struct ShardCf {
         : g(gr), ctx(gr->ctx), comm(c), rt(gr->ctx, c), o(owners_of(gr, c)), st(gr->ctx->stream), n(gr->D_local),
           nwl((gr->D_local + 63) / 64) {}
 
+    // the set bits of a local bitmap (nwl words) as local indices, ascending
+    uint64_t list_bits(const uint64_t *bm, DevBuf<uint64_t> &out) {
+        DevBuf<uint64_t> pc(nwl + 1), wpre(nwl + 1);
+        HIP_OK(hipMemsetAsync(pc.p + nwl, 0, 8, st));
+        uint64_t cnt = 0;
+        if (nwl) {
+            hipLaunchKernelGGL(k_word_popc64, dim3(grid(nwl)), dim3(kBlk), 0, st, bm, nwl, pc.p);
+            LAUNCH_OK();
+            size_t tmp = 0;
+            HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, pc.p, wpre.p, (size_t)(nwl + 1), st));
+            DevBuf<uint8_t> t(tmp);
+            HIP_OK(hipcub::DeviceScan::ExclusiveSum(t.p, tmp, pc.p, wpre.p, (size_t)(nwl + 1), st));
+            d2h(ctx, &cnt, wpre.p + nwl, 8);
+        }
+        out.alloc(cnt ? cnt : 1);
+        if (cnt) {
+            hipLaunchKernelGGL(k_bits_list, dim3(grid(nwl * 64)), dim3(kBlk), 0, st, bm, nwl, (const uint64_t *)wpre.p, out.p);
+            LAUNCH_OK();
+        }
+        return cnt;
+    }
+
+    // in[j] where flags[j] != 0, in order (hipcub select); returns the count
+    uint64_t select(const uint64_t *in, const uint8_t *flags, uint64_t m, uint64_t *out) {
+        DevBuf<unsigned long long> num(1);
+        size_t tmp = 0;
+        HIP_OK(hipcub::DeviceSelect::Flagged(nullptr, tmp, in, flags, out, num.p, (size_t)m, st));
+        DevBuf<uint8_t> t(tmp ? tmp : 1);
+        HIP_OK(hipcub::DeviceSelect::Flagged(t.p, tmp, in, flags, out, num.p, (size_t)m, st));
+        return read_u64(ctx, num.p);
+    }
+
     uint64_t sum(uint64_t v) {
         uint64_t t = 0;
         for (uint64_t x : comm.allgather_one(v)) t += x;
@@ -1011,12 +1103,11 @@ struct ShardCf {
             if (nf) {
                 hipLaunchKernelGGL(k_bfs_req, dim3(grid(nf)), dim3(kBlk), 0, st, (const uint64_t *)front.p, nf,
                                    (const uint64_t *)g->out_info.p, (const uint64_t *)g->in_info.p, (int)backward, o, q.p,
-                                   dest.p, c.p);
+                                   dest.p);
                 LAUNCH_OK();
             }
-            const uint64_t nq = nf ? read_u64(ctx, c.p) : 0;
             Routed r;
-            rt.send(q.p, 1, dest.p, nq, r, false);
+            rt.send(q.p, 1, dest.p, nf, r, false);
             // each received window adds at most 16 edges
             DevBuf<uint64_t> next(16 * r.n_in + 1);
             if (r.n_in) {
@@ -1110,7 +1201,7 @@ void sdbg_finish_sharded(mcaat_ctx *ctx, Comm &comm, mcaat_graph *g) {
         d2h(ctx, &kmax, g->key.p + n - 1, 8);
     }
     int shift = 0;
-    const uint64_t want = std::max<uint64_t>(1, n / 8);
+    const uint64_t want = std::max<uint64_t>(1, n / (uint64_t)std::max<int64_t>(1, knob(ctx, "dist.dir_edges", 2)));
     while (((kmax - kmin) >> shift) + 1 > want) ++shift;
     const uint64_t np = ((kmax - kmin) >> shift) + 1;
     g->dir.alloc(np + 1);
@@ -1125,7 +1216,7 @@ void sdbg_finish_sharded(mcaat_ctx *ctx, Comm &comm, mcaat_graph *g) {
     Router rt(ctx, comm);
     const Owners o = owners_of(g, comm);
     // chunks of edges: two queries each; every rank takes part in as many exchanges
-    const uint64_t chunk = (uint64_t)std::max<int64_t>(1024, knob(ctx, "dist.adj_chunk", 1LL << 27));
+    const uint64_t chunk = (uint64_t)std::max<int64_t>(1024, knob(ctx, "dist.adj_chunk", 1LL << 26));
     uint64_t n_chunks = (n + chunk - 1) / chunk;
     for (uint64_t x : comm.allgather_one(n_chunks)) n_chunks = std::max(n_chunks, x);
     KernelTimer kt(ctx, "adjacency", 32.0 * (double)n);
@@ -1192,58 +1283,53 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
     }
     // filtered out-windows and the candidates' in-windows from their owners
     DevBuf<uint8_t> kind(n + 4), stt(n + 4);
-    DevBuf<uint64_t> nx(n ? n : 1), own(n ? n : 1);
+    DevBuf<uint64_t> nx(n ? n : 1);
     HIP_OK(hipMemsetAsync(kind.p, 0, kind.bytes(), st));
-    DevBuf<uint64_t> cand(n ? n : 1);
-    HIP_OK(hipMemsetAsync(cnt.p + 5, 0, 8, st));
+    DevBuf<uint64_t> cbits(nwl + 1);  // ChunkStartNodes' filter, one bit per local edge
+    HIP_OK(hipMemsetAsync(cbits.p, 0, cbits.bytes(), st));
     // chunks of local edges per exchange (every rank runs as many): bounded transient memory
-    const uint64_t chunk = (uint64_t)std::max<int64_t>(1024, knob(ctx, "dist.adj_chunk", 1LL << 27));
+    const uint64_t chunk = (uint64_t)std::max<int64_t>(1024, knob(ctx, "dist.adj_chunk", 1LL << 26));
     uint64_t n_chunks = (n + chunk - 1) / chunk;
     for (uint64_t x : comm.allgather_one(n_chunks)) n_chunks = std::max(n_chunks, x);
     for (uint64_t c = 0; c < n_chunks; ++c) {
         const uint64_t a0 = std::min(n, c * chunk), a1 = std::min(n, a0 + chunk), m = a1 - a0;
-        DevBuf<uint64_t> q(2 * m + 1), src(2 * m + 1);
+        DevBuf<uint64_t> q(2 * m + 1);
         DevBuf<uint8_t> dest(2 * m + 1);
-        HIP_OK(hipMemsetAsync(cnt.p + 4, 0, 8, st));
         if (m) {
             hipLaunchKernelGGL(k_win_req, dim3(s.grid(m)), dim3(kBlk), 0, st, (const uint64_t *)post.p,
                                (const uint16_t *)g->mult.p, (const uint64_t *)g->out_info.p, (const uint64_t *)g->in_info.p,
-                               a0, a1, (uint64_t)p.threshold_multiplicity, s.o, q.p, dest.p, src.p, cnt.p + 4);
+                               a0, a1, (uint64_t)p.threshold_multiplicity, s.o, q.p, dest.p);
             LAUNCH_OK();
         }
-        const uint64_t nq = m ? read_u64(ctx, cnt.p + 4) : 0;
         Routed r;
-        s.rt.send(q.p, 1, dest.p, nq, r, true);
-        DevBuf<uint64_t> ans(r.n_in + 1), a(nq + 1);
+        s.rt.send(q.p, 1, dest.p, 2 * m, r, true);
+        DevBuf<uint64_t> ans(r.n_in + 1);
         if (r.n_in) {
             hipLaunchKernelGGL(k_win_ans, dim3(s.grid(r.n_in)), dim3(kBlk), 0, st, (const uint64_t *)post.p, n, id_lo,
                                (const uint64_t *)r.in.p, r.n_in, ans.p);
             LAUNCH_OK();
         }
-        s.rt.reply(r, ans.p, 1, a.p);
-        if (nq) {
-            hipLaunchKernelGGL(k_win_apply, dim3(s.grid(nq)), dim3(kBlk), 0, st, (const uint64_t *)src.p,
-                               (const uint64_t *)a.p, nq, (const uint64_t *)g->out_info.p, (const uint64_t *)g->in_info.p,
-                               id_lo, kind.p, nx.p, cand.p, cnt.p + 5);
+        s.rt.reply(r, ans.p, 1, q.p);  // the answers land in their request slots
+        if (m) {
+            hipLaunchKernelGGL(k_win_apply, dim3(s.grid(m)), dim3(kBlk), 0, st, (const uint8_t *)dest.p,
+                               (const uint64_t *)q.p, a0, a1, (const uint64_t *)g->out_info.p, (const uint64_t *)g->in_info.p,
+                               id_lo, kind.p, nx.p, cbits.p);
             LAUNCH_OK();
         }
     }
-    const uint64_t ncand = read_u64(ctx, cnt.p + 5);
     // predecessor flags, as messages to the successors' owners (after every window is in)
     for (uint64_t c = 0; c < n_chunks; ++c) {
         const uint64_t a0 = std::min(n, c * chunk), a1 = std::min(n, a0 + chunk), m = a1 - a0;
         DevBuf<uint64_t> q(4 * m + 1);
         DevBuf<uint8_t> dest(4 * m + 1);
-        HIP_OK(hipMemsetAsync(cnt.p + 4, 0, 8, st));
         if (m) {
             hipLaunchKernelGGL(k_flag_msgs, dim3(s.grid(m)), dim3(kBlk), 0, st, (const uint64_t *)post.p,
                                (const uint64_t *)seed.p, (const uint8_t *)kind.p, (const uint64_t *)g->out_info.p, a0, a1,
-                               s.o, q.p, dest.p, cnt.p + 4, cnt.p);
+                               s.o, q.p, dest.p, cnt.p);
             LAUNCH_OK();
         }
-        const uint64_t nq = m ? read_u64(ctx, cnt.p + 4) : 0;
         Routed r;
-        s.rt.send(q.p, 1, dest.p, nq, r, false);
+        s.rt.send(q.p, 1, dest.p, 4 * m, r, false);
         if (r.n_in) {
             hipLaunchKernelGGL(k_flag_apply, dim3(s.grid(r.n_in)), dim3(kBlk), 0, st, (const uint64_t *)r.in.p, r.n_in,
                                id_lo, kind.p);
@@ -1262,24 +1348,21 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
 
     // 3. RecursiveReduction: rulers, walks, pointer jumping, branch resolution, removal
     const uint64_t rmask = (uint64_t)std::max<int64_t>(0, knob(ctx, "dist.ruler_mask", 15));
-    DevBuf<uint64_t> rl(n ? n : 1), bl(n ? n : 1);
-    HIP_OK(hipMemsetAsync(own.p, 0xFF, own.bytes(), st));
-    HIP_OK(hipMemsetAsync(cnt.p + 4, 0, 16, st));
-    if (n) {
-        hipLaunchKernelGGL(k_prep, dim3(s.grid(n)), dim3(kBlk), 0, st, (const uint64_t *)post.p, (const uint64_t *)seed.p,
-                           kind.p, stt.p, n, id_lo, rmask, rl.p, cnt.p + 4, bl.p, cnt.p + 5);
-        LAUNCH_OK();
-    }
+    DevBuf<uint64_t> rl, bl;
     uint64_t nr = 0, nb = 0;
     {
-        unsigned long long h2[2];
-        d2h(ctx, h2, cnt.p + 4, 16);
-        nr = h2[0];
-        nb = h2[1];
+        DevBuf<uint64_t> rbits(nwl + 1), bbits(nwl + 1);
+        if (n) {
+            hipLaunchKernelGGL(k_prep, dim3(s.grid(nwl * 64)), dim3(kBlk), 0, st, (const uint64_t *)post.p,
+                               (const uint64_t *)seed.p, kind.p, stt.p, n, id_lo, rmask, rbits.p, bbits.p);
+            LAUNCH_OK();
+        }
+        nr = s.list_bits(rbits.p, rl);
+        nb = s.list_bits(bbits.p, bl);
     }
     uint64_t walk_rounds = 0;
     {
-        DevBuf<uint64_t> w(4 * (nr ? nr : 1));
+        DevBuf<uint64_t> w(2 * (nr ? nr : 1));
         if (nr) {
             hipLaunchKernelGGL(k_walk_init, dim3(s.grid(nr)), dim3(kBlk), 0, st, (const uint64_t *)rl.p, nr,
                                (const uint64_t *)nx.p, id_lo, w.p);
@@ -1287,17 +1370,15 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
         }
         uint64_t m = nr;
         for (;; ++walk_rounds) {
-            DevBuf<uint64_t> o4(4 * (m ? m : 1));
+            DevBuf<uint64_t> o2(2 * (m ? m : 1));
             DevBuf<uint8_t> dest(m ? m : 1);
-            HIP_OK(hipMemsetAsync(cnt.p + 6, 0, 8, st));
             if (m) {
                 hipLaunchKernelGGL(k_walk, dim3(s.grid(m)), dim3(kBlk), 0, st, (const uint64_t *)w.p, m,
-                                   (const uint8_t *)kind.p, nx.p, own.p, s.o, o4.p, dest.p, cnt.p + 6);
+                                   (const uint8_t *)kind.p, nx.p, s.o, o2.p, dest.p);
                 LAUNCH_OK();
             }
-            const uint64_t mo = m ? read_u64(ctx, cnt.p + 6) : 0;
             Routed r;
-            s.rt.send(o4.p, 4, dest.p, mo, r, false);
+            s.rt.send(o2.p, 2, dest.p, m, r, false);
             if (!r.total) break;
             w = std::move(r.in);
             m = r.n_in;
@@ -1306,14 +1387,16 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
     // pointer jumping over the rulers still pointing at a ruler
     uint64_t jump_rounds = 0;
     {
-        DevBuf<uint64_t> al(nr ? nr : 1), al2(nr ? nr : 1);
-        HIP_OK(hipMemsetAsync(cnt.p + 6, 0, 8, st));
+        DevBuf<uint64_t> al;
+        DevBuf<uint8_t> keep(nr + 1);
+        uint64_t na = 0;
         if (nr) {
             hipLaunchKernelGGL(k_active_rulers, dim3(s.grid(nr)), dim3(kBlk), 0, st, (const uint64_t *)rl.p, nr,
-                               (const uint64_t *)nx.p, al.p, cnt.p + 6);
+                               (const uint64_t *)nx.p, keep.p);
             LAUNCH_OK();
+            al.alloc(nr);
+            na = s.select(rl.p, keep.p, nr, al.p);
         }
-        uint64_t na = nr ? read_u64(ctx, cnt.p + 6) : 0;
         const uint64_t total_rulers = s.sum(nr);
         int bound = 2;
         while ((1ULL << bound) < total_rulers + 1) ++bound;
@@ -1329,21 +1412,21 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
             }
             Routed r;
             s.rt.send(q.p, 1, dest.p, na, r, true);
-            DevBuf<uint64_t> ans(r.n_in + 1), a(na + 1);
+            DevBuf<uint64_t> ans(r.n_in + 1);
             if (r.n_in) {
                 hipLaunchKernelGGL(k_jump_ans, dim3(s.grid(r.n_in)), dim3(kBlk), 0, st, (const uint64_t *)r.in.p, r.n_in,
                                    (const uint64_t *)nx.p, id_lo, ans.p);
                 LAUNCH_OK();
             }
-            s.rt.reply(r, ans.p, 1, a.p);
-            HIP_OK(hipMemsetAsync(cnt.p + 6, 0, 8, st));
+            s.rt.reply(r, ans.p, 1, q.p);
             if (na) {
                 hipLaunchKernelGGL(k_jump_apply, dim3(s.grid(na)), dim3(kBlk), 0, st, (const uint64_t *)al.p, na,
-                                   (const uint64_t *)a.p, nx.p, al2.p, cnt.p + 6);
+                                   (const uint64_t *)q.p, nx.p, keep.p);
                 LAUNCH_OK();
+                DevBuf<uint64_t> al2(na);
+                na = s.select(al.p, keep.p, na, al2.p);
+                al = std::move(al2);
             }
-            na = na ? read_u64(ctx, cnt.p + 6) : 0;
-            std::swap(al, al2);
         }
         // still pointing at a ruler after the bound: a unary cycle (or a chain into one) survives
         if (na) {
@@ -1351,99 +1434,76 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
             LAUNCH_OK();
         }
     }
-    // branch successors' references (two lookups: the successor, then a passing ruler's terminal)
+    // branch successors' references (two lookups: the successor, then a claiming ruler's terminal)
     DevBuf<uint64_t> ref(4 * (nb ? nb : 1));  // per branch slot: its successor's reference, kPad unused
     if (nb) {
         hipLaunchKernelGGL(k_fill, dim3(s.grid(4 * nb)), dim3(kBlk), 0, st, ref.p, 4 * nb, kPad);
         LAUNCH_OK();
     }
     {
-        DevBuf<uint64_t> q(4 * nb + 1), src(4 * nb + 1);
+        DevBuf<uint64_t> q(4 * nb + 1);
         DevBuf<uint8_t> dest(4 * nb + 1);
-        HIP_OK(hipMemsetAsync(cnt.p + 6, 0, 8, st));
         if (nb) {
             hipLaunchKernelGGL(k_bref_req, dim3(s.grid(nb)), dim3(kBlk), 0, st, (const uint64_t *)bl.p, nb,
-                               (const uint8_t *)kind.p, (const uint64_t *)g->out_info.p, s.o, q.p, dest.p, src.p, cnt.p + 6);
+                               (const uint8_t *)kind.p, (const uint64_t *)g->out_info.p, s.o, q.p, dest.p);
             LAUNCH_OK();
         }
-        const uint64_t nq = nb ? read_u64(ctx, cnt.p + 6) : 0;
         Routed r;
-        s.rt.send(q.p, 1, dest.p, nq, r, true);
-        DevBuf<uint64_t> ans(r.n_in + 1), a(nq + 1);
+        s.rt.send(q.p, 1, dest.p, 4 * nb, r, true);
+        DevBuf<uint64_t> ans(r.n_in + 1);
         if (r.n_in) {
             hipLaunchKernelGGL(k_bref_ans, dim3(s.grid(r.n_in)), dim3(kBlk), 0, st, (const uint64_t *)r.in.p, r.n_in,
-                               (const uint8_t *)kind.p, (const uint64_t *)nx.p, (const uint64_t *)own.p, id_lo, ans.p);
+                               (const uint8_t *)kind.p, (const uint64_t *)nx.p, id_lo, ans.p);
             LAUNCH_OK();
         }
-        s.rt.reply(r, ans.p, 1, a.p);
-        if (nq) {
-            hipLaunchKernelGGL(k_scatter_ref, dim3(s.grid(nq)), dim3(kBlk), 0, st, (const uint64_t *)src.p,
-                               (const uint64_t *)a.p, nq, ref.p);
-            LAUNCH_OK();
-        }
-        // second step: a passing ruler's terminal
-        HIP_OK(hipMemsetAsync(cnt.p + 6, 0, 8, st));
+        s.rt.reply(r, ans.p, 1, ref.p);  // slots without a successor keep kPad
+        // second step: a claiming ruler's terminal replaces kRef | ruler
         if (nb) {
             hipLaunchKernelGGL(k_bref_req2, dim3(s.grid(4 * nb)), dim3(kBlk), 0, st, (const uint64_t *)ref.p, 4 * nb, s.o,
-                               q.p, dest.p, src.p, cnt.p + 6);
+                               q.p, dest.p);
             LAUNCH_OK();
         }
-        const uint64_t nq2 = nb ? read_u64(ctx, cnt.p + 6) : 0;
         Routed r2;
-        s.rt.send(q.p, 1, dest.p, nq2, r2, true);
-        DevBuf<uint64_t> ans2(r2.n_in + 1), a2(nq2 + 1);
+        s.rt.send(q.p, 1, dest.p, 4 * nb, r2, true);
+        DevBuf<uint64_t> ans2(r2.n_in + 1);
         if (r2.n_in) {
             hipLaunchKernelGGL(k_jump_ans, dim3(s.grid(r2.n_in)), dim3(kBlk), 0, st, (const uint64_t *)r2.in.p, r2.n_in,
                                (const uint64_t *)nx.p, id_lo, ans2.p);
             LAUNCH_OK();
         }
-        s.rt.reply(r2, ans2.p, 1, a2.p);
-        if (nq2) {
-            hipLaunchKernelGGL(k_scatter_ref, dim3(s.grid(nq2)), dim3(kBlk), 0, st, (const uint64_t *)src.p,
-                               (const uint64_t *)a2.p, nq2, ref.p);
-            LAUNCH_OK();
-        }
+        s.rt.reply(r2, ans2.p, 1, ref.p);
     }
     // branch resolution rounds (until no branch changes on any rank)
     uint64_t res_rounds = 0;
     {
-        DevBuf<uint64_t> q(4 * nb + 1), src(4 * nb + 1);
-        DevBuf<uint8_t> dest(4 * nb + 1), slot_st(4 * nb + 4);
+        DevBuf<uint64_t> q(4 * nb + 1);
+        DevBuf<uint8_t> dest(4 * nb + 1);
         for (;; ++res_rounds) {
-            HIP_OK(hipMemsetAsync(cnt.p + 6, 0, 16, st));
+            HIP_OK(hipMemsetAsync(cnt.p + 7, 0, 8, st));
             if (nb) {
                 hipLaunchKernelGGL(k_res_req, dim3(s.grid(nb)), dim3(kBlk), 0, st, (const uint64_t *)bl.p,
-                                   (const uint64_t *)ref.p, nb, stt.p, s.o, q.p, dest.p, src.p, cnt.p + 6, cnt.p + 7);
+                                   (const uint64_t *)ref.p, nb, stt.p, s.o, q.p, dest.p, cnt.p + 7);
                 LAUNCH_OK();
             }
-            unsigned long long h2[2] = {0, 0};
-            if (nb) d2h(ctx, h2, cnt.p + 6, 16);
             Routed r;
-            s.rt.send(q.p, 1, dest.p, h2[0], r, true);
-            DevBuf<uint64_t> ans(r.n_in + 1), a(h2[0] + 1);
+            s.rt.send(q.p, 1, dest.p, 4 * nb, r, true);
+            DevBuf<uint64_t> ans(r.n_in + 1);
             if (r.n_in) {
                 hipLaunchKernelGGL(k_st_ans, dim3(s.grid(r.n_in)), dim3(kBlk), 0, st, (const uint64_t *)r.in.p, r.n_in,
                                    (const uint8_t *)stt.p, id_lo, ans.p);
                 LAUNCH_OK();
             }
-            s.rt.reply(r, ans.p, 1, a.p);
-            // padding slots read as removed (they never keep a branch alive)
-            if (nb) HIP_OK(hipMemsetAsync(slot_st.p, kStRem, 4 * nb, st));
-            if (h2[0]) {
-                hipLaunchKernelGGL(k_slot_st, dim3(s.grid(h2[0])), dim3(kBlk), 0, st, (const uint64_t *)src.p,
-                                   (const uint64_t *)a.p, h2[0], slot_st.p);
-                LAUNCH_OK();
-            }
+            s.rt.reply(r, ans.p, 1, q.p);
             if (nb) {
                 hipLaunchKernelGGL(k_res_apply, dim3(s.grid(nb)), dim3(kBlk), 0, st, (const uint64_t *)bl.p, nb,
-                                   (const uint8_t *)slot_st.p, stt.p, cnt.p + 7);
+                                   (const uint64_t *)q.p, (const uint8_t *)dest.p, stt.p, cnt.p + 7);
                 LAUNCH_OK();
             }
             const uint64_t ch = nb ? read_u64(ctx, cnt.p + 7) : 0;
             if (s.sum(ch) == 0) break;
         }
     }
-    // removal: resolved non-unary edges, rulers whose terminal went, and the chains they walked
+    // removal: resolved non-unary edges, rulers whose terminal went, and the chains they claimed
     uint64_t n_rm_rulers = 0;
     {
         if (nwl) {
@@ -1451,31 +1511,31 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
                                (const uint8_t *)kind.p, (const uint8_t *)stt.p, n, g->valid.p);
             LAUNCH_OK();
         }
-        DevBuf<uint64_t> q(nr + 1), src(nr + 1);
+        DevBuf<uint64_t> q(nr + 1);
         DevBuf<uint8_t> dest(nr + 1);
-        HIP_OK(hipMemsetAsync(cnt.p + 6, 0, 16, st));
         if (nr) {
             hipLaunchKernelGGL(k_term_req, dim3(s.grid(nr)), dim3(kBlk), 0, st, (const uint64_t *)rl.p, nr,
-                               (const uint64_t *)nx.p, s.o, q.p, dest.p, src.p, cnt.p + 6);
+                               (const uint64_t *)nx.p, s.o, q.p, dest.p);
             LAUNCH_OK();
         }
-        const uint64_t nq = nr ? read_u64(ctx, cnt.p + 6) : 0;
         Routed r;
-        s.rt.send(q.p, 1, dest.p, nq, r, true);
-        DevBuf<uint64_t> ans(r.n_in + 1), a(nq + 1);
+        s.rt.send(q.p, 1, dest.p, nr, r, true);
+        DevBuf<uint64_t> ans(r.n_in + 1);
         if (r.n_in) {
             hipLaunchKernelGGL(k_st_ans, dim3(s.grid(r.n_in)), dim3(kBlk), 0, st, (const uint64_t *)r.in.p, r.n_in,
                                (const uint8_t *)stt.p, id_lo, ans.p);
             LAUNCH_OK();
         }
-        s.rt.reply(r, ans.p, 1, a.p);
-        DevBuf<uint64_t> rm(nq + 1);
-        if (nq) {
-            hipLaunchKernelGGL(k_rm_rulers, dim3(s.grid(nq)), dim3(kBlk), 0, st, (const uint64_t *)src.p,
-                               (const uint64_t *)a.p, nq, id_lo, g->valid.p, rm.p, cnt.p + 7);
+        s.rt.reply(r, ans.p, 1, q.p);
+        DevBuf<uint64_t> rm(nr + 1), gidr(nr + 1);
+        DevBuf<uint8_t> flag(nr + 1);
+        uint64_t nrm = 0;
+        if (nr) {
+            hipLaunchKernelGGL(k_rm_rulers, dim3(s.grid(nr)), dim3(kBlk), 0, st, (const uint64_t *)rl.p, nr,
+                               (const uint64_t *)q.p, (const uint8_t *)dest.p, g->valid.p, id_lo, gidr.p, flag.p);
             LAUNCH_OK();
+            nrm = s.select(gidr.p, flag.p, nr, rm.p);
         }
-        const uint64_t nrm = nq ? read_u64(ctx, cnt.p + 7) : 0;
         const std::vector<uint64_t> per = comm.allgather_one(nrm);
         std::vector<uint64_t> bytes(comm.world);
         for (int r2 = 0; r2 < comm.world; ++r2) n_rm_rulers += per[r2], bytes[r2] = 8 * per[r2];
@@ -1491,7 +1551,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
             LAUNCH_OK();
             if (nwl) {
                 hipLaunchKernelGGL(k_rm_chains, dim3(s.grid(nwl * 64)), dim3(kBlk), 0, st, (const uint64_t *)post.p,
-                                   (const uint8_t *)kind.p, (const uint64_t *)own.p, n, (const uint64_t *)tab.p, cap,
+                                   (const uint8_t *)kind.p, (const uint64_t *)nx.p, n, (const uint64_t *)tab.p, cap,
                                    g->valid.p);
                 LAUNCH_OK();
             }
@@ -1506,7 +1566,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
                 (unsigned long long)jump_rounds, (unsigned long long)res_rounds, (unsigned long long)n_rm_rulers);
     kind.release();
     stt.release();
-    own.release();
+    nx.release();
     rl.release();
     bl.release();
     ref.release();
@@ -1520,19 +1580,19 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
         LAUNCH_OK();
     }
     out->stats[2] = s.sum(read_u64(ctx, cnt.p));
-    std::vector<uint64_t> cand_mine;
-    DevBuf<uint64_t> kept(ncand + 1);
-    uint64_t nkept = 0;
-    if (ncand) {
-        hipLaunchKernelGGL(k_cand_keep, dim3(s.grid(ncand)), dim3(kBlk), 0, st, (const uint64_t *)cand.p, ncand,
-                           (const uint64_t *)g->valid.p, id_lo, kept.p, cnt.p + 1);
-        LAUNCH_OK();
-        nkept = read_u64(ctx, cnt.p + 1);
-        cand_mine.resize(nkept);
-        if (nkept) d2h(ctx, cand_mine.data(), kept.p, 8 * nkept);
-        std::sort(cand_mine.begin(), cand_mine.end());
+    std::vector<uint64_t> cand_mine;  // the candidates still valid, ascending ids
+    {
+        if (nwl) {
+            hipLaunchKernelGGL(k_and_words, dim3(s.grid(nwl)), dim3(kBlk), 0, st, cbits.p, (const uint64_t *)g->valid.p, nwl);
+            LAUNCH_OK();
+        }
+        DevBuf<uint64_t> cl;
+        const uint64_t nk = s.list_bits(cbits.p, cl);
+        cand_mine.resize(nk);
+        if (nk) d2h(ctx, cand_mine.data(), cl.p, 8 * nk);
+        for (auto &x : cand_mine) x += id_lo;
     }
-    cand.release();
+    cbits.release();
     post.release();
     timer.mark("recount");
 
@@ -1588,45 +1648,58 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
             starts.push_back(id);
         }
     out->stats[4] = out->cand_ids.size();
+    // FindCycle's forward reach (cycle_max_length + 1 hops from the starts) lies inside the
+    // DepthLevelSearch region (the starts are candidates): found on the replica, no exchange
+    std::vector<uint64_t> fwd;  // its edge ids, ascending
+    {
+        const std::vector<uint64_t> sc = to_compact(hgid, starts);
+        const uint64_t nwr = mcaat_graph::bitmap_words(rg.D);
+        DevBuf<uint64_t> rseen(nwr), front(sc.size() + 1);
+        DevBuf<unsigned long long> nn(1);
+        HIP_OK(hipMemsetAsync(rseen.p, 0, rseen.bytes(), st));
+        uint64_t nf = sc.size();
+        if (nf) {
+            h2d(ctx, front.p, sc.data(), 8 * nf);
+            hipLaunchKernelGGL(k_set_ids, dim3(s.grid(nf)), dim3(kBlk), 0, st, (const uint64_t *)front.p, nf, rseen.p);
+            LAUNCH_OK();
+        }
+        for (uint64_t h = 0; h < radius && nf; ++h) {
+            DevBuf<uint64_t> next(4 * nf);
+            HIP_OK(hipMemsetAsync(nn.p, 0, 8, st));
+            hipLaunchKernelGGL(k_cbfs, dim3(s.grid(nf)), dim3(kBlk), 0, st, rg.view(), (const uint64_t *)front.p, nf,
+                               rseen.p, next.p, nn.p);
+            LAUNCH_OK();
+            nf = read_u64(ctx, nn.p);
+            front = std::move(next);
+        }
+        std::vector<uint64_t> words(nwr);
+        d2h(ctx, words.data(), rseen.p, 8 * nwr);
+        for (uint64_t w = 0; w < nwr; ++w)
+            for (uint64_t x = words[w]; x; x &= x - 1) {
+                const uint64_t c = w * 64 + (uint64_t)__builtin_ctzll(x);
+                if (c < hgid.size()) fwd.push_back(hgid[c]);
+            }
+    }
     rg = mcaat_graph{};
     timer.mark("dls");
 
-    // 7. FindCycle region: forward cycle_max_length + 1 hops from the starts, then backward as
-    // many from every edge reached (the lock relaxation's reach)
+    // 7. FindCycle region: the forward reach found on the DepthLevelSearch replica above, then
+    // cycle_max_length + 1 hops backward from every edge of it (the lock relaxation's reach)
     {
-        std::vector<uint64_t> sm;
-        for (uint64_t x : starts)
-            if (x >= id_lo && x < id_lo + n) sm.push_back(x);
-        std::sort(sm.begin(), sm.end());
-        forward_region(sm);
-        // the backward BFS starts from every edge the forward one reached
-        DevBuf<uint64_t> pc(nwl + 1), wpre(nwl + 1);
-        HIP_OK(hipMemsetAsync(pc.p + nwl, 0, 8, st));
-        uint64_t nseen = 0;
-        if (nwl) {
-            hipLaunchKernelGGL(k_word_popc64, dim3(s.grid(nwl)), dim3(kBlk), 0, st, (const uint64_t *)seen.p, nwl, pc.p);
+        // this rank's edges of the forward reach: their groups, and the sources of the backward BFS
+        const auto a = std::lower_bound(fwd.begin(), fwd.end(), id_lo), b = std::lower_bound(fwd.begin(), fwd.end(), id_lo + n);
+        const std::vector<uint64_t> sm(a, b);
+        HIP_OK(hipMemsetAsync(reg.p, 0, reg.bytes(), st));
+        HIP_OK(hipMemsetAsync(seen.p, 0, seen.bytes(), st));
+        const uint64_t m = sm.size();
+        DevBuf<uint64_t> ids(m + 1), front(m + 1);
+        if (m) {
+            h2d(ctx, ids.p, sm.data(), 8 * m);
+            hipLaunchKernelGGL(k_bfs_seed, dim3(s.grid(m)), dim3(kBlk), 0, st, (const uint64_t *)ids.p, m, id_lo, n,
+                               (const uint64_t *)gs.p, reg.p, seen.p, front.p);
             LAUNCH_OK();
-            size_t tmp = 0;
-            HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, pc.p, wpre.p, (size_t)(nwl + 1), st));
-            DevBuf<uint8_t> t(tmp);
-            HIP_OK(hipcub::DeviceScan::ExclusiveSum(t.p, tmp, pc.p, wpre.p, (size_t)(nwl + 1), st));
-            d2h(ctx, &nseen, wpre.p + nwl, 8);
         }
-        DevBuf<uint64_t> front(nseen + 1);
-        if (nseen) {
-            // local indices of the seen edges, via the list kernel's id column
-            DevBuf<uint64_t> rec(4 * nseen);
-            hipLaunchKernelGGL(k_region_list, dim3(s.grid(nwl * 64)), dim3(kBlk), 0, st, (const uint64_t *)seen.p, n,
-                               (const uint64_t *)wpre.p, (uint64_t)0, (const uint64_t *)g->out_info.p,
-                               (const uint64_t *)g->in_info.p, (const uint16_t *)g->mult.p, (const uint64_t *)g->valid.p,
-                               rec.p);
-            LAUNCH_OK();
-            std::vector<uint64_t> h(4 * nseen), li(nseen);
-            d2h(ctx, h.data(), rec.p, 32 * nseen);
-            for (uint64_t j = 0; j < nseen; ++j) li[j] = h[4 * j];
-            h2d(ctx, front.p, li.data(), 8 * nseen);
-        }
-        s.bfs(front, nseen, radius, true, gs.p, reg.p, seen.p);
+        s.bfs(front, m, radius, true, gs.p, reg.p, seen.p);
     }
     mcaat_graph fg;
     std::vector<uint64_t> fgid;

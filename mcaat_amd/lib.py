@@ -135,6 +135,7 @@ SIGNATURES = {
     "mcaat_build_graph_sharded": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.POINTER(C.c_void_p)]),
     "mcaat_cycle_finder_comm": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(_CfParams), C.POINTER(C.c_void_p)]),
     "mcaat_arena_check": (C.c_int, [C.c_void_p, C.POINTER(C.c_int64)]),
+    "mcaat_arena_usage": (C.c_int, [C.c_void_p, C.c_int, _u64p, _u64p, _u64p]),
     "mcaat_graph_shard_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), _u64p, _u64p]),
     "mcaat_graph_unshard": (C.c_int, [C.c_void_p, C.c_void_p]),
 }
@@ -282,6 +283,12 @@ class Context:
         out = (C.c_int64 * 3)()
         _check(self._lib.mcaat_arena_check(self.h, out))
         return bool(out[0]), bool(out[1]), int(out[2])
+
+    def arena_usage(self, reset_peak: bool = False) -> Tuple[int, int, int]:
+        """(bytes in use, peak since the last reset, bytes the arena holds) on this GPU."""
+        a, b, c = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
+        _check(self._lib.mcaat_arena_usage(self.h, int(reset_peak), C.byref(a), C.byref(b), C.byref(c)))
+        return a.value, b.value, c.value
 
     def set_knob(self, name: str, value: int) -> None:
         """Size limit that picks a code path (include/mcaat_gpu.h, mcaat_set_knob); value < 0

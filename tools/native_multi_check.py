@@ -101,7 +101,10 @@ def main() -> int:
             reads = M.Reads.synth(ctx, spec)
             g = M.Graph.build(ctx, reads, k)
             reads.free()
+            cf_base = ctx.arena_usage(reset_peak=True)[0]
             res = g.cycle_finder(prm, as_arrays=False)
+            cf_stages = {kk: round(vv, 2) for kk, vv in ctx.stage_times().items()}
+            cf_mem = (cf_base, ctx.arena_usage()[1])
             comm = None
         else:
             comm = make_comm(ctx)
@@ -115,14 +118,18 @@ def main() -> int:
                 g = M.Graph.build_sharded(ctx, comm, mine, k)
                 build_stages = {kk: round(vv, 2) for kk, vv in ctx.stage_times().items()}
             mine.free()
+            cf_base = ctx.arena_usage(reset_peak=True)[0]
             res = g.cycle_finder(prm, comm=comm)
             cf_stages = {kk: round(vv, 2) for kk, vv in ctx.stage_times().items()}
+            cf_mem = (cf_base, ctx.arena_usage()[1])
             g.unshard(comm)  # a per-shard graph is gathered for the checksums (no-op otherwise)
         d = checksums(g, res)
         d["seconds"] = round(time.time() - t0, 1)
+        d["cf_stages_ms"] = cf_stages
+        # device memory of this process: in use as CycleFinder starts (the graph), its peak during it
+        d["cf_hbm_GB"] = {"graph_at_start": round(cf_mem[0] / 1e9, 2), "peak": round(cf_mem[1] / 1e9, 2)}
         if not a.single:
             d["build_stages_ms"] = build_stages
-            d["cf_stages_ms"] = cf_stages
         g.free()
         if comm is not None:
             comm.barrier()
