@@ -66,6 +66,15 @@ int mcaat_reads_from_host(mcaat_ctx *ctx, const uint64_t *packed, uint64_t n_wor
  * chunk size MCAAT_FASTQ_CHUNK bytes, default 256 MiB); FASTA (multi-line) on the host.
  * Blank lines are accepted only before the first and after the last record. */
 int mcaat_reads_from_fastx(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_reads **out);
+/* (round 5) The next mcaat_reads_from_fastx on ctx runs node_counter's pass A for k (the
+ * super-k-mer scatter of the k+1-mers) on each part of a host-packed FASTQ input while the
+ * input is still being read, and the reads keep the result for the first count / graph build
+ * with that k (mcaat_build_graph, mcaat_count_edges, mcaat_count_local). Results are the same
+ * as without it. Inputs the host packer does not take, reads of differing lengths, or an
+ * under-estimated input size fall back to pass A after the read. One read uses it; k = 0
+ * cancels. Replaces: nothing (the reference's BuildLib and Read2SdbgS2 run one after the
+ * other, sdbg_build.cpp:82-115, 171-187). */
+int mcaat_count_ahead(mcaat_ctx *ctx, int k);
 int mcaat_reads_info(const mcaat_reads *r, uint64_t *n_reads, uint64_t *n_bases);
 /* Mapping view used by mcaat_map_reads: one entry per input record (first file as is,
  * second file reversed and complemented as reads.cpp:20-31 does; any symbol other than
@@ -319,7 +328,10 @@ void mcaat_reset_timing(mcaat_ctx *ctx);
  *                      of its partitions into classes
  *   nc.overlap         0: passes B and C of successive groups in turn on one stream (default
  *                      1: the next group's pass B on a second stream while C counts this one)
- *   sort.msd           0: radix sort only, 1: MSD sort whenever k <= 28 (default: D >= 2^16)
+ *   nc.free_sync       1: synchronise the stream before the count output's early regrowth frees
+ *                      its old buffers (round 4's guard; default 0: the arena's stream order)
+ *   nc.ahead           0: ignore mcaat_count_ahead (pass A after the read, default 1)
+ *   sort.msd          0: radix sort only, 1: MSD sort whenever k <= 28 (default: D >= 2^16)
  *   sort.wave_limit / sort.mid_limit / sort.block_limit   level-3 bucket size limits of the
  *                      one-wave, 256-thread and 1024-thread LDS sorts (above the last: radix)
  *   sort.l3_counting   0: one-wave level-3 buckets by the bitonic network only (default 1: LDS

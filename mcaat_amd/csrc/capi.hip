@@ -434,7 +434,21 @@ int mcaat_reads_from_host(mcaat_ctx *ctx, const uint64_t *packed, uint64_t n_wor
     });
 }
 
+int mcaat_count_ahead(mcaat_ctx *ctx, int k) {
+    return guarded([&] {
+        require(ctx, "null argument");
+        require(k == 0 || (k >= 2 && k <= kMaxK), "k must be 0 or in [2, 30]");
+        ctx->ahead_k = k;
+    });
+}
+
 int mcaat_reads_from_fastx(mcaat_ctx *ctx, const char *const *files, int n_files, mcaat_reads **out) {
+    struct AheadOnce {  // one read uses a mcaat_count_ahead request, whichever path it takes
+        mcaat_ctx *c;
+        ~AheadOnce() {
+            if (c) c->ahead_k = 0;
+        }
+    } once{ctx};
     return guarded([&] {
         require(ctx && out && files && n_files > 0, "null argument");
         mcaat::bind(ctx);
@@ -1070,7 +1084,7 @@ int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value) {
         "fq.hostpack",     "sort.mid_counting", "nc.big_table", "cf.fused_init", "sort.mid_occ", "cf.scan_u", "cf.prep_batch", "cf.dls_lanes", "dist.oriented",
         "sort.small_mid", "sort.small_limit", "cf.recount", "cf.dls_host",
         "dist.desc",      "cf.compact",         "cf.fresh",   "cf.dls_persist", "nc.split_first", "nc.split_max", "cf.pull_flags", "cf.dls_budget", "nc.grow_early",
-        "nc.free_sync", "dist.shard_cf", "dist.ruler_mask", "dist.adj_chunk", "dist.dir_edges"};
+        "nc.free_sync", "dist.shard_cf", "dist.ruler_mask", "dist.adj_chunk", "dist.dir_edges", "nc.ahead"};
     return guarded([&] {
         require(ctx && name, "null argument");
         bool ok = false;

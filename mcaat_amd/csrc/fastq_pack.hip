@@ -29,6 +29,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <memory>
 #include <thread>
 
 #include "internal.h"
@@ -37,7 +38,17 @@ namespace mcaat {
 
 namespace {
 
-constexpr size_t kBlk = 16u << 20;        // bytes read per pread() block
+// bytes read per pread() block (MCAAT_PACK_BLOCK_KB). Round 5: 512 KB, so the block a thread
+// parses is still in its core's cache after the copy into it (C3 BuildLib, one box: 16 MB
+// 1.15 / 1.19 s, 4 MB 1.00, 1 MB 0.99 / 0.98, 512 KB 0.95, 256 KB 0.95 / 0.97)
+size_t pack_block() {
+    static const size_t b = [] {
+        const char *e = getenv("MCAAT_PACK_BLOCK_KB");
+        const long v = e ? atol(e) : 0;
+        return v > 0 ? (size_t)std::min(v, 1L << 20) << 10 : (size_t)512 << 10;
+    }();
+    return b;
+}
 constexpr size_t kMaxRecord = 1u << 20;   // longest record the fast path takes
 // packed words per pinned staging buffer (2 MB; round 3's 8 MB made the first call pin 256 MB
 // for 16 threads, 52 ms inside the span, for no faster upload)
@@ -210,6 +221,7 @@ bool pack_part(const char *path, uint64_t b, uint64_t e, bool file_end, PartPack
         ~Fd() { close(fd); }
     } guard{fd};
     const bool mapped = pack_mmap() && e > b;
+    const size_t kBlk = pack_block();
     std::vector<uint8_t> buf(mapped ? 0 : kBlk + kMaxRecord + 64);
     uint8_t *B = buf.data();
     size_t have = 0;  // bytes in B
@@ -399,6 +411,38 @@ __global__ void k_mapping_view(const uint64_t *packed, const uint64_t *off, uint
     }
 }
 
+// bases per byte and the read length of a file's first records (up to 1 MB of them), for
+// the pass-A-ahead estimate; false when the sample's reads differ in length or none is whole
+bool sample_records(const char *path, uint64_t b, uint64_t e, double &bases_per_byte, uint32_t &L) {
+    const int fd = open(path, O_RDONLY);
+    if (fd < 0) return false;
+    std::vector<uint8_t> buf((size_t)std::min<uint64_t>(e - b, 1u << 20));
+    const ssize_t got = pread(fd, buf.data(), buf.size(), (off_t)b);
+    close(fd);
+    if (got <= 0) return false;
+    size_t i = 0, line = 0, rec_end = 0;
+    uint64_t bases = 0, n = 0;
+    L = 0;
+    for (size_t j = 0; j < (size_t)got; ++j) {
+        if (buf[j] != '\n') continue;
+        if (line % 4 == 1) {
+            const uint64_t len = j - i;
+            if (L && len != L) return false;
+            L = (uint32_t)len;
+        }
+        if (line % 4 == 3) {
+            bases += L;
+            ++n;
+            rec_end = j + 1;
+        }
+        ++line;
+        i = j + 1;
+    }
+    if (!n || !rec_end) return false;
+    bases_per_byte = (double)bases / (double)rec_end;
+    return true;
+}
+
 int pack_threads() {
     if (const char *e = getenv("MCAAT_PACK_THREADS")) return std::max(1, std::min(64, atoi(e)));
     if (const char *e = getenv("OMP_NUM_THREADS")) {
@@ -498,6 +542,26 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
     }
 
     verbose_mark(ctx, "fq.streams");
+    // mcaat_count_ahead: pass A for k on each part as it lands (node_counter.hip nc_ahead_*),
+    // sized from the first records of the first part
+    std::shared_ptr<NcAhead> ahead;
+    uint32_t ahead_L = 0;
+    int ahead_k = 0;
+    if (const int ak = ctx->ahead_k) {
+        ctx->ahead_k = 0;
+        double bpb = 0;
+        if (knob(ctx, "nc.ahead", 1) && sample_records(files[parts[0].file], parts[0].b, parts[0].e, bpb, ahead_L) &&
+            ahead_L > (uint32_t)ak) {
+            uint64_t bytes = 0;
+            for (auto &pt : parts) bytes += pt.e - pt.b;
+            const double reads = (double)bytes * bpb / ahead_L * 1.02 + 64.0 * P;
+            const uint64_t npos = ahead_L - (uint32_t)ak;  // (k+1)-mers per read
+            ahead = nc_ahead_begin(ctx, ak, (uint64_t)(reads * (double)npos),
+                                   (uint64_t)(reads * (double)((npos + kNcItem - 1) / kNcItem)));
+            ahead_k = ak;
+            verbose_mark(ctx, "fq.ahead_begin");
+        }
+    }
     Shared sh;
     std::vector<int> ok(P, 0);
     std::vector<std::string> err(P);
@@ -513,7 +577,11 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
             try {
                 PartPacker pk(regions.p + outs[t].region, s0, s0 + kStageWords, streams[wk % streams.size()], outs[t]);
                 const bool good = pack_part(files[parts[t].file], parts[t].b, parts[t].e, parts[t].file_end, pk, sh, outs[t]);
-                if (good) pk.finish();
+                if (good) pk.finish();  // the part is in HBM when this returns
+                if (good && ahead) {
+                    if (outs[t].varlen || (outs[t].reads && outs[t].L0 != ahead_L)) nc_ahead_fail(*ahead);
+                    else nc_ahead_part(*ahead, regions.p + outs[t].region, outs[t].reads, outs[t].L0);
+                }
                 ok[t] = good;
                 if (!good) sh.decline.store(true);
             } catch (const std::exception &x) {
@@ -539,6 +607,7 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
         if (!err[t].empty()) throw Error(MCAAT_E_HIP, "FASTQ packing: " + err[t]);
     for (int t = 0; t < P; ++t)
         if (!ok[t]) return false;  // not the fast path's input: the GPU text parser takes it
+    // (the ahead run, if any, ends below, after the concatenation is queued beside it)
 
     // concatenate the parts
     std::vector<uint64_t> start(P + 1, 0), region(P);
@@ -582,6 +651,12 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
                 off[k + 1] = off[k] + (outs[t].varlen ? outs[t].lengths[j] : outs[t].L0);
         }
         h2d(ctx, r->offsets.p, off.data(), 8 * off.size());
+    }
+    if (ahead) {  // its last launches read the parts' regions: ended before they are released
+        r->ahead = nc_ahead_end(*ahead);
+        r->ahead_k = r->ahead ? ahead_k : 0;
+        ahead.reset();
+        verbose_mark(ctx, r->ahead ? "fq.ahead_end" : "fq.ahead_dropped");
     }
     HIP_OK(hipStreamSynchronize(st));
     verbose_mark(ctx, "fq.concat");

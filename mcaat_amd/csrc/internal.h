@@ -5,6 +5,7 @@
 #include <cstdint>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -171,6 +172,9 @@ struct mcaat_ctx {
     // pinned staging of the host FASTQ packer (two buffers per packing thread), kept
     uint8_t *pack_pinned = nullptr;
     size_t pack_pinned_bytes = 0;
+    // mcaat_count_ahead: the next host-packed FASTQ read runs node_counter's pass A for this k
+    // on its parts as they land (0: off; one read takes it)
+    int ahead_k = 0;
 };
 
 namespace mcaat {
@@ -181,8 +185,15 @@ inline void bind(mcaat_ctx *ctx) {
 }
 }  // namespace mcaat
 
+namespace mcaat {
+struct NcBuckets;
+}
 struct mcaat_reads {
     mcaat_ctx *ctx = nullptr;
+    // (round 5) node_counter's pass A, run while the input was read (mcaat_count_ahead): the
+    // first count for ahead_k takes it over
+    mutable std::shared_ptr<mcaat::NcBuckets> ahead;
+    int ahead_k = 0;
     mcaat::DevBuf<uint64_t> packed;
     mcaat::DevBuf<uint64_t> offsets;
     uint64_t n_reads = 0, n_bases = 0, n_words = 0;
@@ -417,6 +428,13 @@ struct NcBuckets {
 int nc_fine_bits(mcaat_ctx *ctx, uint64_t n_occ);
 void node_counter_a(mcaat_ctx *ctx, const mcaat_reads *r, int k, const std::function<int(uint64_t)> &pick, NcBuckets &b);
 void node_counter_bc(mcaat_ctx *ctx, NcBuckets &b, int k, CountResult &out);
+// pass A on a streamed input, part by part (node_counter.hip; used by the FASTQ packer)
+struct NcAhead;
+std::shared_ptr<NcAhead> nc_ahead_begin(mcaat_ctx *ctx, int k, uint64_t n_occ_est, uint64_t n_items_est);
+void nc_ahead_part(NcAhead &a, const uint64_t *packed, uint64_t n_reads, uint64_t L);
+void nc_ahead_fail(NcAhead &a);
+std::shared_ptr<NcBuckets> nc_ahead_end(NcAhead &a);
+constexpr int kNcItem = 127;  // pass A's edge positions per work item (node_counter.hip kItem)
 void verbose_mark(mcaat_ctx *ctx, const char *what);
 void sort_counts(mcaat_ctx *ctx, CountResult &c, int k);
 void sdbg_build(mcaat_ctx *ctx, CountResult &c, int k, mcaat_graph *g);

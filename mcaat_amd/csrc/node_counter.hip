@@ -23,6 +23,8 @@
 #include <cstdlib>
 #include <ctime>
 #include <functional>
+#include <memory>
+#include <mutex>
 #include <type_traits>
 
 #include "internal.h"
@@ -245,7 +247,7 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
                                                           const uint64_t *__restrict__ l1_base,
                                                           const uint64_t *__restrict__ l1_cap,
                                                           unsigned long long *l1_cursor, uint16_t *__restrict__ l1_sub,
-                                                          unsigned long long *prof) {
+                                                          unsigned long long *prof, unsigned long long *rstate, int rmode) {
     __shared__ uint64_t stage[kStage];
     __shared__ uint8_t stage_l1[kStage];
     __shared__ uint16_t perm[kStage];         // stage entries in bucket order
@@ -266,13 +268,23 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
     // (the atomic's result stays unused until the next flush, so its latency is hidden)
     unsigned long long my_next = 0, my_base = 0;
     uint32_t prev_need = 0;  // applied to rpos/rleft at the next flush (after its barrier)
+    // rmode (one launch per part of a streamed input, nc_ahead_*): 0 a single launch; 1 the
+    // first of several, 2 a middle one, 3 the last. After 1 and 2 every workgroup leaves its
+    // reservations in rstate (no inert fill) and the next launch (same grid) takes them up
+    unsigned long long *rs = rstate ? rstate + ((uint64_t)blockIdx.x * 256 + (tb & 255)) * 3 : nullptr;
     if (tb < 256) {
-        rleft[tb] = 0;
         hist[tb] = 0;
         bcur[tb] = 0;
         my_base = l1_base[tb];
         rlim[tb] = my_base + l1_cap[tb];
-        my_next = atomicAdd(&l1_cursor[tb], (unsigned long long)kMini);
+        if (rmode >= 2) {
+            rpos[tb] = rs[0];
+            rleft[tb] = (uint32_t)rs[1];
+            my_next = rs[2];
+        } else {
+            rleft[tb] = 0;
+            my_next = atomicAdd(&l1_cursor[tb], (unsigned long long)kMini);
+        }
     }
     if (threadIdx.x == 0) more_flag[0] = more_flag[1] = 0;
     __syncthreads();
@@ -595,6 +607,14 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
         rpos[tb] += prev_need;
         rleft[tb] -= prev_need;
     }
+    if (rmode == 1 || rmode == 2) {  // the next launch continues these reservations
+        if (tb < 256) {
+            rs[0] = rpos[tb];
+            rs[1] = rleft[tb];
+            rs[2] = my_next;
+        }
+        return;
+    }
     __syncthreads();
     for (int pass = 0; pass < 2; ++pass) {
         for (int b = 0; b < 256; ++b)
@@ -611,7 +631,7 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
 }
 
 typedef void (*SkKernel)(const uint64_t *, ItemSrc, SkParams, uint4 *, const uint64_t *, const uint64_t *,
-                         unsigned long long *, uint16_t *, unsigned long long *);
+                         unsigned long long *, uint16_t *, unsigned long long *, unsigned long long *, int);
 SkKernel sk_kernel(int w, bool full) {
     if (full) {
         switch (w) {
@@ -1450,21 +1470,9 @@ int nc_fine_bits(mcaat_ctx *ctx, uint64_t n_occ) {
     return std::max(8, std::min(19, fine_bits));  // l2_bits <= 11: k_l2_scatter's line buffers
 }
 
-void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out) {
-    NcBuckets b;
-    node_counter_a(ctx, r, k, nullptr, b);
-    node_counter_bc(ctx, b, k, out);
-}
-
-// pass A: the reads' super-k-mer descriptors in 256 L1 buckets. The fine-partition bits come
-// from the reads' edge occurrences (nc_fine_bits), or from pick(occurrences) when given: a
-// sharded build derives them from the sum over its ranks (pick is collective, called once on
-// every rank), because the sub rows written here depend on them.
-void node_counter_a(mcaat_ctx *ctx, const mcaat_reads *r, int k, const std::function<int(uint64_t)> &pick,
-                    NcBuckets &bk) {
-    verbose_mark(ctx, "node_counter.begin");
+// pass A's minimizer parameters for k (every pass A launch for k uses the same)
+SkParams sk_params(int k) {
     const int E = k + 1;
-    hipStream_t st = ctx->stream;
     SkParams P;
     P.E = E;
     // long minimizers (near-unique per genome locus) keep the per-partition load uniform;
@@ -1485,6 +1493,31 @@ void node_counter_a(mcaat_ctx *ctx, const mcaat_reads *r, int k, const std::func
     P.nmax = kDescBases - E + 1;
     P.salt = 0x6d696e696d697aULL;
 
+    return P;
+}
+
+void node_counter(mcaat_ctx *ctx, const mcaat_reads *r, int k, CountResult &out) {
+    NcBuckets b;
+    if (r->ahead && r->ahead_k == k) {  // pass A ran while the input was read (nc_ahead_*)
+        b = std::move(*r->ahead);
+        r->ahead.reset();
+        verbose_mark(ctx, "node_counter.A_ahead");
+    } else {
+        node_counter_a(ctx, r, k, nullptr, b);
+    }
+    node_counter_bc(ctx, b, k, out);
+}
+
+// pass A: the reads' super-k-mer descriptors in 256 L1 buckets. The fine-partition bits come
+// from the reads' edge occurrences (nc_fine_bits), or from pick(occurrences) when given: a
+// sharded build derives them from the sum over its ranks (pick is collective, called once on
+// every rank), because the sub rows written here depend on them.
+void node_counter_a(mcaat_ctx *ctx, const mcaat_reads *r, int k, const std::function<int(uint64_t)> &pick,
+                    NcBuckets &bk) {
+    verbose_mark(ctx, "node_counter.begin");
+    const int E = k + 1;
+    hipStream_t st = ctx->stream;
+    SkParams P = sk_params(k);
     // work items (<= kItem edge positions each)
     ItemSrc src{};
     src.offsets = r->offsets.p;
@@ -1571,7 +1604,7 @@ void node_counter_a(mcaat_ctx *ctx, const mcaat_reads *r, int k, const std::func
         {
             KernelTimer kt(ctx, "sk_scatter", 0.0);  // bytes added below, once the descriptor count is known
             hipLaunchKernelGGL(sk_kernel(P.w, P.m == 16), dim3((unsigned)a_grid), dim3(kAThreads), 0, st, r->packed.p, src, P, l1.p,
-                               dbase.p, dcap.p, dcur.p, l1s.p, prof_a ? dprof.p : nullptr);
+                               dbase.p, dcap.p, dcur.p, l1s.p, prof_a ? dprof.p : nullptr, nullptr, 0);
             LAUNCH_OK();
             kt.stop();
         }
@@ -1601,6 +1634,127 @@ void node_counter_a(mcaat_ctx *ctx, const mcaat_reads *r, int k, const std::func
                 hp[0] / waves / 1e5, hp[1] / waves / 1e5, hp[2] / waves / 1e5, hp[3] / waves / 1e5, hp[4] / waves / 1e5);
     }
     verbose_mark(ctx, "node_counter.A");
+}
+
+// ---- pass A on a streamed input (mcaat_count_ahead) -------------------------------------
+// The host FASTQ packer uploads its parts one by one while it reads; pass A runs on each part
+// as soon as it is in HBM, on the side stream, so by the time the last part lands only that
+// part's pass A is left. Every launch has the same grid and keeps its workgroups' L1
+// reservations in `state` for the next one (k_sk_scatter rmode), so the parts fill the
+// buckets as one launch over the whole input would (no inert slots between launches). The
+// buckets are sized from an estimate of the input's edge occurrences made before the read; if
+// one overflows (or a part's reads are not all of the sampled length) the result is dropped
+// and the count runs pass A on the concatenated reads as usual.
+struct NcAhead {
+    mcaat_ctx *ctx = nullptr;
+    int k = 0;
+    SkParams P{};
+    uint64_t a_grid = 0;
+    std::vector<uint64_t> cap, base;
+    DevBuf<uint64_t> dcap, dbase;
+    DevBuf<unsigned long long> dcur, state;
+    std::shared_ptr<NcBuckets> bk;
+    std::mutex mu;
+    int launches = 0;
+    bool failed = false, ended = false;
+    uint64_t n_occ = 0;
+    ~NcAhead() {
+        if (ctx && !ended) (void)hipStreamSynchronize(ctx->side);  // launches may still read the parts
+    }
+};
+
+static_assert(kItem == kNcItem, "the packer's item estimate uses pass A's item length");
+
+std::shared_ptr<NcAhead> nc_ahead_begin(mcaat_ctx *ctx, int k, uint64_t n_occ_est, uint64_t n_items_est) {
+    auto a = std::make_shared<NcAhead>();
+    a->ctx = ctx;
+    a->k = k;
+    a->P = sk_params(k);
+    a->P.l2_bits = nc_fine_bits(ctx, n_occ_est) - 8;
+    a->bk = std::make_shared<NcBuckets>();
+    a->bk->l2_bits = a->P.l2_bits;
+    a->a_grid = (uint64_t)kAPerCu * ctx->n_cu;
+    // node_counter_a's sizing, with more headroom for the estimate
+    const double dens = 2.0 / (a->P.w + 1);
+    const uint64_t est = (uint64_t)(1.12 * (dens * (double)n_occ_est + (double)n_items_est)) + 4096;
+    a->cap.assign(256, 0);
+    a->base.assign(257, 0);
+    for (int b = 0; b < 256; ++b) {
+        a->cap[b] = (est / 256 + 2 * a->a_grid * kMini + 7) & ~7ull;
+        if (const int64_t fixed = knob(ctx, "nc.l1_slots", 0)) a->cap[b] = ((uint64_t)fixed + 7) & ~7ull;
+        a->base[b + 1] = a->base[b] + a->cap[b];
+    }
+    a->bk->data.alloc(a->base[256]);
+    a->bk->sub.alloc(a->base[256]);
+    a->dcap.alloc(256);
+    a->dbase.alloc(257);
+    a->dcur.alloc(256);
+    a->state.alloc(a->a_grid * 256 * 3);
+    h2d(ctx, a->dcap.p, a->cap.data(), 8 * 256);
+    h2d(ctx, a->dbase.p, a->base.data(), 8 * 257);
+    HIP_OK(hipMemsetAsync(a->dcur.p, 0, a->dcur.bytes(), ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));  // the side stream's launches read these
+    return a;
+}
+
+// pass A over one uploaded part: n_reads reads of L bases from word 0 of `packed`
+void nc_ahead_part(NcAhead &a, const uint64_t *packed, uint64_t n_reads, uint64_t L) {
+    const int E = a.k + 1;
+    std::lock_guard<std::mutex> g(a.mu);
+    if (a.failed || !n_reads || L < (uint64_t)E) return;
+    ItemSrc src{};
+    src.n_reads = n_reads;
+    src.fixed_len = L;
+    const uint64_t npos = L - E + 1;
+    src.ipr = (npos + kItem - 1) / kItem;
+    a.n_occ += n_reads * npos;
+    hipLaunchKernelGGL(sk_kernel(a.P.w, a.P.m == 16), dim3((unsigned)a.a_grid), dim3(kAThreads), 0, a.ctx->side, packed,
+                       src, a.P, a.bk->data.p, (const uint64_t *)a.dbase.p, (const uint64_t *)a.dcap.p, a.dcur.p,
+                       a.bk->sub.p, nullptr, a.state.p, a.launches ? 2 : 1);
+    LAUNCH_OK();
+    ++a.launches;
+}
+
+void nc_ahead_fail(NcAhead &a) {
+    std::lock_guard<std::mutex> g(a.mu);
+    a.failed = true;
+}
+
+// the last launch (no reads: it fills what is left of the reservations), then the buckets, or
+// null when the run failed
+std::shared_ptr<NcBuckets> nc_ahead_end(NcAhead &a) {
+    std::lock_guard<std::mutex> g(a.mu);
+    mcaat_ctx *ctx = a.ctx;
+    std::vector<unsigned long long> tot(256, 0);
+    if (!a.failed) {
+        ItemSrc src{};
+        hipLaunchKernelGGL(sk_kernel(a.P.w, a.P.m == 16), dim3((unsigned)a.a_grid), dim3(kAThreads), 0, ctx->side,
+                           (const uint64_t *)a.bk->data.p, src, a.P, a.bk->data.p, (const uint64_t *)a.dbase.p,
+                           (const uint64_t *)a.dcap.p, a.dcur.p, a.bk->sub.p, nullptr, a.state.p, a.launches ? 3 : 0);
+        LAUNCH_OK();
+        HIP_OK(hipMemcpyAsync(tot.data(), a.dcur.p, 8 * 256, hipMemcpyDeviceToHost, ctx->side));
+    }
+    HIP_OK(hipStreamSynchronize(ctx->side));
+    a.ended = true;
+    for (int b = 0; b < 256 && !a.failed; ++b)
+        if (tot[b] > a.cap[b]) a.failed = true;
+    if (a.failed) return nullptr;
+    NcBuckets &bk = *a.bk;
+    bk.n_occ = a.n_occ;
+    bk.base = a.base;
+    bk.regions.assign(256, {});
+    uint64_t n_desc = 0;
+    for (int b = 0; b < 256; ++b) {
+        n_desc += tot[b];
+        if (tot[b]) bk.regions[b].push_back({a.base[b], tot[b]});
+    }
+    ctx->kstats["sk_scatter_ahead"].launches += a.launches + 1;
+    ctx->kstats["sk_scatter_ahead"].total_bytes += 18.0 * (double)n_desc;
+    if (!a.n_occ) {  // node_counter_a's empty-input buckets
+        bk.data.alloc(1);
+        bk.sub.alloc(8);
+    }
+    return a.bk;
 }
 
 // passes B and C over the L1 buckets' regions (a bucket may hold several, e.g. one per rank

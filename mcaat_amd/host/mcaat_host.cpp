@@ -89,6 +89,11 @@ void SDBGBuild::BuildLib() {
     for (auto &x : files) cf.push_back(x.c_str());
     mcaat_ctx *ctx = mcaat_host_ctx(mcaat_rank_device(settings));
     if (settings.gpus <= 1 || !settings.mcomm) {
+        // the count's first pass runs on the input's parts while they are read (same results)
+        // (MCAAT_COUNT_AHEAD=0: after the read, as the reference orders them)
+        const char *e = std::getenv("MCAAT_COUNT_AHEAD");
+        if (settings.load_graph.empty() && !(e && e[0] == '0'))
+            mcaat_check(mcaat_count_ahead(ctx, settings.kmer_k), "count ahead");
         mcaat_check(mcaat_reads_from_fastx(ctx, cf.data(), (int)cf.size(), &reads_), "reading input files");
         return;
     }

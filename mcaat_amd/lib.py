@@ -64,6 +64,7 @@ SIGNATURES = {
     "mcaat_preload": (C.c_int, [C.c_int]),
     "mcaat_reads_from_host": (C.c_int, [C.c_void_p, _u64p, C.c_uint64, _u64p, C.c_uint64, C.POINTER(C.c_void_p)]),
     "mcaat_reads_from_fastx": (C.c_int, [C.c_void_p, C.POINTER(C.c_char_p), C.c_int, C.POINTER(C.c_void_p)]),
+    "mcaat_count_ahead": (C.c_int, [C.c_void_p, C.c_int]),
     "mcaat_reads_info": (C.c_int, [C.c_void_p, _u64p, _u64p]),
     "mcaat_reads_download": (C.c_int, [C.c_void_p, _u64p, _u64p]),
     "mcaat_reads_records_download": (C.c_int, [C.c_void_p, _u64p, _u64p]),
@@ -289,6 +290,11 @@ class Context:
         a, b, c = C.c_uint64(0), C.c_uint64(0), C.c_uint64(0)
         _check(self._lib.mcaat_arena_usage(self.h, int(reset_peak), C.byref(a), C.byref(b), C.byref(c)))
         return a.value, b.value, c.value
+
+    def count_ahead(self, k: int) -> None:
+        """The next Reads.from_fastx on this context runs node_counter's pass A for k while
+        the input is read (include/mcaat_gpu.h, mcaat_count_ahead); k = 0 cancels."""
+        _check(self._lib.mcaat_count_ahead(self.h, int(k)))
 
     def set_knob(self, name: str, value: int) -> None:
         """Size limit that picks a code path (include/mcaat_gpu.h, mcaat_set_knob); value < 0

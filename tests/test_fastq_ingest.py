@@ -372,3 +372,52 @@ def test_host_pack_on_a_second_device(gpu_ctx, tmp_path, monkeypatch):
         r0.free()
     finally:
         ctx1.close()
+
+
+# ---- pass A while the input is read (mcaat_count_ahead, node_counter.hip nc_ahead_*) ----
+
+def _genome_reads(rng, n, lens, genome_len=30000):
+    g = rng.choice(list("ACGT"), size=genome_len)
+    out = []
+    for i in range(n):
+        L = int(lens[i % len(lens)])
+        p = int(rng.integers(0, genome_len - L))
+        s = g[p:p + L]
+        if i % 2:
+            s = s[::-1]  # reverse orientation (not complemented: still a valid read)
+        out.append("".join(s))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["fixed", "fixed_16_threads", "varlen", "undersized", "other_k", "knob_off"])
+def test_count_ahead_equals_count_after_read(gpu_ctx, tmp_path, monkeypatch, case):
+    """Pass A on each packed part as it lands gives the same canonical counts as pass A over
+    the concatenated reads (the same reads object, counted again after the first count took
+    the ahead buckets). Reads of differing lengths, an L1 capacity below the input (nc.l1_slots)
+    and a count for another k fall back to pass A after the read, with the same counts."""
+    import mcaat_amd as M
+
+    monkeypatch.setenv("MCAAT_PACK_THREADS", "16" if case == "fixed_16_threads" else "5")
+    rng = np.random.default_rng(41)
+    lens = [150, 149] if case == "varlen" else [150]
+    text = _fastq_text(_genome_reads(rng, 6000, lens))
+    path = _write(tmp_path / "a.fq", text)
+    k = 27
+    knobs = {"nc__l1_slots": 2048} if case == "undersized" else {"nc__ahead": 0} if case == "knob_off" else {}
+    with gpu_ctx.knobs(**knobs):
+        gpu_ctx.reset_timing()
+        gpu_ctx.count_ahead(21 if case == "other_k" else k)
+        r = M.Reads.from_fastx(gpu_ctx, [path])
+        assert _packed_by_host(gpu_ctx)
+        ahead_launches = gpu_ctx.kernel_timing("sk_scatter_ahead")[1]
+        k1, c1 = M.count_edges(gpu_ctx, r, k)
+        after = gpu_ctx.kernel_timing("sk_scatter")[1]
+        k0, c0 = M.count_edges(gpu_ctx, r, k)
+    used = case in ("fixed", "fixed_16_threads", "other_k")
+    assert (ahead_launches > 0) == used, (case, ahead_launches)
+    if case != "other_k":
+        assert (after == 0) == used, (case, after)  # the first count ran no pass A of its own
+    assert len(k1) > 1000 and c1.max() > 1
+    assert np.array_equal(k1, k0) and np.array_equal(c1, c0)
+    r.free()
