@@ -240,6 +240,8 @@ struct mcaat_graph {
     std::vector<uint64_t> rank_lo, key_split;
     uint64_t dir_base = 0;  // sharded: the local directory's prefixes are (key - dir_base) >> dir_shift
     uint64_t dir_n = 0;     // sharded: its prefix count
+    // sharded: every rank's four target ranges O_W(r) (shard_cf.hip target_ranges), 4 (N + 1) ids
+    std::vector<uint64_t> tgt_lo;
     // search-region replicas (shard_cf.hip): compact id -> edge id, read for FindCycle's frame
     // order (the libstdc++ bucket of an id) and to name results
     mcaat::DevBuf<uint64_t> gid;

@@ -430,6 +430,141 @@ __global__ void __launch_bounds__(kBlk) k_ones(uint64_t *bm, uint64_t n) {
         bm[w] = (w + 1) * 64 <= n ? ~0ULL : (~0ULL >> (64 - (n - w * 64)));
 }
 
+// ---- adjacency by key ranges (round 5, default; dist.adj_ranges=0 keeps the queries above) ----
+// For each W the targets (W, s[1..k-1]) of a sorted run of sources lie in one key range
+// (sdbg_build.hip k_adjacency_own), so rank r's sources target the global id ranges
+// O_W(r) = [lb((W, key[rank_lo[r]] >> 4) << 2), the same for rank r + 1) (rank 0 from the W
+// quarter's start, the last rank to its end), which tile [0, D) over (r, W), and every
+// predecessor of an edge in O_W(r) is a source of rank r (groups do not straddle ranks). So
+// rank r fetches the keys of its four ranges from their owners (contiguous slices, one
+// all-to-all per W), computes out_info of its edges and in_info of its ranges exactly as one
+// GPU does per run (LDS-staged, group-aligned runs), and returns the in_info slices to their
+// owners: 16 B per edge over the links, against four 8-B words of queries and answers per edge.
+__global__ void __launch_bounds__(kBlk) k_count_less(const uint64_t *key, uint64_t n, const uint64_t *qs, int nq,
+                                                     uint64_t *out) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= nq) return;
+    const uint64_t q = qs[t];
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (key[mid] < q) lo = mid + 1;
+        else hi = mid;
+    }
+    out[t] = lo;
+}
+
+struct TgtRanges {  // this rank's four target ranges O_W(r), fetched
+    const uint64_t *key[4];  // their keys
+    uint64_t *in[4];         // their in_info words, computed here
+    uint64_t len[4];
+    uint64_t g0[4];          // global id of the first
+};
+
+__device__ __forceinline__ uint64_t lb_arr(const uint64_t *a, uint64_t n, uint64_t q) {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (a[mid] < q) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+constexpr int kRunT = 1024, kRunB = 2048, kRunMax = kRunB + 16, kRunCap = 3072;
+// bounds[5 r] = local start of run r (group aligned), bounds[5 r + 1 + W] = its first owned
+// position in range W; r = nruns: n and the range ends
+__global__ void __launch_bounds__(kBlk) k_run_bounds(const uint64_t *key, uint64_t n, int k, TgtRanges T, uint64_t nruns,
+                                                     uint64_t *bounds) {
+    const uint64_t top = (uint64_t)1 << (2 * (k - 1));
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r <= nruns; r += stride) {
+        uint64_t s = r * kRunB;
+        if (r == nruns || s >= n) s = n;
+        else if (s > 0) {
+            const uint64_t g0 = key[s - 1] >> 4;
+            while (s < n && (key[s] >> 4) == g0) ++s;
+        }
+        bounds[5 * r] = s;
+        for (int W = 0; W < 4; ++W) {
+            uint64_t b;
+            if (r == 0) b = 0;
+            else if (s >= n) b = T.len[W];
+            else b = lb_arr(T.key[W], T.len[W], (((uint64_t)W * top) | (key[s] >> 4)) << 2);
+            bounds[5 * r + 1 + W] = b;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(kRunT) k_adj_ranges(const uint64_t *key, uint64_t id_lo, int k, TgtRanges T,
+                                                      const uint64_t *bounds, uint64_t *out_info) {
+    __shared__ uint64_t own[kRunMax];
+    __shared__ uint64_t okey[kRunCap];
+    __shared__ uint64_t ist[kRunCap];
+    const uint64_t r = blockIdx.x;
+    const uint64_t s0 = bounds[5 * r], s1 = bounds[5 * (r + 1)];
+    uint64_t a[4];
+    uint32_t len[4], off[4], tot = 0;
+#pragma unroll
+    for (int W = 0; W < 4; ++W) {
+        a[W] = bounds[5 * r + 1 + W];
+        len[W] = (uint32_t)(bounds[5 * (r + 1) + 1 + W] - a[W]);
+        off[W] = tot;
+        tot += len[W];
+    }
+    const uint32_t n = (uint32_t)(s1 - s0);
+    const bool staged = tot <= (uint32_t)kRunCap;
+    for (uint32_t j = threadIdx.x; j < n; j += kRunT) own[j] = key[s0 + j];
+#pragma unroll
+    for (int W = 0; W < 4; ++W)
+        for (uint32_t i = threadIdx.x; i < len[W]; i += kRunT) {
+            if (staged) {
+                okey[off[W] + i] = T.key[W][a[W] + i];
+                ist[off[W] + i] = 0;
+            } else {
+                T.in[W][a[W] + i] = 0;
+            }
+        }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < n; j += kRunT) {
+        const uint64_t K = own[j];
+        const uint32_t W = (uint32_t)(K & 3);
+        const uint64_t Rt = ((uint64_t)W << (2 * (k - 1))) | (K >> 4), qk = Rt << 2;
+        uint64_t lo;
+        unsigned m = 0;
+        if (staged) {
+            const uint64_t *rk = okey + off[W];
+            const uint32_t x = (uint32_t)lb_arr(rk, len[W], qk);
+            lo = a[W] + x;
+            for (uint32_t i = x; i < len[W] && (rk[i] >> 2) == Rt; ++i) m |= 1u << (rk[i] & 3);
+        } else {
+            lo = lb_arr(T.key[W], T.len[W], qk);
+            for (uint64_t i = lo; i < T.len[W] && (T.key[W][i] >> 2) == Rt; ++i) m |= 1u << (T.key[W][i] & 3);
+        }
+        out_info[s0 + j] = (T.g0[W] + lo) | ((uint64_t)m << kIdxBits);
+        if (!m) continue;
+        const uint64_t gk = K >> 4;
+        uint32_t gs = j;
+        while (gs > 0 && (own[gs - 1] >> 4) == gk) --gs;
+        unsigned pm = 0;
+        int t = 0;
+        for (uint32_t q = gs; q < n && (own[q] >> 4) == gk && t < 16; ++q, ++t)
+            if ((own[q] & 3) == W) pm |= 1u << t;
+        if ((uint32_t)(__ffs(pm) - 1) != j - gs) continue;  // another in-edge of the node writes
+        const uint64_t v = (id_lo + s0 + gs) | ((uint64_t)pm << kIdxBits);
+        const int deg = __popc(m);
+        if (staged)
+            for (int q = 0; q < deg; ++q) ist[off[W] + (uint32_t)(lo - a[W]) + q] = v;
+        else
+            for (int q = 0; q < deg; ++q) T.in[W][lo + q] = v;
+    }
+    if (!staged) return;
+    __syncthreads();
+#pragma unroll
+    for (int W = 0; W < 4; ++W)
+        for (uint32_t i = threadIdx.x; i < len[W]; i += kRunT) T.in[W][a[W] + i] = ist[off[W] + i];
+}
+
 // ---------------------------------------------------------------- CycleFinder, D-wide
 // CollectTips (fresh graph: an edge without out-edges) and InvalidateMultiplicityOneNodes,
 // one wave per 64 local edges
@@ -515,6 +650,116 @@ __global__ void __launch_bounds__(kBlk) k_win_apply(const uint8_t *dest, const u
     }
 }
 
+// ---- the windows and flags by target ranges (round 5, default; dist.win_ranges=0: messages) ----
+// The filtered out-window of an edge lies in its target range, so the owners' filter bits of the
+// four ranges are pulled once (a byte per edge); what an edge tells its successors (unary /
+// branch predecessor flags) and ChunkStartNodes' in-degree test of a node (decided by its
+// predecessor group, which lives with the group's rank) are computed for the ranges' edges
+// here and pushed to their owners as one byte per edge.
+constexpr uint8_t kCandPre = 0x80;
+__device__ __forceinline__ void or_byte(uint8_t *a, uint64_t i, uint32_t v) {
+    atomicOr((unsigned int *)(a + (i & ~3ULL)), v << (8 * (i & 3)));
+}  // pushed byte: the node's filter-valid in-degree test passed
+struct TgtBytes {
+    const uint8_t *pb[4];  // filter bits of the range's edges (pulled)
+    uint8_t *tf[4];        // flag / candidate bytes for them (pushed)
+    uint64_t g0[4];
+    uint64_t len[4];
+};
+
+__global__ void __launch_bounds__(kBlk) k_post_bytes(const uint64_t *post, uint64_t n, uint8_t *pb) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) pb[i] = (uint8_t)bit_of(post, i);
+}
+
+// kind (filtered out-window) and the unary successor of every filter-valid edge
+__global__ void __launch_bounds__(kBlk) k_out_win(const uint64_t *post, const uint64_t *key, const uint64_t *out_info,
+                                                  uint64_t n, TgtBytes T, uint8_t *kind, uint64_t *nx) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (!bit_of(post, i)) continue;
+        const uint64_t oi = out_info[i];
+        const int cnt = __popc((unsigned)(oi >> kIdxBits) & 0xF);
+        if (!cnt) continue;
+        const int W = (int)(key[i] & 3);
+        const uint8_t *b = T.pb[W] + ((oi & kIdM) - T.g0[W]);
+        uint32_t pm = 0;
+        for (int q = 0; q < cnt; ++q) pm |= (uint32_t)b[q] << q;
+        kind[i] = (uint8_t)pm;
+        if (__popc(pm) == 1) nx[i] = (oi & kIdM) + (uint64_t)(__ffs(pm) - 1);
+    }
+}
+
+// per local edge: post-filter tips that are not seeds (counts[2]) and the predecessor flags of its
+// filter-valid successors; per group (its first edge): for each W of the group, the in-degree test
+// of the W-edges' common target node (at least two filter-valid predecessors, the node not one of
+// them: _IncomingNotEqualToCurrentNode), into the target bytes
+__global__ void __launch_bounds__(kBlk) k_push_bytes(const uint64_t *post, const uint64_t *seed, const uint64_t *key,
+                                                     const uint64_t *out_info, const uint8_t *kind, uint64_t n,
+                                                     uint64_t id_lo, TgtBytes T, unsigned long long *cnt) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    unsigned long long tpf = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t K = key[i];
+        const bool pv = bit_of(post, i);
+        if (pv) {
+            const uint32_t pm = kind[i] & 0xF;
+            const int od = __popc(pm);
+            if (od == 0 && !bit_of(seed, i)) ++tpf;
+            if (od) {
+                const int W = (int)(K & 3);
+                const uint64_t y0 = (out_info[i] & kIdM) - T.g0[W];
+                for (int b = 0; b < 4; ++b)
+                    if ((pm >> b) & 1) or_byte(T.tf[W], y0 + b, od == 1 ? kUpred : kBpred);
+            }
+        }
+        if (i > 0 && (key[i - 1] >> 4) == (K >> 4)) continue;  // not its group's first edge
+        // the group: up to 16 edges sharing K >> 4
+        uint32_t pmw[4] = {0, 0, 0, 0}, inw[4] = {0, 0, 0, 0};
+        uint64_t first[4] = {kNo, kNo, kNo, kNo};
+        for (int t = 0; t < 16 && i + t < n; ++t) {
+            const uint64_t x = key[i + t];
+            if ((x >> 4) != (K >> 4)) break;
+            const int W = (int)(x & 3);
+            pmw[W] |= 1u << t;
+            if (bit_of(post, i + t)) inw[W] |= 1u << t;
+            if (first[W] == kNo) first[W] = i + t;
+        }
+        const uint64_t gs = id_lo + i;
+        for (int W = 0; W < 4; ++W) {
+            if (first[W] == kNo || __popc(inw[W]) < 2) continue;
+            const uint64_t oi = out_info[first[W]];
+            const int deg = __popc((unsigned)(oi >> kIdxBits) & 0xF);
+            const uint64_t lo = oi & kIdM;
+            for (int q = 0; q < deg; ++q) {
+                const uint64_t t = lo + q;
+                const bool self = t >= gs && t - gs < 16 && ((inw[W] >> (t - gs)) & 1);
+                if (!self) or_byte(T.tf[W], t - T.g0[W], kCandPre);
+            }
+        }
+    }
+    block_add(cnt + 2, tpf);
+}
+
+// the pushed bytes of the local edges: predecessor flags into kind, the in-degree test into the
+// candidate bits (with the edge's own conditions: filter-valid, above the threshold)
+__global__ void __launch_bounds__(kBlk) k_recv_bytes(const uint8_t *inb, const uint64_t *post, const uint16_t *mult,
+                                                     uint64_t thr, uint64_t n, uint8_t *kind, uint64_t *cbits) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (n + 63) / 64, wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nw; w += wstride) {
+        const uint64_t i = w * 64 + lane;
+        bool c = false;
+        if (i < n) {
+            const uint8_t b = inb[i];
+            if (b & (kUpred | kBpred)) kind[i] |= b & (kUpred | kBpred);
+            c = (b & kCandPre) && bit_of(post, i) && (uint64_t)mult[i] > thr;
+        }
+        const unsigned long long m = __ballot(c);
+        if (lane == 0) cbits[w] = m;
+    }
+}
+
 // post-filter tips that are not seeds (counts[2]); predecessor flags as messages to the
 // successors, four slots per local edge: id | 1 << 62 from a unary edge, id | 1 << 63 from a branch
 __global__ void __launch_bounds__(kBlk) k_flag_msgs(const uint64_t *post, const uint64_t *seed, const uint8_t *kind,
@@ -538,9 +783,6 @@ __global__ void __launch_bounds__(kBlk) k_flag_msgs(const uint64_t *post, const 
     block_add(cnt + 2, tpf);
 }
 
-__device__ __forceinline__ void or_byte(uint8_t *a, uint64_t i, uint32_t v) {
-    atomicOr((unsigned int *)(a + (i & ~3ULL)), v << (8 * (i & 3)));
-}
 
 __global__ void __launch_bounds__(kBlk) k_flag_apply(const uint64_t *q, uint64_t m, uint64_t id_lo, uint8_t *kind) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -1190,6 +1432,147 @@ std::vector<uint64_t> to_compact(const std::vector<uint64_t> &hgid, const std::v
 }  // namespace
 
 // ---------------------------------------------------------------- sharded adjacency
+namespace {
+void finish_valid(mcaat_ctx *ctx, mcaat_graph *g) {
+    const uint64_t n = g->D_local;
+    g->valid.alloc(mcaat_graph::bitmap_words(n));
+    HIP_OK(hipMemsetAsync(g->valid.p, 0, g->valid.bytes(), ctx->stream));
+    if (n) {
+        hipLaunchKernelGGL(k_ones, dim3(grid_for((n + 63) / 64, kBlk)), dim3(kBlk), 0, ctx->stream, g->valid.p, n);
+        LAUNCH_OK();
+    }
+    g->all_valid = true;
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+}
+
+// O_W(r) for every rank: O[W * (N + 1) + r] (kept in g->tgt_lo)
+std::vector<uint64_t> target_ranges(mcaat_ctx *ctx, Comm &comm, const mcaat_graph *g) {
+    hipStream_t st = ctx->stream;
+    const int k = g->k, N = comm.world;
+    const uint64_t n = g->D_local, D = g->D;
+    // every rank's first key (empty ranks: the next rank's, or none)
+    uint64_t fk = ~0ULL;
+    if (n) d2h(ctx, &fk, g->key.p, 8);
+    const std::vector<uint64_t> first = comm.allgather_one(fk);
+    const uint64_t top = (uint64_t)1 << (2 * (k - 1));
+    // queries q[W][r], r = 0..N: the start of O_W(r); the global lower bound = sum over ranks of
+    // their local count below q (q past the key space: D)
+    std::vector<uint64_t> qs(4 * (N + 1));
+    for (int W = 0; W < 4; ++W)
+        for (int r = 0; r <= N; ++r) {
+            uint64_t f = ~0ULL;
+            for (int x = r; x < N && f == ~0ULL; ++x) f = first[x];
+            uint64_t t;
+            if (r == 0) t = (uint64_t)W * top;
+            else if (r == N || f == ~0ULL) t = (uint64_t)(W + 1) * top;
+            else t = ((uint64_t)W * top) | (f >> 4);
+            qs[W * (N + 1) + r] = t << 2;
+        }
+    std::vector<uint64_t> cl(qs.size(), 0);
+    if (n) {
+        DevBuf<uint64_t> dq(qs.size()), dc(qs.size());
+        h2d(ctx, dq.p, qs.data(), 8 * qs.size());
+        hipLaunchKernelGGL(k_count_less, dim3(grid_for(qs.size(), kBlk)), dim3(kBlk), 0, st, (const uint64_t *)g->key.p, n,
+                           (const uint64_t *)dq.p, (int)qs.size(), dc.p);
+        LAUNCH_OK();
+        d2h(ctx, cl.data(), dc.p, 8 * cl.size());
+    }
+    const std::vector<uint64_t> all = comm.allgather_vec(cl);
+    std::vector<uint64_t> O(qs.size(), 0);  // O[W * (N + 1) + r]
+    for (size_t i = 0; i < qs.size(); ++i) {
+        if (qs[i] >> (2 * (k + 1))) {
+            O[i] = D;
+            continue;
+        }
+        for (int x = 0; x < N; ++x) O[i] += all[x * qs.size() + i];
+    }
+    return O;
+}
+
+// contiguous-range exchanges over the target ranges: pull = the values of O_W(R)'s edges from
+// their owners; push = values computed here for O_W(R)'s edges to their owners
+struct RangeX {
+    Comm &comm;
+    int N, R;
+    const std::vector<uint64_t> &lo;  // rank_lo
+    const std::vector<uint64_t> &O;
+    uint64_t a(int W, int r) const { return O[W * (N + 1) + r]; }
+    uint64_t len(int W) const { return a(W, R + 1) - a(W, R); }
+    // es-byte elements: local[n] -> out[len(W)]
+    void pull(const void *local, size_t es, int W, void *out) const {
+        std::vector<uint64_t> sb(N), so(N), rb(N), ro(N);
+        for (int q = 0; q < N; ++q) {
+            // to q: my elements inside O_W(q); from q: q's elements inside O_W(R)
+            const uint64_t s0 = std::max(a(W, q), lo[R]), s1 = std::min(a(W, q + 1), lo[R + 1]);
+            sb[q] = s1 > s0 ? es * (s1 - s0) : 0;
+            so[q] = s1 > s0 ? es * (s0 - lo[R]) : 0;
+            const uint64_t r0 = std::max(a(W, R), lo[q]), r1 = std::min(a(W, R + 1), lo[q + 1]);
+            rb[q] = r1 > r0 ? es * (r1 - r0) : 0;
+            ro[q] = r1 > r0 ? es * (r0 - a(W, R)) : 0;
+        }
+        comm.alltoallv_dev(local, sb.data(), out, rb.data(), so.data(), ro.data());
+    }
+    // in[len(W)] -> local[n]
+    void push(const void *in, size_t es, int W, void *local) const {
+        std::vector<uint64_t> sb(N), so(N), rb(N), ro(N);
+        for (int q = 0; q < N; ++q) {
+            const uint64_t s0 = std::max(a(W, R), lo[q]), s1 = std::min(a(W, R + 1), lo[q + 1]);
+            sb[q] = s1 > s0 ? es * (s1 - s0) : 0;
+            so[q] = s1 > s0 ? es * (s0 - a(W, R)) : 0;
+            const uint64_t r0 = std::max(a(W, q), lo[R]), r1 = std::min(a(W, q + 1), lo[R + 1]);
+            rb[q] = r1 > r0 ? es * (r1 - r0) : 0;
+            ro[q] = r1 > r0 ? es * (r0 - lo[R]) : 0;
+        }
+        comm.alltoallv_dev(in, sb.data(), local, rb.data(), so.data(), ro.data());
+    }
+};
+
+// out_info / in_info of the rank's edges through its four target ranges (k_adj_ranges above)
+void adjacency_by_ranges(mcaat_ctx *ctx, Comm &comm, mcaat_graph *g) {
+    hipStream_t st = ctx->stream;
+    const int k = g->k, R = comm.rank;
+    const uint64_t n = g->D_local, id_lo = g->id_lo;
+    KernelTimer kt(ctx, "adjacency", 32.0 * (double)n);
+    g->tgt_lo = target_ranges(ctx, comm, g);
+    const RangeX X{comm, comm.world, R, g->rank_lo, g->tgt_lo};
+    // fetch the keys of O_W(R) from their owners, one all-to-all per W
+    DevBuf<uint64_t> tk[4], ti[4];
+    TgtRanges T{};
+    for (int W = 0; W < 4; ++W) {
+        const uint64_t a = X.a(W, R), b = X.a(W, R + 1);
+        tk[W].alloc(b - a + 1);
+        ti[W].alloc(b - a + 1);
+        X.pull(g->key.p, 8, W, tk[W].p);
+        T.key[W] = tk[W].p;
+        T.in[W] = ti[W].p;
+        T.len[W] = b - a;
+        T.g0[W] = a;
+    }
+    // runs of the own edges, then out_info and the ranges' in_info
+    const uint64_t nruns = (n + kRunB - 1) / kRunB;
+    if (nruns) {
+        DevBuf<uint64_t> bounds(5 * (nruns + 1));
+        hipLaunchKernelGGL(k_run_bounds, dim3(grid_for(nruns + 1, kBlk)), dim3(kBlk), 0, st, (const uint64_t *)g->key.p, n, k,
+                           T, nruns, bounds.p);
+        LAUNCH_OK();
+        hipLaunchKernelGGL(k_adj_ranges, dim3((unsigned)nruns), dim3(kRunT), 0, st, (const uint64_t *)g->key.p, id_lo, k, T,
+                           (const uint64_t *)bounds.p, g->out_info.p);
+        LAUNCH_OK();
+    } else {
+        for (int W = 0; W < 4; ++W)  // no sources: the ranges (empty or not) have no predecessors here
+            if (T.len[W]) HIP_OK(hipMemsetAsync(ti[W].p, 0, 8 * T.len[W], st));
+    }
+    for (int W = 0; W < 4; ++W) tk[W].release();
+    // the in_info slices back to their owners
+    for (int W = 0; W < 4; ++W) X.push(ti[W].p, 8, W, g->in_info.p);
+    kt.stop();
+    if (verbose())
+        fprintf(stderr, "[mcaat] shard %d: adjacency of %llu edges by key ranges (%llu + %llu + %llu + %llu target keys)\n",
+                R, (unsigned long long)n, (unsigned long long)T.len[0], (unsigned long long)T.len[1],
+                (unsigned long long)T.len[2], (unsigned long long)T.len[3]);
+}
+}  // namespace
+
 void sdbg_finish_sharded(mcaat_ctx *ctx, Comm &comm, mcaat_graph *g) {
     hipStream_t st = ctx->stream;
     const int k = g->k;
@@ -1213,6 +1596,11 @@ void sdbg_finish_sharded(mcaat_ctx *ctx, Comm &comm, mcaat_graph *g) {
     LAUNCH_OK();
     g->out_info.alloc(n ? n : 1);
     g->in_info.alloc(n ? n : 1);
+    if (knob(ctx, "dist.adj_ranges", 1)) {
+        adjacency_by_ranges(ctx, comm, g);
+        finish_valid(ctx, g);
+        return;
+    }
     Router rt(ctx, comm);
     const Owners o = owners_of(g, comm);
     // chunks of edges: two queries each; every rank takes part in as many exchanges
@@ -1246,14 +1634,7 @@ void sdbg_finish_sharded(mcaat_ctx *ctx, Comm &comm, mcaat_graph *g) {
         }
     }
     kt.stop();
-    g->valid.alloc(mcaat_graph::bitmap_words(n));
-    HIP_OK(hipMemsetAsync(g->valid.p, 0, g->valid.bytes(), st));
-    if (n) {
-        hipLaunchKernelGGL(k_ones, dim3(grid_for((n + 63) / 64, kBlk)), dim3(kBlk), 0, st, g->valid.p, n);
-        LAUNCH_OK();
-    }
-    g->all_valid = true;
-    HIP_OK(hipStreamSynchronize(st));
+    finish_valid(ctx, g);
     if (verbose())
         fprintf(stderr, "[mcaat] shard %d: adjacency of %llu edges, %llu exchanges, %llu queries\n", comm.rank,
                 (unsigned long long)n, (unsigned long long)rt.rounds, (unsigned long long)rt.records);
@@ -1291,6 +1672,50 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
     const uint64_t chunk = (uint64_t)std::max<int64_t>(1024, knob(ctx, "dist.adj_chunk", 1LL << 26));
     uint64_t n_chunks = (n + chunk - 1) / chunk;
     for (uint64_t x : comm.allgather_one(n_chunks)) n_chunks = std::max(n_chunks, x);
+    if (knob(ctx, "dist.win_ranges", 1)) {
+        n_chunks = 0;  // (the message form below is skipped)
+        if (g->tgt_lo.empty()) g->tgt_lo = target_ranges(ctx, comm, g);
+        const RangeX X{comm, comm.world, comm.rank, g->rank_lo, g->tgt_lo};
+        TgtBytes T{};
+        DevBuf<uint8_t> tpb[4], tf[4];
+        {
+            DevBuf<uint8_t> pb(n + 1);
+            if (n) {
+                hipLaunchKernelGGL(k_post_bytes, dim3(s.grid(n)), dim3(kBlk), 0, st, (const uint64_t *)post.p, n, pb.p);
+                LAUNCH_OK();
+            }
+            for (int W = 0; W < 4; ++W) {
+                const uint64_t len = X.len(W);
+                tpb[W].alloc(len + 8);
+                tf[W].alloc(len + 8);
+                HIP_OK(hipMemsetAsync(tf[W].p, 0, tf[W].bytes(), st));
+                X.pull(pb.p, 1, W, tpb[W].p);
+                T.pb[W] = tpb[W].p;
+                T.tf[W] = tf[W].p;
+                T.g0[W] = X.a(W, comm.rank);
+                T.len[W] = len;
+            }
+        }
+        if (n) {
+            hipLaunchKernelGGL(k_out_win, dim3(s.grid(n)), dim3(kBlk), 0, st, (const uint64_t *)post.p,
+                               (const uint64_t *)g->key.p, (const uint64_t *)g->out_info.p, n, T, kind.p, nx.p);
+            LAUNCH_OK();
+            hipLaunchKernelGGL(k_push_bytes, dim3(s.grid(n)), dim3(kBlk), 0, st, (const uint64_t *)post.p,
+                               (const uint64_t *)seed.p, (const uint64_t *)g->key.p, (const uint64_t *)g->out_info.p,
+                               (const uint8_t *)kind.p, n, id_lo, T, cnt.p);
+            LAUNCH_OK();
+        }
+        for (int W = 0; W < 4; ++W) tpb[W].release();
+        DevBuf<uint8_t> inb(n + 1);
+        HIP_OK(hipMemsetAsync(inb.p, 0, inb.bytes(), st));
+        for (int W = 0; W < 4; ++W) X.push(tf[W].p, 1, W, inb.p);
+        if (n) {
+            hipLaunchKernelGGL(k_recv_bytes, dim3(s.grid(nwl * 64)), dim3(kBlk), 0, st, (const uint8_t *)inb.p,
+                               (const uint64_t *)post.p, (const uint16_t *)g->mult.p, (uint64_t)p.threshold_multiplicity,
+                               n, kind.p, cbits.p);
+            LAUNCH_OK();
+        }
+    }
     for (uint64_t c = 0; c < n_chunks; ++c) {
         const uint64_t a0 = std::min(n, c * chunk), a1 = std::min(n, a0 + chunk), m = a1 - a0;
         DevBuf<uint64_t> q(2 * m + 1);

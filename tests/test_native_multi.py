@@ -99,7 +99,11 @@ def _ranks(world, comm, extra=(), timeout=600):
                                          # per-shard peel with every unary edge a ruler / sparse rulers,
                                          # adjacency and window exchanges in many small chunks
                                          (2, ("--knob", "dist.ruler_mask=0")), (3, ("--knob", "dist.ruler_mask=1023")),
-                                         (3, ("--knob", "dist.adj_chunk=1024"))])
+                                         (3, ("--knob", "dist.adj_chunk=1024", "--knob", "dist.adj_ranges=0")),
+                                         # adjacency, filter windows and flags by request / response
+                                         # messages (round 5's first form) instead of target ranges
+                                         (2, ("--knob", "dist.adj_ranges=0", "--knob", "dist.win_ranges=0")),
+                                         (3, ("--knob", "dist.win_ranges=0"))])
 def test_sharded_build_and_cycle_finder_ranks_share_one_gpu(world, extra):
     """(round 5: per-shard CycleFinder by default) the sharded build + CycleFinder over 1-4 ranks
     sharing the GPU equal the one-GPU path: keys, multiplicities, valid bits after CycleFinder,

@@ -31,8 +31,10 @@ ONE = {"adjacency": ["k_adjacency_own", "k_own_bounds", "k_dir"],
                     "k_peel_final", "k_peel_branch", "k_peel_apply_list", "k_peel_apply_rulers", "k_popcount",
                     "k_still_valid", "k_peel_init"],
        "searches": ["k_dls", "k_dls_lanes", "k_findcycle"]}
-SHARD = {"adjacency": ["k_sdir", "k_adj_queries", "k_adj_answer", "k_adj_store", "k_ones"],
+SHARD = {"adjacency": ["k_sdir", "k_adj_queries", "k_adj_answer", "k_adj_store", "k_ones", "k_count_less", "k_run_bounds",
+                       "k_adj_ranges"],
          "cf_dwide": ["k_sh_filter", "k_win_req", "k_win_ans", "k_win_apply", "k_flag_msgs", "k_flag_apply", "k_prep",
+                      "k_post_bytes", "k_out_win", "k_push_bytes", "k_recv_bytes",
                       "k_bits_list", "k_word_popc64", "k_walk_init", "k_walk", "k_active_rulers", "k_jump_req",
                       "k_jump_ans", "k_jump_apply", "k_jump_cycle", "k_bref_req", "k_bref_ans", "k_bref_req2",
                       "k_res_req", "k_st_ans", "k_res_apply", "k_rm_nonunary", "k_term_req", "k_rm_rulers",
