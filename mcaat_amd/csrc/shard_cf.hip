@@ -43,6 +43,9 @@ constexpr uint64_t kIdM = (1ULL << 40) - 1;  // edge ids
 // kind byte of a local edge: post-filter valid out-edges (4-bit window over the out_info
 // positions), a unary predecessor exists, a branch predecessor exists, ruler
 constexpr uint8_t kUpred = 0x10, kBpred = 0x20, kRuler = 0x40;
+// (round 5, target-range windows) two or more filter-valid unary predecessors: the only edges
+// two ruler walks can both reach, so the only ones a walk claims by compare-and-swap
+constexpr uint8_t kMerge = 0x80;
 constexpr uint8_t kStUnk = 0, kStRem = 1, kStSurv = 2;
 constexpr uint64_t kPad = kNo - 1;  // an unused successor slot of a branch
 
@@ -656,7 +659,7 @@ __global__ void __launch_bounds__(kBlk) k_win_apply(const uint8_t *dest, const u
 // branch predecessor flags) and ChunkStartNodes' in-degree test of a node (decided by its
 // predecessor group, which lives with the group's rank) are computed for the ranges' edges
 // here and pushed to their owners as one byte per edge.
-constexpr uint8_t kCandPre = 0x80;
+constexpr uint8_t kCandPre = 0x80, kMultiPre = 0x01;
 __device__ __forceinline__ void or_byte(uint8_t *a, uint64_t i, uint32_t v) {
     atomicOr((unsigned int *)(a + (i & ~3ULL)), v << (8 * (i & 3)));
 }  // pushed byte: the node's filter-valid in-degree test passed
@@ -690,10 +693,12 @@ __global__ void __launch_bounds__(kBlk) k_out_win(const uint64_t *post, const ui
     }
 }
 
-// per local edge: post-filter tips that are not seeds (counts[2]) and the predecessor flags of its
-// filter-valid successors; per group (its first edge): for each W of the group, the in-degree test
-// of the W-edges' common target node (at least two filter-valid predecessors, the node not one of
-// them: _IncomingNotEqualToCurrentNode), into the target bytes
+// per local edge: post-filter tips that are not seeds (counts[2]); per group (its first edge) and
+// W of the group: the W-edges share their target node, hence their filtered out-window pm, so the
+// node's edges get, from this group alone (their only predecessor group), the predecessor flag of
+// the filter-valid W-edges (unary or branch by popc(pm)) on the pm positions and ChunkStartNodes'
+// in-degree test (at least two filter-valid predecessors, the node not one of them:
+// _IncomingNotEqualToCurrentNode) — one plain byte store per target edge, no atomics
 __global__ void __launch_bounds__(kBlk) k_push_bytes(const uint64_t *post, const uint64_t *seed, const uint64_t *key,
                                                      const uint64_t *out_info, const uint8_t *kind, uint64_t n,
                                                      uint64_t id_lo, TgtBytes T, unsigned long long *cnt) {
@@ -701,40 +706,35 @@ __global__ void __launch_bounds__(kBlk) k_push_bytes(const uint64_t *post, const
     unsigned long long tpf = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint64_t K = key[i];
-        const bool pv = bit_of(post, i);
-        if (pv) {
-            const uint32_t pm = kind[i] & 0xF;
-            const int od = __popc(pm);
-            if (od == 0 && !bit_of(seed, i)) ++tpf;
-            if (od) {
-                const int W = (int)(K & 3);
-                const uint64_t y0 = (out_info[i] & kIdM) - T.g0[W];
-                for (int b = 0; b < 4; ++b)
-                    if ((pm >> b) & 1) or_byte(T.tf[W], y0 + b, od == 1 ? kUpred : kBpred);
-            }
-        }
+        if (bit_of(post, i) && (kind[i] & 0xF) == 0 && !bit_of(seed, i)) ++tpf;
         if (i > 0 && (key[i - 1] >> 4) == (K >> 4)) continue;  // not its group's first edge
-        // the group: up to 16 edges sharing K >> 4
-        uint32_t pmw[4] = {0, 0, 0, 0}, inw[4] = {0, 0, 0, 0};
-        uint64_t first[4] = {kNo, kNo, kNo, kNo};
+        uint32_t inw[4] = {0, 0, 0, 0};
+        uint64_t first[4] = {kNo, kNo, kNo, kNo}, valid_w[4] = {kNo, kNo, kNo, kNo};
         for (int t = 0; t < 16 && i + t < n; ++t) {
             const uint64_t x = key[i + t];
             if ((x >> 4) != (K >> 4)) break;
             const int W = (int)(x & 3);
-            pmw[W] |= 1u << t;
-            if (bit_of(post, i + t)) inw[W] |= 1u << t;
             if (first[W] == kNo) first[W] = i + t;
+            if (bit_of(post, i + t)) {
+                inw[W] |= 1u << t;
+                if (valid_w[W] == kNo) valid_w[W] = i + t;
+            }
         }
         const uint64_t gs = id_lo + i;
         for (int W = 0; W < 4; ++W) {
-            if (first[W] == kNo || __popc(inw[W]) < 2) continue;
+            if (first[W] == kNo) continue;
             const uint64_t oi = out_info[first[W]];
             const int deg = __popc((unsigned)(oi >> kIdxBits) & 0xF);
             const uint64_t lo = oi & kIdM;
+            const uint32_t pm = valid_w[W] != kNo ? kind[valid_w[W]] & 0xF : 0;
+            const uint8_t flag = __popc(pm) == 1 ? kUpred : kBpred;
+            const bool many = __popc(inw[W]) >= 2;
             for (int q = 0; q < deg; ++q) {
                 const uint64_t t = lo + q;
-                const bool self = t >= gs && t - gs < 16 && ((inw[W] >> (t - gs)) & 1);
-                if (!self) or_byte(T.tf[W], t - T.g0[W], kCandPre);
+                uint8_t b = (pm >> q) & 1 ? flag : 0;
+                if (b == kUpred && __popc(inw[W]) >= 2) b |= kMultiPre;  // a merge of unary chains
+                if (many && !(t >= gs && t - gs < 16 && ((inw[W] >> (t - gs)) & 1))) b |= kCandPre;
+                if (b) T.tf[W][t - T.g0[W]] = b;
             }
         }
     }
@@ -752,7 +752,7 @@ __global__ void __launch_bounds__(kBlk) k_recv_bytes(const uint8_t *inb, const u
         bool c = false;
         if (i < n) {
             const uint8_t b = inb[i];
-            if (b & (kUpred | kBpred)) kind[i] |= b & (kUpred | kBpred);
+            if (b & (kUpred | kBpred)) kind[i] |= (b & (kUpred | kBpred)) | (b & kMultiPre ? kMerge : 0);
             c = (b & kCandPre) && bit_of(post, i) && (uint64_t)mult[i] > thr;
         }
         const unsigned long long m = __ballot(c);
@@ -853,7 +853,7 @@ __global__ void __launch_bounds__(kBlk) k_walk_init(const uint64_t *rl, uint64_t
 // before reading its word); walkers advance over this rank's edges and leave for the owner of
 // the next one
 __global__ void __launch_bounds__(kBlk) k_walk(const uint64_t *in, uint64_t m, const uint8_t *kind, uint64_t *nx, Owners o,
-                                               uint64_t *out, uint8_t *dest) {
+                                               uint64_t *out, uint8_t *dest, int merge_known) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x; j0 < m; j0 += stride) {
         const uint64_t j = j0 + threadIdx.x;
@@ -882,7 +882,11 @@ __global__ void __launch_bounds__(kBlk) k_walk(const uint64_t *in, uint64_t m, c
                         res = kRef | x;
                     } else {
                         uint64_t v = nx[li];
-                        if (!is_claim(v)) {
+                        if (!is_claim(v) && merge_known && !(k & kMerge)) {
+                            nx[li] = kOwn | r;  // one unary predecessor: no other walk comes here
+                            x = v;
+                            done = false;
+                        } else if (!is_claim(v)) {
                             const uint64_t prev = atomicCAS((unsigned long long *)&nx[li], v, kOwn | r);
                             if (prev == v) {
                                 x = v;  // claimed: on to the successor
@@ -1672,7 +1676,8 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
     const uint64_t chunk = (uint64_t)std::max<int64_t>(1024, knob(ctx, "dist.adj_chunk", 1LL << 26));
     uint64_t n_chunks = (n + chunk - 1) / chunk;
     for (uint64_t x : comm.allgather_one(n_chunks)) n_chunks = std::max(n_chunks, x);
-    if (knob(ctx, "dist.win_ranges", 1)) {
+    const bool win_ranges = knob(ctx, "dist.win_ranges", 1) != 0;  // (also: merge points known, kMerge)
+    if (win_ranges) {
         n_chunks = 0;  // (the message form below is skipped)
         if (g->tgt_lo.empty()) g->tgt_lo = target_ranges(ctx, comm, g);
         const RangeX X{comm, comm.world, comm.rank, g->rank_lo, g->tgt_lo};
@@ -1799,7 +1804,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
             DevBuf<uint8_t> dest(m ? m : 1);
             if (m) {
                 hipLaunchKernelGGL(k_walk, dim3(s.grid(m)), dim3(kBlk), 0, st, (const uint64_t *)w.p, m,
-                                   (const uint8_t *)kind.p, nx.p, s.o, o2.p, dest.p);
+                                   (const uint8_t *)kind.p, nx.p, s.o, o2.p, dest.p, (int)win_ranges);
                 LAUNCH_OK();
             }
             Routed r;

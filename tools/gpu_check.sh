@@ -3,6 +3,9 @@
 #   bash tools/gpu_check.sh suite                       the whole GPU suite + smoke
 #   bash tools/gpu_check.sh abq [c3|c2|c5] [steps]      quick timing (tools/abq.sh)
 #   bash tools/gpu_check.sh bench                       the driver's default bench line
+#   bash tools/gpu_check.sh rccl1 [c3]                  the sharded build's stages at one RCCL rank
+#                                                       (second build; the exchanges are local copies)
+#   bash tools/gpu_check.sh shard2 [c3]                 2 shm ranks vs one GPU, kernels profiled per rank
 # Every GPU step has its own time limit; the first failure ends the job.
 set -e
 mkdir -p gpurun_out
@@ -22,5 +25,13 @@ case "$what" in
   bench)
     timeout -k 10 900 python -u bench.py > gpurun_out/bench.log 2>&1 || { tail -30 gpurun_out/bench.log; exit 1; }
     tail -1 gpurun_out/bench.log ;;
+  rccl1)
+    rm -f gpurun_out/rccl1.uid
+    timeout -k 10 600 python -u tools/native_multi_check.py --world 1 --rank 0 --comm rccl --uid-file gpurun_out/rccl1.uid \
+      --config ${1:-c3} --repeat 2 --digest gpurun_out/rccl1.json > gpurun_out/rccl1.log 2>&1 || { tail -30 gpurun_out/rccl1.log; exit 1; }
+    rm -f gpurun_out/rccl1.uid
+    tail -2 gpurun_out/rccl1.log ;;
+  shard2)
+    PROF=1 VERB=1 WORLD=2 bash tools/shard_compare.sh ${1:-c3} && python3 tools/prof_compare.py > gpurun_out/prof_w2.txt ;;
   *) echo "unknown job $what"; exit 2 ;;
 esac
