@@ -1342,7 +1342,6 @@ struct ShardCf {
              uint64_t *seen) {
         DevBuf<unsigned long long> c(2);
         for (uint64_t h = 0; h < rounds; ++h) {
-            if (sum(nf) == 0) break;
             DevBuf<uint64_t> q(nf ? nf : 1);
             DevBuf<uint8_t> dest(nf ? nf : 1);
             HIP_OK(hipMemsetAsync(c.p, 0, 16, st));
@@ -1354,6 +1353,7 @@ struct ShardCf {
             }
             Routed r;
             rt.send(q.p, 1, dest.p, nf, r, false);
+            if (!r.total) break;  // every rank's frontier was empty (the routing's count exchange says so)
             // each received window adds at most 16 edges
             DevBuf<uint64_t> next(16 * r.n_in + 1);
             if (r.n_in) {
