@@ -380,7 +380,11 @@ int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value);
 /*   dist.shard_cf     0: the sharded build all-gathers the whole graph on every rank and
  *                      CycleFinder runs over the ranks on replicas (round 4; default 1: per shard)
  *   dist.ruler_mask   per-shard peel: 1 in (mask + 1) unary edges is a ruler besides the chain
- *                      heads (default 15)
+ *                      heads (default 15 up to two ranks, 3 above: fewer walk rounds)
+ *   dist.adj_ranges   0: sharded adjacency by per-edge request / response (default 1: the four
+ *                      target key ranges pulled, in_info pushed back)
+ *   dist.win_ranges   0: the filter windows and predecessor flags as per-edge messages (default 1:
+ *                      target-range bytes pulled and pushed)
  *   dist.adj_chunk    sharded adjacency: edges per request/response exchange (default 2^26)
  *   dist.dir_edges    sharded adjacency: edges per prefix of the range's radix directory (default 2) */
 
