@@ -9,8 +9,11 @@
 //   3. the ranks sum a histogram of the top BOSS-key bits and cut it into owner ranges,
 //      contiguous in BOSS order; the counted canonical edges expand to their oriented edges and
 //      go to their BOSS-range owners (route_oriented, one all-to-all), which sort their ranges;
-//   4. an exact-size all-gather in rank order concatenates the ranges into the single-GPU edge
-//      array (edge ids bit-identical), and every rank builds the adjacency (sdbg_finish).
+//   4. round 5 (default, dist.shard_cf): each rank keeps its range as a sharded graph and builds
+//      its adjacency from its four target key ranges (sdbg_finish_sharded, shard_cf.hip); the
+//      per-shard CycleFinder runs on it. dist.shard_cf=0: an exact-size all-gather in rank order
+//      concatenates the ranges into the single-GPU edge array (edge ids bit-identical), and every
+//      rank builds the whole adjacency (sdbg_finish), round 4's form.
 // dist.desc=0 keeps round 3's route (each rank counts its own reads, partial counts to the owner
 // of the smaller BOSS key, summed there: canon_reduce), dist.oriented=1 round 2's (both
 // orientations with 32-bit partial counts).
