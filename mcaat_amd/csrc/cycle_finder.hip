@@ -957,6 +957,85 @@ __global__ void __launch_bounds__(kBlock) k_dls_lanes(GraphView g, const uint64_
     }
 }
 
+// (round 5) The same search with its visited set and stack in LDS (cf.dls_lds, default): a wave
+// runs kLdsLanes searches, each with a kLdsVis-slot visited table of 32-bit ids (overflow at
+// vmax <= 3/4, as set_insert) and a kLdsStk-entry stack (id + depth byte): 26 KB per 64-thread
+// workgroup, six per CU, one launch for any number of candidates (no scratch). Searches that
+// overflow report -1 and run again with the global-scratch kernel and larger caps, as before;
+// results are the same for any caps that do not overflow. Needs D < 2^32 - 1 (~0 marks an empty
+// slot). Pushed neighbours come from dev_outgoing (valid only), so only the start's validity is
+// tested (the loop's first pop did that). Measured at C5 (3.8 M candidates): 41.7 ms against
+// 42.4 for the global-scratch batches — DepthLevelSearch is bound by its two dependent graph
+// reads per expansion (out_info, then the targets' validity window), not by the visited set or
+// the stack; a variant feeding each lane its next candidate from a counter (so no lane waits
+// for its wave's longest search) took 47.7 ms (fewer resident searches, a ballot per step).
+constexpr int kLdsLanes = 16, kLdsVis = 256, kLdsStk = 128;
+__global__ void __launch_bounds__(64) k_dls_lds(GraphView g, const uint64_t *cand, uint64_t n, int limit, int8_t *res,
+                                                uint32_t vmax, uint32_t smax) {
+    __shared__ uint32_t vis_s[kLdsLanes][kLdsVis];
+    __shared__ uint32_t stk_s[kLdsLanes][kLdsStk];
+    __shared__ uint8_t dep_s[kLdsLanes][kLdsStk];
+    const int lane = threadIdx.x;
+    for (int j = lane; j < kLdsLanes * kLdsVis; j += 64) (&vis_s[0][0])[j] = ~0u;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    if (lane >= kLdsLanes) return;
+    const uint64_t i = (uint64_t)blockIdx.x * kLdsLanes + lane;
+    if (i >= n) return;
+    uint32_t *vis = vis_s[lane];
+    uint32_t *stk = stk_s[lane];
+    uint8_t *dep = dep_s[lane];
+    const uint64_t start = cand[i];
+    if (!bit_get(g.valid, start)) {
+        res[i] = 0;
+        return;
+    }
+    uint32_t sp = 1, vsize = 0;
+    bool over = false;
+    stk[0] = (uint32_t)start;
+    dep[0] = 0;
+    int8_t found = 0;
+    while (sp > 0) {
+        --sp;
+        const uint64_t v = stk[sp];
+        const int depth = dep[sp];
+        uint64_t nb[4];
+        const int od = dev_outgoing(g, v, nb);
+        if (od == 0) continue;  // EdgeOutdegreeZero
+        if (depth >= limit) continue;
+        for (int j = 0; j < od; ++j) {
+            const uint32_t x = (uint32_t)nb[j];
+            uint32_t sl = (uint32_t)(mix64(nb[j]) & (kLdsVis - 1));
+            bool present = false;
+            for (;;) {
+                const uint32_t c = vis[sl];
+                if (c == x) { present = true; break; }
+                if (c == ~0u) break;
+                sl = (sl + 1) & (kLdsVis - 1);
+            }
+            const bool sr = (nb[j] == start && depth > 0);
+            if (!present || sr) {
+                if (!present) {
+                    if (vsize + 1 > vmax) over = true;
+                    else {
+                        vis[sl] = x;
+                        ++vsize;
+                    }
+                }
+                if (sp >= smax) over = true;
+                if (over) break;
+                stk[sp] = x;
+                dep[sp] = (uint8_t)(depth + 1);
+                ++sp;
+            }
+        }
+        if (over) break;
+        if (v == start && depth > 1) { found = 1; break; }
+    }
+    res[i] = over ? -1 : found;
+}
+
 // ---------------------------- FindCycle ----------------------------------------
 struct FcCaps {
     uint32_t P;    // path/frames capacity (max_len + 2)
@@ -1866,7 +1945,26 @@ static std::vector<uint64_t> run_dls_dev(mcaat_graph *g, const uint64_t *dcand, 
     hipLaunchKernelGGL(k_iota, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, idx.p, n);
     LAUNCH_OK();
     uint64_t nt = n;
-    for (bool first = true; nt; first = false) {
+    bool first = true;
+    // (round 5) first pass in LDS (cf.dls_lds, default 1, graphs below 2^32 - 1 edges); what
+    // overflows its tables continues below with global scratch at 8x the first caps
+    if (!persist && knob(ctx, "cf.dls_lds", 1) != 0 && g->D < 0xFFFFFFFFull && limit < 255) {
+        DevBuf<int8_t> r(n);
+        // cf.dls_lds_cap (tests): fewer visited / stack entries, so searches overflow to the re-run
+        const uint32_t lc = (uint32_t)std::max<int64_t>(1, knob(ctx, "cf.dls_lds_cap", kLdsVis));
+        hipLaunchKernelGGL(k_dls_lds, dim3((unsigned)((n + kLdsLanes - 1) / kLdsLanes)), dim3(64), 0, st, g->view(), dcand,
+                           n, limit, r.p, std::min<uint32_t>(lc, kLdsVis / 4 * 3), std::min<uint32_t>(lc, kLdsStk));
+        LAUNCH_OK();
+        hipLaunchKernelGGL(k_scatter_res, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, (const int8_t *)r.p,
+                           (const uint64_t *)idx.p, n, res.p, flags.p);
+        LAUNCH_OK();
+        nt = select_dev(ctx, (const uint64_t *)idx.p, flags.p, n, idx2.p);
+        std::swap(idx, idx2);
+        first = false;
+        cs = std::max<uint32_t>(cs, 8 * kLdsStk);
+        cv = std::max<uint32_t>(cv, 8 * kLdsVis);
+    }
+    for (; nt; first = false) {
         const uint64_t batch_cap = std::max<uint64_t>(64, budget / (8ULL * (cs + cv)));
         const uint64_t *src = dcand;
         if (!first) {  // the candidates to search again, in candidate order

@@ -73,7 +73,7 @@ KNOBS = {
     "scan_u1_prep16": {"cf.scan_u": 1, "cf.prep_batch": 16},
     # DepthLevelSearch with one search per wave and with a full wave of them
     "dls_lanes1": {"cf.dls_lanes": 1},
-    "dls_lanes64": {"cf.dls_lanes": 64, "cf.dls_stack": 1, "cf.dls_visited": 2},
+    "dls_lanes64": {"cf.dls_lanes": 64, "cf.dls_stack": 1, "cf.dls_visited": 2, "cf.dls_lds": 0},
     "sort_block": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_limit": 0},
     "sort_radix": {"sort.msd": 1, "sort.wave_limit": 0, "sort.mid_limit": 0, "sort.block_limit": 0},
     "sort_radix_only": {"sort.msd": 0},
@@ -98,7 +98,11 @@ KNOBS = {
     "recount_pass_regrow": {"cf.recount": 1, "cf.cand_cap": 1},
     # DepthLevelSearch through the host lists, and the device driver's scratch regrowth
     "dls_host": {"cf.dls_host": 1},
-    "dls_dev_regrow": {"cf.dls_stack": 1, "cf.dls_visited": 2},
+    "dls_dev_regrow": {"cf.dls_stack": 1, "cf.dls_visited": 2, "cf.dls_lds": 0},
+    # (round 5) LDS first pass whose tables overflow at 2 entries: nearly every search re-runs
+    # with global scratch; and the global-scratch kernel alone
+    "dls_lds_overflow": {"cf.dls_lds_cap": 2},
+    "dls_global_only": {"cf.dls_lds": 0},
     # the peel's first pass as its own kernel instead of inside the tips / filter pass
     "peel_own_init": {"cf.fused_init": 0},
     # (round 4) peel arrays over compact slots instead of edge ids, with and without the fused
