@@ -103,7 +103,13 @@ struct RcclComm final : Comm {
     }
     ~RcclComm() override {
         if (comm) (void)rccl().CommDestroy(comm);
+        if (pin) (void)hipHostFree(pin);
     }
+    // small host all-gathers (the routers' count exchanges, one per bulk-synchronous round): one
+    // fixed-slot ncclAllGather through pinned staging — the slot carries the size and the payload —
+    // instead of a size all-gather, a data all-gather and four pageable copies
+    static constexpr uint64_t kSmallSlot = 1024;
+    uint8_t *pin = nullptr;  // (world + 1) slots: this rank's, then everyone's
     const char *kind() const override { return "rccl"; }
 
     void sync() { HIP_OK(hipStreamSynchronize(ctx->stream)); }
@@ -126,6 +132,32 @@ struct RcclComm final : Comm {
 
     void allgatherv_host(const void *send, uint64_t bytes, std::vector<uint8_t> &out,
                          std::vector<uint64_t> &sizes) override {
+        // every rank takes the slot path or none: whether it fits is agreed in the slot itself
+        // (a size past the slot sends the size only, and every rank then runs the general path)
+        if (!pin) HIP_OK(hipHostMalloc((void **)&pin, (world + 1) * kSmallSlot, hipHostMallocDefault));
+        {
+            const bool fits = bytes + 8 <= kSmallSlot;
+            memcpy(pin, &bytes, 8);
+            if (fits && bytes) memcpy(pin + 8, send, bytes);
+            DevBuf<uint8_t> a(kSmallSlot), b((uint64_t)world * kSmallSlot);
+            HIP_OK(hipMemcpyAsync(a.p, pin, kSmallSlot, hipMemcpyHostToDevice, ctx->stream));
+            NCCL_OK(rccl().AllGather(a.p, b.p, kSmallSlot, ncclUint8, comm, ctx->stream));
+            HIP_OK(hipMemcpyAsync(pin + kSmallSlot, b.p, (uint64_t)world * kSmallSlot, hipMemcpyDeviceToHost, ctx->stream));
+            sync();
+            sizes.resize(world);
+            bool all = true;
+            for (int r = 0; r < world; ++r) {
+                memcpy(&sizes[r], pin + (uint64_t)(r + 1) * kSmallSlot, 8);
+                if (sizes[r] + 8 > kSmallSlot) all = false;
+            }
+            if (all) {
+                const auto off = offsets_of(sizes.data(), world);
+                out.resize(off[world]);
+                for (int r = 0; r < world; ++r)
+                    if (sizes[r]) memcpy(out.data() + off[r], pin + (uint64_t)(r + 1) * kSmallSlot + 8, sizes[r]);
+                return;
+            }
+        }
         allgather_u64(bytes, sizes);
         const auto off = offsets_of(sizes.data(), world);
         out.resize(off[world]);
