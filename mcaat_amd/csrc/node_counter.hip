@@ -320,7 +320,6 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
     uint64_t s = 0;
     int np = 0, c = 0, ph = 0, nck = 0;
     uint32_t prev_hm = 0, h_open = 0, p7 = 0, ihc = 0, fill = 0, par = 1, bsf = 0;
-    uint32_t *seg32 = (uint32_t *)seg;
     bool active = false;
     auto fetch = [&](uint64_t bt, uint64_t &sb, int &n, uint64_t *w) {
         const uint64_t item = bt * 64 + lane;
@@ -369,8 +368,9 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
                 if (cl) {
                     const uint32_t idx =
                         __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, fill));
-                    seg32[2 * idx] = h_open;
-                    seg32[2 * idx + 1] = p7 + ihc + (uint32_t)i;
+                    // one 8-B LDS store per close (two 4-B stores at a 2-word stride were 2-way
+                    // bank conflicts for consecutive lanes)
+                    seg[idx] = ((uint64_t)(p7 + ihc + (uint32_t)i) << 32) | h_open;
                     p7 = (uint32_t)i << kPeP;
                     h_open = hm[t];
                 }
