@@ -26,6 +26,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <map>
@@ -242,6 +243,12 @@ struct Router {
     mcaat_ctx *ctx;
     Comm &comm;
     uint64_t rounds = 0, records = 0;  // collectives and records moved (diagnostics)
+    // host time per part of a round (MCAAT_VERBOSE diagnostics): grouping kernels + count read,
+    // count all-gather, placement + sync, all-to-all, reply
+    double t_count = 0, t_gather = 0, t_place = 0, t_a2a = 0, t_reply = 0;
+    static double now() {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
     Router(mcaat_ctx *c, Comm &cm) : ctx(c), comm(cm) {}
 
     // n slots (rec: n x W words; dest[i] a rank or kNoDest). keep: a reply follows (dest must
@@ -258,6 +265,7 @@ struct Router {
         DevBuf<uint32_t> cnt((uint64_t)std::max(rt.G, 1) * N);
         rt.base.alloc((uint64_t)std::max(rt.G, 1) * N);
         DevBuf<uint64_t> tot(N);
+        double t0 = now();
         if (n) {
             hipLaunchKernelGGL(k_route_count, dim3(rt.G), dim3(kBlk), 0, st, dest, n, rt.per, N, cnt.p);
             LAUNCH_OK();
@@ -267,7 +275,11 @@ struct Router {
         }
         rt.sent = 0;
         for (uint64_t x : rt.out_cnt) rt.sent += x;
+        double t1 = now();
+        t_count += t1 - t0;
         const std::vector<uint64_t> mat = comm.allgather_vec(rt.out_cnt);
+        t0 = now();
+        t_gather += t0 - t1;
         rt.in_cnt.assign(N, 0);
         rt.n_in = rt.total = 0;
         for (int s2 = 0; s2 < N; ++s2) {
@@ -297,13 +309,22 @@ struct Router {
         }
         sb[R] = rb[R] = 0;  // placed already
         HIP_OK(hipStreamSynchronize(st));
+        t1 = now();
+        t_place += t1 - t0;
         if (N > 1) comm.alltoallv_dev(sendb.p, sb.data(), rt.in.p, rb.data(), so.data(), ro.data());
+        t_a2a += now() - t1;
         ++rounds;
         records += rt.sent;
     }
     // answers (Wa words per received record, in received order) back to their slots: out[slot * Wa ..]
     // (slots without a request keep what out held); this rank's own answers are read in place
     void reply(Routed &rt, uint64_t *ans, int Wa, uint64_t *out) {
+        const double t0 = now();
+        struct Acc {
+            double &t;
+            double t0;
+            ~Acc() { t += now() - t0; }
+        } acc{t_reply, t0};
         hipStream_t st = ctx->stream;
         const int N = comm.world, R = comm.rank;
         DevBuf<uint64_t> back((N > 1 && rt.sent ? rt.sent : 1) * Wa);
@@ -2146,6 +2167,10 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
                 comm.rank, starts.size(), (unsigned long long)fgid.size(), (unsigned long long)s.rt.rounds,
                 (unsigned long long)s.rt.records);
     ctx->kstats["shard_exchanges"].launches = s.rt.rounds;
+    if (verbose())
+        fprintf(stderr, "[mcaat] shard %d: routing host ms: grouping %.1f, count all-gather %.1f, placement %.1f, "
+                        "all-to-all %.1f, replies %.1f\n",
+                comm.rank, s.rt.t_count, s.rt.t_gather, s.rt.t_place, s.rt.t_a2a, s.rt.t_reply);
     mcaat_cycles local;
     cf_find_cycles(&fg, p, to_compact(fgid, starts), &local, &comm);
     for (size_t i = 0; i < local.starts.size(); ++i) {
