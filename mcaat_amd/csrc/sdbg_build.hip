@@ -515,6 +515,37 @@ struct LinePlace {
         nline = lc[b] / kIL;
         bl[b] = nline;
     }
+    // (round 5) the lines completed this round leave the wave cooperatively, as pass B's do
+    // (node_counter.hip k_l2_scatter): kIL lanes per line, one 8-B piece each, so one store
+    // instruction writes 64 / kIL whole lines instead of each completing lane storing its line in
+    // kIL pieces. Called by every lane of the wave (live: the lane has an item here).
+    __device__ __forceinline__ void flush_coop(uint32_t b, uint32_t r, uint32_t line, bool live, bool buffered,
+                                               uint32_t &nline) {
+        const bool done = live && buffered && (r & (kIL - 1)) == kIL - 1;
+        const unsigned long long dm = __ballot(done);
+        const uint32_t lane = threadIdx.x & 63;
+        const uint64_t dst = done ? ((uint64_t)lb[b] + line) * kIL - gbase : 0;
+        const uint32_t src = done ? b * kIL : 0;
+        const int nd = __popcll(dm);
+        for (int b0 = 0; b0 < nd; b0 += 64 / kIL) {
+            const int j = b0 + (int)(lane / kIL);  // the line this lane helps write
+            int pos = 0;                           // lane holding the j-th set bit of dm
+            if (j < nd) {
+#pragma unroll
+                for (int step = 32; step; step >>= 1) {
+                    const unsigned long long below = dm & ((pos + step >= 64) ? ~0ull : ((1ull << (pos + step)) - 1));
+                    if (__popcll(below) <= j) pos += step;
+                }
+            }
+            const uint64_t d = __shfl(dst, pos);
+            const uint32_t sidx = __shfl(src, pos);
+            if (j < nd) out[d + (lane & (kIL - 1))] = buf[sidx + (lane & (kIL - 1))];
+        }
+        if (live) {
+            nline = lc[b] / kIL;
+            bl[b] = nline;
+        }
+    }
     __device__ __forceinline__ void backfill(uint32_t b, uint64_t it, uint32_t r, bool buffered, uint32_t nline) {
         if (!buffered && r / kIL == nline) buf[b * kIL + (r & (kIL - 1))] = it;
     }
@@ -565,7 +596,7 @@ __global__ void __launch_bounds__(kSBlock) k_msd1_scatter(const uint64_t *ckeys,
         if (i < c1) no = msd_items(a, cn, k, bk, it);
         for (int j = 0; j < no; ++j) lp.put(bk[j], it[j], r[j], line[j], bf[j]);
         lds_barrier();
-        for (int j = 0; j < no; ++j) lp.flush(bk[j], r[j], line[j], bf[j], nl[j]);
+        for (int j = 0; j < 2; ++j) lp.flush_coop(bk[j], r[j], line[j], j < no, bf[j], nl[j]);
         lds_barrier();
         for (int j = 0; j < no; ++j) lp.backfill(bk[j], it[j], r[j], bf[j], nl[j]);
     }
@@ -631,7 +662,7 @@ __global__ void __launch_bounds__(kSBlock) k_msd2_scatter(const uint64_t *in, co
             lp.put(b, it, r, line, bf);
         }
         lds_barrier();
-        if (live) lp.flush(b, r, line, bf, nl);
+        lp.flush_coop(b, r, line, live, bf, nl);
         lds_barrier();
         if (live) lp.backfill(b, it, r, bf, nl);
     }
