@@ -39,6 +39,12 @@ struct Comm {
     virtual void alltoallv_dev_segs(const std::vector<std::vector<Seg>> &send, void *out,
                                     const std::vector<std::vector<uint64_t>> &recv) = 0;
 
+    // every rank's n 64-bit words from device memory, in rank order (a bulk-synchronous round's
+    // counts): the default reads them to the host first; RCCL gathers them on the device and
+    // reads the result once
+    // (dev is written by work queued on the context's stream; the transports read it after that)
+    virtual void allgather_dev_words(const uint64_t *dev, int n, std::vector<uint64_t> &out) = 0;
+
     // typed helpers over allgatherv_host
     template <class T>
     std::vector<T> allgather_vec(const std::vector<T> &mine, std::vector<uint64_t> *counts = nullptr) {

@@ -169,6 +169,24 @@ struct RcclComm final : Comm {
         sync();
     }
 
+    void allgather_dev_words(const uint64_t *dev, int n, std::vector<uint64_t> &out) override {
+        out.resize((size_t)world * n);
+        if (!n) return;
+        if (!pin) HIP_OK(hipHostMalloc((void **)&pin, (world + 1) * kSmallSlot, hipHostMallocDefault));
+        if ((uint64_t)n * 8 > kSmallSlot) {  // larger than the pinned slots: through the host
+            std::vector<uint64_t> mine(n);
+            HIP_OK(hipMemcpyAsync(mine.data(), dev, 8 * (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+            sync();
+            out = allgather_vec(mine);
+            return;
+        }
+        DevBuf<uint64_t> b((uint64_t)world * n);
+        NCCL_OK(rccl().AllGather(dev, b.p, 8 * (size_t)n, ncclUint8, comm, ctx->stream));
+        HIP_OK(hipMemcpyAsync(pin, b.p, (uint64_t)world * n * 8, hipMemcpyDeviceToHost, ctx->stream));
+        sync();
+        memcpy(out.data(), pin, (uint64_t)world * n * 8);
+    }
+
     void alltoallv_dev(const void *send, const uint64_t *send_bytes, void *recv, const uint64_t *recv_bytes,
                        const uint64_t *send_off, const uint64_t *recv_off) override {
         auto so = offsets_of(send_bytes, world), ro = offsets_of(recv_bytes, world);
@@ -431,6 +449,13 @@ struct ShmComm final : Comm {
             }
             barrier();
         }
+    }
+
+    void allgather_dev_words(const uint64_t *dev, int n, std::vector<uint64_t> &out) override {
+        need_ctx();  // the stream's writes of dev are done
+        std::vector<uint64_t> mine(n);
+        if (n) HIP_OK(hipMemcpy(mine.data(), dev, 8 * (size_t)n, hipMemcpyDeviceToHost));
+        out = allgather_vec(mine);
     }
 
     void allgatherv_host(const void *send, uint64_t bytes, std::vector<uint8_t> &out,

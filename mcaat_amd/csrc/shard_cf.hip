@@ -271,13 +271,17 @@ struct Router {
             LAUNCH_OK();
             hipLaunchKernelGGL(k_route_offsets, dim3(1), dim3(1024), 0, st, (const uint32_t *)cnt.p, rt.G, N, rt.base.p, tot.p);
             LAUNCH_OK();
-            d2h(ctx, rt.out_cnt.data(), tot.p, 8 * N);
+        } else {
+            HIP_OK(hipMemsetAsync(tot.p, 0, 8 * N, st));
         }
-        rt.sent = 0;
-        for (uint64_t x : rt.out_cnt) rt.sent += x;
         double t1 = now();
         t_count += t1 - t0;
-        const std::vector<uint64_t> mat = comm.allgather_vec(rt.out_cnt);
+        // every rank's send counts straight from the device (one read of the gathered matrix)
+        std::vector<uint64_t> mat;
+        comm.allgather_dev_words(tot.p, N, mat);
+        for (int q = 0; q < N; ++q) rt.out_cnt[q] = mat[(uint64_t)R * N + q];
+        rt.sent = 0;
+        for (uint64_t x : rt.out_cnt) rt.sent += x;
         t0 = now();
         t_gather += t0 - t1;
         rt.in_cnt.assign(N, 0);
@@ -308,7 +312,8 @@ struct Router {
             so[q] = 8ULL * W * rt.out_off[q], ro[q] = 8ULL * W * rt.in_off[q];
         }
         sb[R] = rb[R] = 0;  // placed already
-        HIP_OK(hipStreamSynchronize(st));
+        // (the transports order the exchange after the placement on the context stream: RCCL
+        // queues on it, the shared-memory transport synchronises it first)
         t1 = now();
         t_place += t1 - t0;
         if (N > 1) comm.alltoallv_dev(sendb.p, sb.data(), rt.in.p, rb.data(), so.data(), ro.data());
@@ -334,7 +339,6 @@ struct Router {
             so[q] = 8ULL * Wa * rt.in_off[q], ro[q] = 8ULL * Wa * rt.out_off[q];
         }
         sb[R] = rb[R] = 0;  // read in place
-        HIP_OK(hipStreamSynchronize(st));
         if (N > 1) comm.alltoallv_dev(ans, sb.data(), back.p, rb.data(), so.data(), ro.data());
         if (rt.sent) {
             hipLaunchKernelGGL(k_route_place<true>, dim3(rt.G), dim3(kBlk), 0, st, (const uint64_t *)back.p, Wa, rt.dest,
