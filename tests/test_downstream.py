@@ -219,8 +219,11 @@ def test_downstream_several_arrays_with_errors(tmp_path):
 # gpus > 1: the CLI forks one rank per GPU; on the one-GPU box the ranks share it through the
 # shared-memory transport (FASTQ parts, sharded build, CycleFinder over ranks, gathered reads)
 @pytest.mark.gpu
-@pytest.mark.parametrize("paired,gpus", [(False, 1), (True, 1), (False, 3), (True, 2)])
-def test_cli_crispr_arrays_match_oracle_path(tmp_path, paired, gpus):
+@pytest.mark.parametrize("paired,gpus,ahead", [(False, 1, "1"), (True, 1, "1"), (False, 3, "1"), (True, 2, "1"),
+                                               (True, 1, "0")])
+def test_cli_crispr_arrays_match_oracle_path(tmp_path, paired, gpus, ahead):
+    """(round 5) the single-GPU CLI counts while it reads (mcaat_count_ahead) unless
+    MCAAT_COUNT_AHEAD=0; both give the oracle path's CRISPR_Arrays.txt."""
     spec = M.SynthSpec()
     packed, offs = M.synth_host(spec)
     seqs = [unpack_read(packed, int(offs[i]), int(offs[i + 1])) for i in range(len(offs) - 1)]
@@ -236,8 +239,9 @@ def test_cli_crispr_arrays_match_oracle_path(tmp_path, paired, gpus):
                 f.write(f"@r{i}\n{s}\n+\n{'I' * len(s)}\n")
         files.append(str(p))
     multi = ["--gpus", str(gpus), "--comm", "shm"] if gpus > 1 else []
+    env = dict(os.environ, MCAAT_COUNT_AHEAD=ahead)
     out = subprocess.run([CLI, "-i", *files, "--output-folder", str(tmp_path / "o"), "--threads", "2", "--ram", "2G",
-                          *multi], capture_output=True, text=True, timeout=600)
+                          *multi], capture_output=True, text=True, timeout=600, env=env)
     assert out.returncode == 0, out.stderr + out.stdout[-2000:]
     got = (tmp_path / "o" / "CRISPR_Arrays.txt").read_text()
 

@@ -390,7 +390,7 @@ def _genome_reads(rng, n, lens, genome_len=30000):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("case", ["fixed", "fixed_16_threads", "varlen", "undersized", "other_k", "knob_off"])
+@pytest.mark.parametrize("case", ["fixed", "fixed_16_threads", "varlen", "undersized", "other_k", "knob_off", "paired"])
 def test_count_ahead_equals_count_after_read(gpu_ctx, tmp_path, monkeypatch, case):
     """Pass A on each packed part as it lands gives the same canonical counts as pass A over
     the concatenated reads (the same reads object, counted again after the first count took
@@ -402,19 +402,21 @@ def test_count_ahead_equals_count_after_read(gpu_ctx, tmp_path, monkeypatch, cas
     rng = np.random.default_rng(41)
     lens = [150, 149] if case == "varlen" else [150]
     text = _fastq_text(_genome_reads(rng, 6000, lens))
-    path = _write(tmp_path / "a.fq", text)
+    paths = [_write(tmp_path / "a.fq", text)]
+    if case == "paired":  # two files: the counting view is both in file order
+        paths.append(_write(tmp_path / "b.fq", _fastq_text(_genome_reads(rng, 5000, lens))))
     k = 27
     knobs = {"nc__l1_slots": 2048} if case == "undersized" else {"nc__ahead": 0} if case == "knob_off" else {}
     with gpu_ctx.knobs(**knobs):
         gpu_ctx.reset_timing()
         gpu_ctx.count_ahead(21 if case == "other_k" else k)
-        r = M.Reads.from_fastx(gpu_ctx, [path])
+        r = M.Reads.from_fastx(gpu_ctx, paths)
         assert _packed_by_host(gpu_ctx)
         ahead_launches = gpu_ctx.kernel_timing("sk_scatter_ahead")[1]
         k1, c1 = M.count_edges(gpu_ctx, r, k)
         after = gpu_ctx.kernel_timing("sk_scatter")[1]
         k0, c0 = M.count_edges(gpu_ctx, r, k)
-    used = case in ("fixed", "fixed_16_threads", "other_k")
+    used = case in ("fixed", "fixed_16_threads", "other_k", "paired")
     assert (ahead_launches > 0) == used, (case, ahead_launches)
     if case != "other_k":
         assert (after == 0) == used, (case, after)  # the first count ran no pass A of its own
