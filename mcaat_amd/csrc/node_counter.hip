@@ -215,7 +215,10 @@ __device__ __forceinline__ void window_min(const uint32_t *H, uint32_t *hm) {
     }
 }
 
-constexpr uint32_t kMini = 1024;  // descriptors reserved per (workgroup, L1 bucket) grab
+#ifndef MCAAT_AMINI
+#define MCAAT_AMINI 1024
+#endif
+constexpr uint32_t kMini = MCAAT_AMINI;  // descriptors reserved per (workgroup, L1 bucket) grab
 constexpr uint16_t kDeadSub = 0xffff;  // sub-partition mark of an inert (n = 0) slot
 
 
