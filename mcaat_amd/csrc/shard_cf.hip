@@ -941,13 +941,20 @@ __global__ void __launch_bounds__(kBlk) k_walk(const uint64_t *in, uint64_t m, c
 }
 
 // pointer jumping: requests of the rulers still pointing at a ruler
+// (round 5) a target on this rank is answered here at once (kNoDest: the slot keeps it); the
+// round stays Jacobi, as every rank's apply follows the round's exchange
 __global__ void __launch_bounds__(kBlk) k_jump_req(const uint64_t *al, uint64_t na, const uint64_t *nx, Owners o, uint64_t *q,
                                                    uint8_t *dest) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < na; j += stride) {
         const uint64_t t = nx[al[j]] & kIdM;
-        q[j] = t;
-        dest[j] = (uint8_t)owner_of_id(o, t);
+        if (t >= o.id_lo && t < o.id_lo + o.n) {
+            q[j] = nx[t - o.id_lo];
+            dest[j] = kNoDest;
+        } else {
+            q[j] = t;
+            dest[j] = (uint8_t)owner_of_id(o, t);
+        }
     }
 }
 __global__ void __launch_bounds__(kBlk) k_jump_ans(const uint64_t *q, uint64_t m, const uint64_t *nx, uint64_t id_lo, uint64_t *ans) {
