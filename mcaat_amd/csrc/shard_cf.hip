@@ -49,6 +49,12 @@ constexpr uint8_t kUpred = 0x10, kBpred = 0x20, kRuler = 0x40;
 constexpr uint8_t kMerge = 0x80;
 constexpr uint8_t kStUnk = 0, kStRem = 1, kStSurv = 2;
 constexpr uint64_t kPad = kNo - 1;  // an unused successor slot of a branch
+// (round 5) the successor word of a unary edge carries the edge's own walk kind, so a walk step
+// reads one scattered word instead of the kind byte and the word: kChain on every unary edge that
+// is not a ruler (set with the successor, cleared on rulers by k_prep), kMergeW where several
+// unary chains meet (walks claim it by compare-and-swap)
+constexpr uint64_t kChain = 1ULL << 59, kMergeW = 1ULL << 58;
+__device__ __forceinline__ bool is_chain(uint64_t v) { return v < kPad && (v & kChain) && !(v & (kRef | (1ULL << 61))); }
 
 bool verbose() {
     static const bool v = getenv("MCAAT_VERBOSE") && getenv("MCAAT_VERBOSE")[0] == '1';
@@ -666,7 +672,7 @@ __global__ void __launch_bounds__(kBlk) k_win_apply(const uint8_t *dest, const u
             const int cnt = __popc((unsigned)(oi >> kIdxBits) & 0xF);
             const uint32_t pm = (uint32_t)ans[2 * j] & ((1u << cnt) - 1);
             kind[i] = (uint8_t)pm;  // the flag bits come later (k_flag_apply)
-            if (__popc(pm) == 1) nx[i] = (oi & kIdM) + (uint64_t)(__ffs(pm) - 1);
+            if (__popc(pm) == 1) nx[i] = ((oi & kIdM) + (uint64_t)(__ffs(pm) - 1)) | kChain;
         }
         if (dest[2 * j + 1] != kNoDest) {
             const uint64_t ii = in_info[i], l = ii & kIdM, e = id_lo + i;
@@ -708,13 +714,15 @@ __global__ void __launch_bounds__(kBlk) k_out_win(const uint64_t *post, const ui
         if (!bit_of(post, i)) continue;
         const uint64_t oi = out_info[i];
         const int cnt = __popc((unsigned)(oi >> kIdxBits) & 0xF);
-        if (!cnt) continue;
-        const int W = (int)(key[i] & 3);
-        const uint8_t *b = T.pb[W] + ((oi & kIdM) - T.g0[W]);
         uint32_t pm = 0;
-        for (int q = 0; q < cnt; ++q) pm |= (uint32_t)b[q] << q;
-        kind[i] = (uint8_t)pm;
-        if (__popc(pm) == 1) nx[i] = (oi & kIdM) + (uint64_t)(__ffs(pm) - 1);
+        if (cnt) {
+            const int W = (int)(key[i] & 3);
+            const uint8_t *b = T.pb[W] + ((oi & kIdM) - T.g0[W]);
+            for (int q = 0; q < cnt; ++q) pm |= (uint32_t)b[q] << q;
+            kind[i] = (uint8_t)pm;
+        }
+        // every filter-valid edge's word is written: a walk reads the word first
+        nx[i] = __popc(pm) == 1 ? ((oi & kIdM) + (uint64_t)(__ffs(pm) - 1)) | kChain : kNo;
     }
 }
 
@@ -769,7 +777,7 @@ __global__ void __launch_bounds__(kBlk) k_push_bytes(const uint64_t *post, const
 // the pushed bytes of the local edges: predecessor flags into kind, the in-degree test into the
 // candidate bits (with the edge's own conditions: filter-valid, above the threshold)
 __global__ void __launch_bounds__(kBlk) k_recv_bytes(const uint8_t *inb, const uint64_t *post, const uint16_t *mult,
-                                                     uint64_t thr, uint64_t n, uint8_t *kind, uint64_t *cbits) {
+                                                     uint64_t thr, uint64_t n, uint8_t *kind, uint64_t *nx, uint64_t *cbits) {
     const int lane = threadIdx.x & 63;
     const uint64_t nw = (n + 63) / 64, wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < nw; w += wstride) {
@@ -777,7 +785,11 @@ __global__ void __launch_bounds__(kBlk) k_recv_bytes(const uint8_t *inb, const u
         bool c = false;
         if (i < n) {
             const uint8_t b = inb[i];
-            if (b & (kUpred | kBpred)) kind[i] |= (b & (kUpred | kBpred)) | (b & kMultiPre ? kMerge : 0);
+            if (b & (kUpred | kBpred)) {
+                const uint8_t k = kind[i];
+                kind[i] = k | (b & (kUpred | kBpred)) | (b & kMultiPre ? kMerge : 0);
+                if ((b & kMultiPre) && __popc(k & 0xF) == 1) nx[i] |= kMergeW;
+            }
             c = (b & kCandPre) && bit_of(post, i) && (uint64_t)mult[i] > thr;
         }
         const unsigned long long m = __ballot(c);
@@ -821,7 +833,7 @@ __global__ void __launch_bounds__(kBlk) k_flag_apply(const uint64_t *q, uint64_t
 // the non-unary edges (dead ends: removed iff a seed; branches unresolved); lists of rulers
 // and branches (local indices)
 __global__ void __launch_bounds__(kBlk) k_prep(const uint64_t *post, const uint64_t *seed, uint8_t *kind, uint8_t *st,
-                                               uint64_t n, uint64_t id_lo, uint64_t rmask, uint64_t *rbits,
+                                               uint64_t *nx, uint64_t n, uint64_t id_lo, uint64_t rmask, uint64_t *rbits,
                                                uint64_t *bbits) {
     const int lane = threadIdx.x & 63;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -833,7 +845,10 @@ __global__ void __launch_bounds__(kBlk) k_prep(const uint64_t *post, const uint6
         const bool ruler = pv && od == 1 && (!(k & kUpred) || (mix64((id_lo + i) ^ 0x5eed) & rmask) == 0);
         const bool branch = pv && od >= 2;
         if (pv) {
-            if (ruler) kind[i] = k | kRuler;
+            if (ruler) {
+                kind[i] = k | kRuler;
+                nx[i] &= kIdM;  // a ruler's word is its successor, then its jump
+            }
             st[i] = od == 0 ? (bit_of(seed, i) ? kStRem : kStSurv) : kStUnk;
         }
         const unsigned long long rm = __ballot(ruler), bm = __ballot(branch);
@@ -898,29 +913,32 @@ __global__ void __launch_bounds__(kBlk) k_walk(const uint64_t *in, uint64_t m, c
                         break;
                     }
                     const uint64_t li = x - o.id_lo;
-                    const uint8_t k = kind[li];
+                    uint64_t v = nx[li];
                     uint64_t res = 0;
                     bool done = true;
-                    if (__popc(k & 0xF) != 1) {
-                        res = x;
-                    } else if (k & kRuler) {
-                        res = kRef | x;
-                    } else {
-                        uint64_t v = nx[li];
-                        if (!is_claim(v) && merge_known && !(k & kMerge)) {
-                            nx[li] = kOwn | r;  // one unary predecessor: no other walk comes here
-                            x = v;
+                    if (is_chain(v)) {  // a unary edge, not a ruler, unclaimed
+                        const uint64_t own = kOwn | r;
+                        if (merge_known && !(v & kMergeW)) {
+                            nx[li] = own;  // one unary predecessor: no other walk comes here
+                            x = v & kIdM;
                             done = false;
-                        } else if (!is_claim(v)) {
-                            const uint64_t prev = atomicCAS((unsigned long long *)&nx[li], v, kOwn | r);
+                        } else {
+                            const uint64_t prev = atomicCAS((unsigned long long *)&nx[li], v, own);
                             if (prev == v) {
-                                x = v;  // claimed: on to the successor
+                                x = v & kIdM;  // claimed: on to the successor
                                 done = false;
                             } else {
-                                v = prev;
+                                v = prev;  // another walk's claim
                             }
                         }
-                        if (done) res = (v & kIdM) == r ? kNo : (kRef | (v & kIdM));
+                    }
+                    if (done) {
+                        if (is_claim(v)) {
+                            res = (v & kIdM) == r ? kNo : (kRef | (v & kIdM));
+                        } else {
+                            const uint8_t k = kind[li];  // once per walk: where it ends
+                            res = __popc(k & 0xF) != 1 ? x : (kRef | x);  // a non-unary edge or a ruler
+                        }
                     }
                     if (done) {
                         emit = true;
@@ -1749,10 +1767,11 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
         if (n) {
             hipLaunchKernelGGL(k_recv_bytes, dim3(s.grid(nwl * 64)), dim3(kBlk), 0, st, (const uint8_t *)inb.p,
                                (const uint64_t *)post.p, (const uint16_t *)g->mult.p, (uint64_t)p.threshold_multiplicity,
-                               n, kind.p, cbits.p);
+                               n, kind.p, nx.p, cbits.p);
             LAUNCH_OK();
         }
     }
+    if (n_chunks) HIP_OK(hipMemsetAsync(nx.p, 0xFF, nx.bytes(), st));  // kNo: no successor word
     for (uint64_t c = 0; c < n_chunks; ++c) {
         const uint64_t a0 = std::min(n, c * chunk), a1 = std::min(n, a0 + chunk), m = a1 - a0;
         DevBuf<uint64_t> q(2 * m + 1);
@@ -1819,7 +1838,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
         DevBuf<uint64_t> rbits(nwl + 1), bbits(nwl + 1);
         if (n) {
             hipLaunchKernelGGL(k_prep, dim3(s.grid(nwl * 64)), dim3(kBlk), 0, st, (const uint64_t *)post.p,
-                               (const uint64_t *)seed.p, kind.p, stt.p, n, id_lo, rmask, rbits.p, bbits.p);
+                               (const uint64_t *)seed.p, kind.p, stt.p, nx.p, n, id_lo, rmask, rbits.p, bbits.p);
             LAUNCH_OK();
         }
         nr = s.list_bits(rbits.p, rl);
