@@ -210,7 +210,9 @@ __global__ void __launch_bounds__(kBlock) k_word_pop(const uint64_t *bm, uint64_
 // (valid, mult > thr, at least two valid in-edges, not its own in-edge) into cand (counts[3]
 // counts them all). A removed edge had no valid successor, so the peel changes no surviving
 // edge's valid in-edges: the final candidates are these, still valid after the peel.
-template <int kScanU>
+// (round 5) fresh and pull are template parameters: the default form (fresh, no pull) then keeps
+// none of the other forms' registers (C3: 105 VGPRs, four waves per SIMD, in one kernel for all)
+template <int kScanU, bool kFresh, bool kPull>
 // fresh: every edge is valid before the filter (mcaat_graph::all_valid), so an edge is a tip
 // iff it has no out-edges at all, and no window of the unfiltered bitmap is read
 // pull (round 4, with the peel's arrays): an edge writes its own predecessor flags instead of
@@ -221,12 +223,13 @@ template <int kScanU>
 // filter-valid edge. One 4-byte store per edge, no scattered byte stores and no clearing pass.
 __global__ void __launch_bounds__(kBlock) k_tips_filter(GraphView g, uint64_t w_lo, uint64_t w_hi, uint64_t *tip_bm,
                                                         const uint64_t *post, unsigned long long *counts, PeelArrays pa,
-                                                        uint64_t thr, uint64_t *cand, uint64_t cap, bool fresh, bool pull) {
+                                                        uint64_t thr, uint64_t *cand, uint64_t cap) {
     const int lane = threadIdx.x & 63;
     const uint64_t nw = (g.D + 63) / 64;
     const uint64_t wstride = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const bool peel = pa.nf != nullptr, fold = cand != nullptr;
-    pull = pull && peel;
+    constexpr bool fresh = kFresh;
+    const bool pull = kPull && peel;
     const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     __shared__ uint64_t cbuf[kBlock / 64][128];
     WaveList cl{cbuf[threadIdx.x >> 6], cand, counts + 3, cap};
@@ -2521,10 +2524,16 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
         DevBuf<uint64_t> mseeds;  // this rank's words when the bitmap is gathered
         if (comm) mseeds.alloc(std::max<uint64_t>(w_hi - w_lo, 1));
         if (w_hi > w_lo) {
-            auto kern = scan_u == 1 ? k_tips_filter<1> : scan_u == 4 ? k_tips_filter<4> : k_tips_filter<kScanUDefault>;
+            auto pick = [&](auto su) {
+                constexpr int U = decltype(su)::value;
+                return fresh ? (pull ? k_tips_filter<U, true, true> : k_tips_filter<U, true, false>)
+                             : (pull ? k_tips_filter<U, false, true> : k_tips_filter<U, false, false>);
+            };
+            auto kern = scan_u == 1 ? pick(std::integral_constant<int, 1>{})
+                        : scan_u == 4 ? pick(std::integral_constant<int, 4>{}) : pick(std::integral_constant<int, kScanUDefault>{});
             hipLaunchKernelGGL(kern, dim3(wgrid), dim3(kBlock), 0, st, v, w_lo, w_hi, comm ? mseeds.p : seeds.p + w_lo,
                                (const uint64_t *)post.p, c2.p, fa, (uint64_t)p.threshold_multiplicity,
-                               fold ? clist.p : (uint64_t *)nullptr, ccap, fresh, pull);
+                               fold ? clist.p : (uint64_t *)nullptr, ccap);
             LAUNCH_OK();
         }
         unsigned long long hc[4];
