@@ -235,6 +235,24 @@ def test_bench_regime_sample_matches_oracle(gpu_ctx, name):
     reads.free()
 
 
+def test_repeated_steps_take_no_new_device_memory(gpu_ctx):
+    """(round 5) After one build + CycleFinder, repeating it takes no new arena chunk: every
+    buffer of a step fits in memory the arena already holds (csrc/alloc.hip rounds large chunks
+    up, so a buffer regrown to a slightly different size next step reuses its chunk)."""
+    spec, k, thr = SAMPLES["c2_sample"]
+    reads = M.Reads.synth(gpu_ctx, spec)
+    prm = M.CfParams(threshold_multiplicity=thr)
+    held = []
+    for _ in range(3):
+        g = M.Graph.build(gpu_ctx, reads, k)
+        g.cycle_finder(prm)
+        g.free()
+        held.append(gpu_ctx.arena_usage()[2])
+    reads.free()
+    assert held[0] > 0
+    assert held[1] == held[0] and held[2] == held[0], held
+
+
 # ---- full-size properties (bench configs) ---------------------------------------------
 FULL = {
     # bench.py "c2": 50M PE reads over 400 Mbp (500 arrays), 0.5 % errors -> D > 2^31
