@@ -162,8 +162,37 @@ __device__ __forceinline__ uint64_t win32(uint64_t a, uint64_t b, uint64_t B) {
 
 // hashes of the kCk canonical m-mers starting at the bases 0..kCk-1 of win (m <= 16);
 // FULL: m == 16, so the m-mers need no mask
+#ifndef MCAAT_HTOP
+#define MCAAT_HTOP 1
+#endif
 template <bool FULL>
 __device__ __forceinline__ void hash_step(uint64_t win, int m, uint32_t mmask, uint32_t salt, uint32_t *h) {
+#if MCAAT_HTOP
+    // both m-mers extracted with their bases in the top 2m bits of a 32-bit word (one
+    // alignbit each, none at t = 0; the bits below are other bases), so the mask becomes one
+    // shift after the min: min(f_top, r_top) >> (32 - 2m) == min(f, r) (equal top fields
+    // give equal results whichever one the min takes)
+    const int lo = 32 - 2 * m;
+    const uint64_t Wt = win << lo;          // base j at bits 2j + lo
+    const uint64_t R = rev2_dev(win) ^ ~0ULL;  // complement of base j at bits 62 - 2j
+    const uint32_t wl = (uint32_t)Wt, wh = (uint32_t)(Wt >> 32);
+    const uint32_t rl = (uint32_t)R, rh = (uint32_t)(R >> 32);
+    (void)mmask;
+#pragma unroll
+    for (int t = 0; t < kCk; ++t) {
+        const uint32_t f = t ? __builtin_amdgcn_alignbit(wh, wl, 2 * t) : wl;
+        const uint32_t r = t ? __builtin_amdgcn_alignbit(rh, rl, 32 - 2 * t) : rh;
+        const uint32_t c = FULL ? min(f, r) : min(f, r) >> lo;
+#if MCAAT_HASH == 2
+        h[t] = (c ^ salt) * 0x9E3779B1u;
+#elif MCAAT_HASH == 1
+        uint32_t x = (c ^ salt) * 0x9E3779B1u;
+        h[t] = x ^ (x >> 15);
+#else
+        h[t] = mix32(c ^ salt);
+#endif
+    }
+#else
     const uint64_t R = (rev2_dev(win) ^ ~0ULL) >> (2 * (25 - m));  // rc, aligned for t = 7
     const uint32_t wl = (uint32_t)win, wh = (uint32_t)(win >> 32);
     const uint32_t rl = (uint32_t)R, rh = (uint32_t)(R >> 32);
@@ -186,6 +215,7 @@ __device__ __forceinline__ void hash_step(uint64_t win, int m, uint32_t mmask, u
         h[t] = mix32(min(f, r) ^ salt);
 #endif
     }
+#endif
 }
 
 // minimum over the hashes u .. u+W-1 (u < kCk) of the 3*kCk-entry ring H whose logical
@@ -232,6 +262,9 @@ constexpr int kAPF = MCAAT_APF;  // scan steps of window words in flight (1 or 2
 constexpr int kWB = MCAAT_WB;
 #ifndef MCAAT_WPIPE
 #define MCAAT_WPIPE 0
+#endif
+#ifndef MCAAT_CLOSEMASK
+#define MCAAT_CLOSEMASK 1
 #endif
 constexpr bool kWPipe = MCAAT_WPIPE != 0;  // write phase: the next batch's loads before this batch's stores  // write batch (entries per thread per round: 3 loads each in flight)
 
@@ -291,7 +324,7 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
     }
     if (threadIdx.x == 0) more_flag[0] = more_flag[1] = 0;
     __syncthreads();
-    uint64_t *seg = stage + wave * kSeg;
+    uint64_t *seg = stage + __builtin_amdgcn_readfirstlane(wave * kSeg);  // wave-uniform: a scalar base
     uint8_t *seg_l1 = stage_l1 + wave * kSeg;
     uint32_t nflush = 0;
 
@@ -360,6 +393,33 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
             h_open = hm[0];
             p7 = 0;
         }
+#if MCAAT_CLOSEMASK
+        // the close test as four compares straight into lane masks (no bool materialised
+        // between the ballot and the branch), the closing lanes' region entered on the mask
+        // itself; the entry's hash is the previous position's (a super-k-mer's minimizer hash
+        // is constant from its open to its close), so no open hash is carried. The fill count
+        // is wave-uniform: kept in a scalar register, its additions are scalar
+        fill = __builtin_amdgcn_readfirstlane(fill);
+#pragma unroll
+        for (int t = 0; t < kCk; ++t) {
+            const int i = kCk * c + t;
+            const uint32_t prv = t ? hm[t - 1] : prev_hm;
+            const unsigned long long bm = __builtin_amdgcn_ballot_w64((uint32_t)(i - 1) < (uint32_t)np) &
+                                          (__builtin_amdgcn_ballot_w64(i == np) |
+                                           __builtin_amdgcn_ballot_w64(hm[t] != prv) |
+                                           __builtin_amdgcn_ballot_w64((int)p7 <= (i - nmax) * 128));
+            if (bm) {
+                if (__builtin_amdgcn_inverse_ballot_w64(bm)) {
+                    const uint32_t idx =
+                        __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+                    seg[fill + idx] = ((uint64_t)(p7 + ihc + (uint32_t)i) << 32) | prv;
+                    p7 = (uint32_t)i << kPeP;
+                }
+                fill += (uint32_t)__popcll(bm);
+            }
+        }
+        (void)h_open;
+#else
 #pragma unroll
         for (int t = 0; t < kCk; ++t) {
             const int i = kCk * c + t;
@@ -380,6 +440,7 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
                 fill += (uint32_t)__popcll(bm);
             }
         }
+#endif
         prev_hm = hm[kCk - 1];
     };
 
