@@ -107,7 +107,9 @@ __device__ __forceinline__ uint64_t canon_edge(uint64_t lsb, int E) {
 #define MCAAT_APERCU 3
 #endif
 #ifndef MCAAT_HASH
-#define MCAAT_HASH 1
+// minimizer hash: 2 the multiply alone (default since round 5: sk_scatter -1.5 ms at C3, pass C
+// unchanged at C3 and -2 ms at C5), 1 multiply-xorshift, 0 mix32
+#define MCAAT_HASH 2
 #endif
 constexpr int kAWaves = MCAAT_AWAVES;
 constexpr int kAThreads = kAWaves * 64;
@@ -184,6 +186,9 @@ __device__ __forceinline__ void hash_step(uint64_t win, int m, uint32_t mmask, u
         const uint32_t r = t ? __builtin_amdgcn_alignbit(rh, rl, 32 - 2 * t) : rh;
         const uint32_t c = FULL ? min(f, r) : min(f, r) >> lo;
 #if MCAAT_HASH == 2
+        // a multiply by an odd constant: a bijection whose high bits, which decide the
+        // minimizer order, mix every key bit (the buckets and sub-partitions come from a
+        // re-hash, so the weak low bits do not matter)
         h[t] = (c ^ salt) * 0x9E3779B1u;
 #elif MCAAT_HASH == 1
         uint32_t x = (c ^ salt) * 0x9E3779B1u;
