@@ -152,8 +152,11 @@ struct __attribute__((aligned(8))) u64x2 {
 
 // 2-bit-group reversal by the hardware bit reverse
 __device__ __forceinline__ uint64_t rev2_dev(uint64_t x) {
-    const uint64_t y = __builtin_bitreverse64(x);
-    return ((y >> 1) & 0x5555555555555555ULL) | ((y & 0x5555555555555555ULL) << 1);
+    // per 32-bit half (two 32-bit shifts and one bitfield select each, no 64-bit shifts)
+    const uint32_t lo = __builtin_bitreverse32((uint32_t)(x >> 32)), hi = __builtin_bitreverse32((uint32_t)x);
+    const uint32_t l = ((lo >> 1) & 0x55555555u) | ((lo << 1) & 0xAAAAAAAAu);
+    const uint32_t h = ((hi >> 1) & 0x55555555u) | ((hi << 1) & 0xAAAAAAAAu);
+    return ((uint64_t)h << 32) | l;
 }
 
 // 32 bases starting at absolute base B of the packed stream, from its two words
