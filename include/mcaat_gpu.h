@@ -267,6 +267,13 @@ int mcaat_comm_init_rccl(mcaat_ctx *ctx, int world, int rank, const uint8_t *id,
 int mcaat_comm_init_shm(mcaat_ctx *ctx, int world, int rank, const char *name, uint64_t slot_bytes,
                         mcaat_comm **out);
 int mcaat_comm_info(const mcaat_comm *c, int *world, int *rank);
+/* Host-only self-check of the RCCL segment all-to-all's schedule (csrc/comm.hip seg_schedule, the
+ * function the RCCL transport runs): every rank's schedule for random segment lists of `world`
+ * ranks cut into piece_bytes pieces; checks that each pair's j-th send piece equals the peer's
+ * j-th receive piece and that the pieces tile the segments and the output. *rounds = the most
+ * rounds of any rank. No GPU, no communicator (this pool's boxes have one GPU, so the RCCL
+ * transport's multi-rank grouping is exercised here on the host, not over xGMI). */
+int mcaat_comm_schedule_check(int world, uint64_t seed, uint64_t piece_bytes, uint64_t *rounds);
 int mcaat_comm_barrier(mcaat_comm *c);
 /* host memory: sizes[world] = every rank's byte count; then the bytes in rank order */
 int mcaat_comm_allgather_sizes(mcaat_comm *c, uint64_t bytes, uint64_t *sizes);
@@ -393,7 +400,10 @@ int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value);
  * is freed while a kernel queued on the context's main stream still writes it, then taken for
  * a kernel on the side stream. out[0] = 1 when the side allocation got the same block, out[1] =
  * 1 when every word holds the side kernel's value afterwards (the side kernel waited for the
- * fence), out[2] = the arena's fence waits during the check. */
+ * fence), out[2] = the arena's fence waits during the check. Then the same with a consumer the
+ * arena does not watch (a stream created for the check, the block taken with no allocation
+ * stream, as the FASTQ packer's upload streams take theirs): out[3] = the same block, out[4] = 1
+ * when every word holds that stream's value. out must hold 5 entries. */
 int mcaat_arena_check(mcaat_ctx *ctx, int64_t *out);
 /* Device memory of the library on the ctx's GPU (the arena behind every buffer): bytes in use
  * now, the most in use since the last reset (reset_peak != 0 starts a new window after

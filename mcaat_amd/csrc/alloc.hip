@@ -294,10 +294,19 @@ void *dev_alloc(size_t bytes) {
 
 void dev_free(void *p, size_t, int device) {
     if (!p) return;
-    std::lock_guard<std::mutex> lk(pools().mu);
-    Arena &a = pools().by_device[device];
-    a.retire();
-    a.give((char *)p, a.fence_now());
+    // the fences are events of the buffer's device, recorded on its streams: a free from a thread
+    // whose current device is another one switches for the call (a DevBuf destructor or a free
+    // entry point that did not bind its context)
+    int cur = device;
+    (void)hipGetDevice(&cur);
+    if (cur != device) (void)hipSetDevice(device);
+    {
+        std::lock_guard<std::mutex> lk(pools().mu);
+        Arena &a = pools().by_device[device];
+        a.retire();
+        a.give((char *)p, a.fence_now());
+    }
+    if (cur != device) (void)hipSetDevice(cur);
 }
 
 void dev_trim() {
@@ -350,6 +359,35 @@ void arena_check(mcaat_ctx *ctx, int64_t *out) {
     out[0] = b.p == first;
     out[1] = all2;
     out[2] = (int64_t)(w1 - w0);
+    b.release();
+    // (round 6) a consumer the arena does not watch (a stream of its own, as the FASTQ packer's
+    // upload streams): the block is taken with no allocation stream, so the host waits for every
+    // pending fence, the allocating stream's own included, before the foreign stream may write it
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    {
+        DevBuf<uint64_t> a(n);
+        first = a.p;
+        hipLaunchKernelGGL(k_arena_fill, dim3(256), dim3(256), 0, ctx->stream, a.p, n, 1ull, spin);
+        LAUNCH_OK();
+    }
+    hipStream_t fs = nullptr;
+    HIP_OK(hipStreamCreateWithFlags(&fs, hipStreamNonBlocking));
+    DevBuf<uint64_t> c;
+    {
+        AllocStreamScope scope(nullptr);
+        c.alloc(n);
+    }
+    hipLaunchKernelGGL(k_arena_fill, dim3(256), dim3(256), 0, fs, c.p, n, 3ull, 0ull);
+    const hipError_t le = hipGetLastError();
+    (void)hipStreamSynchronize(fs);
+    (void)hipStreamDestroy(fs);
+    if (le != hipSuccess) throw Error(MCAAT_E_HIP, std::string("arena check launch: ") + hipGetErrorString(le));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+    HIP_OK(hipMemcpy(h.data(), c.p, 8 * n, hipMemcpyDeviceToHost));
+    bool all3 = true;
+    for (uint64_t x : h) all3 = all3 && x == 3;
+    out[3] = c.p == first;
+    out[4] = all3;
 }
 
 void arena_usage(uint64_t *in_use, uint64_t *peak, uint64_t *reserved, bool reset_peak) {

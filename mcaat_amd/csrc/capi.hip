@@ -1103,6 +1103,13 @@ int mcaat_comm_unique_id(uint8_t *id) {
     });
 }
 
+int mcaat_comm_schedule_check(int world, uint64_t seed, uint64_t piece_bytes, uint64_t *rounds) {
+    return guarded([&] {
+        const uint64_t r = comm_schedule_check(world, seed, piece_bytes);
+        if (rounds) *rounds = r;
+    });
+}
+
 int mcaat_comm_init_rccl(mcaat_ctx *ctx, int world, int rank, const uint8_t *id, mcaat_comm **out) {
     return guarded([&] {
         require(ctx && id && out, "null argument");

@@ -12,6 +12,17 @@ namespace mcaat {
 // this rank's part is complete. Device buffers live on the context's GPU.
 struct Comm {
     int rank = 0, world = 1;
+    // collective calls so far (diagnostics: the exchange rounds of a bulk-synchronous stage);
+    // a collective that calls another one internally counts once
+    uint64_t n_coll = 0;
+    int coll_depth = 0;
+    struct Counted {
+        Comm &c;
+        explicit Counted(Comm &x) : c(x) {
+            if (c.coll_depth++ == 0) ++c.n_coll;
+        }
+        ~Counted() { --c.coll_depth; }
+    };
     virtual ~Comm() = default;
     virtual const char *kind() const = 0;
     virtual void barrier() = 0;
@@ -64,6 +75,17 @@ struct Comm {
         return allgather_vec(std::vector<T>{v});
     }
 };
+
+// one piece of alltoallv_dev_segs' schedule: send side (segment index, offset in it, bytes) or
+// receive side (seg -1, offset in the output, bytes)
+struct SegPiece {
+    int seg;
+    uint64_t off, n;
+};
+void seg_schedule(int world, int rank, const std::vector<std::vector<uint64_t>> &send_sizes,
+                  const std::vector<std::vector<uint64_t>> &recv_sizes, uint64_t piece,
+                  std::vector<std::vector<SegPiece>> &sends, std::vector<std::vector<SegPiece>> &recvs, size_t &rounds);
+uint64_t comm_schedule_check(int world, uint64_t seed, uint64_t piece);  // mcaat_comm_schedule_check
 
 std::unique_ptr<Comm> comm_rccl(mcaat_ctx *ctx, int world, int rank, const uint8_t *unique_id);
 std::unique_ptr<Comm> comm_shm(mcaat_ctx *ctx, int world, int rank, const char *name, uint64_t slot_bytes);

@@ -90,6 +90,39 @@ const Rccl &rccl() {
 // ranges all RCCL versions test
 constexpr uint64_t kPiece = 1ULL << 30;
 
+}  // namespace
+
+// The op schedule of RcclComm::alltoallv_dev_segs on one rank: to each peer q the segments
+// send_sizes[q] (in order) cut into pieces, from each peer q the segments recv_sizes[q] cut the
+// same way and placed back to back from the start of q's block of `out` (sources in rank order).
+// Round j of the exchange holds, per peer, the j-th send piece and the j-th receive piece, so the
+// k-th operation between two ranks sits in the same round on both sides (one ncclGroupEnd per
+// round: a round-agnostic split could wait on a peer's later round). Shared with
+// mcaat_comm_schedule_check, which builds every rank's schedule and checks the pairing on the host.
+void seg_schedule(int world, int rank, const std::vector<std::vector<uint64_t>> &send_sizes,
+                  const std::vector<std::vector<uint64_t>> &recv_sizes, uint64_t piece,
+                  std::vector<std::vector<SegPiece>> &sends, std::vector<std::vector<SegPiece>> &recvs, size_t &rounds) {
+    sends.assign(world, {});
+    recvs.assign(world, {});
+    rounds = 0;
+    uint64_t d = 0;  // receive offset in out
+    for (int q = 0; q < world; ++q)
+        for (const uint64_t n : recv_sizes[q]) {
+            if (q != rank)
+                for (uint64_t c0 = 0; c0 < n; c0 += piece) recvs[q].push_back({-1, d + c0, std::min(piece, n - c0)});
+            d += n;
+        }
+    for (int q = 0; q < world; ++q) {
+        if (q == rank) continue;
+        for (size_t i = 0; i < send_sizes[q].size(); ++i)
+            for (uint64_t c0 = 0; c0 < send_sizes[q][i]; c0 += piece)
+                sends[q].push_back({(int)i, c0, std::min(piece, send_sizes[q][i] - c0)});
+        rounds = std::max({rounds, sends[q].size(), recvs[q].size()});
+    }
+}
+
+namespace {
+
 struct RcclComm final : Comm {
     mcaat_ctx *ctx;
     ncclComm_t comm = nullptr;
@@ -115,6 +148,7 @@ struct RcclComm final : Comm {
     void sync() { HIP_OK(hipStreamSynchronize(ctx->stream)); }
 
     void barrier() override {
+        Counted cc__(*this);
         DevBuf<uint64_t> a(1), b(world);
         HIP_OK(hipMemsetAsync(a.p, 0, 8, ctx->stream));
         NCCL_OK(rccl().AllGather(a.p, b.p, 8, ncclUint8, comm, ctx->stream));
@@ -132,6 +166,7 @@ struct RcclComm final : Comm {
 
     void allgatherv_host(const void *send, uint64_t bytes, std::vector<uint8_t> &out,
                          std::vector<uint64_t> &sizes) override {
+        Counted cc__(*this);
         // every rank takes the slot path or none: whether it fits is agreed in the slot itself
         // (a size past the slot sends the size only, and every rank then runs the general path)
         if (!pin) HIP_OK(hipHostMalloc((void **)&pin, (world + 1) * kSmallSlot, hipHostMallocDefault));
@@ -170,6 +205,7 @@ struct RcclComm final : Comm {
     }
 
     void allgather_dev_words(const uint64_t *dev, int n, std::vector<uint64_t> &out) override {
+        Counted cc__(*this);
         out.resize((size_t)world * n);
         if (!n) return;
         if (!pin) HIP_OK(hipHostMalloc((void **)&pin, (world + 1) * kSmallSlot, hipHostMallocDefault));
@@ -189,6 +225,7 @@ struct RcclComm final : Comm {
 
     void alltoallv_dev(const void *send, const uint64_t *send_bytes, void *recv, const uint64_t *recv_bytes,
                        const uint64_t *send_off, const uint64_t *recv_off) override {
+        Counted cc__(*this);
         auto so = offsets_of(send_bytes, world), ro = offsets_of(recv_bytes, world);
         if (send_off) so.assign(send_off, send_off + world);
         if (recv_off) ro.assign(recv_off, recv_off + world);
@@ -223,20 +260,13 @@ struct RcclComm final : Comm {
     // the stream; a round-agnostic split could wait on a peer's later round).
     void alltoallv_dev_segs(const std::vector<std::vector<Seg>> &send, void *out,
                             const std::vector<std::vector<uint64_t>> &recv) override {
-        struct Op {
-            const uint8_t *s;
-            uint8_t *d;
-            uint64_t n;
-        };
-        std::vector<std::vector<Op>> sends(world), recvs(world);
-        uint8_t *d = (uint8_t *)out;
-        for (int q = 0; q < world; ++q) {
-            for (const uint64_t n : recv[q]) {
-                if (q != rank)
-                    for (uint64_t c0 = 0; c0 < n; c0 += kPiece) recvs[q].push_back({nullptr, d + c0, std::min(kPiece, n - c0)});
-                d += n;
-            }
-        }
+        Counted cc__(*this);
+        std::vector<std::vector<uint64_t>> ssz(world);
+        for (int q = 0; q < world; ++q)
+            for (const Seg &g : send[q]) ssz[q].push_back(g.bytes);
+        std::vector<std::vector<SegPiece>> sends, recvs;
+        size_t rounds = 0;
+        seg_schedule(world, rank, ssz, recv, kPiece, sends, recvs, rounds);
         // own segments: copies on the stream, in place
         {
             uint8_t *o = (uint8_t *)out;
@@ -250,20 +280,17 @@ struct RcclComm final : Comm {
                 o += send[rank][i].bytes;
             }
         }
-        size_t rounds = 0;
-        for (int q = 0; q < world; ++q) {
-            if (q == rank) continue;
-            for (const Seg &g : send[q])
-                for (uint64_t c0 = 0; c0 < g.bytes; c0 += kPiece)
-                    sends[q].push_back({(const uint8_t *)g.p + c0, nullptr, std::min(kPiece, g.bytes - c0)});
-            rounds = std::max({rounds, sends[q].size(), recvs[q].size()});
-        }
+        uint8_t *d = (uint8_t *)out;
         for (size_t j = 0; j < rounds; ++j) {
             NCCL_OK(rccl().GroupStart());
             for (int q = 0; q < world; ++q) {
                 if (q == rank) continue;
-                if (j < sends[q].size()) NCCL_OK(rccl().Send(sends[q][j].s, sends[q][j].n, ncclUint8, q, comm, ctx->stream));
-                if (j < recvs[q].size()) NCCL_OK(rccl().Recv(recvs[q][j].d, recvs[q][j].n, ncclUint8, q, comm, ctx->stream));
+                if (j < sends[q].size()) {
+                    const SegPiece &x = sends[q][j];
+                    NCCL_OK(rccl().Send((const uint8_t *)send[q][x.seg].p + x.off, x.n, ncclUint8, q, comm, ctx->stream));
+                }
+                if (j < recvs[q].size())
+                    NCCL_OK(rccl().Recv(d + recvs[q][j].off, recvs[q][j].n, ncclUint8, q, comm, ctx->stream));
             }
             NCCL_OK(rccl().GroupEnd());
         }
@@ -272,6 +299,7 @@ struct RcclComm final : Comm {
 
     // exact-size all-gather: one broadcast per root into its place in the output, grouped
     void allgatherv_dev(const void *send, void *recv, const uint64_t *sizes) override {
+        Counted cc__(*this);
         const auto off = offsets_of(sizes, world);
         uint8_t *d = (uint8_t *)recv;
         uint64_t most = 0;
@@ -372,6 +400,7 @@ struct ShmComm final : Comm {
     }
 
     void barrier() override {
+        Counted cc__(*this);
         const uint32_t g = hdr->generation.load(std::memory_order_acquire);
         if (hdr->arrived.fetch_add(1, std::memory_order_acq_rel) == (uint32_t)world - 1) {
             hdr->arrived.store(0, std::memory_order_relaxed);
@@ -452,6 +481,7 @@ struct ShmComm final : Comm {
     }
 
     void allgather_dev_words(const uint64_t *dev, int n, std::vector<uint64_t> &out) override {
+        Counted cc__(*this);
         need_ctx();  // the stream's writes of dev are done
         std::vector<uint64_t> mine(n);
         if (n) HIP_OK(hipMemcpy(mine.data(), dev, 8 * (size_t)n, hipMemcpyDeviceToHost));
@@ -460,6 +490,7 @@ struct ShmComm final : Comm {
 
     void allgatherv_host(const void *send, uint64_t bytes, std::vector<uint8_t> &out,
                          std::vector<uint64_t> &sizes) override {
+        Counted cc__(*this);
         sizes = exchange(bytes);
         const auto off = offsets_of(sizes.data(), world);
         out.resize(off[world]);
@@ -474,6 +505,7 @@ struct ShmComm final : Comm {
 
     void alltoallv_dev(const void *send, const uint64_t *send_bytes, void *recv, const uint64_t *recv_bytes,
                        const uint64_t *send_off, const uint64_t *recv_off) override {
+        Counted cc__(*this);
         need_ctx();
         auto so = offsets_of(send_bytes, world), ro = offsets_of(recv_bytes, world);
         if (send_off) so.assign(send_off, send_off + world);
@@ -501,6 +533,7 @@ struct ShmComm final : Comm {
     }
 
     void allgatherv_dev(const void *send, void *recv, const uint64_t *sizes) override {
+        Counted cc__(*this);
         need_ctx();
         gather_through_slots(send, recv, sizes, true);
     }
@@ -526,6 +559,7 @@ struct ShmComm final : Comm {
     // copy: ranks sharing one GPU cannot afford a third copy of the descriptors)
     void alltoallv_dev_segs(const std::vector<std::vector<Seg>> &send, void *out,
                             const std::vector<std::vector<uint64_t>> &recv) override {
+        Counted cc__(*this);
         need_ctx();
         std::vector<uint64_t> sb(world, 0), rb(world, 0);
         for (int q = 0; q < world; ++q) {
@@ -567,6 +601,77 @@ std::unique_ptr<Comm> comm_rccl(mcaat_ctx *ctx, int world, int rank, const uint8
 std::unique_ptr<Comm> comm_shm(mcaat_ctx *ctx, int world, int rank, const char *name, uint64_t slot_bytes) {
     if (world > kMaxRanks) throw Error(MCAAT_E_INVALID, "shared-memory comm: at most 64 ranks");
     return std::make_unique<ShmComm>(ctx, world, rank, name, slot_bytes);
+}
+
+// every rank's schedule for random segment lists (world ranks, piece bytes): each pair's j-th send
+// piece on one side equals the j-th receive piece on the other, pieces tile the segments in order,
+// and the receive pieces tile each source's block of `out`; returns the most rounds of any rank
+uint64_t comm_schedule_check(int world, uint64_t seed, uint64_t piece) {
+    if (world < 1 || world > 64 || !piece) throw Error(MCAAT_E_INVALID, "schedule check: bad arguments");
+    uint64_t x = seed * 0x9E3779B97F4A7C15ULL + 1;
+    auto rnd = [&](uint64_t m) {
+        x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+        return m ? x % m : 0;
+    };
+    // sz[r][q]: the segment sizes rank r sends to q (empty lists, empty segments, and sizes around
+    // multiples of the piece included)
+    std::vector<std::vector<std::vector<uint64_t>>> sz(world, std::vector<std::vector<uint64_t>>(world));
+    for (int r = 0; r < world; ++r)
+        for (int q = 0; q < world; ++q) {
+            const uint64_t ns = rnd(5);
+            for (uint64_t i = 0; i < ns; ++i) {
+                const uint64_t kind = rnd(4);
+                sz[r][q].push_back(kind == 0 ? 0 : kind == 1 ? piece * (1 + rnd(3)) + rnd(3) - 1 : rnd(4 * piece) + 1);
+            }
+        }
+    std::vector<std::vector<std::vector<SegPiece>>> S(world), Rv(world);
+    uint64_t most = 0;
+    for (int r = 0; r < world; ++r) {
+        std::vector<std::vector<uint64_t>> recv(world);
+        for (int q = 0; q < world; ++q) recv[q] = sz[q][r];
+        size_t rounds = 0;
+        seg_schedule(world, r, sz[r], recv, piece, S[r], Rv[r], rounds);
+        most = std::max<uint64_t>(most, rounds);
+        // receive pieces tile each source's block, in order
+        uint64_t off = 0;
+        for (int q = 0; q < world; ++q) {
+            uint64_t tot = 0;
+            for (uint64_t n : recv[q]) tot += n;
+            if (q != r) {
+                uint64_t at = off;
+                for (const SegPiece &p : Rv[r][q]) {
+                    if (p.off != at || p.n == 0 || p.n > piece) throw Error(MCAAT_E_INVALID, "schedule check: receive pieces do not tile");
+                    at += p.n;
+                }
+                if (at != off + tot) throw Error(MCAAT_E_INVALID, "schedule check: receive pieces miss bytes");
+            }
+            off += tot;
+        }
+        // send pieces tile the segments in order
+        for (int q = 0; q < world; ++q) {
+            if (q == r) continue;
+            size_t j = 0;
+            for (size_t i = 0; i < sz[r][q].size(); ++i) {
+                uint64_t at = 0;
+                while (at < sz[r][q][i]) {
+                    if (j >= S[r][q].size() || S[r][q][j].seg != (int)i || S[r][q][j].off != at)
+                        throw Error(MCAAT_E_INVALID, "schedule check: send pieces do not tile");
+                    at += S[r][q][j++].n;
+                }
+                if (at != sz[r][q][i]) throw Error(MCAAT_E_INVALID, "schedule check: send pieces overrun");
+            }
+            if (j != S[r][q].size()) throw Error(MCAAT_E_INVALID, "schedule check: extra send pieces");
+        }
+    }
+    // pairing: the j-th piece r -> q is the j-th piece q receives from r, same size
+    for (int r = 0; r < world; ++r)
+        for (int q = 0; q < world; ++q) {
+            if (q == r) continue;
+            if (S[r][q].size() != Rv[q][r].size()) throw Error(MCAAT_E_INVALID, "schedule check: piece counts differ");
+            for (size_t j = 0; j < S[r][q].size(); ++j)
+                if (S[r][q][j].n != Rv[q][r][j].n) throw Error(MCAAT_E_INVALID, "schedule check: paired pieces differ");
+        }
+    return most;
 }
 
 void comm_unique_id(uint8_t *out) {

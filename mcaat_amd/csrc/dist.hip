@@ -72,7 +72,9 @@ static void exchange_descriptors(mcaat_ctx *ctx, Comm &comm, NcBuckets &bk, NcBu
         if (bk.regions[b].size() > 1) throw Error(MCAAT_E_INVALID, "descriptor exchange: one region per bucket expected");
         for (const auto &rg : bk.regions[b]) mine[b] += rg.second;
     }
-    if (N == 1) {  // every bucket is this rank's: nothing moves
+    // dist.segs_at_one=1 (tests): one rank runs the exchange too (its segments are the
+    // transport's self-copies), so the segment all-to-all is exercised on a one-GPU box
+    if (N == 1 && !knob(ctx, "dist.segs_at_one", 0)) {  // every bucket is this rank's: nothing moves
         own = std::move(bk);
         own.n_occ = occ_total;
         return;
@@ -128,6 +130,7 @@ void build_graph_sharded(mcaat_ctx *ctx, Comm &comm, const mcaat_reads *r, int k
     hipStream_t st = ctx->stream;
     const int N = comm.world, R = comm.rank;
     StageTimer timer(ctx);
+    const uint64_t xr0 = comm.n_coll;  // the build's collectives (kstats "xr_build")
     CountResult c;
     const bool desc_route = knob(ctx, "dist.desc", 1) != 0 && !knob(ctx, "dist.oriented", 0);
     if (desc_route) {
@@ -287,6 +290,7 @@ void build_graph_sharded(mcaat_ctx *ctx, Comm &comm, const mcaat_reads *r, int k
         timer.mark("sdbg_build");
         HIP_OK(hipStreamSynchronize(st));
         timer.finish();
+        ctx->kstats["xr_build"].launches += comm.n_coll - xr0;
         return;
     }
     g->key.alloc(D ? D : 1);
@@ -303,6 +307,7 @@ void build_graph_sharded(mcaat_ctx *ctx, Comm &comm, const mcaat_reads *r, int k
     timer.mark("sdbg_build");
     HIP_OK(hipStreamSynchronize(st));
     timer.finish();
+    ctx->kstats["xr_build"].launches += comm.n_coll - xr0;
 }
 
 }  // namespace mcaat

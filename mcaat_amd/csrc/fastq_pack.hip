@@ -508,7 +508,14 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
         rw += outs[t].cap;
     }
     verbose_mark(ctx, "fq.parts");
-    DevBuf<uint64_t> regions(rw);
+    // written by the upload streams, which the arena does not watch: taken with no allocation
+    // stream, so the host waits for every fence still pending on the block (alloc.hip); the
+    // stream guard below synchronises those streams before the block is freed
+    DevBuf<uint64_t> regions;
+    {
+        AllocStreamScope foreign(nullptr);
+        regions.alloc(rw);
+    }
     verbose_mark(ctx, "fq.regions");
     const int NW = K > 1 ? std::min(P, T) : P;  // worker threads (K = 1: one per part, as round 3)
     const size_t stage_bytes = (size_t)NW * 2 * kStageWords * 8;
@@ -556,9 +563,19 @@ bool fastq_hostpack(mcaat_ctx *ctx, const char *const *files, int n_files,
             for (auto &pt : parts) bytes += pt.e - pt.b;
             const double reads = (double)bytes * bpb / ahead_L * 1.02 + 64.0 * P;
             const uint64_t npos = ahead_L - (uint32_t)ak;  // (k+1)-mers per read
-            ahead = nc_ahead_begin(ctx, ak, (uint64_t)(reads * (double)npos),
-                                   (uint64_t)(reads * (double)((npos + kNcItem - 1) / kNcItem)));
-            ahead_k = ak;
+            // the buckets are live beside the part regions and the packed reads: if they cannot be
+            // had, the read goes on without the ahead run (pass A then runs after it, as when a
+            // part does not fit) instead of failing
+            try {
+                ahead = nc_ahead_begin(ctx, ak, (uint64_t)(reads * (double)npos),
+                                       (uint64_t)(reads * (double)((npos + kNcItem - 1) / kNcItem)));
+                ahead_k = ak;
+            } catch (const Error &x) {
+                (void)hipGetLastError();
+                ahead.reset();
+                if (getenv("MCAAT_VERBOSE") && getenv("MCAAT_VERBOSE")[0] == '1')
+                    fprintf(stderr, "[mcaat] fq: count ahead skipped (%s)\n", x.what());
+            }
             verbose_mark(ctx, "fq.ahead_begin");
         }
     }

@@ -1631,7 +1631,7 @@ void sdbg_finish_sharded(mcaat_ctx *ctx, Comm &comm, mcaat_graph *g) {
     hipStream_t st = ctx->stream;
     const int k = g->k;
     const uint64_t n = g->D_local;
-    // local radix directory over the range's keys (~8 edges per prefix)
+    // local radix directory over the range's keys (dist.dir_edges edges per prefix, default 2)
     uint64_t kmin = 0, kmax = 0;
     if (n) {
         d2h(ctx, &kmin, g->key.p, 8);
@@ -1704,6 +1704,13 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
     g->all_valid = false;
     ShardCf s(g, comm);
     const uint64_t n = s.n, nwl = s.nwl, id_lo = g->id_lo;
+    // collectives per stage (kstats "xr_<stage>".launches): the bulk-synchronous rounds that bound
+    // this path at N ranks (DESIGN.md §7's model)
+    uint64_t xr_last = comm.n_coll;
+    auto xr = [&](const char *stage) {
+        ctx->kstats[std::string("xr_") + stage].launches += comm.n_coll - xr_last;
+        xr_last = comm.n_coll;
+    };
     DevBuf<unsigned long long> cnt(8);
     HIP_OK(hipMemsetAsync(cnt.p, 0, 64, st));
 
@@ -1826,6 +1833,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
             out->stats[0] += all[3 * r], out->stats[1] += all[3 * r + 1], out->stats[3] += all[3 * r + 2];
     }
     timer.mark("tips_filter");
+    xr("tips_filter");
 
     // 3. RecursiveReduction: rulers, walks, pointer jumping, branch resolution, removal
     // ruler density: a walk's rounds are the rank crossings of the longest walk (≈ (N-1)/N x its
@@ -2056,6 +2064,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
     ref.release();
     seed.release();
     timer.mark("peel");
+    xr("peel");
 
     // 4-5. valid count; the candidates still valid, ascending on every rank
     HIP_OK(hipMemsetAsync(cnt.p, 0, 16, st));
@@ -2079,6 +2088,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
     cbits.release();
     post.release();
     timer.mark("recount");
+    xr("recount");
 
     // 6. search regions: groups of the (k-1)-suffix (whole nodes' out-edges and in-groups)
     DevBuf<uint64_t> gs(nwl + 1), reg(nwl + 1), seen(nwl + 1);
@@ -2112,6 +2122,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
         return a;
     }();
     timer.mark("candidates");
+    xr("candidates");
     if (verbose())
         fprintf(stderr, "[mcaat] shard %d: %zu candidates, DLS region %llu edges\n", comm.rank, cand_all.size(),
                 (unsigned long long)hgid.size());
@@ -2166,6 +2177,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
     }
     rg = mcaat_graph{};
     timer.mark("dls");
+    xr("dls");
 
     // 7. FindCycle region: the forward reach found on the DepthLevelSearch replica above, then
     // cycle_max_length + 1 hops backward from every edge of it (the lock relaxation's reach)
@@ -2214,6 +2226,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
     out->stats[6] = local.stats[6];
     out->stats[7] = local.stats[7];
     timer.mark("find_cycle");
+    xr("find_cycle");
     HIP_OK(hipStreamSynchronize(st));
     timer.finish();
 }

@@ -123,6 +123,7 @@ SIGNATURES = {
     "mcaat_graph_valid_subgraph": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), _u64p, C.POINTER(C.c_uint32),
                                              _u8p]),
     "mcaat_comm_unique_id": (C.c_int, [_u8p]),
+    "mcaat_comm_schedule_check": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, _u64p]),
     "mcaat_comm_init_rccl": (C.c_int, [C.c_void_p, C.c_int, C.c_int, _u8p, C.POINTER(C.c_void_p)]),
     "mcaat_comm_init_shm": (C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_char_p, C.c_uint64, C.POINTER(C.c_void_p)]),
     "mcaat_comm_info": (C.c_int, [C.c_void_p, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
@@ -278,12 +279,13 @@ class Context:
         """Release device memory the arena keeps but nothing uses (mcaat_trim)."""
         self._lib.mcaat_trim(self.h)
 
-    def arena_check(self) -> Tuple[bool, bool, int]:
+    def arena_check(self) -> Tuple[bool, bool, int, bool, bool]:
         """The device arena's stream order (mcaat_arena_check): (same block reused, the side
-        stream's writes survived the main stream's queued ones, fence waits)."""
-        out = (C.c_int64 * 3)()
+        stream's writes survived the main stream's queued ones, fence waits, and for a consumer
+        stream the arena does not watch: same block reused, its writes survived)."""
+        out = (C.c_int64 * 5)()
         _check(self._lib.mcaat_arena_check(self.h, out))
-        return bool(out[0]), bool(out[1]), int(out[2])
+        return bool(out[0]), bool(out[1]), int(out[2]), bool(out[3]), bool(out[4])
 
     def arena_usage(self, reset_peak: bool = False) -> Tuple[int, int, int]:
         """(bytes in use, peak since the last reset, bytes the arena holds) on this GPU."""
@@ -339,6 +341,14 @@ class Comm:
         buf = np.zeros(Comm.ID_BYTES, dtype=np.uint8)
         _check(load_library().mcaat_comm_unique_id(_ptr(buf, _u8p)))
         return buf.tobytes()
+
+    @staticmethod
+    def schedule_check(world: int, seed: int, piece_bytes: int) -> int:
+        """Host self-check of the RCCL segment all-to-all's schedule (mcaat_comm_schedule_check):
+        raises on a pairing or tiling error, returns the most rounds of any rank."""
+        n = C.c_uint64(0)
+        _check(load_library().mcaat_comm_schedule_check(int(world), int(seed), int(piece_bytes), C.byref(n)))
+        return n.value
 
     @classmethod
     def rccl(cls, ctx: "Context", world: int, rank: int, uid: bytes) -> "Comm":

@@ -441,8 +441,12 @@ def test_sharded_build_blocks_two_owners_equal_one_gpu(gpu_ctx):
 def test_arena_reuse_is_stream_ordered(gpu_ctx):
     """(round 5) A block freed while a slow kernel queued on the main stream
     still writes it is taken for a kernel on the side stream: the side stream waits for the
-    free's fence, so the side kernel's writes are the ones left (csrc/alloc.hip)."""
-    same, kept, waits = gpu_ctx.arena_check()
+    free's fence, so the side kernel's writes are the ones left (csrc/alloc.hip). (round 6, ADVICE
+    r5) The same with a consumer stream the arena does not watch: the block is taken with no
+    allocation stream, so the host waits for the main stream's fence first."""
+    same, kept, waits, same_f, kept_f = gpu_ctx.arena_check()
     assert same, "the side allocation did not get the freed block (the check tests nothing)"
     assert waits >= 1
     assert kept, "the side kernel ran before the main stream's queued writes to the same block"
+    assert same_f, "the foreign-stream allocation did not get the freed block (the check tests nothing)"
+    assert kept_f, "the unwatched stream wrote the block before the main stream's queued writes"

@@ -116,10 +116,11 @@ def test_sharded_build_and_cycle_finder_ranks_share_one_gpu(world, extra):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["pe_err", "low_thr", "c3_sample", "c5_sample"])
-@pytest.mark.parametrize("world", [1, 2, 4])
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
 def test_per_shard_cycle_finder_parity_cases(case, world):
-    """ The per-shard CycleFinder on the parity cases (paired-end with errors,
-    threshold 2, the C3 and C5 coverage-matched samples) through 1, 2 and 4 shared-memory ranks
+    """ The per-shard CycleFinder on the parity cases (paired-end
+    with errors, threshold 2, the C3 and C5 coverage-matched samples) through 1, 2, 4 and 8
+    shared-memory ranks (8: C4's partition, denser rulers above two ranks, eight target ranges)
     equals the one-GPU path: valid bitmap, candidates, buckets, entries, stats."""
     outs = _ranks(world, "shm", ("--case", case, "--slot", "0"))
     for rc, o, e in outs:
@@ -156,11 +157,27 @@ def test_c3_full_dataset_two_shm_ranks_equal_one_gpu(gpu_ctx, tmp_path):
 
 
 @pytest.mark.gpu
-def test_rccl_single_rank_matches_one_gpu():
-    outs = _ranks(1, "rccl")
+@pytest.mark.parametrize("extra", [(), ("--knob", "dist.segs_at_one=1")])
+def test_rccl_single_rank_matches_one_gpu(extra):
+    """RCCL at one rank equals one GPU; with dist.segs_at_one the descriptor exchange runs through
+    the RCCL segment all-to-all (its self-copy path) instead of keeping the buckets."""
+    outs = _ranks(1, "rccl", extra)
     rc, o, e = outs[0]
     assert rc == 0, (o[-2000:], e[-3000:])
     assert "NATIVE_MULTI_OK" in o
+
+
+@pytest.mark.parametrize("world", [2, 3, 8, 64])
+def test_rccl_segment_schedule_pairs_pieces(world):
+    """ The RCCL segment all-to-all's op schedule (comm.hip seg_schedule, the code the
+    transport runs), built for every rank of `world` on the host from random segment lists: each
+    pair's j-th send piece equals the peer's j-th receive piece, and the pieces tile the segments
+    and the output. Multi-rank RCCL itself cannot run on this pool's one-GPU boxes."""
+    for seed in range(1, 40):
+        rounds = M.Comm.schedule_check(world, seed, 4096)
+        assert rounds >= 0
+    with pytest.raises(M.McaatError):
+        M.Comm.schedule_check(0, 1, 4096)
 
 
 @pytest.mark.gpu

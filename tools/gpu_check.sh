@@ -6,6 +6,7 @@
 #   bash tools/gpu_check.sh rccl1 [c3]                  the sharded build's stages at one RCCL rank
 #                                                       (second build; the exchanges are local copies)
 #   bash tools/gpu_check.sh shard2 [c3]                 2 shm ranks vs one GPU, kernels profiled per rank
+#   bash tools/gpu_check.sh shardn [c3] [world]         world shm ranks vs one GPU (digests, peaks, collectives)
 # Every GPU step has its own time limit; the first failure ends the job.
 set -e
 mkdir -p gpurun_out
@@ -31,6 +32,8 @@ case "$what" in
       --config ${1:-c3} --repeat 2 --digest gpurun_out/rccl1.json > gpurun_out/rccl1.log 2>&1 || { tail -30 gpurun_out/rccl1.log; exit 1; }
     rm -f gpurun_out/rccl1.uid
     tail -2 gpurun_out/rccl1.log ;;
+  shardn)  # bash tools/gpu_check.sh shardn <config> <world>: WORLD shm ranks vs one GPU (full dataset)
+    VERB=${VERB:-1} WORLD=${2:-4} bash tools/shard_compare.sh ${1:-c3} ;;
   shard2)
     PROF=1 VERB=1 WORLD=2 bash tools/shard_compare.sh ${1:-c3} && python3 tools/prof_compare.py > gpurun_out/prof_w2.txt ;;
   *) echo "unknown job $what"; exit 2 ;;

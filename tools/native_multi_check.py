@@ -47,6 +47,9 @@ def checksums(g, res) -> dict:
             "entries": len(res.entries), "cycles": res.stats[5]}
 
 
+XR_STAGES = ("build", "tips_filter", "peel", "recount", "candidates", "dls", "find_cycle")
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, required=True)
@@ -111,12 +114,14 @@ def main() -> int:
             first = a.rank * spec.n_reads // a.world
             count = (a.rank + 1) * spec.n_reads // a.world - first
             mine = M.Reads.synth_range(ctx, spec, first, count)
+            ctx.arena_usage(reset_peak=True)
             for rep in range(a.repeat):  # stage times of the last build (the first pays allocations)
                 if rep:
                     g.free()
                 ctx.stage_times()
                 g = M.Graph.build_sharded(ctx, comm, mine, k)
                 build_stages = {kk: round(vv, 2) for kk, vv in ctx.stage_times().items()}
+            build_peak = ctx.arena_usage()[1]  # this rank's device memory peak through the build
             mine.free()
             cf_base = ctx.arena_usage(reset_peak=True)[0]
             res = g.cycle_finder(prm, comm=comm)
@@ -130,6 +135,9 @@ def main() -> int:
         d["cf_hbm_GB"] = {"graph_at_start": round(cf_mem[0] / 1e9, 2), "peak": round(cf_mem[1] / 1e9, 2)}
         if not a.single:
             d["build_stages_ms"] = build_stages
+            d["build_hbm_peak_GB"] = round(build_peak / 1e9, 2)
+            # collectives per stage on this rank (each a bulk-synchronous exchange round)
+            d["collectives"] = {st: ctx.kernel_timing("xr_" + st)[1] for st in XR_STAGES}
         g.free()
         if comm is not None:
             comm.barrier()
@@ -194,6 +202,8 @@ def main() -> int:
     # every rank holds the same results
     digest = repr((res.entries, res.stats[:6])).encode()
     same = len(set(comm.allgather_bytes(digest))) == 1
+    xr = {st: ctx.kernel_timing("xr_" + st)[1] for st in XR_STAGES}
+    print(f"rank {a.rank}: collectives {xr}", flush=True)
     print(f"rank {a.rank}: D={len(keys)} (single {len(k1)}) entries={len(res.entries)} cycles={res.stats[5]} "
           f"rounds={res.stats[6]} reruns={res.stats[7]} sharded={sharded} match={ok} ranks_agree={same}", flush=True)
     if not ok:

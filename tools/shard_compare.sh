@@ -16,7 +16,10 @@ for r in range(${WORLD:-2}):
     b = json.load(open(f"gpurun_out/shard_rank{r}.json"))
     same = {k: a[k] == b[k] for k in ("D", "keys", "mult", "valid", "stats", "results", "entries", "cycles")}
     print("rank", r, "equal to one GPU:", all(same.values()), same)
-    print("  cf hbm", b.get("cf_hbm_GB"), "one GPU", a.get("cf_hbm_GB"))
+    print("  cf hbm", b.get("cf_hbm_GB"), "one GPU", a.get("cf_hbm_GB"), "build peak", b.get("build_hbm_peak_GB"))
+    print("  collectives", b.get("collectives"))
+    print("  build ms", b.get("build_stages_ms"))
+    print("  cf ms", b.get("cf_stages_ms"))
 PY
 # keep the kernel statistics only (the traces exceed what gpurun copies back)
 if [ -n "$PROF" ]; then find gpurun_out/prof_shard -name "*kernel_trace*" -delete; fi
