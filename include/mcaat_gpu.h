@@ -166,6 +166,20 @@ int mcaat_graph_keep_region(mcaat_graph *g, const uint64_t *seeds, size_t n, uin
  * out-neighbours (OutgoingEdges order, DESCENDING ids) as positions in ids[] at nbr[4i..4i+counts[i]).
  * With ids, nbr and counts all NULL only *n_valid is set (size the arrays, call again). */
 int mcaat_graph_valid_subgraph(const mcaat_graph *g, uint64_t *n_valid, uint64_t *ids, uint32_t *nbr, uint8_t *counts);
+/* Succinct (BOSS) view. Replaces: the representation of MEGAHIT's SDBG (sdbg_build.cpp:175-186
+ * writes it, main.cpp:522-530 loads it; SURVEY.md §8a5, ~3 B/edge): per edge a nibble of W, last
+ * and W-minus, per node (sources and targets, colex order) a sink and a has-in bit, 16-bit block
+ * ranks and select samples; neighbour queries by rank/select (csrc/sdbg_succinct.hip). Built from
+ * the graph as it is (valid bits included), checked against its arrays (every edge's valid out-
+ * and in-neighbours, order included, when check != 0) and timed beside them. out[8]: [0] bytes of
+ * the view, [1] bytes of the arrays it replaces (keys, out_info, in_info; mult and the valid
+ * bitmap are shared), [2] out-list mismatches (+2^40 when the two out-degree scans disagree),
+ * [3] in-list mismatches, [4] nodes (sources and sinks), [5] sinks, [6] / [7] the sums of the
+ * valid out- / in-degrees of the valid edges. ms[6]: [0] the build, [1] / [2] the out-degree scan
+ * on out_info / on the view (per-lane rank/select), [3] / [4] the in-degree scan on in_info / on
+ * the view, [5] the out-degree scan on the view with the selects streamed over each wave. One
+ * GPU (not a sharded graph). */
+int mcaat_graph_succinct_check(mcaat_graph *g, int check, uint64_t *out, double *ms);
 /* Checkpoint / resume. Replaces: the on-disk graph between SDBGBuild and CycleFinder
  * (MEGAHIT graph.sdbg* + SDBG::LoadFromFile, main.cpp:386-393, 522-530). The library's own
  * format (MEGAHIT's is unpinned offline): sorted BOSS keys, multiplicities and valid bits with
@@ -393,7 +407,9 @@ int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value);
  *   dist.win_ranges   0: the filter windows and predecessor flags as per-edge messages (default 1:
  *                      target-range bytes pulled and pushed)
  *   dist.adj_chunk    sharded adjacency: edges per request/response exchange (default 2^26)
- *   dist.dir_edges    sharded adjacency: edges per prefix of the range's radix directory (default 2) */
+ *   dist.dir_edges    sharded adjacency: edges per prefix of the range's radix directory (default 2)
+ *   dist.segs_at_one  1: one rank runs the descriptor exchange through the segment all-to-all too
+ *                      (its self-copy path; default 0 keeps the buckets in place) */
 
 /* ---- allocator check ----------------------------------------------------------------------
  * Replaces: nothing in the reference. The device arena's stream order (csrc/alloc.hip): a block

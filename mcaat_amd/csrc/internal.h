@@ -441,6 +441,9 @@ void verbose_mark(mcaat_ctx *ctx, const char *what);
 void sort_counts(mcaat_ctx *ctx, CountResult &c, int k);
 void sdbg_build(mcaat_ctx *ctx, CountResult &c, int k, mcaat_graph *g);
 void sdbg_finish(mcaat_ctx *ctx, mcaat_graph *g);
+// the succinct (BOSS) view of a built graph, checked and timed beside its arrays
+// (sdbg_succinct.hip, mcaat_graph_succinct_check)
+void graph_succinct_check(mcaat_graph *g, bool check, uint64_t *out, double *ms);
 // multi-GPU build pieces (shard.hip)
 void counts_histogram(mcaat_ctx *ctx, const CountResult &c, int k, int bits, uint64_t *hist_host);
 void counts_partition(mcaat_ctx *ctx, const CountResult &c, int k, int n_owners, const uint64_t *splits_host,

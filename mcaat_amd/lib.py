@@ -120,6 +120,7 @@ SIGNATURES = {
     "mcaat_graph_download_range": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, _u64p, _u16p, _u8p]),
     "mcaat_graph_valid_words": (C.c_int, [C.c_void_p, _u64p]),
     "mcaat_graph_keep_region": (C.c_int, [C.c_void_p, _u64p, C.c_size_t, C.c_uint64]),
+    "mcaat_graph_succinct_check": (C.c_int, [C.c_void_p, C.c_int, _u64p, C.POINTER(C.c_double)]),
     "mcaat_graph_valid_subgraph": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), _u64p, C.POINTER(C.c_uint32),
                                              _u8p]),
     "mcaat_comm_unique_id": (C.c_int, [_u8p]),
@@ -685,6 +686,17 @@ class Graph:
         mm = np.zeros(max(ids.size, 1), dtype=np.uint16)
         _check(self.ctx._lib.mcaat_graph_gather(self.h, _ptr(ids, _u64p), ids.size, _ptr(kk, _u64p), _ptr(mm, _u16p)))
         return kk[: ids.size], mm[: ids.size]
+
+    def succinct_check(self, check: bool = True) -> dict:
+        """The succinct (BOSS) view of this graph, built, checked against the arrays and timed
+        beside them (mcaat_graph_succinct_check)."""
+        out = np.zeros(8, dtype=np.uint64)
+        ms = (C.c_double * 6)()
+        _check(self.ctx._lib.mcaat_graph_succinct_check(self.h, int(check), _ptr(out, _u64p), ms))
+        o = [int(x) for x in out]
+        return {"view_bytes": o[0], "array_bytes": o[1], "out_mismatch": o[2], "in_mismatch": o[3], "nodes": o[4],
+                "sinks": o[5], "outdeg_sum": o[6], "indeg_sum": o[7], "build_ms": ms[0], "outdeg_info_ms": ms[1],
+                "outdeg_sv_ms": ms[2], "indeg_info_ms": ms[3], "indeg_sv_ms": ms[4], "outdeg_sv_stream_ms": ms[5]}
 
     def keep_region(self, seeds: np.ndarray, hops: int) -> None:
         """valid &= seeds grown by `hops` rounds over valid neighbours (mcaat_graph_keep_region)."""
