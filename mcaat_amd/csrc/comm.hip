@@ -9,6 +9,8 @@
 #include <dlfcn.h>
 #include <fcntl.h>
 #include <sched.h>
+#include <signal.h>
+#include <cerrno>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -328,6 +330,7 @@ struct ShmHeader {
     uint32_t world;
     uint64_t slot_bytes;
     uint64_t pub[kMaxRanks];  // per-rank published value of the current operation
+    int32_t pid[kMaxRanks];   // each rank's process (a rank that died ends the others' waits)
 };
 static_assert(std::atomic<uint32_t>::is_always_lock_free, "process-shared atomics must be lock-free");
 
@@ -380,6 +383,7 @@ struct ShmComm final : Comm {
             hdr->world = (uint32_t)world;
             hdr->slot_bytes = slot;
         }
+        hdr->pid[rank] = (int32_t)getpid();
         hdr->attached.fetch_add(1, std::memory_order_acq_rel);
         while (hdr->attached.load(std::memory_order_acquire) < (uint32_t)world) {
             check_timeout(t0, "attach");
@@ -398,6 +402,27 @@ struct ShmComm final : Comm {
         if (s > timeout_s)
             throw Error(MCAAT_E_IO, std::string("shared-memory comm: ") + what + " timed out (a rank is missing?)");
     }
+    // a rank whose process has exited (e.g. it failed an allocation) will never arrive: the first
+    // such rank, or -1
+    int dead_peer() const {
+        if (!hdr || hdr->attached.load(std::memory_order_acquire) < (uint32_t)world) return -1;
+        for (int r = 0; r < world; ++r)
+            if (r != rank && hdr->pid[r] > 0 && !alive(hdr->pid[r])) return r;
+        return -1;
+    }
+    // gone, or exited and not yet reaped by its parent (a zombie still answers kill(pid, 0))
+    static bool alive(int32_t pid) {
+        if (kill(pid, 0) != 0 && errno == ESRCH) return false;
+        char path[64], buf[256];
+        snprintf(path, sizeof(path), "/proc/%d/stat", (int)pid);
+        FILE *f = fopen(path, "r");
+        if (!f) return true;  // no /proc: kill's answer stands
+        const size_t n = fread(buf, 1, sizeof(buf) - 1, f);
+        fclose(f);
+        buf[n] = 0;
+        const char *p = strrchr(buf, ')');  // "pid (comm) state ..."
+        return !(p && p[1] == ' ' && (p[2] == 'Z' || p[2] == 'X'));
+    }
 
     void barrier() override {
         Counted cc__(*this);
@@ -410,7 +435,16 @@ struct ShmComm final : Comm {
         const auto t0 = std::chrono::steady_clock::now();
         for (uint32_t spin = 0; hdr->generation.load(std::memory_order_acquire) == g; ++spin) {
             if (spin < 1024) continue;
-            if ((spin & 1023) == 0) check_timeout(t0, "barrier");
+            if ((spin & 1023) == 0) {
+                check_timeout(t0, "barrier");
+                // every other rank stops waiting for a rank that exited, instead of at the time
+                // limit (the barrier may have completed just before that rank left: re-read it)
+                if ((spin & 0xFFFFF) == 0) {
+                    const int d = dead_peer();
+                    if (d >= 0 && hdr->generation.load(std::memory_order_acquire) == g)
+                        throw Error(MCAAT_E_IO, "shared-memory comm: rank " + std::to_string(d) + " exited (barrier)");
+                }
+            }
             sched_yield();
         }
     }

@@ -1305,6 +1305,13 @@ __global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_coun
             cnt[i] = 0;
         }
         __syncthreads();
+        if (PROF && !raw) {  // expansion inserts: the distinct descriptors' edges
+            unsigned long long ins = 0;
+#pragma unroll
+            for (int j = 0; j < kSlots; ++j) ins += rc[j] ? (r1[j] >> kNShift) & 63 : 0;
+            for (int o = 32; o; o >>= 1) ins += __shfl_down(ins, o);
+            if (lane == 0 && ins) atomicAdd(&prof[8], ins);
+        }
         if (!raw) {
 #pragma unroll
             for (int j = 0; j < kSlots; ++j) spread(r0[j], r1[j], (int)((r1[j] >> kNShift) & 63), rc[j]);
@@ -1343,6 +1350,7 @@ __global__ void __launch_bounds__(kCThreads, PERCU * kCThreads / 256) k_lds_coun
             __syncthreads();
             continue;
         }
+        if (PROF && threadIdx.x == 0) atomicAdd(&prof[9], (unsigned long long)n_distinct);
         // ---- 3: block-wide compaction of the occupied slots ----
         constexpr int per = kCap / kCThreads;
         int mine = 0;
@@ -1850,7 +1858,7 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
     P.l2_bits = bk.l2_bits;
     const uint32_t S = 1u << P.l2_bits;
     const uint64_t F = 256ull * S;
-    DevBuf<unsigned long long> dprof(8);
+    DevBuf<unsigned long long> dprof(10);
 
     // ---- B + C, over groups of L1 buckets whose fine partitions fit a memory budget ----
     // The sub histogram of every chunk gives all fine-partition offsets at once; each group
@@ -2127,11 +2135,14 @@ void node_counter_bc(mcaat_ctx *ctx, NcBuckets &bk, int k, CountResult &out) {
     }
     for (auto *t : btimers) t->finish();
     if (prof_c) {
-        unsigned long long hp[8];
-        HIP_OK(hipMemcpy(hp, dprof.p, 64, hipMemcpyDeviceToHost));
+        unsigned long long hp[10];
+        HIP_OK(hipMemcpy(hp, dprof.p, 80, hipMemcpyDeviceToHost));
         const double waves = (double)ctx->n_cu * kCWaves;
         fprintf(stderr, "[mcaat] pass C per-wave ms: clear %.1f collapse %.1f expand %.1f emit %.1f; raw partitions %.0f (probe fails %llu), distinct descriptors %llu of %llu\n",
                 hp[0] / waves / 1e5, hp[1] / waves / 1e5, hp[2] / waves / 1e5, hp[3] / waves / 1e5, (double)hp[4], hp[5], hp[6], hp[7]);
+        // edges inserted by the expansion (each distinct descriptor's n) against the distinct edges
+        fprintf(stderr, "[mcaat] pass C expansion: %llu edge inserts for %llu distinct edges (%.2f per edge)\n", hp[8], hp[9],
+                hp[9] ? (double)hp[8] / (double)hp[9] : 0.0);
     }
     l1.release();
     l1s.release();

@@ -64,6 +64,35 @@ def test_shm_comm_host_allgather_between_processes(world):
     assert not os.path.exists("/dev/shm" + name), "the segment name must be removed once all ranks attached"
 
 
+_DYING_RANK = r"""
+import os, sys, time
+sys.path.insert(0, {root!r})
+import mcaat_amd as M
+world, rank, name = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+c = M.Comm.shm(None, world, rank, name, 4096)
+if rank == world - 1:
+    os._exit(3)  # leaves without a word, as a rank that failed an allocation does
+t0 = time.time()
+try:
+    c.allgather_bytes(b"x" * 100)
+except M.McaatError as e:
+    print("PEER_GONE", round(time.time() - t0, 1), str(e))
+"""
+
+
+def test_shm_comm_ends_waits_for_a_rank_that_exited():
+    """(round 6) A rank that exits (an allocation failure on a shared GPU) ends the other ranks'
+    waits with an error within seconds, instead of at the 900-s time limit."""
+    name = f"/mcaat_t_{uuid.uuid4().hex[:12]}"
+    code = _DYING_RANK.format(root=ROOT)
+    outs = _spawn([[sys.executable, "-c", code, "3", str(r), name] for r in range(3)], timeout=120)
+    for r, (rc, o, e) in enumerate(outs[:2]):
+        assert rc == 0, e[-2000:]
+        assert "PEER_GONE" in o and "rank 2 exited" in o, (o, e)
+        assert float(o.split()[1]) < 30, o
+    assert outs[2][0] == 3
+
+
 def test_shm_comm_rejects_bad_arguments():
     with pytest.raises(M.McaatError):
         M.Comm.shm(None, 2, 2, "/mcaat_bad")
