@@ -60,7 +60,7 @@ std::vector<uint64_t> choose_splits(const std::vector<uint64_t> &hist, int world
 // descriptors of its buckets give final counts, each canonical edge on exactly one rank: no
 // partial sums, no owner-side sort of ~D_c pairs whatever N (the count exchange's canon_reduce).
 // The owners are contiguous bucket ranges of equal descriptor weight; a rank sends bucket b's
-// reservations (whole 1024-slot runs, inert padding included) to b's owner, which keeps one
+// reservations (whole reservation runs, inert padding included) to b's owner, which keeps one
 // region per (bucket, source rank) for pass B.
 // Replaces: the S2 counting of Read2SdbgS2::Run (sdbg_build.cpp:171-187) over reads split by rank.
 // Round 5: the buckets go out from where pass A wrote them (one segment per bucket, grouped per

@@ -419,7 +419,7 @@ struct NcBuckets {
     DevBuf<uint4> data;     // 16-B super-k-mer descriptors
     DevBuf<uint16_t> sub;   // each one's fine sub-partition row (same slots)
     // per L1 bucket: its regions (first slot, slots) in data/sub, each a whole number of
-    // 1024-slot reservations (so every region starts 16-B aligned in sub)
+    // kMini-slot reservations (256 slots: every region starts 16-B aligned in sub)
     std::vector<std::vector<std::pair<uint64_t, uint64_t>>> regions;
     // pass A's layout: bucket b's slots start at base[b] (257 entries; a bucket's reserved but
     // unused tail is not part of its region). Empty when the regions came from an exchange.

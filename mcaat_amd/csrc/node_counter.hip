@@ -254,7 +254,11 @@ __device__ __forceinline__ void window_min(const uint32_t *H, uint32_t *hm) {
 }
 
 #ifndef MCAAT_AMINI
-#define MCAAT_AMINI 1024
+// (round 6) 256 slots (was 1024): the L1 buckets' headroom for every workgroup's two partly used
+// reservations per bucket falls from 7.2 GB to 1.8 GB per GPU (a rank at any N: eight ranks of C3
+// then fit one GPU), at the same speed (round 5 A/B: node_counter 179.1 ms at 256, 179.3-180.1
+// at 1024)
+#define MCAAT_AMINI 256
 #endif
 constexpr uint32_t kMini = MCAAT_AMINI;  // descriptors reserved per (workgroup, L1 bucket) grab
 constexpr uint16_t kDeadSub = 0xffff;  // sub-partition mark of an inert (n = 0) slot
@@ -1701,7 +1705,7 @@ void node_counter_a(mcaat_ctx *ctx, const mcaat_reads *r, int k, const std::func
     bk.base = base;
     for (int b = 0; b < 256; ++b) {
         n_desc += tot[b];
-        if (tot[b]) bk.regions[b].push_back({base[b], tot[b]});  // tot: whole 1024-slot reservations
+        if (tot[b]) bk.regions[b].push_back({base[b], tot[b]});  // tot: whole kMini-slot reservations
     }
     // algorithmic bytes of the launch: the 2-bit stream read once, a 16-B descriptor and its
     // 2-B sub row written per reserved slot (the tail slots of a reservation are written inert)

@@ -53,6 +53,27 @@ struct SvView {
     const uint64_t *valid = nullptr;
 };
 
+// position of the n-th (0-based) set bit of m (popcount(m) > n): a binary search over the
+// halves' popcounts, six steps whatever n is
+__device__ __forceinline__ int select64(uint64_t m, uint32_t n) {
+    int pos = 0;
+    uint32_t c = (uint32_t)__popc((uint32_t)m);
+    if (n >= c) {
+        n -= c;
+        pos = 32;
+        m >>= 32;
+    }
+#pragma unroll
+    for (int w = 16; w; w >>= 1) {
+        c = (uint32_t)__popc((uint32_t)m & ((1u << w) - 1));
+        if (n >= c) {
+            n -= c;
+            pos += w;
+            m >>= w;
+        }
+    }
+    return pos;
+}
 __device__ __forceinline__ uint32_t nib(const uint64_t *sym, uint64_t e) { return (uint32_t)(sym[e >> 4] >> (4 * (e & 15))) & 15; }
 // bit 4i set where nibble i is a non-minus edge with W == c
 __device__ __forceinline__ uint64_t match_c(uint64_t w, uint32_t c) {
@@ -89,10 +110,7 @@ __device__ uint64_t e_select(const SvView &v, int kind, uint64_t j) {
     for (uint64_t w = lo * 4;; ++w) {
         uint64_t m = match_kind(v.sym[w], kind);
         const uint64_t pc = __popcll(m);
-        if (r + pc > j) {
-            for (uint64_t q = j - r; q; --q) m &= m - 1;
-            return w * 16 + (uint64_t)((__ffsll((long long)m) - 1) >> 2);
-        }
+        if (r + pc > j) return w * 16 + (uint64_t)(select64(m, (uint32_t)(j - r)) >> 2);
         r += pc;
     }
 }
@@ -124,8 +142,7 @@ __device__ uint64_t u_select(const SvView &v, int kind, uint64_t j) {
     }
     uint64_t m = u_word(v, kind, lo);
     if (lo == nb - 1 && (v.nU & 63)) m &= (1ULL << (v.nU & 63)) - 1;  // bits past nU (non-sink reads them as ones)
-    for (uint64_t q = j - u_before_block(v, kind, lo); q; --q) m &= m - 1;
-    return lo * 64 + (uint64_t)(__ffsll((long long)m) - 1);
+    return lo * 64 + (uint64_t)select64(m, (uint32_t)(j - u_before_block(v, kind, lo)));
 }
 
 // the edges [first, last] of the source node at U position u (not a sink)
@@ -235,10 +252,7 @@ __global__ void __launch_bounds__(kB) k_sv_esamples(SvView v, uint64_t nb, uint6
             for (uint64_t w = 4 * b; w < 4 * b + 4 && w < (v.D + 15) / 16; ++w) {
                 uint64_t m = match_kind(v.sym[w], k);
                 const uint64_t pc = __popcll(m);
-                if (want >= r && want < r + pc) {
-                    for (uint64_t q = want - r; q; --q) m &= m - 1;
-                    S[k][want >> kSamp] = w * 16 + (uint64_t)((__ffsll((long long)m) - 1) >> 2);
-                }
+                if (want >= r && want < r + pc) S[k][want >> kSamp] = w * 16 + (uint64_t)(select64(m, (uint32_t)(want - r)) >> 2);
                 r += pc;
             }
         }
@@ -340,10 +354,7 @@ __global__ void __launch_bounds__(kB) k_sv_usamples(SvView v, uint64_t nb, uint6
             if (b == nb - 1 && (v.nU & 63)) m &= (1ULL << (v.nU & 63)) - 1;
             const uint64_t pc = __popcll(m);
             const uint64_t want = (r + (1u << kSamp) - 1) & ~(uint64_t)((1u << kSamp) - 1);
-            if (want < r + pc) {
-                for (uint64_t q = want - r; q; --q) m &= m - 1;
-                S[k][want >> kSamp] = b * 64 + (uint64_t)(__ffsll((long long)m) - 1);
-            }
+            if (want < r + pc) S[k][want >> kSamp] = b * 64 + (uint64_t)select64(m, (uint32_t)(want - r));
         }
 }
 
@@ -434,10 +445,7 @@ __device__ __forceinline__ uint64_t nth_one_from(const uint64_t *bm, uint64_t fr
     uint64_t w = from >> 6, m = bm[w] & (~0ULL << (from & 63));
     for (;;) {
         const uint64_t pc = __popcll(m);
-        if (n < pc) {
-            for (; n; --n) m &= m - 1;
-            return w * 64 + (uint64_t)(__ffsll((long long)m) - 1);
-        }
+        if (n < pc) return w * 64 + (uint64_t)select64(m, (uint32_t)n);
         n -= pc;
         m = bm[++w];
     }
@@ -447,10 +455,7 @@ __device__ __forceinline__ uint64_t nth_last_from(const uint64_t *sym, uint64_t 
     uint64_t w = from >> 4, m = (sym[w] >> 2) & kRep & (~0ULL << (4 * (from & 15)));
     for (;;) {
         const uint64_t pc = __popcll(m);
-        if (n < pc) {
-            for (; n; --n) m &= m - 1;
-            return w * 16 + (uint64_t)((__ffsll((long long)m) - 1) >> 2);
-        }
+        if (n < pc) return w * 16 + (uint64_t)(select64(m, (uint32_t)n) >> 2);
         n -= pc;
         m = (sym[++w] >> 2) & kRep;
     }
