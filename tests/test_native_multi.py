@@ -157,32 +157,42 @@ def test_per_shard_cycle_finder_parity_cases(case, world):
         assert "NATIVE_MULTI_OK" in o and "sharded=True" in o, o
 
 
+_SINGLE_DIGEST = {}
+
+
 @pytest.mark.gpu
 @pytest.mark.timeout(1500)
-def test_c3_full_dataset_two_shm_ranks_equal_one_gpu(gpu_ctx, tmp_path):
-    """The C4 data path at full size: the whole C3 dataset (300M reads, D ~ 1e9) through
-    mcaat_build_graph_sharded + mcaat_cycle_finder_comm with 2 shared-memory ranks sharing the
-    GPU; keys, multiplicities, post-CycleFinder valid bits (order-sensitive checksums) and the
-    full CycleFinder results (entries, candidates, buckets, stats) equal the one-GPU path's."""
+@pytest.mark.parametrize("config,world", [("c3", 2), ("c3", 8), ("c5", 2)])
+def test_full_dataset_shm_ranks_equal_one_gpu(gpu_ctx, tmp_path, config, world):
+    """The C4 / C5 data paths at full size: a whole bench dataset through
+    mcaat_build_graph_sharded + mcaat_cycle_finder_comm with `world` shared-memory ranks sharing
+    the GPU; keys, multiplicities, post-CycleFinder valid bits (order-sensitive checksums) and the
+    full CycleFinder results (entries, candidates, buckets, stats) equal the one-GPU path's.
+    (c3, 8): C4's 8-way partition at C3 scale (round 6: fits one GPU with 256-slot pass-A
+    reservations, ~30 GB per rank); (c5, 2): D = 3.9e9, so one rank holds only ids above 2^31."""
     import json
 
     gpu_ctx.trim()  # the ranks need the memory this process's arena keeps from earlier tests
+    script = os.path.join(ROOT, "tools", "native_multi_check.py")
+    if config not in _SINGLE_DIGEST:
+        single = str(tmp_path / "single.json")
+        (rc, o, e), = _spawn([[sys.executable, script, "--world", "1", "--rank", "0", "--single", "--config", config,
+                               "--digest", single]], timeout=900)
+        assert rc == 0, (o[-2000:], e[-3000:])
+        _SINGLE_DIGEST[config] = json.load(open(single))
+    want = _SINGLE_DIGEST[config]
+    assert want["D"] > 9e8 and want["cycles"] > 0
     dig = str(tmp_path / "rank{rank}.json")
-    outs = _ranks(2, "shm", ("--config", "c3", "--digest", dig, "--slot", "0"), timeout=900)
+    outs = _ranks(world, "shm", ("--config", config, "--digest", dig, "--slot", "0"), timeout=1200)
     for rc, o, e in outs:
         assert rc == 0, (o[-2000:], e[-3000:])
         assert "NATIVE_MULTI_DIGEST" in o, o
-    single = str(tmp_path / "single.json")
-    script = os.path.join(ROOT, "tools", "native_multi_check.py")
-    (rc, o, e), = _spawn([[sys.executable, script, "--world", "1", "--rank", "0", "--single", "--config", "c3",
-                           "--digest", single]], timeout=600)
-    assert rc == 0, (o[-2000:], e[-3000:])
-    want = json.load(open(single))
-    assert want["D"] > 9e8 and want["cycles"] > 0
-    for r in range(2):
+    for r in range(world):
         got = json.load(open(dig.format(rank=r)))
         for key in ("D", "keys", "mult", "valid", "stats", "results", "entries", "cycles"):
             assert got[key] == want[key], (r, key, got[key], want[key])
+        # every rank holds about 1/world of the graph through CycleFinder
+        assert got["cf_hbm_GB"]["graph_at_start"] < 1.5 * want["cf_hbm_GB"]["graph_at_start"] / world + 1, got
 
 
 @pytest.mark.gpu
