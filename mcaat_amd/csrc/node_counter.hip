@@ -49,6 +49,7 @@ struct SkParams {
     int nmax;     // max edges per descriptor = kDescBases - E + 1
     int l2_bits;  // hash bits after the 8 L1 bits used for fine partitions
     uint64_t salt;
+    uint32_t mini;  // slots per reservation (a multiple of 8: every region starts 16-B aligned in the sub rows)
 };
 
 __device__ __forceinline__ uint64_t desc_window(uint64_t w0, uint64_t w1, int i, int E) {
@@ -253,14 +254,12 @@ __device__ __forceinline__ void window_min(const uint32_t *H, uint32_t *hm) {
     }
 }
 
-#ifndef MCAAT_AMINI
-// (round 6) 256 slots (was 1024): the L1 buckets' headroom for every workgroup's two partly used
-// reservations per bucket falls from 7.2 GB to 1.8 GB per GPU (a rank at any N: eight ranks of C3
-// then fit one GPU), at the same speed (round 5 A/B: node_counter 179.1 ms at 256, 179.3-180.1
-// at 1024)
-#define MCAAT_AMINI 256
-#endif
-constexpr uint32_t kMini = MCAAT_AMINI;  // descriptors reserved per (workgroup, L1 bucket) grab
+// descriptors reserved per (workgroup, L1 bucket) grab (SkParams::mini, a power of two): 1024 on
+// one GPU; (round 6) 256 for a rank of a sharded build, where the L1 buckets' headroom for every
+// workgroup's two partly used reservations per bucket falls from 7.2 GB to 1.8 GB, so eight ranks
+// of C3 fit one GPU in the tests (1024 ran out of memory). Pass A at C3: 72.3 ms at 1024, 73.3-73.8
+// at 256 (more reservation atomics); knob nc.a_mini sets it
+constexpr uint32_t kMiniOne = 1024, kMiniShard = 256;
 constexpr uint16_t kDeadSub = 0xffff;  // sub-partition mark of an inert (n = 0) slot
 
 
@@ -331,7 +330,7 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
             my_next = rs[2];
         } else {
             rleft[tb] = 0;
-            my_next = atomicAdd(&l1_cursor[tb], (unsigned long long)kMini);
+            my_next = atomicAdd(&l1_cursor[tb], (unsigned long long)P.mini);
         }
     }
     if (threadIdx.x == 0) more_flag[0] = more_flag[1] = 0;
@@ -564,12 +563,12 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
             const uint32_t need = hist[tb];
             if (need > rleft[tb]) {
                 for (uint32_t z = 0; z < rleft[tb]; ++z) put(tb, rpos[tb] + z, make_uint4(0, 0, 0, 0));
-                if (need <= kMini) {
+                if (need <= P.mini) {
                     rpos[tb] = my_base + my_next;
-                    rleft[tb] = kMini;
-                    my_next = atomicAdd(&l1_cursor[tb], (unsigned long long)kMini);
+                    rleft[tb] = P.mini;
+                    my_next = atomicAdd(&l1_cursor[tb], (unsigned long long)P.mini);
                 } else {  // more than a reservation in one flush: grab synchronously
-                    const uint32_t grab = ((need + kMini - 1) / kMini) * kMini;
+                    const uint32_t grab = ((need + P.mini - 1) / P.mini) * P.mini;
                     rpos[tb] = my_base + atomicAdd(&l1_cursor[tb], (unsigned long long)grab);
                     rleft[tb] = grab;
                 }
@@ -698,7 +697,7 @@ __global__ void __launch_bounds__(kAThreads) k_sk_scatter(const uint64_t *__rest
         __syncthreads();
         if (tb < 256) {
             rpos[tb] = my_base + my_next;
-            rleft[tb] = kMini;
+            rleft[tb] = P.mini;
         }
         __syncthreads();
     }
@@ -1576,6 +1575,7 @@ SkParams sk_params(int k) {
     if (P.w > 16) throw Error(MCAAT_E_INVALID, "node_counter: minimizer window above 16");
     P.nmax = kDescBases - E + 1;
     P.salt = 0x6d696e696d697aULL;
+    P.mini = kMiniOne;
 
     return P;
 }
@@ -1650,6 +1650,8 @@ void node_counter_a(mcaat_ctx *ctx, const mcaat_reads *r, int k, const std::func
     }
     const int fine_bits = pick ? pick(n_occ) : nc_fine_bits(ctx, n_occ);
     P.l2_bits = fine_bits - 8;
+    if (pick) P.mini = kMiniShard;  // a rank of a sharded build
+    if (knob_set(ctx, "nc.a_mini")) P.mini = (uint32_t)std::max<int64_t>(8, knob(ctx, "nc.a_mini", 1024)) & ~7u;
     bk.l2_bits = P.l2_bits;
     bk.n_occ = n_occ;
     bk.regions.assign(256, {});
@@ -1666,7 +1668,7 @@ void node_counter_a(mcaat_ctx *ctx, const mcaat_reads *r, int k, const std::func
     std::vector<uint64_t> cap(256), base(257);
     // + one partially used reservation per (workgroup, bucket)
     const uint64_t a_grid = (uint64_t)kAPerCu * ctx->n_cu;
-    for (int b = 0; b < 256; ++b) cap[b] = (est / 256 + 2 * a_grid * kMini + 7) & ~7ull;  // 16-B aligned sub rows
+    for (int b = 0; b < 256; ++b) cap[b] = (est / 256 + 2 * a_grid * P.mini + 7) & ~7ull;  // 16-B aligned sub rows
     if (const int64_t fixed = knob(ctx, "nc.l1_slots", 0))  // test knob: undersize -> resize and re-run
         for (int b = 0; b < 256; ++b) cap[b] = ((uint64_t)fixed + 7) & ~7ull;
     DevBuf<uint64_t> dcap(256), dbase(257);
@@ -1705,7 +1707,7 @@ void node_counter_a(mcaat_ctx *ctx, const mcaat_reads *r, int k, const std::func
     bk.base = base;
     for (int b = 0; b < 256; ++b) {
         n_desc += tot[b];
-        if (tot[b]) bk.regions[b].push_back({base[b], tot[b]});  // tot: whole kMini-slot reservations
+        if (tot[b]) bk.regions[b].push_back({base[b], tot[b]});  // tot: whole reservations
     }
     // algorithmic bytes of the launch: the 2-bit stream read once, a 16-B descriptor and its
     // 2-B sub row written per reserved slot (the tail slots of a reservation are written inert)
@@ -1755,6 +1757,7 @@ std::shared_ptr<NcAhead> nc_ahead_begin(mcaat_ctx *ctx, int k, uint64_t n_occ_es
     a->k = k;
     a->P = sk_params(k);
     a->P.l2_bits = nc_fine_bits(ctx, n_occ_est) - 8;
+    if (knob_set(ctx, "nc.a_mini")) a->P.mini = (uint32_t)std::max<int64_t>(8, knob(ctx, "nc.a_mini", 1024)) & ~7u;
     a->bk = std::make_shared<NcBuckets>();
     a->bk->l2_bits = a->P.l2_bits;
     a->a_grid = (uint64_t)kAPerCu * ctx->n_cu;
@@ -1764,7 +1767,7 @@ std::shared_ptr<NcAhead> nc_ahead_begin(mcaat_ctx *ctx, int k, uint64_t n_occ_es
     a->cap.assign(256, 0);
     a->base.assign(257, 0);
     for (int b = 0; b < 256; ++b) {
-        a->cap[b] = (est / 256 + 2 * a->a_grid * kMini + 7) & ~7ull;
+        a->cap[b] = (est / 256 + 2 * a->a_grid * a->P.mini + 7) & ~7ull;
         if (const int64_t fixed = knob(ctx, "nc.l1_slots", 0)) a->cap[b] = ((uint64_t)fixed + 7) & ~7ull;
         a->base[b + 1] = a->base[b] + a->cap[b];
     }

@@ -45,6 +45,10 @@ KNOBS = {
     "grow_early_free_sync": {"nc.group_budget": 1, "nc.out_cap": 64, "nc.grow_early": 1, "nc.free_sync": 1},
     # L1 buckets undersized on the first pass-A attempt: resize and re-run
     "l1_resize": {"nc.l1_slots": 64, "nc.fine_bits": 12},
+    # (round 6) pass A's reservations of 256 slots (a sharded rank's) and of 8 (many grabs per
+    # flush, every bucket's run larger than a reservation: the synchronous grab path)
+    "a_mini256": {"nc.a_mini": 256},
+    "a_mini8": {"nc.a_mini": 8},
     # every partition overflows the LDS edge table: class split, then the class-filtered global
     # fallback, one (partition, class) per batch
     "fallback": {"nc.edge_cap": 8, "nc.fallback_budget": 1},
