@@ -1267,6 +1267,22 @@ __global__ void __launch_bounds__(kBlk) k_cbfs(GraphView g, const uint64_t *fron
     }
 }
 
+// (round 6) the same hop with the frontier size read on the device: the hops run back to back
+// with no host round trip between them (the frontier buffers hold every edge of the replica, and
+// each edge joins a frontier at most once)
+__global__ void __launch_bounds__(kBlk) k_cbfs_dev(GraphView g, const uint64_t *front, const unsigned long long *nf_p,
+                                                   uint64_t *seen, uint64_t *next, unsigned long long *nn) {
+    const uint64_t nf = *nf_p, stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nf; j += stride) {
+        uint64_t out[4];
+        const int od = dev_outgoing(g, front[j], out);
+        for (int b = 0; b < od; ++b) {
+            const uint64_t x = out[b], bit = 1ULL << (x & 63);
+            if (!(atomicOr((unsigned long long *)&seen[x >> 6], bit) & bit)) next[atomicAdd(nn, 1ull)] = x;
+        }
+    }
+}
+
 // the region's edges of this rank as records {id, out_info, in_info, mult | valid << 16}
 __global__ void __launch_bounds__(kBlk) k_region_list(const uint64_t *reg, uint64_t n, const uint64_t *wpre, uint64_t id_lo,
                                                       const uint64_t *out_info, const uint64_t *in_info, const uint16_t *mult,
@@ -2149,23 +2165,45 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
     {
         const std::vector<uint64_t> sc = to_compact(hgid, starts);
         const uint64_t nwr = mcaat_graph::bitmap_words(rg.D);
-        DevBuf<uint64_t> rseen(nwr), front(sc.size() + 1);
-        DevBuf<unsigned long long> nn(1);
+        DevBuf<uint64_t> rseen(nwr);
         HIP_OK(hipMemsetAsync(rseen.p, 0, rseen.bytes(), st));
-        uint64_t nf = sc.size();
-        if (nf) {
+        const uint64_t nf = sc.size();
+        if (nf && knob(ctx, "dist.bfs_sync", 0) == 0) {
+            // (round 6) the hops back to back on the device: ping-pong frontiers of the replica's
+            // size, per-hop counts in device memory (one host wait after the last hop instead of
+            // one per hop: C3 at one rank, the DLS stage's 78 waits)
+            DevBuf<uint64_t> fr[2];
+            fr[0].alloc(rg.D + 1);
+            fr[1].alloc(rg.D + 1);
+            DevBuf<unsigned long long> cnt(radius + 1);
+            HIP_OK(hipMemsetAsync(cnt.p, 0, cnt.bytes(), st));
+            h2d(ctx, fr[0].p, sc.data(), 8 * nf);
+            h2d(ctx, cnt.p, &nf, 8);
+            hipLaunchKernelGGL(k_set_ids, dim3(s.grid(nf)), dim3(kBlk), 0, st, (const uint64_t *)fr[0].p, nf, rseen.p);
+            LAUNCH_OK();
+            const unsigned gcap = s.grid(rg.D);
+            for (uint64_t h = 0; h < radius; ++h) {
+                hipLaunchKernelGGL(k_cbfs_dev, dim3(gcap), dim3(kBlk), 0, st, rg.view(), (const uint64_t *)fr[h & 1].p,
+                                   (const unsigned long long *)(cnt.p + h), rseen.p, fr[(h + 1) & 1].p, cnt.p + h + 1);
+                LAUNCH_OK();
+            }
+            HIP_OK(hipStreamSynchronize(st));
+        } else if (nf) {  // dist.bfs_sync=1: round 5's form, the frontier size read after every hop
+            DevBuf<uint64_t> front(nf + 1);
+            DevBuf<unsigned long long> nn(1);
+            uint64_t m = nf;
             h2d(ctx, front.p, sc.data(), 8 * nf);
             hipLaunchKernelGGL(k_set_ids, dim3(s.grid(nf)), dim3(kBlk), 0, st, (const uint64_t *)front.p, nf, rseen.p);
             LAUNCH_OK();
-        }
-        for (uint64_t h = 0; h < radius && nf; ++h) {
-            DevBuf<uint64_t> next(4 * nf);
-            HIP_OK(hipMemsetAsync(nn.p, 0, 8, st));
-            hipLaunchKernelGGL(k_cbfs, dim3(s.grid(nf)), dim3(kBlk), 0, st, rg.view(), (const uint64_t *)front.p, nf,
-                               rseen.p, next.p, nn.p);
-            LAUNCH_OK();
-            nf = read_u64(ctx, nn.p);
-            front = std::move(next);
+            for (uint64_t h = 0; h < radius && m; ++h) {
+                DevBuf<uint64_t> next(4 * m);
+                HIP_OK(hipMemsetAsync(nn.p, 0, 8, st));
+                hipLaunchKernelGGL(k_cbfs, dim3(s.grid(m)), dim3(kBlk), 0, st, rg.view(), (const uint64_t *)front.p, m,
+                                   rseen.p, next.p, nn.p);
+                LAUNCH_OK();
+                m = read_u64(ctx, nn.p);
+                front = std::move(next);
+            }
         }
         std::vector<uint64_t> words(nwr);
         d2h(ctx, words.data(), rseen.p, 8 * nwr);

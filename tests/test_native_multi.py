@@ -132,7 +132,10 @@ def _ranks(world, comm, extra=(), timeout=600):
                                          # adjacency, filter windows and flags by request / response
                                          # messages (round 5's first form) instead of target ranges
                                          (2, ("--knob", "dist.adj_ranges=0", "--knob", "dist.win_ranges=0")),
-                                         (3, ("--knob", "dist.win_ranges=0"))])
+                                         (3, ("--knob", "dist.win_ranges=0")),
+                                         # (round 6) the FindCycle reach on the replica hop by hop
+                                         # with host waits (round 5's form)
+                                         (2, ("--knob", "dist.bfs_sync=1"))])
 def test_sharded_build_and_cycle_finder_ranks_share_one_gpu(world, extra):
     """(round 5: per-shard CycleFinder by default) the sharded build + CycleFinder over 1-4 ranks
     sharing the GPU equal the one-GPU path: keys, multiplicities, valid bits after CycleFinder,
