@@ -383,6 +383,10 @@ void mcaat_reset_timing(mcaat_ctx *ctx);
  *                      bits are popcounted)
  *   cf.dls_host        1: DepthLevelSearch candidates and results through the host (default 0:
  *                      on one GPU they stay on the device and only the passing ids come back)
+ *   cf.compact         1: the peel's per-edge arrays over compact slots of the filter-valid edges,
+ *                      0: one slot per edge id; unset (round 6): compact when the multiplicity
+ *                      filter keeps under cf.compact_pct % (default 30) of a fresh graph's edges
+ *                      (C5 keeps 18 %: its peel state 63 -> 12 GB at the same peel time)
  *   cf.peel_list_div   first ruler-list capacity D / div (default 16; the prep pass runs again
  *                      with the counted size when it overflows)
  *   cf.peel_list_cap / cf.cand_cap   first capacity of the ruler and branch lists / of the

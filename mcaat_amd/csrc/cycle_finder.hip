@@ -2447,7 +2447,11 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
     // removal walks of long chains pay a binary search per edge (PeelArrays::gid) and the tips
     // pass a prefix load per successor; C5 68.1 either way. Off by default (the memory saving
     // stays available: C5's peel state 63 -> 12 GB).
-    const bool compact = knob(ctx, "cf.compact", 0) != 0 && D && D < (1ULL << 32) && knob(ctx, "cf.walk_budget", 0) <= 0;
+    // (round 6) unset, it is decided after the multiplicity filter (below): compact when the filter
+    // keeps under cf.compact_pct % (30) of a fresh graph's edges. C5 keeps 18 %: its peel state
+    // falls from 63 to 12 GB at the same peel time (68.1 ms either way); C3 keeps 59 % and stays
+    // per id (compact costs it 12 ms there)
+    bool compact = knob(ctx, "cf.compact", 0) != 0 && D && D < (1ULL << 32) && knob(ctx, "cf.walk_budget", 0) <= 0;
     // the recount's counts and ChunkStartNodes' filter come from the tips / filter pass
     // (cf.recount = 1: the separate post-peel pass of round 2)
     const bool fold = knob(ctx, "cf.recount", 0) == 0;
@@ -2488,6 +2492,13 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
                 HIP_OK(hipStreamSynchronize(st));
                 comm->allgatherv_dev(mpost.p, post.p, sz.data());
             }
+        }
+        if (!knob_set(ctx, "cf.compact") && !comm && fresh && fuse && D && D < (1ULL << 32) &&
+            knob(ctx, "cf.walk_budget", 0) <= 0) {
+            unsigned long long low = 0;  // every mult <= 1 edge: on a fresh graph, the edges the filter clears
+            d2h(ctx, &low, c2.p + 1, 8);
+            const uint64_t kept = D - std::min<uint64_t>(D, low);
+            compact = kept * 100 < (uint64_t)std::max<int64_t>(0, knob(ctx, "cf.compact_pct", 30)) * D;
         }
         if (compact) {  // compact slots: exclusive prefix of the filtered words' popcounts
             DevBuf<uint32_t> pc(nw + 1);

@@ -1868,6 +1868,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
         nr = s.list_bits(rbits.p, rl);
         nb = s.list_bits(bbits.p, bl);
     }
+    verbose_mark(ctx, "shard_cf.peel_prep");
     uint64_t walk_rounds = 0;
     {
         DevBuf<uint64_t> w(2 * (nr ? nr : 1));
@@ -1892,6 +1893,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
             m = r.n_in;
         }
     }
+    verbose_mark(ctx, "shard_cf.peel_walk");
     // pointer jumping over the rulers still pointing at a ruler
     uint64_t jump_rounds = 0;
     {
@@ -1942,6 +1944,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
             LAUNCH_OK();
         }
     }
+    verbose_mark(ctx, "shard_cf.peel_jumps");
     // branch successors' references (two lookups: the successor, then a claiming ruler's terminal)
     DevBuf<uint64_t> ref(4 * (nb ? nb : 1));  // per branch slot: its successor's reference, kPad unused
     if (nb) {
@@ -1981,6 +1984,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
         }
         s.rt.reply(r2, ans2.p, 1, ref.p);
     }
+    verbose_mark(ctx, "shard_cf.peel_bref");
     // branch resolution rounds (until no branch changes on any rank)
     uint64_t res_rounds = 0;
     {
@@ -2011,6 +2015,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
             if (s.sum(ch) == 0) break;
         }
     }
+    verbose_mark(ctx, "shard_cf.peel_resolution");
     // removal: resolved non-unary edges, rulers whose terminal went, and the chains they claimed
     uint64_t n_rm_rulers = 0;
     {
@@ -2072,6 +2077,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
                 "%llu removed rulers\n",
                 comm.rank, (unsigned long long)nr, (unsigned long long)nb, (unsigned long long)walk_rounds,
                 (unsigned long long)jump_rounds, (unsigned long long)res_rounds, (unsigned long long)n_rm_rulers);
+    verbose_mark(ctx, "shard_cf.peel_removal");
     kind.release();
     stt.release();
     nx.release();
@@ -2143,7 +2149,9 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
         fprintf(stderr, "[mcaat] shard %d: %zu candidates, DLS region %llu edges\n", comm.rank, cand_all.size(),
                 (unsigned long long)hgid.size());
     ctx->kstats["shard_dls_region_edges"].launches = hgid.size();
+    verbose_mark(ctx, "shard_cf.dls_begin");
     std::vector<uint64_t> pass_c = cf_depth_level_search(&rg, to_compact(hgid, cand_all), p.cycle_max_length, &comm);
+    verbose_mark(ctx, "shard_cf.dls_search");
     // buckets by ceil(log2 mult) (cycle_finder.cpp:414), descending; ascending ids within
     std::map<int, std::vector<uint64_t>, std::greater<int>> chunks;
     if (!pass_c.empty()) {
@@ -2159,6 +2167,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
             starts.push_back(id);
         }
     out->stats[4] = out->cand_ids.size();
+    verbose_mark(ctx, "shard_cf.dls_buckets");
     // FindCycle's forward reach (cycle_max_length + 1 hops from the starts) lies inside the
     // DepthLevelSearch region (the starts are candidates): found on the replica, no exchange
     std::vector<uint64_t> fwd;  // its edge ids, ascending
@@ -2213,6 +2222,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
                 if (c < hgid.size()) fwd.push_back(hgid[c]);
             }
     }
+    verbose_mark(ctx, "shard_cf.fc_reach");
     rg = mcaat_graph{};
     timer.mark("dls");
     xr("dls");

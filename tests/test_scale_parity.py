@@ -112,6 +112,9 @@ KNOBS = {
     # (round 4) peel arrays over compact slots instead of edge ids, with and without the fused
     # first pass; the tips pass reading the unfiltered bitmap although every edge is valid
     "peel_compact": {"cf.compact": 1},
+    # (round 6) the automatic choice taking compact slots on every case, and never
+    "compact_auto_all": {"cf.compact_pct": 101},
+    "compact_auto_never": {"cf.compact_pct": 0},
     "peel_compact_own_init": {"cf.compact": 1, "cf.fused_init": 0},
     "tips_not_fresh": {"cf.fresh": 0},
     "compact_lists_regrow": {"cf.compact": 1, "cf.peel_list_cap": 1, "cf.cand_cap": 1, "cf.fresh": 0},
