@@ -19,6 +19,7 @@ from .lib import (  # noqa: F401
     edges_reduce,
     device_count,
     load_library,
+    preload,
     synth_arrays,
     synth_genome_host,
     synth_host,

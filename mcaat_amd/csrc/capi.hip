@@ -365,6 +365,9 @@ int mcaat_preload(int device) {
         mcaat::preload_sdbg_build();
         mcaat::preload_cycle_finder();
         mcaat::preload_read_mapping();
+        mcaat::preload_shard();
+        mcaat::preload_shard_cf();
+        mcaat::preload_sdbg_succinct();
         (void)hipGetLastError();
     });
 }

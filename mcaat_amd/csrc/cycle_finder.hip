@@ -1966,6 +1966,7 @@ static std::vector<uint64_t> run_dls_dev(mcaat_graph *g, const uint64_t *dcand, 
         first = false;
         cs = std::max<uint32_t>(cs, 8 * kLdsStk);
         cv = std::max<uint32_t>(cv, 8 * kLdsVis);
+        verbose_mark(ctx, "dls.lds_pass");
     }
     for (; nt; first = false) {
         const uint64_t batch_cap = std::max<uint64_t>(64, budget / (8ULL * (cs + cv)));
@@ -2010,6 +2011,7 @@ static std::vector<uint64_t> run_dls_dev(mcaat_graph *g, const uint64_t *dcand, 
             cv *= 8;
         }
     }
+    verbose_mark(ctx, "dls.reruns");
     hipLaunchKernelGGL(k_res_pass, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, st, (const int8_t *)res.p, n, flags.p);
     LAUNCH_OK();
     const uint64_t np = select_dev(ctx, dcand, flags.p, n, ids.p);
@@ -2399,6 +2401,7 @@ std::vector<uint64_t> cf_depth_level_search(mcaat_graph *g, const std::vector<ui
     if (knob(g->ctx, "cf.dls_host", 0) != 0 || cand.empty()) return run_dls(g, cand, limit);
     DevBuf<uint64_t> d(cand.size());
     h2d(g->ctx, d.p, cand.data(), 8 * cand.size());
+    verbose_mark(g->ctx, "dls.upload");
     return run_dls_dev(g, d.p, cand.size(), limit);
 }
 

@@ -71,6 +71,9 @@ void preload_sdbg_build();
 void preload_cycle_finder();
 void preload_fastq_pack();
 void preload_read_mapping();
+void preload_shard();  // the multi-GPU build, per-shard CycleFinder and succinct view modules
+void preload_shard_cf();
+void preload_sdbg_succinct();
 
 // owning device buffer
 template <class T>

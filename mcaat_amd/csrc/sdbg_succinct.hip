@@ -805,4 +805,9 @@ void graph_succinct_check(mcaat_graph *g, bool check, uint64_t *out, double *ms)
     event_put(ctx, b);
 }
 
+void preload_sdbg_succinct() {
+    hipFuncAttributes a;
+    (void)hipFuncGetAttributes(&a, (const void *)k_sv_sym);
+}
+
 }  // namespace mcaat

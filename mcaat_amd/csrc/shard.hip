@@ -398,4 +398,9 @@ void graph_from_sorted(mcaat_ctx *ctx, int k, const uint64_t *keys, const uint16
     sdbg_finish(ctx, g);
 }
 
+void preload_shard() {
+    hipFuncAttributes a;
+    (void)hipFuncGetAttributes(&a, (const void *)k_boss_hist);
+}
+
 }  // namespace mcaat

@@ -868,6 +868,31 @@ __global__ void __launch_bounds__(kBlk) k_bits_list(const uint64_t *bm, uint64_t
     }
 }
 
+// a search region's ids: the position of each edge id in the region's ascending gid list (its
+// compact id; ~0 when it is not in the region), and back (~0 for positions past the list)
+__global__ void __launch_bounds__(kBlk) k_gid_find(const uint64_t *gid, uint64_t rn, const uint64_t *ids, uint64_t m,
+                                                   uint64_t *out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const uint64_t x = ids[i];
+    uint64_t lo = 0, hi = rn;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (gid[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    out[i] = (lo < rn && gid[lo] == x) ? lo : ~0ULL;
+}
+__global__ void __launch_bounds__(kBlk) k_gid_of(const uint64_t *gid, uint64_t rn, const uint64_t *c, uint64_t m,
+                                                 uint64_t *out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) out[i] = c[i] < rn ? gid[c[i]] : ~0ULL;
+}
+__global__ void __launch_bounds__(kBlk) k_mult_of(const uint16_t *mult, const uint64_t *c, uint64_t m, uint16_t *out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) out[i] = mult[c[i]];
+}
+
 // walkers: {ruler, edge}; results: {ruler | 1 << 63, reached} (reached: a non-unary edge, kRef |
 // a ruler, or kNo on a unary cycle). A walker claims each non-ruler unary edge it passes by
 // swapping its successor word for kOwn | ruler (compare-and-swap: one claimer per edge); a
@@ -1366,25 +1391,62 @@ struct ShardCf {
           nwl((gr->D_local + 63) / 64) {}
 
     // the set bits of a local bitmap (nwl words) as local indices, ascending
-    uint64_t list_bits(const uint64_t *bm, DevBuf<uint64_t> &out) {
-        DevBuf<uint64_t> pc(nwl + 1), wpre(nwl + 1);
-        HIP_OK(hipMemsetAsync(pc.p + nwl, 0, 8, st));
+    // (nw: the bitmap's words, default this rank's)
+    uint64_t list_bits(const uint64_t *bm, DevBuf<uint64_t> &out, uint64_t nw = ~0ULL) {
+        if (nw == ~0ULL) nw = nwl;
+        DevBuf<uint64_t> pc(nw + 1), wpre(nw + 1);
+        HIP_OK(hipMemsetAsync(pc.p + nw, 0, 8, st));
         uint64_t cnt = 0;
-        if (nwl) {
-            hipLaunchKernelGGL(k_word_popc64, dim3(grid(nwl)), dim3(kBlk), 0, st, bm, nwl, pc.p);
+        if (nw) {
+            hipLaunchKernelGGL(k_word_popc64, dim3(grid(nw)), dim3(kBlk), 0, st, bm, nw, pc.p);
             LAUNCH_OK();
             size_t tmp = 0;
-            HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, pc.p, wpre.p, (size_t)(nwl + 1), st));
+            HIP_OK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, pc.p, wpre.p, (size_t)(nw + 1), st));
             DevBuf<uint8_t> t(tmp);
-            HIP_OK(hipcub::DeviceScan::ExclusiveSum(t.p, tmp, pc.p, wpre.p, (size_t)(nwl + 1), st));
-            d2h(ctx, &cnt, wpre.p + nwl, 8);
+            HIP_OK(hipcub::DeviceScan::ExclusiveSum(t.p, tmp, pc.p, wpre.p, (size_t)(nw + 1), st));
+            d2h(ctx, &cnt, wpre.p + nw, 8);
         }
         out.alloc(cnt ? cnt : 1);
         if (cnt) {
-            hipLaunchKernelGGL(k_bits_list, dim3(grid(nwl * 64)), dim3(kBlk), 0, st, bm, nwl, (const uint64_t *)wpre.p, out.p);
+            hipLaunchKernelGGL(k_bits_list, dim3(grid(nw * 64)), dim3(kBlk), 0, st, bm, nw, (const uint64_t *)wpre.p, out.p);
             LAUNCH_OK();
         }
         return cnt;
+    }
+
+    // (round 6) a search region's id translations on the device, where its gid list stays (its
+    // 8 B per edge were read back whole before: C3 at one rank, 20 ms for the DLS region's 5.5 M
+    // ids and 16 ms of host binary searches for the candidates)
+    // edge ids -> compact ids of region rg (rn edges); every id must lie in the region
+    std::vector<uint64_t> to_compact(const mcaat_graph &rg, uint64_t rn, const std::vector<uint64_t> &ids) {
+        const uint64_t m = ids.size();
+        std::vector<uint64_t> c(m);
+        if (!m) return c;
+        DevBuf<uint64_t> d(m), o(m);
+        h2d(ctx, d.p, ids.data(), 8 * m);
+        hipLaunchKernelGGL(k_gid_find, dim3(grid(m)), dim3(kBlk), 0, st, (const uint64_t *)rg.gid.p, rn,
+                           (const uint64_t *)d.p, m, o.p);
+        LAUNCH_OK();
+        d2h(ctx, c.data(), o.p, 8 * m);
+        for (uint64_t x : c)
+            if (x == ~0ULL) throw Error(MCAAT_E_INVALID, "per-shard CycleFinder: a start is outside its region");
+        return c;
+    }
+    // compact ids (device list of m) -> edge ids (~0 past the region's edges)
+    std::vector<uint64_t> to_global(const mcaat_graph &rg, uint64_t rn, const uint64_t *c, uint64_t m) {
+        std::vector<uint64_t> g(m);
+        if (!m) return g;
+        DevBuf<uint64_t> o(m);
+        hipLaunchKernelGGL(k_gid_of, dim3(grid(m)), dim3(kBlk), 0, st, (const uint64_t *)rg.gid.p, rn, c, m, o.p);
+        LAUNCH_OK();
+        d2h(ctx, g.data(), o.p, 8 * m);
+        return g;
+    }
+    std::vector<uint64_t> to_global(const mcaat_graph &rg, uint64_t rn, const std::vector<uint64_t> &c) {
+        if (c.empty()) return {};
+        DevBuf<uint64_t> d(c.size());
+        h2d(ctx, d.p, c.data(), 8 * c.size());
+        return to_global(rg, rn, d.p, c.size());
     }
 
     // in[j] where flags[j] != 0, in order (hipcub select); returns the count
@@ -1433,7 +1495,8 @@ struct ShardCf {
     }
 
     // every rank: the compact replica of the groups marked in reg on all ranks
-    void gather_region(const uint64_t *reg, mcaat_graph *rg, std::vector<uint64_t> &hgid) {
+    // returns the region's edge count (rg->gid: their ascending ids, kept on the device)
+    uint64_t gather_region(const uint64_t *reg, mcaat_graph *rg) {
         DevBuf<uint64_t> pc(nwl + 1), wpre(nwl + 1);
         HIP_OK(hipMemsetAsync(pc.p + nwl, 0, 8, st));
         uint64_t mine = 0;
@@ -1453,6 +1516,7 @@ struct ShardCf {
                                (const uint16_t *)g->mult.p, (const uint64_t *)g->valid.p, rec.p);
             LAUNCH_OK();
         }
+        verbose_mark(ctx, "region.list");
         const std::vector<uint64_t> per = comm.allgather_one(mine);
         uint64_t rn = 0;
         std::vector<uint64_t> bytes(comm.world);
@@ -1460,6 +1524,7 @@ struct ShardCf {
         DevBuf<uint64_t> all(4 * (rn ? rn : 1));
         HIP_OK(hipStreamSynchronize(st));
         if (rn) comm.allgatherv_dev(rec.p, all.p, bytes.data());
+        verbose_mark(ctx, "region.gather");
         // rank order = ascending ids (every rank's list ascends): compact id = position
         const uint64_t D = rn + 16;  // + the null group
         rg->ctx = ctx;
@@ -1484,20 +1549,10 @@ struct ShardCf {
             LAUNCH_OK();
         }
         rg->all_valid = false;
-        hgid.resize(rn);
-        if (rn) d2h(ctx, hgid.data(), rg->gid.p, 8 * rn);
+        verbose_mark(ctx, "region.build");
+        return rn;
     }
 };
-
-std::vector<uint64_t> to_compact(const std::vector<uint64_t> &hgid, const std::vector<uint64_t> &ids) {
-    std::vector<uint64_t> c(ids.size());
-    for (size_t i = 0; i < ids.size(); ++i) {
-        auto it = std::lower_bound(hgid.begin(), hgid.end(), ids[i]);
-        if (it == hgid.end() || *it != ids[i]) throw Error(MCAAT_E_INVALID, "per-shard CycleFinder: a start is outside its region");
-        c[i] = (uint64_t)(it - hgid.begin());
-    }
-    return c;
-}
 
 }  // namespace
 
@@ -2135,9 +2190,9 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
     };
     // DepthLevelSearch region: valid edges within cycle_max_length + 1 hops of the candidates
     forward_region(cand_mine);
+    verbose_mark(ctx, "shard_cf.dls_region_bfs");
     mcaat_graph rg;
-    std::vector<uint64_t> hgid;
-    s.gather_region(reg.p, &rg, hgid);
+    const uint64_t rn = s.gather_region(reg.p, &rg);
     const std::vector<uint64_t> cand_all = [&] {
         std::vector<uint64_t> a = comm.allgather_vec(cand_mine);
         std::sort(a.begin(), a.end());
@@ -2147,17 +2202,27 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
     xr("candidates");
     if (verbose())
         fprintf(stderr, "[mcaat] shard %d: %zu candidates, DLS region %llu edges\n", comm.rank, cand_all.size(),
-                (unsigned long long)hgid.size());
-    ctx->kstats["shard_dls_region_edges"].launches = hgid.size();
+                (unsigned long long)rn);
+    ctx->kstats["shard_dls_region_edges"].launches = rn;
     verbose_mark(ctx, "shard_cf.dls_begin");
-    std::vector<uint64_t> pass_c = cf_depth_level_search(&rg, to_compact(hgid, cand_all), p.cycle_max_length, &comm);
+    const std::vector<uint64_t> cand_c = s.to_compact(rg, rn, cand_all);
+    verbose_mark(ctx, "shard_cf.dls_compact_ids");
+    std::vector<uint64_t> pass_c = cf_depth_level_search(&rg, cand_c, p.cycle_max_length, &comm);
     verbose_mark(ctx, "shard_cf.dls_search");
     // buckets by ceil(log2 mult) (cycle_finder.cpp:414), descending; ascending ids within
     std::map<int, std::vector<uint64_t>, std::greater<int>> chunks;
     if (!pass_c.empty()) {
-        std::vector<uint16_t> hm(rg.D);
-        d2h(ctx, hm.data(), rg.mult.p, 2 * rg.D);
-        for (uint64_t c : pass_c) chunks[(int)std::ceil(std::log2(double(hm[c])))].push_back(hgid[c]);
+        const uint64_t m = pass_c.size();
+        DevBuf<uint64_t> dc(m);
+        DevBuf<uint16_t> dm(m);
+        h2d(ctx, dc.p, pass_c.data(), 8 * m);
+        hipLaunchKernelGGL(k_mult_of, dim3(s.grid(m)), dim3(kBlk), 0, st, (const uint16_t *)rg.mult.p,
+                           (const uint64_t *)dc.p, m, dm.p);
+        LAUNCH_OK();
+        std::vector<uint16_t> hm(m);
+        d2h(ctx, hm.data(), dm.p, 2 * m);
+        const std::vector<uint64_t> ids = s.to_global(rg, rn, dc.p, m);
+        for (uint64_t i = 0; i < m; ++i) chunks[(int)std::ceil(std::log2(double(hm[i])))].push_back(ids[i]);
     }
     std::vector<uint64_t> starts;
     for (auto &kv : chunks)
@@ -2172,7 +2237,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
     // DepthLevelSearch region (the starts are candidates): found on the replica, no exchange
     std::vector<uint64_t> fwd;  // its edge ids, ascending
     {
-        const std::vector<uint64_t> sc = to_compact(hgid, starts);
+        const std::vector<uint64_t> sc = s.to_compact(rg, rn, starts);
         const uint64_t nwr = mcaat_graph::bitmap_words(rg.D);
         DevBuf<uint64_t> rseen(nwr);
         HIP_OK(hipMemsetAsync(rseen.p, 0, rseen.bytes(), st));
@@ -2214,13 +2279,12 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
                 front = std::move(next);
             }
         }
-        std::vector<uint64_t> words(nwr);
-        d2h(ctx, words.data(), rseen.p, 8 * nwr);
-        for (uint64_t w = 0; w < nwr; ++w)
-            for (uint64_t x = words[w]; x; x &= x - 1) {
-                const uint64_t c = w * 64 + (uint64_t)__builtin_ctzll(x);
-                if (c < hgid.size()) fwd.push_back(hgid[c]);
-            }
+        // the reached compact ids, ascending, as edge ids (ascending too); the null group's
+        // positions past the region's edges come last and are dropped
+        DevBuf<uint64_t> rl;
+        const uint64_t nl = s.list_bits(rseen.p, rl, nwr);
+        fwd = s.to_global(rg, rn, rl.p, nl);
+        while (!fwd.empty() && fwd.back() == ~0ULL) fwd.pop_back();
     }
     verbose_mark(ctx, "shard_cf.fc_reach");
     rg = mcaat_graph{};
@@ -2246,15 +2310,14 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
         s.bfs(front, m, radius, true, gs.p, reg.p, seen.p);
     }
     mcaat_graph fg;
-    std::vector<uint64_t> fgid;
-    s.gather_region(reg.p, &fg, fgid);
+    const uint64_t fn = s.gather_region(reg.p, &fg);
     reg.release();
     seen.release();
     gs.release();
-    ctx->kstats["shard_fc_region_edges"].launches = fgid.size();
+    ctx->kstats["shard_fc_region_edges"].launches = fn;
     if (verbose())
         fprintf(stderr, "[mcaat] shard %d: %zu FindCycle starts, region %llu edges; %llu exchanges, %llu records\n",
-                comm.rank, starts.size(), (unsigned long long)fgid.size(), (unsigned long long)s.rt.rounds,
+                comm.rank, starts.size(), (unsigned long long)fn, (unsigned long long)s.rt.rounds,
                 (unsigned long long)s.rt.records);
     ctx->kstats["shard_exchanges"].launches = s.rt.rounds;
     if (verbose())
@@ -2262,13 +2325,19 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
                         "all-to-all %.1f, replies %.1f\n",
                 comm.rank, s.rt.t_count, s.rt.t_gather, s.rt.t_place, s.rt.t_a2a, s.rt.t_reply);
     mcaat_cycles local;
-    cf_find_cycles(&fg, p, to_compact(fgid, starts), &local, &comm);
-    for (size_t i = 0; i < local.starts.size(); ++i) {
-        out->starts.push_back(fgid[local.starts[i]]);
-        std::vector<uint64_t> fl(local.flat[i].size());
-        for (size_t j = 0; j < fl.size(); ++j) fl[j] = fgid[local.flat[i][j]];
-        out->flat.push_back(std::move(fl));
-        out->offsets.push_back(std::move(local.offsets[i]));
+    cf_find_cycles(&fg, p, s.to_compact(fg, fn, starts), &local, &comm);
+    {
+        // the results' compact ids back to edge ids in one translation: the starts, then every flat list
+        std::vector<uint64_t> all(local.starts);
+        for (const auto &fl : local.flat) all.insert(all.end(), fl.begin(), fl.end());
+        const std::vector<uint64_t> g_all = s.to_global(fg, fn, all);
+        size_t at = local.starts.size();
+        for (size_t i = 0; i < local.starts.size(); ++i) {
+            out->starts.push_back(g_all[i]);
+            out->flat.emplace_back(g_all.begin() + at, g_all.begin() + at + local.flat[i].size());
+            at += local.flat[i].size();
+            out->offsets.push_back(std::move(local.offsets[i]));
+        }
     }
     out->stats[5] = local.stats[5];
     out->stats[6] = local.stats[6];
@@ -2341,6 +2410,11 @@ void graph_unshard(mcaat_graph *g, Comm &comm) {
     }
     g->rank_lo.clear();
     g->key_split.clear();
+}
+
+void preload_shard_cf() {
+    hipFuncAttributes a;
+    (void)hipFuncGetAttributes(&a, (const void *)k_route_count);
 }
 
 }  // namespace mcaat

@@ -178,6 +178,12 @@ def device_count() -> int:
     return n.value
 
 
+def preload(device: int = 0) -> None:
+    """Load every module's kernel code objects on `device` now (mcaat_preload), so that the
+    first launch of a stage does not pay HIP's deferred code-object load inside a timed region."""
+    _check(load_library().mcaat_preload(device))
+
+
 @dataclass
 class SynthSpec:
     """Synthetic metagenome. Defaults: the C1 tiny config."""

@@ -96,6 +96,7 @@ def main() -> int:
         cfg = CONFIGS[a.config]
         spec, k, prm = cfg["spec"], cfg["k"], M.CfParams(threshold_multiplicity=cfg["thr"])
         ctx = M.Context(a.rank % max(1, M.device_count()) if a.comm == "rccl" else 0)
+        M.preload(ctx.device)  # stage times without code-object loads
         for kv in a.knob:
             kn, kval = kv.split("=")
             ctx.set_knob(kn, int(kval))
