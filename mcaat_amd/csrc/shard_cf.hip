@@ -869,28 +869,31 @@ __global__ void __launch_bounds__(kBlk) k_bits_list(const uint64_t *bm, uint64_t
 }
 
 // a search region's ids: the position of each edge id in the region's ascending gid list (its
-// compact id; ~0 when it is not in the region), and back (~0 for positions past the list)
+// compact id; ~0 when it is not in the region), and back (~0 for positions past the list);
+// grid-stride (ShardCf::grid caps the grid)
 __global__ void __launch_bounds__(kBlk) k_gid_find(const uint64_t *gid, uint64_t rn, const uint64_t *ids, uint64_t m,
                                                    uint64_t *out) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= m) return;
-    const uint64_t x = ids[i];
-    uint64_t lo = 0, hi = rn;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (gid[mid] < x) lo = mid + 1;
-        else hi = mid;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+        const uint64_t x = ids[i];
+        uint64_t lo = 0, hi = rn;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (gid[mid] < x) lo = mid + 1;
+            else hi = mid;
+        }
+        out[i] = (lo < rn && gid[lo] == x) ? lo : ~0ULL;
     }
-    out[i] = (lo < rn && gid[lo] == x) ? lo : ~0ULL;
 }
 __global__ void __launch_bounds__(kBlk) k_gid_of(const uint64_t *gid, uint64_t rn, const uint64_t *c, uint64_t m,
                                                  uint64_t *out) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < m) out[i] = c[i] < rn ? gid[c[i]] : ~0ULL;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride)
+        out[i] = c[i] < rn ? gid[c[i]] : ~0ULL;
 }
 __global__ void __launch_bounds__(kBlk) k_mult_of(const uint16_t *mult, const uint64_t *c, uint64_t m, uint16_t *out) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < m) out[i] = mult[c[i]];
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) out[i] = mult[c[i]];
 }
 
 // walkers: {ruler, edge}; results: {ruler | 1 << 63, reached} (reached: a non-unary edge, kRef |
