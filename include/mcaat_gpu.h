@@ -414,8 +414,15 @@ int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value);
  *   dist.dir_edges    sharded adjacency: edges per prefix of the range's radix directory (default 2)
  *   nc.a_mini         pass A's slots per (workgroup, L1 bucket) reservation (default 1024 on one GPU,
  *                      256 for a rank of a sharded build; rounded down to a multiple of 8)
- *   dist.bfs_sync     1: the FindCycle reach on the search replica reads its frontier size after every
- *                      hop (round 5's form; default 0: the hops run back to back on the device)
+ *   dist.bfs_sync     1: the region BFS (candidates' forward region, FindCycle's backward region)
+ *                      runs one routed exchange with host waits per hop, and the FindCycle reach on
+ *                      the search replica reads its frontier size after every hop (round 5's forms;
+ *                      default 0: the hops run back to back on the device, fixed-capacity blocks
+ *                      exchanged by an all-to-all that RCCL leaves queued on the stream)
+ *   dist.bfs_block    region BFS: requests per block to another rank (default 2^14; an overflow on
+ *                      any rank reruns the BFS with larger blocks)
+ *   dist.bfs_frontier region BFS: first frontier / own-block capacity (tests; default D_local/16,
+ *                      at least 2^20; an overflow reruns with more)
  *   dist.segs_at_one  1: one rank runs the descriptor exchange through the segment all-to-all too
  *                      (its self-copy path; default 0 keeps the buckets in place) */
 

@@ -56,6 +56,18 @@ struct Comm {
     // (dev is written by work queued on the context's stream; the transports read it after that)
     virtual void allgather_dev_words(const uint64_t *dev, int n, std::vector<uint64_t> &out) = 0;
 
+    // (round 6) fixed-size all-to-all of device blocks: block d of `send` (`bytes` each, N blocks)
+    // goes to rank d and lands as block `rank` of rank d's `recv`; this rank's own block is not
+    // moved. Queued on the context's stream: the RCCL transport returns without waiting for it
+    // (a device-resident loop of exchanges, e.g. the per-shard region BFS, needs no host round
+    // trip per exchange); the default runs it through alltoallv_dev, which does wait.
+    virtual void alltoall_fixed(const void *send, uint64_t bytes, void *recv) {
+        std::vector<uint64_t> sz(world, bytes), off(world);
+        for (int q = 0; q < world; ++q) off[q] = (uint64_t)q * bytes;
+        sz[rank] = 0;
+        alltoallv_dev(send, sz.data(), recv, sz.data(), off.data(), off.data());
+    }
+
     // typed helpers over allgatherv_host
     template <class T>
     std::vector<T> allgather_vec(const std::vector<T> &mine, std::vector<uint64_t> *counts = nullptr) {

@@ -256,6 +256,20 @@ struct RcclComm final : Comm {
         sync();
     }
 
+    // one ncclSend / ncclRecv per peer, grouped, left running on the stream (no synchronise)
+    void alltoall_fixed(const void *send, uint64_t bytes, void *recv) override {
+        Counted cc__(*this);
+        if (world == 1 || !bytes) return;
+        if (bytes > kPiece) throw Error(MCAAT_E_INVALID, "alltoall_fixed: blocks above 1 GiB");
+        NCCL_OK(rccl().GroupStart());
+        for (int p = 0; p < world; ++p) {
+            if (p == rank) continue;
+            NCCL_OK(rccl().Send((const uint8_t *)send + (uint64_t)p * bytes, bytes, ncclUint8, p, comm, ctx->stream));
+            NCCL_OK(rccl().Recv((uint8_t *)recv + (uint64_t)p * bytes, bytes, ncclUint8, p, comm, ctx->stream));
+        }
+        NCCL_OK(rccl().GroupEnd());
+    }
+
     // Segments in rounds: round j holds, for every peer, the j-th send segment and the j-th
     // receive segment (pieces of 1 GiB), so the k-th operation between two ranks sits in the
     // same round on both sides (ncclGroupEnd of one round completes before the next starts on

@@ -1281,6 +1281,109 @@ __global__ void __launch_bounds__(kBlk) k_bfs_claim(const uint64_t *q, uint64_t 
     }
 }
 
+// (round 6) The region BFS with its hops back to back on the device. A hop's requests go into
+// fixed-capacity blocks, one per rank (word 0: the block's request count, then up to its capacity
+// of requests; this rank's own block is separate and holds a whole frontier), exchanged by
+// Comm::alltoall_fixed, which the RCCL transport leaves queued on the stream: no host round trip
+// per hop (round 5's form took three: the count all-gather, the all-to-all, the next frontier's
+// size). Frontier sizes stay in device memory (one counter per hop). A block or frontier that
+// overflows its capacity sets a flag (with the count it needed); the host reads the flags once
+// after the last hop, and if any rank overflowed every rank runs the BFS again with larger blocks.
+struct BfsCaps {
+    uint64_t P;   // requests per block to another rank
+    uint64_t F;   // requests in the own block, edges per frontier
+};
+// flags: [0] a peer block overflowed, [1] the most requests one peer block needed,
+// [2] the own block or a frontier overflowed, [3] the largest own block / frontier needed
+__global__ void __launch_bounds__(kBlk) k_bfs_zero(uint64_t *send, int N, uint64_t P, uint64_t *self_blk) {
+    const int t = threadIdx.x;
+    if (t < N) send[(uint64_t)t * (1 + P)] = 0;
+    if (t == 0) self_blk[0] = 0;
+}
+__global__ void __launch_bounds__(kBlk) k_bfs_req_dev(const uint64_t *front, const unsigned long long *nf_p,
+                                                      const uint64_t *out_info, const uint64_t *in_info, int backward,
+                                                      Owners o, uint64_t *send, BfsCaps c, uint64_t *self_blk,
+                                                      unsigned long long *flags) {
+    const uint64_t nf = min((uint64_t)*nf_p, c.F), stride = (uint64_t)gridDim.x * blockDim.x;  // (past F: flagged)
+    for (uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x; j0 < nf; j0 += stride) {
+        const uint64_t j = j0 + threadIdx.x;
+        uint64_t rec = 0;
+        int d = -1;
+        if (j < nf) {
+            const uint64_t li = front[j];
+            uint64_t lo, pos;
+            if (backward) {
+                const uint64_t ii = in_info[li];
+                lo = ii & kIdM;
+                pos = (ii >> kIdxBits) & 0xFFFF;
+            } else {
+                const uint64_t oi = out_info[li];
+                lo = oi & kIdM;
+                pos = (1ULL << __popc((unsigned)(oi >> kIdxBits) & 0xF)) - 1;
+            }
+            rec = lo | (pos << kIdxBits);
+            if (pos) d = owner_of_id(o, lo);
+        }
+        // one count atomic per destination present in the wave
+        unsigned long long pend = __ballot(d >= 0);
+        while (pend) {
+            const int lead = __ffsll((long long)pend) - 1;
+            const int dd = __shfl(d, lead);
+            const unsigned long long m = __ballot(d == dd);
+            const bool self = dd == o.R;
+            uint64_t *blk = self ? self_blk : send + (uint64_t)dd * (1 + c.P);
+            const uint64_t cap = self ? c.F : c.P;
+            uint64_t base = 0;
+            if ((int)(threadIdx.x & 63) == lead) base = atomicAdd((unsigned long long *)blk, (unsigned long long)__popcll(m));
+            base = __shfl(base, lead);
+            if (d == dd) {
+                const uint64_t at = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+                if (at < cap) blk[1 + at] = rec;
+                if (at + 1 == base + __popcll(m) && base + __popcll(m) > cap) {  // the wave's last slot
+                    atomicOr(&flags[self ? 2 : 0], 1ull);
+                    atomicMax(&flags[self ? 3 : 1], (unsigned long long)(base + __popcll(m)));
+                }
+            }
+            pend &= ~m;
+        }
+    }
+}
+// the owner side of a hop, over every rank's block (blockIdx.y: the source rank); as k_bfs_claim
+__global__ void __launch_bounds__(kBlk) k_bfs_claim_dev(const uint64_t *recv, const uint64_t *self_blk, int R, BfsCaps c,
+                                                        uint64_t id_lo, uint64_t n, const uint64_t *gs,
+                                                        const uint64_t *valid, uint64_t *reg, uint64_t *seen,
+                                                        uint64_t *next, unsigned long long *nn,
+                                                        unsigned long long *flags) {
+    const int src = blockIdx.y;
+    const uint64_t *blk = src == R ? self_blk : recv + (uint64_t)src * (1 + c.P);
+    const uint64_t m = min(blk[0], src == R ? c.F : c.P);
+    const uint64_t *q = blk + 1;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x; j0 < m; j0 += stride) {
+        const uint64_t j = j0 + threadIdx.x;
+        const uint64_t li = j < m ? (q[j] & kIdM) - id_lo : 0;
+        const uint32_t pos = j < m ? (uint32_t)(q[j] >> kIdxBits) & 0xFFFF : 0;
+        if (j < m) mark_group(gs, n, li, reg);
+        for (int b = 0; b < 16; ++b) {
+            const uint64_t y = li + b;
+            bool f = ((pos >> b) & 1) && y < n && bit_of(valid, y);
+            if (f) {
+                const unsigned long long bit = 1ULL << (y & 63);
+                f = !(atomicOr((unsigned long long *)&seen[y >> 6], bit) & bit);
+            }
+            unsigned long long mk;
+            const uint64_t at = wave_reserve(f, nn, mk);
+            if (f) {
+                if (at < c.F) next[at] = y;
+                else {
+                    atomicOr(&flags[2], 1ull);
+                    atomicMax(&flags[3], (unsigned long long)(at + 1));
+                }
+            }
+        }
+    }
+}
+
 // a BFS hop on a region replica (compact ids, every rank alike): the valid successors not seen yet
 __global__ void __launch_bounds__(kBlk) k_cbfs(GraphView g, const uint64_t *front, uint64_t nf, uint64_t *seen, uint64_t *next,
                                                unsigned long long *nn) {
@@ -1494,6 +1597,75 @@ struct ShardCf {
             }
             nf = r.n_in ? read_u64(ctx, c.p + 1) : 0;
             front = std::move(next);
+        }
+    }
+
+    // (round 6) the BFS from this rank's edges `ids` (global ids), hops back to back on the device
+    // (see k_bfs_req_dev); reg and seen are cleared and seeded here, and cleared again for a run
+    // with larger blocks after an overflow on any rank
+    void bfs_dev(const std::vector<uint64_t> &ids, uint64_t rounds, bool backward, const uint64_t *gs, uint64_t *reg,
+                 uint64_t *seen) {
+        const int N = comm.world, R = comm.rank;
+        const uint64_t m = ids.size();
+        DevBuf<uint64_t> dids(m + 1);
+        if (m) h2d(ctx, dids.p, ids.data(), 8 * m);
+        BfsCaps c;
+        c.P = (uint64_t)std::max<int64_t>(64, knob(ctx, "dist.bfs_block", 1 << 14));
+        // a frontier or the own block: the whole local graph in the end (each edge joins one
+        // frontier at most once), a sixteenth of it (and the seeds) first
+        c.F = std::min<uint64_t>(n + 1, std::max<uint64_t>({m + 1, n / 16 + 1, 1u << 20}));
+        if (knob_set(ctx, "dist.bfs_frontier")) c.F = std::max<uint64_t>(m + 1, (uint64_t)knob(ctx, "dist.bfs_frontier", 1));
+        for (int attempt = 0;; ++attempt) {
+            HIP_OK(hipMemsetAsync(reg, 0, 8 * (nwl + 1), st));
+            HIP_OK(hipMemsetAsync(seen, 0, 8 * (nwl + 1), st));
+            DevBuf<uint64_t> fr[2];
+            fr[0].alloc(c.F);
+            fr[1].alloc(c.F);
+            DevBuf<uint64_t> send((uint64_t)N * (1 + c.P)), recv((uint64_t)N * (1 + c.P)), self_blk(1 + c.F);
+            DevBuf<unsigned long long> cnt(rounds + 1), flags(4);
+            HIP_OK(hipMemsetAsync(cnt.p, 0, cnt.bytes(), st));
+            HIP_OK(hipMemsetAsync(flags.p, 0, flags.bytes(), st));
+            if (m) {
+                hipLaunchKernelGGL(k_bfs_seed, dim3(grid(m)), dim3(kBlk), 0, st, (const uint64_t *)dids.p, m, g->id_lo, n, gs,
+                                   reg, seen, fr[0].p);
+                LAUNCH_OK();
+                h2d(ctx, cnt.p, &m, 8);
+            }
+            const unsigned gq = grid(std::min<uint64_t>(c.F, 1u << 22));
+            const unsigned gc = grid(std::min<uint64_t>(std::max(c.F, c.P), 1u << 22)) / (unsigned)N + 1;
+            for (uint64_t h = 0; h < rounds; ++h) {
+                hipLaunchKernelGGL(k_bfs_zero, dim3(1), dim3(kBlk), 0, st, send.p, N, c.P, self_blk.p);
+                LAUNCH_OK();
+                hipLaunchKernelGGL(k_bfs_req_dev, dim3(gq), dim3(kBlk), 0, st, (const uint64_t *)fr[h & 1].p,
+                                   (const unsigned long long *)(cnt.p + h), (const uint64_t *)g->out_info.p,
+                                   (const uint64_t *)g->in_info.p, (int)backward, o, send.p, c, self_blk.p, flags.p);
+                LAUNCH_OK();
+                comm.alltoall_fixed(send.p, 8 * (1 + c.P), recv.p);
+                hipLaunchKernelGGL(k_bfs_claim_dev, dim3(gc, (unsigned)N), dim3(kBlk), 0, st, (const uint64_t *)recv.p,
+                                   (const uint64_t *)self_blk.p, R, c, g->id_lo, n, gs, (const uint64_t *)g->valid.p, reg,
+                                   seen, fr[(h + 1) & 1].p, cnt.p + h + 1, flags.p);
+                LAUNCH_OK();
+            }
+            unsigned long long fl[4];
+            d2h(ctx, fl, flags.p, 32);
+            // every rank takes the same decision (the exchanges are collective)
+            const auto all = comm.allgather_vec(std::vector<uint64_t>{fl[0] | fl[2], fl[1], fl[3]});
+            bool again = false;
+            uint64_t needP = 0, needF = 0;
+            for (int r = 0; r < N; ++r) {
+                again |= all[3 * r] != 0;
+                needP = std::max<uint64_t>(needP, all[3 * r + 1]);
+                needF = std::max<uint64_t>(needF, all[3 * r + 2]);
+            }
+            if (!again) break;
+            if (attempt >= 8) throw Error(MCAAT_E_CAPACITY, "per-shard region BFS: blocks still overflow");
+            // a hop after an overflowed one saw a partial frontier: twice what was counted, at least
+            c.P = std::max(c.P, next_pow2(2 * needP));
+            c.F = std::min<uint64_t>(n + 1, std::max(c.F, 2 * needF));
+            if (needF > c.F) c.F = n + 1;
+            if (verbose())
+                fprintf(stderr, "[mcaat] shard %d: region BFS again with %llu-request blocks, %llu-edge frontiers\n", R,
+                        (unsigned long long)c.P, (unsigned long long)c.F);
         }
     }
 
@@ -2178,7 +2350,14 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
         LAUNCH_OK();
     }
     const uint64_t radius = (uint64_t)p.cycle_max_length + 1;
+    // (round 6) the region BFS hops run back to back on the device (ShardCf::bfs_dev);
+    // dist.bfs_sync=1: round 5's form, one routed exchange with host waits per hop
+    const bool bfs_sync = knob(ctx, "dist.bfs_sync", 0) != 0;
     auto forward_region = [&](const std::vector<uint64_t> &starts_mine) {
+        if (!bfs_sync) {
+            s.bfs_dev(starts_mine, radius, false, gs.p, reg.p, seen.p);
+            return;
+        }
         HIP_OK(hipMemsetAsync(reg.p, 0, reg.bytes(), st));
         HIP_OK(hipMemsetAsync(seen.p, 0, seen.bytes(), st));
         const uint64_t m = starts_mine.size();
@@ -2300,6 +2479,8 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
         // this rank's edges of the forward reach: their groups, and the sources of the backward BFS
         const auto a = std::lower_bound(fwd.begin(), fwd.end(), id_lo), b = std::lower_bound(fwd.begin(), fwd.end(), id_lo + n);
         const std::vector<uint64_t> sm(a, b);
+        if (!bfs_sync) s.bfs_dev(sm, radius, true, gs.p, reg.p, seen.p);
+        else {
         HIP_OK(hipMemsetAsync(reg.p, 0, reg.bytes(), st));
         HIP_OK(hipMemsetAsync(seen.p, 0, seen.bytes(), st));
         const uint64_t m = sm.size();
@@ -2311,6 +2492,7 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
             LAUNCH_OK();
         }
         s.bfs(front, m, radius, true, gs.p, reg.p, seen.p);
+        }
     }
     mcaat_graph fg;
     const uint64_t fn = s.gather_region(reg.p, &fg);

@@ -133,9 +133,14 @@ def _ranks(world, comm, extra=(), timeout=600):
                                          # messages (round 5's first form) instead of target ranges
                                          (2, ("--knob", "dist.adj_ranges=0", "--knob", "dist.win_ranges=0")),
                                          (3, ("--knob", "dist.win_ranges=0")),
-                                         # (round 6) the FindCycle reach on the replica hop by hop
-                                         # with host waits (round 5's form)
-                                         (2, ("--knob", "dist.bfs_sync=1"))])
+                                         # (round 6) the region BFS and the FindCycle reach hop by
+                                         # hop with host waits (round 5's forms)
+                                         (2, ("--knob", "dist.bfs_sync=1")), (3, ("--knob", "dist.bfs_sync=1")),
+                                         # (round 6) the device-resident region BFS with blocks and
+                                         # frontiers too small: every rank reruns it with larger ones
+                                         (3, ("--knob", "dist.bfs_block=64")),
+                                         (2, ("--knob", "dist.bfs_block=64", "--knob", "dist.bfs_frontier=1")),
+                                         (1, ("--knob", "dist.bfs_frontier=1"))])
 def test_sharded_build_and_cycle_finder_ranks_share_one_gpu(world, extra):
     """(round 5: per-shard CycleFinder by default) the sharded build + CycleFinder over 1-4 ranks
     sharing the GPU equal the one-GPU path: keys, multiplicities, valid bits after CycleFinder,
