@@ -178,6 +178,10 @@ struct mcaat_ctx {
     // mcaat_count_ahead: the next host-packed FASTQ read runs node_counter's pass A for this k
     // on its parts as they land (0: off; one read takes it)
     int ahead_k = 0;
+    // per-shard region BFS (shard_cf.hip): the request-block size the last forward / backward BFS
+    // ended with, so the next step starts there instead of rerunning after an overflow (every
+    // rank learns the same size: it is agreed over all ranks)
+    uint64_t bfs_block[2] = {0, 0};
 };
 
 namespace mcaat {

@@ -1611,6 +1611,7 @@ struct ShardCf {
         if (m) h2d(ctx, dids.p, ids.data(), 8 * m);
         BfsCaps c;
         c.P = (uint64_t)std::max<int64_t>(64, knob(ctx, "dist.bfs_block", 1 << 14));
+        if (!knob_set(ctx, "dist.bfs_block")) c.P = std::max(c.P, ctx->bfs_block[backward]);
         // a frontier or the own block: the whole local graph in the end (each edge joins one
         // frontier at most once), a sixteenth of it (and the seeds) first
         c.F = std::min<uint64_t>(n + 1, std::max<uint64_t>({m + 1, n / 16 + 1, 1u << 20}));
@@ -1657,7 +1658,10 @@ struct ShardCf {
                 needP = std::max<uint64_t>(needP, all[3 * r + 1]);
                 needF = std::max<uint64_t>(needF, all[3 * r + 2]);
             }
-            if (!again) break;
+            if (!again) {
+                ctx->bfs_block[backward] = c.P;
+                break;
+            }
             if (attempt >= 8) throw Error(MCAAT_E_CAPACITY, "per-shard region BFS: blocks still overflow");
             // a hop after an overflowed one saw a partial frontier: twice what was counted, at least
             c.P = std::max(c.P, next_pow2(2 * needP));
