@@ -9,7 +9,8 @@
 namespace mcaat {
 
 // One rank of `world`. Every call is collective (all ranks, same order) and returns when
-// this rank's part is complete. Device buffers live on the context's GPU.
+// this rank's part is complete (RCCL's device all-to-alls: when queued on the context stream,
+// ahead of everything later on it). Device buffers live on the context's GPU.
 struct Comm {
     int rank = 0, world = 1;
     // collective calls so far (diagnostics: the exchange rounds of a bulk-synchronous stage);

@@ -5,7 +5,9 @@
 //         opened on first use, so single-GPU runs never load it.
 //   SHM   a POSIX shared-memory segment on the host: device buffers are staged through it
 //         (ranks sharing one GPU, rehearsals, and host-only tests without a GPU).
-// Every operation is collective and synchronous: it returns once this rank's part is done.
+// Every operation is collective. It returns once this rank's part is done, except the RCCL
+// all-to-alls (alltoallv_dev, alltoall_fixed), which return once queued on the context stream:
+// their results are for work ordered behind them on that stream (kernels, d2h).
 #include <dlfcn.h>
 #include <fcntl.h>
 #include <sched.h>
@@ -253,7 +255,10 @@ struct RcclComm final : Comm {
             }
             NCCL_OK(rccl().GroupEnd());
         }
-        sync();
+        // (round 6) no synchronise: the exchange stays queued on the context stream, and every
+        // consumer of `recv` (kernels, d2h) is ordered behind it on that stream, as every reuse of
+        // `send` through the stream-ordered arena is; a routed round now waits on the host once,
+        // for its count all-gather, instead of three times
     }
 
     // one ncclSend / ncclRecv per peer, grouped, left running on the stream (no synchronise)

@@ -352,7 +352,7 @@ struct Router {
                                rt.out_off[R]);
             LAUNCH_OK();
         }
-        HIP_OK(hipStreamSynchronize(st));
+        // (no synchronise: `out` is read by kernels or d2h on the same stream)
         ++rounds;
     }
 };
