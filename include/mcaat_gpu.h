@@ -423,6 +423,11 @@ int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value);
  *                      any rank reruns the BFS with larger blocks)
  *   dist.bfs_frontier region BFS: first frontier / own-block capacity (tests; default D_local/16,
  *                      at least 2^20; an overflow reruns with more)
+ *   dist.res_fixed    0: the peel's branch resolution by routed rounds (round 5's form; default 1:
+ *                      fixed blocks, rounds back to back on the device, one check per batch)
+ *   dist.res_batch    branch resolution rounds per batch between checks (default 8)
+ *   dist.res_block_mb largest block set (MB) for fixed-block resolution; larger graphs keep the
+ *                      routed rounds (default 64)
  *   dist.segs_at_one  1: one rank runs the descriptor exchange through the segment all-to-all too
  *                      (its self-copy path; default 0 keeps the buckets in place) */
 

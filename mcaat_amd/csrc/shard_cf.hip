@@ -1348,6 +1348,55 @@ __global__ void __launch_bounds__(kBlk) k_bfs_req_dev(const uint64_t *front, con
         }
     }
 }
+// (round 6) fixed-block request / reply (branch resolution): slot j's request q[j] goes to rank
+// dest[j] (kNoDest: none) into that rank's block (word 0: count; this rank's own requests into
+// its own block, which holds every slot), its position kept in pos[j]; the answers come back in
+// the same positions
+__global__ void __launch_bounds__(kBlk) k_fx_post(const uint64_t *q, const uint8_t *dest, uint64_t m, int R,
+                                                  uint64_t *send, uint64_t P, uint64_t *self_blk, uint32_t *pos) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x; j0 < m; j0 += stride) {
+        const uint64_t j = j0 + threadIdx.x;
+        const int d = j < m && dest[j] != kNoDest ? (int)dest[j] : -1;
+        unsigned long long pend = __ballot(d >= 0);
+        while (pend) {
+            const int lead = __ffsll((long long)pend) - 1;
+            const int dd = __shfl(d, lead);
+            const unsigned long long mk = __ballot(d == dd);
+            uint64_t *blk = dd == R ? self_blk : send + (uint64_t)dd * (1 + P);
+            uint64_t base = 0;
+            if ((int)(threadIdx.x & 63) == lead) base = atomicAdd((unsigned long long *)blk, (unsigned long long)__popcll(mk));
+            base = __shfl(base, lead);
+            if (d == dd) {
+                const uint64_t at = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0));
+                blk[1 + at] = q[j];  // (P holds every slot of the largest rank: no overflow)
+                pos[j] = (uint32_t)at;
+            }
+            pend &= ~mk;
+        }
+    }
+}
+// the owner: each received request's state (as k_st_ans) into the reply block at its position
+__global__ void __launch_bounds__(kBlk) k_fx_st_ans(const uint64_t *recv, const uint64_t *self_blk, int R, uint64_t P,
+                                                    const uint8_t *st, uint64_t id_lo, uint64_t *rsend, uint64_t *rself) {
+    const int src = blockIdx.y;
+    const uint64_t *blk = src == R ? self_blk : recv + (uint64_t)src * (1 + P);
+    uint64_t *out = src == R ? rself : rsend + (uint64_t)src * (1 + P);
+    const uint64_t m = blk[0];
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += stride) out[1 + j] = st[blk[1 + j] - id_lo];
+}
+// the requester: slot j's answer from its destination's reply block
+__global__ void __launch_bounds__(kBlk) k_fx_gather(const uint8_t *dest, const uint32_t *pos, uint64_t m, int R,
+                                                    const uint64_t *rrecv, uint64_t P, const uint64_t *rself, uint64_t *out) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += stride) {
+        if (dest[j] == kNoDest) continue;
+        const int d = dest[j];
+        out[j] = d == R ? rself[1 + pos[j]] : rrecv[(uint64_t)d * (1 + P) + 1 + pos[j]];
+    }
+}
+
 // the owner side of a hop, over every rank's block (blockIdx.y: the source rank); as k_bfs_claim
 __global__ void __launch_bounds__(kBlk) k_bfs_claim_dev(const uint64_t *recv, const uint64_t *self_blk, int R, BfsCaps c,
                                                         uint64_t id_lo, uint64_t n, const uint64_t *gs,
@@ -2221,7 +2270,61 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
     verbose_mark(ctx, "shard_cf.peel_bref");
     // branch resolution rounds (until no branch changes on any rank)
     uint64_t res_rounds = 0;
-    {
+    // (round 6) in fixed blocks, the rounds back to back on the device in batches (a round after
+    // one without a change changes nothing, so the batch's last round decides): one queued
+    // all-to-all each way per round and one host wait per batch, against a routed exchange, a
+    // reply and a sum (three host waits) per round. Blocks hold every slot of the rank with the
+    // most branches; above dist.res_block_mb (64 MB of blocks) the routed rounds stay.
+    const uint64_t nb_most = [&] {
+        uint64_t x = 0;
+        for (uint64_t v : comm.allgather_one(nb)) x = std::max(x, v);
+        return x;
+    }();
+    const uint64_t resP = 4 * nb_most;
+    const bool res_fixed = knob(ctx, "dist.res_fixed", 1) != 0 &&
+                           8 * (uint64_t)comm.world * (1 + resP) <= ((uint64_t)std::max<int64_t>(1, knob(ctx, "dist.res_block_mb", 64)) << 20);
+    if (res_fixed) {
+        const int N = comm.world, R = comm.rank;
+        const uint64_t m = 4 * nb, P = resP;
+        DevBuf<uint64_t> q(m + 1), a(m + 1);
+        DevBuf<uint8_t> dest(m + 1);
+        DevBuf<uint32_t> pos(m + 1);
+        DevBuf<uint64_t> send((uint64_t)N * (1 + P)), recv((uint64_t)N * (1 + P)), self_blk(1 + m);
+        DevBuf<uint64_t> rsend((uint64_t)N * (1 + P)), rrecv((uint64_t)N * (1 + P)), rself(1 + m);
+        const int K = (int)std::max<int64_t>(1, knob(ctx, "dist.res_batch", 8));
+        for (bool done = false; !done;) {
+            for (int b = 0; b < K; ++b, ++res_rounds) {
+                HIP_OK(hipMemsetAsync(cnt.p + 7, 0, 8, st));
+                hipLaunchKernelGGL(k_bfs_zero, dim3(1), dim3(kBlk), 0, st, send.p, N, P, self_blk.p);
+                LAUNCH_OK();
+                if (nb) {
+                    hipLaunchKernelGGL(k_res_req, dim3(s.grid(nb)), dim3(kBlk), 0, st, (const uint64_t *)bl.p,
+                                       (const uint64_t *)ref.p, nb, stt.p, s.o, q.p, dest.p, cnt.p + 7);
+                    LAUNCH_OK();
+                    hipLaunchKernelGGL(k_fx_post, dim3(s.grid(m)), dim3(kBlk), 0, st, (const uint64_t *)q.p,
+                                       (const uint8_t *)dest.p, m, R, send.p, P, self_blk.p, pos.p);
+                    LAUNCH_OK();
+                }
+                comm.alltoall_fixed(send.p, 8 * (1 + P), recv.p);
+                hipLaunchKernelGGL(k_fx_st_ans, dim3(s.grid(std::max<uint64_t>(m, 1)) / (unsigned)N + 1, (unsigned)N),
+                                   dim3(kBlk), 0, st, (const uint64_t *)recv.p, (const uint64_t *)self_blk.p, R, P,
+                                   (const uint8_t *)stt.p, id_lo, rsend.p, rself.p);
+                LAUNCH_OK();
+                comm.alltoall_fixed(rsend.p, 8 * (1 + P), rrecv.p);
+                if (nb) {
+                    hipLaunchKernelGGL(k_fx_gather, dim3(s.grid(m)), dim3(kBlk), 0, st, (const uint8_t *)dest.p,
+                                       (const uint32_t *)pos.p, m, R, (const uint64_t *)rrecv.p, P,
+                                       (const uint64_t *)rself.p, a.p);
+                    LAUNCH_OK();
+                    hipLaunchKernelGGL(k_res_apply, dim3(s.grid(nb)), dim3(kBlk), 0, st, (const uint64_t *)bl.p, nb,
+                                       (const uint64_t *)a.p, (const uint8_t *)dest.p, stt.p, cnt.p + 7);
+                    LAUNCH_OK();
+                }
+            }
+            const uint64_t ch = read_u64(ctx, cnt.p + 7);  // the batch's last round
+            done = s.sum(ch) == 0;
+        }
+    } else {
         DevBuf<uint64_t> q(4 * nb + 1);
         DevBuf<uint8_t> dest(4 * nb + 1);
         for (;; ++res_rounds) {
