@@ -426,6 +426,10 @@ int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value);
  *   dist.res_fixed    0: the peel's branch resolution by routed rounds (round 5's form; default 1:
  *                      fixed blocks, rounds back to back on the device, one check per batch)
  *   dist.res_batch    branch resolution rounds per batch between checks (default 8)
+ *   dist.walk_block   the peel walk's tail: once every rank's records in flight fit this many, its
+ *                      rounds run in fixed blocks back to back on the device (default 2^15; 0: every
+ *                      round routed, round 5's form)
+ *   dist.walk_batch   walk tail rounds per batch between checks (default 8)
  *   dist.res_block_mb largest block set (MB) for fixed-block resolution; larger graphs keep the
  *                      routed rounds (default 64)
  *   dist.segs_at_one  1: one rank runs the descriptor exchange through the segment all-to-all too

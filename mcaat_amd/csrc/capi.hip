@@ -1096,7 +1096,7 @@ int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value) {
         "fq.hostpack",     "sort.mid_counting", "nc.big_table", "cf.fused_init", "sort.mid_occ", "cf.scan_u", "cf.prep_batch", "cf.dls_lanes", "dist.oriented",
         "sort.small_mid", "sort.small_limit", "cf.recount", "cf.dls_host",
         "dist.desc",      "cf.compact",         "cf.fresh",   "cf.dls_persist", "nc.split_first", "nc.split_max", "cf.pull_flags", "cf.dls_budget", "nc.grow_early",
-        "nc.free_sync", "dist.shard_cf", "dist.ruler_mask", "dist.adj_chunk", "dist.dir_edges", "nc.ahead", "dist.adj_ranges", "dist.win_ranges", "cf.dls_lds", "cf.dls_lds_cap", "dist.segs_at_one", "nc.a_mini", "dist.bfs_sync", "cf.compact_pct", "dist.bfs_block", "dist.bfs_frontier", "dist.res_fixed", "dist.res_batch", "dist.res_block_mb"};
+        "nc.free_sync", "dist.shard_cf", "dist.ruler_mask", "dist.adj_chunk", "dist.dir_edges", "nc.ahead", "dist.adj_ranges", "dist.win_ranges", "cf.dls_lds", "cf.dls_lds_cap", "dist.segs_at_one", "nc.a_mini", "dist.bfs_sync", "cf.compact_pct", "dist.bfs_block", "dist.bfs_frontier", "dist.res_fixed", "dist.res_batch", "dist.res_block_mb", "dist.walk_block", "dist.walk_batch"};
     return guarded([&] {
         require(ctx && name, "null argument");
         bool ok = false;

@@ -16,6 +16,9 @@ struct Comm {
     // collective calls so far (diagnostics: the exchange rounds of a bulk-synchronous stage);
     // a collective that calls another one internally counts once
     uint64_t n_coll = 0;
+    // of them, the device all-to-alls (alltoallv_dev, alltoall_fixed): RCCL leaves them queued on
+    // the stream, so they cost no host round trip (diagnostics: the rest are the host waits)
+    uint64_t n_queued = 0;
     int coll_depth = 0;
     struct Counted {
         Comm &c;

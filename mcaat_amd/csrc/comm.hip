@@ -230,6 +230,7 @@ struct RcclComm final : Comm {
     void alltoallv_dev(const void *send, const uint64_t *send_bytes, void *recv, const uint64_t *recv_bytes,
                        const uint64_t *send_off, const uint64_t *recv_off) override {
         Counted cc__(*this);
+        if (coll_depth == 1) ++n_queued;
         auto so = offsets_of(send_bytes, world), ro = offsets_of(recv_bytes, world);
         if (send_off) so.assign(send_off, send_off + world);
         if (recv_off) ro.assign(recv_off, recv_off + world);
@@ -264,6 +265,7 @@ struct RcclComm final : Comm {
     // one ncclSend / ncclRecv per peer, grouped, left running on the stream (no synchronise)
     void alltoall_fixed(const void *send, uint64_t bytes, void *recv) override {
         Counted cc__(*this);
+        if (coll_depth == 1) ++n_queued;
         if (world == 1 || !bytes) return;
         if (bytes > kPiece) throw Error(MCAAT_E_INVALID, "alltoall_fixed: blocks above 1 GiB");
         NCCL_OK(rccl().GroupStart());
@@ -559,6 +561,7 @@ struct ShmComm final : Comm {
     void alltoallv_dev(const void *send, const uint64_t *send_bytes, void *recv, const uint64_t *recv_bytes,
                        const uint64_t *send_off, const uint64_t *recv_off) override {
         Counted cc__(*this);
+        if (coll_depth == 1) ++n_queued;
         need_ctx();
         auto so = offsets_of(send_bytes, world), ro = offsets_of(recv_bytes, world);
         if (send_off) so.assign(send_off, send_off + world);

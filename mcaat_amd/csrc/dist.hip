@@ -130,7 +130,7 @@ void build_graph_sharded(mcaat_ctx *ctx, Comm &comm, const mcaat_reads *r, int k
     hipStream_t st = ctx->stream;
     const int N = comm.world, R = comm.rank;
     StageTimer timer(ctx);
-    const uint64_t xr0 = comm.n_coll;  // the build's collectives (kstats "xr_build")
+    const uint64_t xr0 = comm.n_coll, xq0 = comm.n_queued;  // the build's collectives (kstats "xr_build", queued "xq_build")
     CountResult c;
     const bool desc_route = knob(ctx, "dist.desc", 1) != 0 && !knob(ctx, "dist.oriented", 0);
     if (desc_route) {
@@ -291,6 +291,7 @@ void build_graph_sharded(mcaat_ctx *ctx, Comm &comm, const mcaat_reads *r, int k
         HIP_OK(hipStreamSynchronize(st));
         timer.finish();
         ctx->kstats["xr_build"].launches += comm.n_coll - xr0;
+        ctx->kstats["xq_build"].launches += comm.n_queued - xq0;
         return;
     }
     g->key.alloc(D ? D : 1);
@@ -308,6 +309,7 @@ void build_graph_sharded(mcaat_ctx *ctx, Comm &comm, const mcaat_reads *r, int k
     HIP_OK(hipStreamSynchronize(st));
     timer.finish();
     ctx->kstats["xr_build"].launches += comm.n_coll - xr0;
+    ctx->kstats["xq_build"].launches += comm.n_queued - xq0;
 }
 
 }  // namespace mcaat

@@ -917,72 +917,127 @@ __global__ void __launch_bounds__(kBlk) k_walk_init(const uint64_t *rl, uint64_t
     }
 }
 
-// one round: results land in their rulers' jump words (nx of the ruler: a walk stops at a ruler
-// before reading its word); walkers advance over this rank's edges and leave for the owner of
-// the next one
-__global__ void __launch_bounds__(kBlk) k_walk(const uint64_t *in, uint64_t m, const uint8_t *kind, uint64_t *nx, Owners o,
-                                               uint64_t *out, uint8_t *dest, int merge_known) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x; j0 < m; j0 += stride) {
-        const uint64_t j = j0 + threadIdx.x;
-        bool emit = false;
-        uint64_t r = 0, x = 0;
-        int to = 0;
-        if (j < m) {
-            r = in[2 * j];
-            x = in[2 * j + 1];
-            if (r & kResult) {
-                nx[(r & kIdM) - o.id_lo] = x;
+// one record of a walk round: a result lands in its ruler's jump word (nx of the ruler: a walk
+// stops at a ruler before reading its word); a walker advances over this rank's edges and leaves
+// for the owner of the next one, or ends with a result for its ruler's owner. Returns whether a
+// record goes out (to rank `to`, as {r, x})
+__device__ __forceinline__ bool walk_one(uint64_t &r, uint64_t &x, const uint8_t *kind, uint64_t *nx, const Owners &o,
+                                         int merge_known, int &to) {
+    if (r & kResult) {
+        nx[(r & kIdM) - o.id_lo] = x;
+        return false;
+    }
+    for (;;) {
+        if (x < o.id_lo || x >= o.id_lo + o.n) {  // leaves for the owner of x
+            to = owner_of_id(o, x);
+            return true;
+        }
+        const uint64_t li = x - o.id_lo;
+        uint64_t v = nx[li];
+        bool done = true;
+        if (is_chain(v)) {  // a unary edge, not a ruler, unclaimed
+            const uint64_t own = kOwn | r;
+            if (merge_known && !(v & kMergeW)) {
+                nx[li] = own;  // one unary predecessor: no other walk comes here
+                x = v & kIdM;
+                done = false;
             } else {
-                for (;;) {
-                    if (x < o.id_lo || x >= o.id_lo + o.n) {  // leaves for the owner of x
-                        emit = true;
-                        to = owner_of_id(o, x);
-                        break;
-                    }
-                    const uint64_t li = x - o.id_lo;
-                    uint64_t v = nx[li];
-                    uint64_t res = 0;
-                    bool done = true;
-                    if (is_chain(v)) {  // a unary edge, not a ruler, unclaimed
-                        const uint64_t own = kOwn | r;
-                        if (merge_known && !(v & kMergeW)) {
-                            nx[li] = own;  // one unary predecessor: no other walk comes here
-                            x = v & kIdM;
-                            done = false;
-                        } else {
-                            const uint64_t prev = atomicCAS((unsigned long long *)&nx[li], v, own);
-                            if (prev == v) {
-                                x = v & kIdM;  // claimed: on to the successor
-                                done = false;
-                            } else {
-                                v = prev;  // another walk's claim
-                            }
-                        }
-                    }
-                    if (done) {
-                        if (is_claim(v)) {
-                            res = (v & kIdM) == r ? kNo : (kRef | (v & kIdM));
-                        } else {
-                            const uint8_t k = kind[li];  // once per walk: where it ends
-                            res = __popc(k & 0xF) != 1 ? x : (kRef | x);  // a non-unary edge or a ruler
-                        }
-                    }
-                    if (done) {
-                        emit = true;
-                        to = owner_of_id(o, r);
-                        r |= kResult;
-                        x = res;
-                        break;
-                    }
+                const uint64_t prev = atomicCAS((unsigned long long *)&nx[li], v, own);
+                if (prev == v) {
+                    x = v & kIdM;  // claimed: on to the successor
+                    done = false;
+                } else {
+                    v = prev;  // another walk's claim
                 }
             }
         }
-        if (j < m) {  // one output slot per input record
-            out[2 * j] = r;
-            out[2 * j + 1] = x;
-            dest[j] = emit ? (uint8_t)to : kNoDest;
+        if (done) {
+            uint64_t res;
+            if (is_claim(v)) {
+                res = (v & kIdM) == r ? kNo : (kRef | (v & kIdM));
+            } else {
+                const uint8_t k = kind[li];  // once per walk: where it ends
+                res = __popc(k & 0xF) != 1 ? x : (kRef | x);  // a non-unary edge or a ruler
+            }
+            to = owner_of_id(o, r);
+            r |= kResult;
+            x = res;
+            return true;
         }
+    }
+}
+
+__global__ void __launch_bounds__(kBlk) k_walk(const uint64_t *in, uint64_t m, const uint8_t *kind, uint64_t *nx, Owners o,
+                                               uint64_t *out, uint8_t *dest, int merge_known) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < m; j += stride) {
+        uint64_t r = in[2 * j], x = in[2 * j + 1];
+        int to = 0;
+        const bool emit = walk_one(r, x, kind, nx, o, merge_known, to);
+        out[2 * j] = r;  // one output slot per input record
+        out[2 * j + 1] = x;
+        dest[j] = emit ? (uint8_t)to : kNoDest;
+    }
+}
+
+// (round 6) the walk's tail in fixed blocks (once every rank's records in flight fit one block):
+// the records of every source block (blockIdx.y; this rank's own from self_in) walk, and what goes
+// out lands in the destination's block of `send` or in self_out (word 0 of a block: its records)
+__global__ void __launch_bounds__(kBlk) k_walk_fx(const uint64_t *recv, const uint64_t *self_in, int R, uint64_t P,
+                                                  const uint8_t *kind, uint64_t *nx, Owners o, uint64_t *send,
+                                                  uint64_t *self_out, int merge_known) {
+    const int src = blockIdx.y;
+    const uint64_t *blk = src == R ? self_in : recv + (uint64_t)src * (1 + 2 * P);
+    const uint64_t m = blk[0];
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j0 = (uint64_t)blockIdx.x * blockDim.x; j0 < m; j0 += stride) {
+        const uint64_t j = j0 + threadIdx.x;
+        uint64_t r = 0, x = 0;
+        int to = -1;
+        if (j < m) {
+            r = blk[1 + 2 * j];
+            x = blk[2 + 2 * j];
+            if (!walk_one(r, x, kind, nx, o, merge_known, to)) to = -1;
+        }
+        unsigned long long pend = __ballot(to >= 0);
+        while (pend) {
+            const int lead = __ffsll((long long)pend) - 1;
+            const int dd = __shfl(to, lead);
+            const unsigned long long mk = __ballot(to == dd);
+            uint64_t *ob = dd == R ? self_out : send + (uint64_t)dd * (1 + 2 * P);
+            uint64_t base = 0;
+            if ((int)(threadIdx.x & 63) == lead) base = atomicAdd((unsigned long long *)ob, (unsigned long long)__popcll(mk));
+            base = __shfl(base, lead);
+            if (to == dd) {
+                // (records never multiply: a block holds every record in flight when the tail began)
+                const uint64_t at = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0));
+                ob[1 + 2 * at] = r;
+                ob[2 + 2 * at] = x;
+            }
+            pend &= ~mk;
+        }
+    }
+}
+// zero the counts of N blocks of `stride` words, and of one more block
+__global__ void k_blk_zero(uint64_t *blocks, int N, uint64_t stride, uint64_t *one) {
+    const int t = threadIdx.x;
+    if (t < N) blocks[(uint64_t)t * stride] = 0;
+    if (t == 0 && one) one[0] = 0;
+}
+// a routed round's received records (n of them) into the own block of the tail's first round
+__global__ void __launch_bounds__(kBlk) k_walk_fx_seed(const uint64_t *in, uint64_t n, uint64_t *self_blk) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < 2 * n; j += stride) self_blk[1 + j] = in[j];
+    if (blockIdx.x == 0 && threadIdx.x == 0) self_blk[0] = n;
+}
+// the records one round put out on this rank (every block's count), added into *tot
+__global__ void k_walk_fx_count(const uint64_t *send, int N, int R, uint64_t P, const uint64_t *self_out,
+                                unsigned long long *tot) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        unsigned long long t = self_out[0];
+        for (int q = 0; q < N; ++q)
+            if (q != R) t += send[(uint64_t)q * (1 + 2 * P)];
+        *tot = t;
     }
 }
 
@@ -2005,10 +2060,12 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
     const uint64_t n = s.n, nwl = s.nwl, id_lo = g->id_lo;
     // collectives per stage (kstats "xr_<stage>".launches): the bulk-synchronous rounds that bound
     // this path at N ranks (DESIGN.md §7's model)
-    uint64_t xr_last = comm.n_coll;
+    uint64_t xr_last = comm.n_coll, xq_last = comm.n_queued;
     auto xr = [&](const char *stage) {
         ctx->kstats[std::string("xr_") + stage].launches += comm.n_coll - xr_last;
+        ctx->kstats[std::string("xq_") + stage].launches += comm.n_queued - xq_last;  // of them queued
         xr_last = comm.n_coll;
+        xq_last = comm.n_queued;
     };
     DevBuf<unsigned long long> cnt(8);
     HIP_OK(hipMemsetAsync(cnt.p, 0, 64, st));
@@ -2153,6 +2210,10 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
     }
     verbose_mark(ctx, "shard_cf.peel_prep");
     uint64_t walk_rounds = 0;
+    // (round 6) the walk's tail in fixed blocks of dist.walk_block records (default 2^15; 0: every
+    // round routed, round 5's form)
+    const uint64_t walkP = (uint64_t)std::max<int64_t>(0, knob(ctx, "dist.walk_block", 1 << 15));
+    const bool walk_fixed = walkP > 0;
     {
         DevBuf<uint64_t> w(2 * (nr ? nr : 1));
         if (nr) {
@@ -2174,6 +2235,41 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
             if (!r.total) break;
             w = std::move(r.in);
             m = r.n_in;
+            // (round 6) the tail: once every rank's records in flight fit one block (they never
+            // multiply), the rounds run in fixed blocks back to back on the device, one queued
+            // all-to-all each, checked once per batch (an empty round changes nothing)
+            if (walk_fixed && r.total <= walkP) {
+                const int N = comm.world, R = comm.rank;
+                const uint64_t P = walkP, bs = 1 + 2 * P;
+                DevBuf<uint64_t> send((uint64_t)N * bs), recv((uint64_t)N * bs), sb[2];
+                sb[0].alloc(bs);
+                sb[1].alloc(bs);
+                DevBuf<unsigned long long> tot(1);
+                hipLaunchKernelGGL(k_blk_zero, dim3(1), dim3(kBlk), 0, st, recv.p, N, bs, (uint64_t *)nullptr);
+                LAUNCH_OK();
+                hipLaunchKernelGGL(k_walk_fx_seed, dim3(s.grid(2 * m + 1)), dim3(kBlk), 0, st, (const uint64_t *)w.p, m,
+                                   sb[0].p);
+                LAUNCH_OK();
+                const unsigned gy = s.grid(P) / (unsigned)N + 1;
+                const int K = (int)std::max<int64_t>(1, knob(ctx, "dist.walk_batch", 8));
+                int t = 0;
+                for (bool done = false; !done;) {
+                    for (int b = 0; b < K; ++b, ++t, ++walk_rounds) {
+                        hipLaunchKernelGGL(k_blk_zero, dim3(1), dim3(kBlk), 0, st, send.p, N, bs, sb[(t + 1) & 1].p);
+                        LAUNCH_OK();
+                        hipLaunchKernelGGL(k_walk_fx, dim3(gy, (unsigned)N), dim3(kBlk), 0, st, (const uint64_t *)recv.p,
+                                           (const uint64_t *)sb[t & 1].p, R, P, (const uint8_t *)kind.p, nx.p, s.o, send.p,
+                                           sb[(t + 1) & 1].p, (int)win_ranges);
+                        LAUNCH_OK();
+                        comm.alltoall_fixed(send.p, 8 * bs, recv.p);
+                    }
+                    hipLaunchKernelGGL(k_walk_fx_count, dim3(1), dim3(64), 0, st, (const uint64_t *)send.p, N, R, P,
+                                       (const uint64_t *)sb[t & 1].p, tot.p);
+                    LAUNCH_OK();
+                    done = s.sum(read_u64(ctx, tot.p)) == 0;  // the batch's last round put nothing out
+                }
+                break;
+            }
         }
     }
     verbose_mark(ctx, "shard_cf.peel_walk");

@@ -143,7 +143,12 @@ def _ranks(world, comm, extra=(), timeout=600):
                                          (1, ("--knob", "dist.bfs_frontier=1")),
                                          # (round 6) branch resolution: routed rounds (round 5's
                                          # form) / fixed blocks checked after every round
-                                         (3, ("--knob", "dist.res_fixed=0")), (2, ("--knob", "dist.res_batch=1"))])
+                                         (3, ("--knob", "dist.res_fixed=0")), (2, ("--knob", "dist.res_batch=1")),
+                                         # (round 6) the walk: every round routed / the fixed-block
+                                         # tail from the first round on, checked every round
+                                         (3, ("--knob", "dist.walk_block=0")),
+                                         (3, ("--knob", "dist.walk_block=4194304", "--knob", "dist.walk_batch=1")),
+                                         (4, ("--knob", "dist.walk_block=4194304"))])
 def test_sharded_build_and_cycle_finder_ranks_share_one_gpu(world, extra):
     """(round 5: per-shard CycleFinder by default) the sharded build + CycleFinder over 1-4 ranks
     sharing the GPU equal the one-GPU path: keys, multiplicities, valid bits after CycleFinder,

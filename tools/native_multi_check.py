@@ -139,6 +139,8 @@ def main() -> int:
             d["build_hbm_peak_GB"] = round(build_peak / 1e9, 2)
             # collectives per stage on this rank (each a bulk-synchronous exchange round)
             d["collectives"] = {st: ctx.kernel_timing("xr_" + st)[1] for st in XR_STAGES}
+            # of them the device all-to-alls RCCL leaves queued (the rest wait on the host)
+            d["collectives_queued"] = {st: ctx.kernel_timing("xq_" + st)[1] for st in XR_STAGES}
         g.free()
         if comm is not None:
             comm.barrier()

@@ -17,7 +17,7 @@ for r in range(${WORLD:-2}):
     same = {k: a[k] == b[k] for k in ("D", "keys", "mult", "valid", "stats", "results", "entries", "cycles")}
     print("rank", r, "equal to one GPU:", all(same.values()), same)
     print("  cf hbm", b.get("cf_hbm_GB"), "one GPU", a.get("cf_hbm_GB"), "build peak", b.get("build_hbm_peak_GB"))
-    print("  collectives", b.get("collectives"))
+    print("  collectives", b.get("collectives"), "queued", b.get("collectives_queued"))
     print("  build ms", b.get("build_stages_ms"))
     print("  cf ms", b.get("cf_stages_ms"))
 PY
