@@ -128,7 +128,11 @@ def main() -> int:
             res = g.cycle_finder(prm, comm=comm)
             cf_stages = {kk: round(vv, 2) for kk, vv in ctx.stage_times().items()}
             cf_mem = (cf_base, ctx.arena_usage()[1])
-            g.unshard(comm)  # a per-shard graph is gathered for the checksums (no-op otherwise)
+            # a per-shard graph is gathered for the checksums (no-op otherwise); the arena's cached
+            # chunks go back first (eight ranks sharing one GPU each gather the whole graph)
+            ctx.trim()
+            comm.barrier()
+            g.unshard(comm)
         d = checksums(g, res)
         d["seconds"] = round(time.time() - t0, 1)
         d["cf_stages_ms"] = cf_stages
