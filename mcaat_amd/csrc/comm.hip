@@ -267,14 +267,17 @@ struct RcclComm final : Comm {
         Counted cc__(*this);
         if (coll_depth == 1) ++n_queued;
         if (world == 1 || !bytes) return;
-        if (bytes > kPiece) throw Error(MCAAT_E_INVALID, "alltoall_fixed: blocks above 1 GiB");
-        NCCL_OK(rccl().GroupStart());
-        for (int p = 0; p < world; ++p) {
-            if (p == rank) continue;
-            NCCL_OK(rccl().Send((const uint8_t *)send + (uint64_t)p * bytes, bytes, ncclUint8, p, comm, ctx->stream));
-            NCCL_OK(rccl().Recv((uint8_t *)recv + (uint64_t)p * bytes, bytes, ncclUint8, p, comm, ctx->stream));
+        // blocks above 1 GiB in pieces, every peer's piece c in group c (as alltoallv_dev)
+        for (uint64_t c0 = 0; c0 < bytes; c0 += kPiece) {
+            const uint64_t n = std::min(kPiece, bytes - c0);
+            NCCL_OK(rccl().GroupStart());
+            for (int p = 0; p < world; ++p) {
+                if (p == rank) continue;
+                NCCL_OK(rccl().Send((const uint8_t *)send + (uint64_t)p * bytes + c0, n, ncclUint8, p, comm, ctx->stream));
+                NCCL_OK(rccl().Recv((uint8_t *)recv + (uint64_t)p * bytes + c0, n, ncclUint8, p, comm, ctx->stream));
+            }
+            NCCL_OK(rccl().GroupEnd());
         }
-        NCCL_OK(rccl().GroupEnd());
     }
 
     // Segments in rounds: round j holds, for every peer, the j-th send segment and the j-th
