@@ -350,6 +350,10 @@ def measure_ingest(ctx, spec, n_reads: int) -> dict:
                 "and GPU parse",
     }
 
+# per-stage collective counters of the sharded path (kstats "xr_<stage>" / "xq_<stage>")
+XR_STAGES = ("build", "tips_filter", "peel", "recount", "candidates", "dls", "find_cycle")
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -573,6 +577,12 @@ def main() -> int:
             },
             "stages_ms": {kk: round(vv, 3) for kk, vv in stages.items()},
             "post_path": post,
+            # N > 1 (sharded): rank 0's collectives per step and stage, and of them the device
+            # all-to-alls RCCL leaves queued on the stream (the rest are host round trips)
+            "collectives_per_step": ({st: ctx.kernel_timing("xr_" + st)[1] / max(1, args.steps) for st in XR_STAGES}
+                                     if sharded and not args.dry_run else None),
+            "collectives_queued_per_step": ({st: ctx.kernel_timing("xq_" + st)[1] / max(1, args.steps) for st in XR_STAGES}
+                                            if sharded and not args.dry_run else None),
             "fastq_ingest": ingest,
             "cpu_baseline": None,
         }
