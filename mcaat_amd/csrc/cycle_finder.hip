@@ -1544,6 +1544,20 @@ __global__ void k_fc_pairs(const uint64_t *nodes, const uint32_t *nodej, uint64_
     }
 }
 
+// (round 6) a pair (i << 32 | j) as the sort key (j << b | i): by the start reached, then by the
+// start whose cycles reach it (b bits hold any start index of the round)
+__global__ void k_fc_pair_keys(const uint64_t *pairs, uint64_t n, int b, uint64_t *keys) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t a = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; a < n; a += stride)
+        keys[a] = ((pairs[a] & 0xFFFFFFFFull) << b) | (pairs[a] >> 32);
+}
+// segments of a device list into one compact list (one block per segment; seg = {from, count, to})
+__global__ void k_fc_segs(const uint64_t *src, const uint64_t *seg, uint64_t *dst) {
+    const uint64_t *sg = seg + 3 * (uint64_t)blockIdx.x;
+    const uint64_t from = sg[0], n = sg[1], to = sg[2];
+    for (uint64_t i = threadIdx.x; i < n; i += blockDim.x) dst[to + i] = src[from + i];
+}
+
 // first[x] = the smallest committing start whose cycles pass through x, for x not yet visited
 __global__ void k_fc_first(const uint64_t *nodes, const uint32_t *nodej, uint64_t n, const uint8_t *active,
                            const uint64_t *vis, uint64_t *hkeys, uint32_t *hvals, uint32_t cap) {
@@ -2128,20 +2142,37 @@ struct FcRunner {
         HIP_OK(hipMemcpyAsync(pv.data(), prev.p, nb, hipMemcpyDeviceToHost, st));
         HIP_OK(hipMemcpyAsync(&np, dnp.p, 8, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
-        std::vector<uint64_t> pairs(np);
+        // (round 6) the pairs sorted and made unique on the device, as (j << pb | i): a start's
+        // cycles pass through another start once per cycle and node, so the raw pairs repeat
+        // (C5: 6.5 ms of copies and a host sort per round before)
+        int pb = 1;
+        while ((1ull << pb) < (uint64_t)nb) ++pb;
+        std::vector<uint64_t> pairs;
         if (np) {
-            HIP_OK(hipMemcpyAsync(pairs.data(), dpairs.p, 8 * np, hipMemcpyDeviceToHost, st));
-            HIP_OK(hipStreamSynchronize(st));
-            std::sort(pairs.begin(), pairs.end(), [](uint64_t a, uint64_t b) {
-                return (uint32_t)a != (uint32_t)b ? (uint32_t)a < (uint32_t)b : a < b;
-            });
+            DevBuf<uint64_t> k1(np), k2(np);
+            DevBuf<unsigned long long> nu(1);
+            hipLaunchKernelGGL(k_fc_pair_keys, dim3(grid_for(np, kBlock)), dim3(kBlock), 0, st, (const uint64_t *)dpairs.p,
+                               (uint64_t)np, pb, k1.p);
+            LAUNCH_OK();
+            size_t t1 = 0, t2 = 0;
+            HIP_OK(hipcub::DeviceRadixSort::SortKeys(nullptr, t1, k1.p, k2.p, (int)np, 0, 2 * pb, st));
+            HIP_OK(hipcub::DeviceSelect::Unique(nullptr, t2, k2.p, k1.p, nu.p, (int)np, st));
+            DevBuf<uint8_t> tmp(std::max<size_t>({t1, t2, 1}));
+            HIP_OK(hipcub::DeviceRadixSort::SortKeys(tmp.p, t1, k1.p, k2.p, (int)np, 0, 2 * pb, st));
+            HIP_OK(hipcub::DeviceSelect::Unique(tmp.p, t2, k2.p, k1.p, nu.p, (int)np, st));
+            unsigned long long nuq = 0;
+            d2h(g->ctx, &nuq, nu.p, 8);
+            pairs.resize(nuq);
+            if (nuq) d2h(g->ctx, pairs.data(), k1.p, 8 * nuq);
         }
+        const uint64_t pmask = (1ull << pb) - 1;
+        verbose_mark(g->ctx, "fc.commit_pairs");
         // (1) skips, in start order (pairs sorted by the start they reach)
         std::vector<uint8_t> active(nb, 0);
         for (uint32_t j = 0, q = 0; j < nb; ++j) {
             bool sk = pv[j] != 0;
-            for (; q < pairs.size() && (uint32_t)pairs[q] == j; ++q)
-                if (!skip[pairs[q] >> 32]) sk = true;
+            for (; q < pairs.size() && (pairs[q] >> pb) == j; ++q)
+                if (!skip[pairs[q] & pmask]) sk = true;
             skip[j] = sk ? 1 : 0;
             active[j] = sk ? 0 : 1;
         }
@@ -2154,6 +2185,7 @@ struct FcRunner {
                                act.p, dvis.p, hkeys.p, hvals.p, hcap);
             LAUNCH_OK();
         }
+        verbose_mark(g->ctx, "fc.commit_first");
         // (3) conflicts: only starts that commit after some other start can conflict
         uint64_t f = first_bad;
         std::vector<uint32_t> jm, js;
@@ -2181,6 +2213,7 @@ struct FcRunner {
             HIP_OK(hipStreamSynchronize(st));
             if (h != none) my_first = h;
         }
+        verbose_mark(g->ctx, "fc.commit_conf");
         if (N > 1)
             for (uint64_t x : comm->allgather_one(my_first)) my_first = std::min(my_first, x);
         f = std::min(f, my_first);
@@ -2274,7 +2307,9 @@ struct FcRunner {
                         coff.push_back(coff.back() + mine.st[i].ncyc);
                     }
                 }
-                mine.nodes.resize(noff.back());
+                // (round 6) one GPU: the nodes stay on the device until the commit says which
+                // starts' cycles are results (a window's skipped starts often hold most of them)
+                if (N > 1) mine.nodes.resize(noff.back());
                 mine.lens.resize(coff.back());
                 if (!sel.empty()) {
                     DevBuf<uint64_t> dsel(sel.size()), dno(noff.size()), dco(coff.size()), dn(noff.back());
@@ -2285,7 +2320,7 @@ struct FcRunner {
                     hipLaunchKernelGGL(k_fc_gather, dim3((unsigned)sel.size()), dim3(256), 0, st, (uint64_t *)scratch.p,
                                        pa, caps, dsel.p, dno.p, dco.p, dn.p, dl.p, (uint64_t)sel.size());
                     LAUNCH_OK();
-                    d2h(g->ctx, mine.nodes.data(), dn.p, 8 * mine.nodes.size());
+                    if (N > 1) d2h(g->ctx, mine.nodes.data(), dn.p, 8 * mine.nodes.size());
                     d2h(g->ctx, mine.lens.data(), dl.p, 2 * mine.lens.size());
                     if (N == 1) {  // one GPU: slot i is start i
                         dj_keep.alloc(noff.back());
@@ -2297,6 +2332,7 @@ struct FcRunner {
                     HIP_OK(hipStreamSynchronize(st));
                 }
             }
+            verbose_mark(g->ctx, "fc.gather_nodes");
             // every rank's outputs (one GPU: its own)
             std::vector<RankOut> others;
             std::vector<const RankOut *> ro(N);
@@ -2328,6 +2364,7 @@ struct FcRunner {
             }
             std::vector<const uint64_t *> jn(W, nullptr);
             std::vector<const uint16_t *> jc(W, nullptr);
+            std::vector<uint64_t> joff(N == 1 ? W : 0);  // one GPU: start j's nodes at joff[j] on the device
             std::vector<uint32_t> selj;  // starts before the first overflow that found cycles
             uint64_t n_nodes = 0;
             {
@@ -2337,7 +2374,8 @@ struct FcRunner {
                 for (uint64_t j = 0; j < first_bad; ++j) {
                     const int o = (int)(j % N);
                     if (hs[j]->ncyc > 0) {
-                        jn[j] = ro[o]->nodes.data() + nptr[o];
+                        if (N == 1) joff[j] = nptr[o];
+                        else jn[j] = ro[o]->nodes.data() + nptr[o];
                         jc[j] = ro[o]->lens.data() + cptr[o];
                         nptr[o] += hs[j]->nnodes;
                         cptr[o] += hs[j]->ncyc;
@@ -2351,6 +2389,32 @@ struct FcRunner {
             const uint64_t f = commit_round(pending, W, first_bad, selj, jn, hs, n_nodes, scratch.p, pa, skip,
                                             dn_keep.p ? dn_keep.p : nullptr, dj_keep.p ? dj_keep.p : nullptr);
             verbose_mark(g->ctx, "fc.commit_device");
+            // one GPU: the committed results' nodes, gathered from the device in one copy
+            std::vector<uint64_t> hres;
+            if (N == 1 && dn_keep.p) {
+                std::vector<uint64_t> seg;
+                uint64_t tot = 0;
+                for (uint64_t j = 0; j < f; ++j)
+                    if (!skip[j] && hs[j]->ncyc > 0 && hs[j]->nnodes) {
+                        seg.insert(seg.end(), {joff[j], (uint64_t)hs[j]->nnodes, tot});
+                        tot += hs[j]->nnodes;
+                    }
+                if (tot) {
+                    DevBuf<uint64_t> dseg(seg.size()), dres(tot);
+                    h2d(g->ctx, dseg.p, seg.data(), 8 * seg.size());
+                    hipLaunchKernelGGL(k_fc_segs, dim3((unsigned)(seg.size() / 3)), dim3(256), 0, st,
+                                       (const uint64_t *)dn_keep.p, (const uint64_t *)dseg.p, dres.p);
+                    LAUNCH_OK();
+                    hres.resize(tot);
+                    d2h(g->ctx, hres.data(), dres.p, 8 * tot);
+                    uint64_t at = 0;
+                    for (uint64_t j = 0; j < f; ++j)
+                        if (!skip[j] && hs[j]->ncyc > 0 && hs[j]->nnodes) {
+                            jn[j] = hres.data() + at;
+                            at += hs[j]->nnodes;
+                        }
+                }
+            }
             // results of the committed prefix [0, f)
             for (uint64_t j = 0; j < f; ++j) {
                 if (skip[j]) continue;
