@@ -419,8 +419,8 @@ int mcaat_set_knob(mcaat_ctx *ctx, const char *name, int64_t value);
  *                      the search replica reads its frontier size after every hop (round 5's forms;
  *                      default 0: the hops run back to back on the device, fixed-capacity blocks
  *                      exchanged by an all-to-all that RCCL leaves queued on the stream)
- *   dist.bfs_block    region BFS: requests per block to another rank (default 2^14; an overflow on
- *                      any rank reruns the BFS with larger blocks)
+ *   dist.bfs_block    region BFS: requests per block to another rank (default 2^16; an overflow on
+ *                      any rank reruns the BFS with larger blocks, kept for the next step)
  *   dist.bfs_frontier region BFS: first frontier / own-block capacity (tests; default D_local/16,
  *                      at least 2^20; an overflow reruns with more)
  *   dist.res_fixed    0: the peel's branch resolution by routed rounds (round 5's form; default 1:

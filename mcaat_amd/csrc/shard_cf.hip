@@ -1714,7 +1714,8 @@ struct ShardCf {
         DevBuf<uint64_t> dids(m + 1);
         if (m) h2d(ctx, dids.p, ids.data(), 8 * m);
         BfsCaps c;
-        c.P = (uint64_t)std::max<int64_t>(64, knob(ctx, "dist.bfs_block", 1 << 14));
+        // (C3 at 8 ranks needs up to 2^15 requests a block: 2^16 is 512 KB a peer and hop)
+        c.P = (uint64_t)std::max<int64_t>(64, knob(ctx, "dist.bfs_block", 1 << 16));
         if (!knob_set(ctx, "dist.bfs_block")) c.P = std::max(c.P, ctx->bfs_block[backward]);
         // a frontier or the own block: the whole local graph in the end (each edge joins one
         // frontier at most once), a sixteenth of it (and the seeds) first
