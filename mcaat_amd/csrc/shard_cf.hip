@@ -233,6 +233,8 @@ __global__ void __launch_bounds__(kBlk) k_route_place(const uint64_t *rec, int W
     }
 }
 
+__global__ void k_set_word(uint64_t *p, uint64_t v) { *p = v; }
+
 struct Routed {
     int W = 1;
     uint64_t n = 0, sent = 0, n_in = 0, total = 0;  // slots, records sent, received, sent by all ranks
@@ -259,7 +261,10 @@ struct Router {
 
     // n slots (rec: n x W words; dest[i] a rank or kNoDest). keep: a reply follows (dest must
     // stay valid until it). Records for this rank go straight to the receive buffer.
-    void send(const uint64_t *rec, int W, const uint8_t *dest, uint64_t n, Routed &rt, bool keep) {
+    // extra_sum: the sum over the ranks of `extra`, carried in the same count all-gather (a loop's
+    // global condition without a collective of its own)
+    void send(const uint64_t *rec, int W, const uint8_t *dest, uint64_t n, Routed &rt, bool keep,
+              uint64_t extra = 0, uint64_t *extra_sum = nullptr) {
         hipStream_t st = ctx->stream;
         const int N = comm.world, R = comm.rank;
         rt.W = W;
@@ -270,7 +275,12 @@ struct Router {
         rt.G = n ? (int)((n + rt.per - 1) / rt.per) : 0;
         DevBuf<uint32_t> cnt((uint64_t)std::max(rt.G, 1) * N);
         rt.base.alloc((uint64_t)std::max(rt.G, 1) * N);
-        DevBuf<uint64_t> tot(N);
+        const int NW = N + (extra_sum ? 1 : 0);
+        DevBuf<uint64_t> tot(NW);
+        if (extra_sum) {
+            hipLaunchKernelGGL(k_set_word, dim3(1), dim3(1), 0, st, tot.p + N, extra);
+            LAUNCH_OK();
+        }
         double t0 = now();
         if (n) {
             hipLaunchKernelGGL(k_route_count, dim3(rt.G), dim3(kBlk), 0, st, dest, n, rt.per, N, cnt.p);
@@ -284,7 +294,16 @@ struct Router {
         t_count += t1 - t0;
         // every rank's send counts straight from the device (one read of the gathered matrix)
         std::vector<uint64_t> mat;
-        comm.allgather_dev_words(tot.p, N, mat);
+        comm.allgather_dev_words(tot.p, NW, mat);
+        if (extra_sum) {  // back to the N x N count matrix, the extra words summed
+            std::vector<uint64_t> m2((uint64_t)N * N);
+            *extra_sum = 0;
+            for (int r = 0; r < N; ++r) {
+                for (int q = 0; q < N; ++q) m2[(uint64_t)r * N + q] = mat[(uint64_t)r * NW + q];
+                *extra_sum += mat[(uint64_t)r * NW + N];
+            }
+            mat.swap(m2);
+        }
         for (int q = 0; q < N; ++q) rt.out_cnt[q] = mat[(uint64_t)R * N + q];
         rt.sent = 0;
         for (uint64_t x : rt.out_cnt) rt.sent += x;
@@ -2292,7 +2311,6 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
         while ((1ULL << bound) < total_rulers + 1) ++bound;
         bound += 1;
         for (; jump_rounds < (uint64_t)bound; ++jump_rounds) {
-            if (s.sum(na) == 0) break;
             DevBuf<uint64_t> q(na ? na : 1);
             DevBuf<uint8_t> dest(na ? na : 1);
             if (na) {
@@ -2301,7 +2319,9 @@ void cycle_finder_sharded(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles
                 LAUNCH_OK();
             }
             Routed r;
-            s.rt.send(q.p, 1, dest.p, na, r, true);
+            uint64_t active_all = 0;  // every rank's active rulers (round 5: a sum of its own first)
+            s.rt.send(q.p, 1, dest.p, na, r, true, na, &active_all);
+            if (active_all == 0) break;  // (the round carried nothing on any rank)
             DevBuf<uint64_t> ans(r.n_in + 1);
             if (r.n_in) {
                 hipLaunchKernelGGL(k_jump_ans, dim3(s.grid(r.n_in)), dim3(kBlk), 0, st, (const uint64_t *)r.in.p, r.n_in,
