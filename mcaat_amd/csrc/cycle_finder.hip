@@ -104,7 +104,9 @@ struct PeelArrays {
 // self-loop test of the candidate filter are two bitmap words as well
 // (knob cf.scan_u). More words per wave means fewer waves: C3 recount with 1 / 2 / 4 / 8 words
 // 5.5 / 5.7 / 8.3 / 18.0 ms (79 VGPRs at 2, 141 at 4, 256 at 8), the occupancy matters more
-constexpr int kScanUDefault = 2;
+// (round 6) default 1: the tips / filter pass C3 14.3 -> 13.8 ms, C5 50.1 -> 46.0 (4: 61.2);
+// cf.scan_u=2 keeps round 3's two words
+constexpr int kScanUDefault = 1;
 
 // A wave's appends to a global id list, staged in LDS and published 64 at a time with one
 // cursor atomic (at C5 the candidates and the peel's branch nodes occur in most waves, and an
@@ -2550,7 +2552,7 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
             DevBuf<uint64_t> mpost;
             if (comm) mpost.alloc(std::max<uint64_t>(w_hi - w_lo, 1));
             if (w_hi > w_lo) {
-                auto kern = scan_u == 1 ? k_post_filter<1> : scan_u == 4 ? k_post_filter<4> : k_post_filter<kScanUDefault>;
+                auto kern = scan_u == 1 ? k_post_filter<1> : scan_u == 4 ? k_post_filter<4> : k_post_filter<2>;
                 hipLaunchKernelGGL(kern, dim3(wgrid), dim3(kBlock), 0, st, v, w_lo, w_hi, comm ? mpost.p : post.p + w_lo,
                                    c2.p, fresh);
                 LAUNCH_OK();
@@ -2608,7 +2610,7 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
                              : (pull ? k_tips_filter<U, false, true> : k_tips_filter<U, false, false>);
             };
             auto kern = scan_u == 1 ? pick(std::integral_constant<int, 1>{})
-                        : scan_u == 4 ? pick(std::integral_constant<int, 4>{}) : pick(std::integral_constant<int, kScanUDefault>{});
+                        : scan_u == 4 ? pick(std::integral_constant<int, 4>{}) : pick(std::integral_constant<int, 2>{});
             hipLaunchKernelGGL(kern, dim3(wgrid), dim3(kBlock), 0, st, v, w_lo, w_hi, comm ? mseeds.p : seeds.p + w_lo,
                                (const uint64_t *)post.p, c2.p, fa, (uint64_t)p.threshold_multiplicity,
                                fold ? clist.p : (uint64_t *)nullptr, ccap);
@@ -2709,7 +2711,7 @@ void cycle_finder(mcaat_graph *g, const mcaat_cf_params &p, mcaat_cycles *out, C
             HIP_OK(hipMemsetAsync(c3.p, 0, 24, st));
             if (w_hi > w_lo) {
                 auto kern = scan_u == 1 ? k_recount_candidates<1> : scan_u == 4 ? k_recount_candidates<4>
-                                                                                : k_recount_candidates<kScanUDefault>;
+                                                                                : k_recount_candidates<2>;
                 hipLaunchKernelGGL(kern, dim3(wgrid), dim3(kBlock), 0, st, v,
                                    (uint64_t)p.threshold_multiplicity, lo, hi, w_lo, w_hi, list.p, cap, c3.p);
                 LAUNCH_OK();

@@ -75,6 +75,7 @@ KNOBS = {
     # the scans with four 64-edge words in flight per wave, the peel prep with eight edges
     "scan_u4_prep8": {"cf.scan_u": 4, "cf.prep_batch": 8},
     "scan_u1_prep16": {"cf.scan_u": 1, "cf.prep_batch": 16},
+    "scan_u2": {"cf.scan_u": 2},  # (round 6: 1 is the default, 2 round 3's)
     # DepthLevelSearch with one search per wave and with a full wave of them
     "dls_lanes1": {"cf.dls_lanes": 1},
     "dls_lanes64": {"cf.dls_lanes": 64, "cf.dls_stack": 1, "cf.dls_visited": 2, "cf.dls_lds": 0},
