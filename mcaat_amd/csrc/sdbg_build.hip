@@ -561,6 +561,12 @@ struct LinePlace {
 };
 
 constexpr int kSBlock = 1024;
+// rounds of entries in flight in the level-1/2 scatters (MCAAT_SPF). Measured (round 6, C3):
+// 1 / 2 / 4 rounds: sdbg_build 36.0 / 39.3 / 37.9 ms (more registers, fewer waves), so 1
+#ifndef MCAAT_SPF
+#define MCAAT_SPF 1
+#endif
+constexpr int kSPF = MCAAT_SPF;
 
 __global__ void __launch_bounds__(kSBlock) k_msd1_scatter(const uint64_t *ckeys, const uint32_t *ccnt, uint64_t n,
                                                           int k, const uint32_t *off, uint64_t *out) {
@@ -574,20 +580,27 @@ __global__ void __launch_bounds__(kSBlock) k_msd1_scatter(const uint64_t *ckeys,
     }
     __syncthreads();
     LinePlace lp{buf, lb, lc, bl, out, 0};
-    // the next round's entry is loaded while this round places its items
-    uint64_t na = 0;
-    uint32_t nc = 0;
-    if (c0 + threadIdx.x < c1) {
-        na = ckeys[c0 + threadIdx.x];
-        nc = ccnt[c0 + threadIdx.x];
+    // the entries of the next kSPF rounds are loaded while this round places its items
+    uint64_t na[kSPF];
+    uint32_t nc[kSPF];
+#pragma unroll
+    for (int u = 0; u < kSPF; ++u) {
+        const uint64_t i = c0 + (uint64_t)u * kSBlock + threadIdx.x;
+        na[u] = i < c1 ? ckeys[i] : 0;
+        nc[u] = i < c1 ? ccnt[i] : 0;
     }
-    for (uint64_t i0 = c0; i0 < c1; i0 += kSBlock) {
+    for (uint64_t i00 = c0; i00 < c1; i00 += (uint64_t)kSPF * kSBlock)
+#pragma unroll
+    for (int u = 0; u < kSPF; ++u) {
+        const uint64_t i0 = i00 + (uint64_t)u * kSBlock;
+        if (i0 >= c1) break;  // uniform: every thread reaches the same barriers
         const uint64_t i = i0 + threadIdx.x;
-        const uint64_t a = na;
-        const uint32_t cn = nc;
-        if (i + kSBlock < c1) {
-            na = ckeys[i + kSBlock];
-            nc = ccnt[i + kSBlock];
+        const uint64_t a = na[u];
+        const uint32_t cn = nc[u];
+        const uint64_t ni = i + (uint64_t)kSPF * kSBlock;
+        if (ni < c1) {
+            na[u] = ckeys[ni];
+            nc[u] = ccnt[ni];
         }
         uint32_t bk[2] = {0, 0}, r[2] = {0, 0}, line[2] = {0, 0}, nl[2] = {0, 0};
         uint64_t it[2] = {0, 0};
@@ -649,11 +662,20 @@ __global__ void __launch_bounds__(kSBlock) k_msd2_scatter(const uint64_t *in, co
     const uint64_t s0 = cstart[c];
     const uint32_t n = clen[c];
     LinePlace lp{buf, lb, lc, bl, out, 0};
-    uint64_t nxt = threadIdx.x < n ? in[s0 + threadIdx.x] : kPad;
-    for (uint32_t i0 = 0; i0 < n; i0 += kSBlock) {
-        const uint64_t it = nxt;
-        const uint32_t ni = i0 + kSBlock + threadIdx.x;
-        nxt = ni < n ? in[s0 + ni] : kPad;
+    uint64_t nxt[kSPF];
+#pragma unroll
+    for (int u = 0; u < kSPF; ++u) {
+        const uint32_t i = (uint32_t)u * kSBlock + threadIdx.x;
+        nxt[u] = i < n ? in[s0 + i] : kPad;
+    }
+    for (uint32_t i00 = 0; i00 < n; i00 += (uint32_t)kSPF * kSBlock)
+#pragma unroll
+    for (int u = 0; u < kSPF; ++u) {
+        const uint32_t i0 = i00 + (uint32_t)u * kSBlock;
+        if (i0 >= n) break;  // uniform
+        const uint64_t it = nxt[u];
+        const uint32_t ni = i0 + (uint32_t)kSPF * kSBlock + threadIdx.x;
+        nxt[u] = ni < n ? in[s0 + ni] : kPad;
         const bool live = it != kPad;
         uint32_t b = 0, r = 0, line = 0, nl = 0;
         bool bf = false;
