@@ -562,7 +562,7 @@ struct LinePlace {
 
 constexpr int kSBlock = 1024;
 // rounds of entries in flight in the level-1/2 scatters (MCAAT_SPF). Measured (round 6, C3):
-// 1 / 2 / 4 rounds: sdbg_build 36.0 / 39.3 / 37.9 ms (more registers, fewer waves), so 1
+// 1 / 2 / 4 rounds: sdbg_build 36.0 / 39.3 / 37.9 ms, so 1 (profiles/r06_c3_msd_prefetch_ab.txt)
 #ifndef MCAAT_SPF
 #define MCAAT_SPF 1
 #endif
