@@ -974,7 +974,17 @@ __global__ void __launch_bounds__(kBlock) k_dls_lanes(GraphView g, const uint64_
 // reads per expansion (out_info, then the targets' validity window), not by the visited set or
 // the stack; a variant feeding each lane its next candidate from a counter (so no lane waits
 // for its wave's longest search) took 47.7 ms (fewer resident searches, a ballot per step).
-constexpr int kLdsLanes = 16, kLdsVis = 256, kLdsStk = 128;
+// (round 6) Being latency-bound, it gains from more resident searches at smaller caps (overflows
+// re-run): 40 searches per wave with 128 visited slots (96 used) and 16 stack entries, 23.7 KB,
+// six workgroups and 240 searches per CU (round 5: 16 x 256 / 128, 96 per CU). C5 DLS 41.6 ->
+// 34.1 ms, C3 2.9 -> 2.5 (`profiles/r06_c5_dls_lanes_ab.txt`: 32 x 128 / 64 39.1, 40 x 128 / 32
+// 36.3, 48 x 128 / 16 34.8, 64 x 64 / 32 51.9).
+#ifndef MCAAT_DLS_LANES
+#define MCAAT_DLS_LANES 40
+#define MCAAT_DLS_VIS 128
+#define MCAAT_DLS_STK 16
+#endif
+constexpr int kLdsLanes = MCAAT_DLS_LANES, kLdsVis = MCAAT_DLS_VIS, kLdsStk = MCAAT_DLS_STK;
 __global__ void __launch_bounds__(64) k_dls_lds(GraphView g, const uint64_t *cand, uint64_t n, int limit, int8_t *res,
                                                 uint32_t vmax, uint32_t smax) {
     __shared__ uint32_t vis_s[kLdsLanes][kLdsVis];
